@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: toy-MLP DDP training throughput (samples/s for the whole node).
+
+Metric / config from BASELINE.json: "samples/sec (whole node) toy-MLP DDP at 1/2/4/8 MI355X".
+Model: ToyMLP 9216 -> 4096 -> 4096 -> 10 (Linear+ReLU; = the reference AlexNet's classifier),
+per-rank batch 128 (REF/multi-GPU-training-torch.py:88), synthetic on-device data, random init,
+fp32 (the reference's dtype), CrossEntropyLoss, SGD(momentum=0.9) (the north star's fused SGD),
+one full DDP step per iteration: sampler-ordered batch gather -> forward -> loss -> backward with
+bucketed RCCL all-reduce -> optimizer step. Weak scaling: per-GPU work is fixed.
+
+  python bench.py                                   # 1 GPU
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  python bench.py --impl torch                      # stock torch DDP + torch.optim (comparison)
+
+Timing: W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
+both sides; the max over ranks is reported; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+METRIC = "samples/sec (whole node) toy-MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
+ROOT = Path(__file__).resolve().parent
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128, help="per-rank batch")
+    ap.add_argument("--impl", choices=["tdp", "torch"], default="tdp")
+    ap.add_argument("--optim", choices=["sgd", "adam"], default="sgd")
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
+    ap.add_argument("--dataset", type=int, default=8192, help="synthetic samples per rank")
+    ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
+    ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    return ap.parse_args()
+
+
+def baseline_for(n_gpus: int, impl: str, syncbn: bool):
+    """Stock torch DDP number on MI355X for the same config (bench_baseline.json), if measured."""
+    f = ROOT / "bench_baseline.json"
+    if impl != "tdp" or not f.exists():
+        return None
+    try:
+        tab = json.loads(f.read_text())
+        key = f"{'mlp_syncbn' if syncbn else 'mlp'}_dp{n_gpus}"
+        v = tab.get(key)
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus and "RANK" in os.environ:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    use_gpu = torch.cuda.is_available() and not a.cpu
+
+    if a.impl == "tdp":
+        import tutorial_torch_distributed_data_parallel_amd as tdp
+        from tutorial_torch_distributed_data_parallel_amd.data import (DeviceLoader,
+                                                                        DistributedSampler,
+                                                                        SyntheticDataset)
+        from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+        from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+
+        tdp.init_process_group("nccl" if use_gpu else "gloo")
+        rank, world, dev = rt.get_rank(), rt.get_world_size(), rt.device()
+        torch.manual_seed(1234 + rank)
+        model = ToyMLP(batchnorm=a.syncbn, device=dev)
+        if a.syncbn:
+            model = tdp.nn.convert_sync_batchnorm(model)
+        ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
+                      bucket_cap_mb=a.bucket_mb,
+                      grad_compression=None if a.compression == "none" else a.compression)
+        crit = tdp.nn.CrossEntropyLoss()
+        if a.optim == "sgd":
+            opt = tdp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
+        else:
+            opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
+        data = SyntheticDataset(a.dataset, (9216,), 10, seed=rank, device=dev)
+        sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
+        loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+        barrier = rt.barrier
+        finish = tdp.destroy_process_group
+        acc = torch.zeros(3, device=dev)
+
+        def loss_fn(out, y):
+            return tdp.ops.cross_entropy(out, y, acc=acc)
+    else:
+        import torch.distributed as dist
+        import torch.nn as nn
+        from torch.nn.parallel import DistributedDataParallel as TorchDDP
+        from torch.utils.data import DistributedSampler as TorchSampler
+
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if use_gpu:
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cpu")
+        if world > 1 or "MASTER_ADDR" in os.environ:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world)
+        else:
+            os.environ["MASTER_ADDR"] = "127.0.0.1"
+            os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 300)
+            dist.init_process_group("nccl" if use_gpu else "gloo", rank=0, world_size=1)
+        torch.manual_seed(1234 + rank)
+        layers = [nn.Linear(9216, 4096)]
+        if a.syncbn:
+            layers.append(nn.BatchNorm1d(4096))
+        layers += [nn.ReLU(inplace=True), nn.Linear(4096, 4096)]
+        if a.syncbn:
+            layers.append(nn.BatchNorm1d(4096))
+        layers += [nn.ReLU(inplace=True), nn.Linear(4096, 10)]
+        model = nn.Sequential(*layers).to(dev)
+        if a.syncbn:
+            model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        ddp = TorchDDP(model, device_ids=[local] if use_gpu else None,
+                       bucket_cap_mb=a.bucket_mb if a.bucket_mb else 25)
+        crit = nn.CrossEntropyLoss()
+        opt = (torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9) if a.optim == "sgd"
+               else torch.optim.Adam(ddp.parameters(), lr=1e-3))
+        g = torch.Generator(device=dev)
+        g.manual_seed(rank)
+        X = torch.randn(a.dataset, 9216, generator=g, device=dev)
+        Y = torch.randint(0, 10, (a.dataset,), generator=g, device=dev)
+
+        class _DS:
+            def __len__(self):
+                return a.dataset
+        sampler = TorchSampler(_DS(), num_replicas=world, rank=rank, shuffle=True)
+
+        class _Loader:
+            def __iter__(self):
+                idx = torch.as_tensor(list(sampler), dtype=torch.long)
+                for s in range(0, len(idx) - len(idx) % a.batch, a.batch):
+                    b = idx[s:s + a.batch].to(dev, non_blocking=True)
+                    yield X.index_select(0, b), Y.index_select(0, b)
+        loader = _Loader()
+
+        def barrier():
+            dist.barrier()
+
+        def finish():
+            dist.destroy_process_group()
+
+        def loss_fn(out, y):
+            return crit(out, y)
+
+    sync = (torch.cuda.synchronize if use_gpu else (lambda: None))
+    epoch = [0]
+    it = [iter(loader)]
+
+    def next_batch():
+        try:
+            return next(it[0])
+        except StopIteration:
+            epoch[0] += 1
+            sampler.set_epoch(epoch[0])
+            it[0] = iter(loader)
+            return next(it[0])
+
+    def step():
+        x, y = next_batch()
+        opt.zero_grad(set_to_none=True)
+        out = ddp(x)
+        loss = loss_fn(out, y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync()
+    barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    # max over ranks (the slowest rank defines the job's throughput)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if use_gpu else "cpu")
+    if world > 1:
+        if a.impl == "tdp":
+            rt.all_reduce(t, "max")
+        else:
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt * 1000.0 / a.steps
+    value = a.batch * world * a.steps / dt
+    base = baseline_for(world, a.impl, a.syncbn)
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world if use_gpu else 0,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 4) if base else None,
+            "dtype": "fp32",
+            "data": "synthetic (on-device random features, random-init weights)",
+            "config": {
+                "model": "toy-MLP 9216-4096-4096-10 (Linear+ReLU" +
+                         (", +SyncBatchNorm" if a.syncbn else "") + ")",
+                "global_batch": a.batch * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "impl": "tdp (native gfx950 kernels + RCCL reducer)" if a.impl == "tdp"
+                        else "stock torch DDP + torch.optim",
+                "optimizer": a.optim,
+                "final_loss": round(float(loss.item()), 5),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    finish()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,504 @@
+// pybind11 bindings: PyTorch tensors -> raw pointers + the current HIP stream for every native
+// launcher in kernels.h, plus the RCCL communicator and the gradient reducer.
+//
+// Every op checks device/dtype/layout and raises on misuse: there is no silent fallback to ATen
+// inside the extension (CPU execution is handled, explicitly, by the Python ops layer).
+#include <c10/hip/HIPStream.h>
+#include <pybind11/functional.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+#include <cmath>
+#include <map>
+#include <mutex>
+
+#include "comm.h"
+#include "kernels.h"
+#include "reducer.h"
+
+namespace py = pybind11;
+using at::Tensor;
+using namespace tdp;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int num_cus(int device) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  int v = 0;
+  check_hip(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device),
+            "hipDeviceGetAttribute");
+  cache[device] = v;
+  return v;
+}
+
+#define CHECK_GPU(x) TORCH_CHECK((x).is_cuda(), #x " must be on the GPU")
+#define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be float32")
+#define CHECK_ROWMAJOR(x) \
+  TORCH_CHECK((x).dim() == 2 && (x).stride(1) == 1, #x " must be 2-D with unit inner stride")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+float* fptr(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+// --------------------------------------------------------------------------------------- GEMM
+// A: [M,K] if a_kcontig else [K,M];  B: [N,K] if b_kcontig else [K,N];  C: [M,N]
+void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
+                 const c10::optional<Tensor>& mask, const c10::optional<Tensor>& bias,
+                 const c10::optional<Tensor>& rowsum, double beta, double rowsum_beta,
+                 bool relu) {
+  CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
+  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
+  CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_ROWMAJOR(C);
+  const int M = (int)C.size(0), N = (int)C.size(1);
+  const int K = (int)(a_kcontig ? A.size(1) : A.size(0));
+  TORCH_CHECK((a_kcontig ? A.size(0) : A.size(1)) == M, "gemm: A rows != C rows");
+  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm: B cols != C cols");
+  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm: inner dims differ");
+  GemmF32Args a;
+  a.A = A.data_ptr<float>(); a.B = B.data_ptr<float>(); a.C = C.data_ptr<float>();
+  a.lda = A.stride(0); a.ldb = B.stride(0); a.ldc = C.stride(0);
+  a.M = M; a.N = N; a.K = K;
+  a.a_kcontig = a_kcontig; a.b_kcontig = b_kcontig;
+  if (mask.has_value() && mask->defined()) {
+    CHECK_GPU(*mask); CHECK_F32(*mask); CHECK_ROWMAJOR(*mask);
+    TORCH_CHECK(mask->sizes() == A.sizes(), "gemm: mask must have A's shape");
+    a.mask = mask->data_ptr<float>();
+    a.ldmask = mask->stride(0);
+  }
+  if (bias.has_value() && bias->defined()) {
+    CHECK_GPU(*bias); CHECK_F32(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == N, "gemm: bias must have N elements");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (rowsum.has_value() && rowsum->defined()) {
+    CHECK_GPU(*rowsum); CHECK_F32(*rowsum); CHECK_CONTIG(*rowsum);
+    TORCH_CHECK(rowsum->numel() == M, "gemm: rowsum must have M elements");
+    a.rowsum = rowsum->data_ptr<float>();
+  }
+  a.beta = (float)beta;
+  a.rowsum_beta = (float)rowsum_beta;
+  a.relu = relu;
+  const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
+  gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+}
+
+std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus) {
+  GemmF32Args a;
+  a.M = M; a.N = N; a.K = K;
+  a.rowsum = rowsum ? reinterpret_cast<float*>(16) : nullptr;
+  const GemmPlan p = gemm_f32_plan(a, cus);
+  return {p.tile, p.bm, p.bn, p.splits, p.k_per_split, p.ws_floats};
+}
+
+// ----------------------------------------------------------------------------------------- loss
+std::vector<Tensor> ce_fwd_op(const Tensor& logits, const Tensor& labels, int64_t ignore_index,
+                              double smoothing, bool mean, const c10::optional<Tensor>& acc) {
+  CHECK_GPU(logits); CHECK_F32(logits); CHECK_ROWMAJOR(logits);
+  CHECK_GPU(labels); CHECK_CONTIG(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  const int B = (int)logits.size(0), C = (int)logits.size(1);
+  TORCH_CHECK(labels.numel() == B, "labels must have one entry per row");
+  auto loss = at::empty({}, logits.options());
+  auto lse = at::empty({B + 1}, logits.options());
+  float* accp = nullptr;
+  if (acc.has_value() && acc->defined()) {
+    CHECK_GPU(*acc); CHECK_F32(*acc);
+    TORCH_CHECK(acc->numel() >= 3, "acc needs 3 floats");
+    accp = acc->data_ptr<float>();
+  }
+  cross_entropy_fwd(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), B, C, logits.stride(0),
+                    (int)ignore_index, (float)smoothing, mean, loss.data_ptr<float>(),
+                    lse.data_ptr<float>(), accp, cur_stream());
+  return {loss, lse};
+}
+
+Tensor ce_bwd_op(const Tensor& logits, const Tensor& labels, const Tensor& lse,
+                 const Tensor& gout, int64_t ignore_index, double smoothing, bool mean) {
+  CHECK_GPU(logits); CHECK_F32(logits); CHECK_ROWMAJOR(logits);
+  CHECK_GPU(gout); CHECK_F32(gout);
+  const int B = (int)logits.size(0), C = (int)logits.size(1);
+  auto d = at::empty({B, C}, logits.options());
+  auto g = gout.contiguous();
+  cross_entropy_bwd(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                    g.data_ptr<float>(), B, C, logits.stride(0), (int)ignore_index,
+                    (float)smoothing, mean, d.data_ptr<float>(), cur_stream());
+  return d;
+}
+
+void count_correct_op(const Tensor& logits, const Tensor& labels, Tensor& acc) {
+  CHECK_GPU(logits); CHECK_F32(logits); CHECK_ROWMAJOR(logits);
+  CHECK_GPU(acc); CHECK_F32(acc);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  count_correct(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)logits.size(0),
+                (int)logits.size(1), logits.stride(0), acc.data_ptr<float>(), cur_stream());
+}
+
+// ---------------------------------------------------------------------------------- optimizers
+void sgd_flat_op(Tensor& p, const Tensor& g, const c10::optional<Tensor>& buf, double lr,
+                 double momentum, double dampening, double wd, bool nesterov, bool maximize,
+                 bool first_step, double grad_scale) {
+  CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
+  TORCH_CHECK(p.numel() == g.numel(), "sgd: p/g size mismatch");
+  if (momentum != 0.0)
+    TORCH_CHECK(buf.has_value() && buf->numel() == p.numel(), "sgd: momentum buffer required");
+  SgdHyper h{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
+             first_step, (float)grad_scale};
+  sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), fptr(buf), p.numel(), h, cur_stream());
+}
+
+void adam_flat_op(Tensor& p, const Tensor& g, Tensor& m, Tensor& v,
+                  const c10::optional<Tensor>& vmax, double lr, double b1, double b2, double eps,
+                  double wd, bool amsgrad, bool maximize, bool decoupled, int64_t step,
+                  double grad_scale) {
+  CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(),
+              "adam: size mismatch");
+  if (amsgrad) TORCH_CHECK(vmax.has_value() && vmax->numel() == p.numel(), "adam: need vmax");
+  AdamHyper h{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, amsgrad, maximize,
+              decoupled, (float)(1.0 - std::pow(b1, (double)step)),
+              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale};
+  adam_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+            fptr(vmax), p.numel(), h, cur_stream());
+}
+
+// Build the chunk table (<= 64K elements per workgroup) on the host, ship it with the launch.
+Tensor chunk_table(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
+                   const std::vector<Tensor>& s0, const std::vector<Tensor>& s1,
+                   const std::vector<Tensor>& s2, int* count) {
+  constexpr long CH = 65536;
+  std::vector<TensorChunk> tab;
+  for (size_t i = 0; i < ps.size(); ++i) {
+    const long n = ps[i].numel();
+    TORCH_CHECK(gs[i].numel() == n, "multi-tensor: grad size mismatch");
+    for (long o = 0; o < n; o += CH) {
+      TensorChunk c;
+      c.p = ps[i].data_ptr<float>() + o;
+      c.g = gs[i].data_ptr<float>() + o;
+      c.s0 = s0.empty() ? nullptr : s0[i].data_ptr<float>() + o;
+      c.s1 = s1.empty() ? nullptr : s1[i].data_ptr<float>() + o;
+      c.s2 = s2.empty() ? nullptr : s2[i].data_ptr<float>() + o;
+      c.n = std::min(CH, n - o);
+      tab.push_back(c);
+    }
+  }
+  *count = (int)tab.size();
+  auto host = at::empty({(int64_t)(tab.size() * sizeof(TensorChunk))},
+                        at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  std::memcpy(host.data_ptr(), tab.data(), tab.size() * sizeof(TensorChunk));
+  return host.to(ps[0].device(), /*non_blocking=*/true);
+}
+
+void sgd_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
+                  const std::vector<Tensor>& bufs, double lr, double momentum, double dampening,
+                  double wd, bool nesterov, bool maximize, bool first_step, double grad_scale) {
+  if (ps.empty()) return;
+  for (auto& t : ps) { CHECK_GPU(t); CHECK_F32(t); CHECK_CONTIG(t); }
+  for (auto& t : gs) { CHECK_F32(t); CHECK_CONTIG(t); }
+  int count = 0;
+  auto tab = chunk_table(ps, gs, bufs, {}, {}, &count);
+  SgdHyper h{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
+             first_step, (float)grad_scale};
+  sgd_multi(reinterpret_cast<const TensorChunk*>(tab.data_ptr()), count, h, cur_stream());
+}
+
+void adam_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
+                   const std::vector<Tensor>& ms, const std::vector<Tensor>& vs,
+                   const std::vector<Tensor>& vmaxs, double lr, double b1, double b2, double eps,
+                   double wd, bool amsgrad, bool maximize, bool decoupled, int64_t step,
+                   double grad_scale) {
+  if (ps.empty()) return;
+  for (auto& t : ps) { CHECK_GPU(t); CHECK_F32(t); CHECK_CONTIG(t); }
+  int count = 0;
+  auto tab = chunk_table(ps, gs, ms, vs, amsgrad ? vmaxs : std::vector<Tensor>{}, &count);
+  AdamHyper h{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, amsgrad, maximize,
+              decoupled, (float)(1.0 - std::pow(b1, (double)step)),
+              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale};
+  adam_multi(reinterpret_cast<const TensorChunk*>(tab.data_ptr()), count, h, cur_stream());
+}
+
+// ------------------------------------------------------------------------------------ misc ops
+void scale_op(Tensor& x, double a) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  scale_inplace(x.data_ptr<float>(), x.numel(), (float)a, cur_stream());
+}
+
+Tensor sumsq_op(const Tensor& x, const c10::optional<Tensor>& into) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  Tensor out = (into.has_value() && into->defined()) ? *into : at::zeros({1}, x.options());
+  sumsq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), true, cur_stream());
+  return out;
+}
+
+void clip_op(Tensor& x, const Tensor& total, double max_norm) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  clip_scale(x.data_ptr<float>(), x.numel(), total.data_ptr<float>(), (float)max_norm,
+             cur_stream());
+}
+
+void cast_f32_bf16_op(const Tensor& x, Tensor& y) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_CONTIG(y);
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.numel() == x.numel(), "cast: bad output");
+  f32_to_bf16_copy(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(),
+                   cur_stream());
+}
+
+// ------------------------------------------------------------------------------------ batchnorm
+// x viewed as [N, C, HW]
+void bn_dims(const Tensor& x, int& N, int& C, int& HW) {
+  TORCH_CHECK(x.dim() >= 2, "batchnorm input must be at least 2-D");
+  N = (int)x.size(0);
+  C = (int)x.size(1);
+  HW = (int)(x.numel() / ((int64_t)N * C));
+}
+
+std::vector<Tensor> bn_moments_op(const Tensor& x) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  int N, C, HW;
+  bn_dims(x, N, C, HW);
+  const int splits = bn_splits(N, C, HW, num_cus(x.get_device()));
+  auto out = at::empty({2 * C + 1}, x.options());  // [mean | var | count]
+  Tensor ws = at::empty({bn_ws_floats(C, splits)}, x.options());
+  bn_moments(x.data_ptr<float>(), N, C, HW, splits, ws.data_ptr<float>(), out.data_ptr<float>(),
+             out.data_ptr<float>() + C, cur_stream());
+  out.narrow(0, 2 * C, 1).fill_((double)N * HW);
+  return {out};
+}
+
+// gathered: R rows of [mean | var | count] -> stats [mean | invstd | total count]
+Tensor bn_merge_op(const Tensor& gathered, int64_t C, double eps, double momentum,
+                   const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar) {
+  CHECK_GPU(gathered); CHECK_F32(gathered); CHECK_CONTIG(gathered);
+  const int R = (int)(gathered.numel() / (2 * C + 1));
+  TORCH_CHECK((int64_t)R * (2 * C + 1) == gathered.numel(), "bn_merge: bad gathered size");
+  auto stats = at::empty({2 * C + 1}, gathered.options());
+  float* sp = stats.data_ptr<float>();
+  bn_merge(gathered.data_ptr<float>(), R, (int)C, (float)eps, (float)momentum, sp, sp + C,
+           fptr(rmean), fptr(rvar), cur_stream());
+  return stats;
+}
+
+Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Tensor>& w,
+                   const c10::optional<Tensor>& b, bool relu) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  int N, C, HW;
+  bn_dims(x, N, C, HW);
+  TORCH_CHECK(stats.numel() == 2 * C + 1, "bn_elemt: stats must be [2C+1]");
+  auto y = at::empty_like(x);
+  const float* sp = stats.data_ptr<float>();
+  bn_elemt(x.data_ptr<float>(), sp, sp + C, fptr(w), fptr(b), N, C, HW, relu,
+           y.data_ptr<float>(), cur_stream());
+  return y;
+}
+
+Tensor bn_eval_op(const Tensor& x, const Tensor& rmean, const Tensor& rvar,
+                  const c10::optional<Tensor>& w, const c10::optional<Tensor>& b, double eps,
+                  bool relu) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  int N, C, HW;
+  bn_dims(x, N, C, HW);
+  auto y = at::empty_like(x);
+  bn_eval(x.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(), fptr(w), fptr(b),
+          N, C, HW, (float)eps, relu, y.data_ptr<float>(), cur_stream());
+  return y;
+}
+
+// returns sums [sum_dy(C) | sum_dy_xmu(C)] ; writes dw/db when given (grad_beta: accumulate)
+Tensor bn_bwd_reduce_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
+                        const c10::optional<Tensor>& y_relu, const c10::optional<Tensor>& dw,
+                        const c10::optional<Tensor>& db, double grad_beta) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  int N, C, HW;
+  bn_dims(x, N, C, HW);
+  const int splits = bn_splits(N, C, HW, num_cus(x.get_device()));
+  auto sums = at::empty({2 * C}, x.options());
+  Tensor ws = at::empty({2L * C * splits}, x.options());
+  const float* sp = stats.data_ptr<float>();
+  bn_bwd_reduce(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(y_relu), N, C, HW,
+                splits, ws.data_ptr<float>(), sums.data_ptr<float>(), fptr(dw), fptr(db),
+                (float)grad_beta, cur_stream());
+  return sums;
+}
+
+Tensor bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
+                       const c10::optional<Tensor>& w, const Tensor& sums,
+                       const c10::optional<Tensor>& y_relu) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  int N, C, HW;
+  bn_dims(x, N, C, HW);
+  auto dx = at::empty_like(x);
+  const float* sp = stats.data_ptr<float>();
+  bn_bwd_elemt(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(w),
+               sums.data_ptr<float>(), fptr(y_relu), sp + 2 * C, N, C, HW, dx.data_ptr<float>(),
+               cur_stream());
+  return dx;
+}
+
+// ---------------------------------------------------------------------------------------- comm
+ncclDataType_t nccl_dt(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kDouble: return ncclFloat64;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL");
+  }
+  return ncclFloat32;
+}
+
+ncclRedOp_t nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  TORCH_CHECK(false, "unknown reduce op ", op);
+  return ncclSum;
+}
+
+py::bytes unique_id_op() {
+  auto v = Communicator::unique_id();
+  return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+std::shared_ptr<Communicator> make_comm(py::bytes uid, int rank, int world, int device) {
+  std::string s = uid;
+  std::vector<uint8_t> v(s.begin(), s.end());
+  py::gil_scoped_release nogil;  // ncclCommInitRank blocks until every rank joined
+  return std::make_shared<Communicator>(v, rank, world, device);
+}
+
+// Python-callable reducer backend (torch.distributed / gloo for CPU runs and tests).
+struct PyBackend : ReducerBackend {
+  py::function launch_fn, wait_fn, zero_fn;
+  PyBackend(py::function l, py::function w, py::function z)
+      : launch_fn(std::move(l)), wait_fn(std::move(w)), zero_fn(std::move(z)) {}
+  void launch(int bucket, int64_t begin, int64_t end, hipStream_t) override {
+    launch_fn(bucket, begin, end);
+  }
+  void wait_all(hipStream_t) override { wait_fn(); }
+  void zero(int64_t begin, int64_t end, hipStream_t) override { zero_fn(begin, end); }
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950-native kernels, RCCL communicator and gradient reducer";
+  m.def("num_cus", &num_cus);
+  m.def("gemm_f32", &gemm_f32_op, py::arg("A"), py::arg("B"), py::arg("C"),
+        py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("mask") = py::none(),
+        py::arg("bias") = py::none(), py::arg("rowsum") = py::none(), py::arg("beta") = 0.0,
+        py::arg("rowsum_beta") = 0.0, py::arg("relu") = false);
+  m.def("gemm_f32_plan", &gemm_f32_plan_op);
+  m.def("ce_fwd", &ce_fwd_op);
+  m.def("ce_bwd", &ce_bwd_op);
+  m.def("count_correct", &count_correct_op);
+  m.def("sgd_flat", &sgd_flat_op);
+  m.def("adam_flat", &adam_flat_op);
+  m.def("sgd_multi", &sgd_multi_op);
+  m.def("adam_multi", &adam_multi_op);
+  m.def("scale_", &scale_op);
+  m.def("sumsq", &sumsq_op, py::arg("x"), py::arg("into") = py::none());
+  m.def("clip_", &clip_op);
+  m.def("cast_f32_bf16", &cast_f32_bf16_op);
+  m.def("bn_moments", &bn_moments_op);
+  m.def("bn_merge", &bn_merge_op);
+  m.def("bn_elemt", &bn_elemt_op);
+  m.def("bn_eval", &bn_eval_op);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce_op);
+  m.def("bn_bwd_elemt", &bn_bwd_elemt_op);
+
+  m.def("rccl_unique_id", &unique_id_op);
+  py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
+      .def(py::init(&make_comm))
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("world", &Communicator::world)
+      .def_property_readonly("device", &Communicator::device)
+      // collectives enqueued on the CURRENT stream (ordered with surrounding PyTorch work)
+      .def("all_reduce",
+           [](Communicator& c, Tensor& t, const std::string& op) {
+             CHECK_GPU(t); CHECK_CONTIG(t);
+             c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dt(t), nccl_op(op),
+                          cur_stream());
+           })
+      .def("broadcast",
+           [](Communicator& c, Tensor& t, int root) {
+             CHECK_GPU(t); CHECK_CONTIG(t);
+             c.broadcast(t.data_ptr(), t.numel(), nccl_dt(t), root, cur_stream());
+           })
+      .def("all_gather",
+           [](Communicator& c, Tensor& out, const Tensor& in) {
+             CHECK_GPU(in); CHECK_CONTIG(in); CHECK_CONTIG(out);
+             TORCH_CHECK(out.numel() == in.numel() * c.world(), "all_gather: bad output size");
+             c.all_gather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dt(in), cur_stream());
+           })
+      .def("reduce_scatter",
+           [](Communicator& c, Tensor& out, const Tensor& in, const std::string& op) {
+             CHECK_GPU(in); CHECK_CONTIG(in); CHECK_CONTIG(out);
+             TORCH_CHECK(in.numel() == out.numel() * c.world(), "reduce_scatter: bad sizes");
+             c.reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dt(in),
+                              nccl_op(op), cur_stream());
+           })
+      .def("send",
+           [](Communicator& c, const Tensor& t, int peer) {
+             c.send(t.data_ptr(), t.numel(), nccl_dt(t), peer, cur_stream());
+           })
+      .def("recv",
+           [](Communicator& c, Tensor& t, int peer) {
+             c.recv(t.data_ptr(), t.numel(), nccl_dt(t), peer, cur_stream());
+           })
+      .def("group_start", &Communicator::group_start)
+      .def("group_end", &Communicator::group_end)
+      .def("abort", &Communicator::abort)
+      // block the host until everything enqueued on the current stream (incl. comms) finished
+      .def("synchronize_current", [](Communicator&) {
+        py::gil_scoped_release nogil;
+        check_hip(hipStreamSynchronize(cur_stream()), "hipStreamSynchronize");
+      });
+
+  py::class_<ReducerBackend, std::shared_ptr<ReducerBackend>>(m, "ReducerBackend")
+      .def("last_comm_ms", &ReducerBackend::last_comm_ms);
+  py::class_<RcclBackend, ReducerBackend, std::shared_ptr<RcclBackend>>(m, "RcclBackend")
+      .def(py::init([](std::shared_ptr<Communicator> comm, Tensor arena, int num_buckets,
+                       int compression, bool timing, bool skip_single_rank) {
+             CHECK_GPU(arena); CHECK_CONTIG(arena);
+             return std::make_shared<RcclBackend>(
+                 comm, arena.data_ptr(), arena.numel(), (int)arena.element_size(), num_buckets,
+                 static_cast<Compression>(compression), timing, skip_single_rank);
+           }),
+           py::arg("comm"), py::arg("arena"), py::arg("num_buckets"),
+           py::arg("compression") = 0, py::arg("timing") = false,
+           py::arg("skip_single_rank") = true);
+  py::class_<PyBackend, ReducerBackend, std::shared_ptr<PyBackend>>(m, "PyBackend")
+      .def(py::init<py::function, py::function, py::function>());
+
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
+                    std::shared_ptr<ReducerBackend>>())
+      .def_static("compute_bucket_bounds", &Reducer::compute_bucket_bounds)
+      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("mark_ready",
+           [](Reducer& r, int p, bool gpu) { r.mark_ready(p, gpu ? cur_stream() : nullptr); })
+      .def("finalize", [](Reducer& r, bool gpu,
+                          bool allow_unused) { r.finalize(gpu ? cur_stream() : nullptr,
+                                                          allow_unused); })
+      .def_property_readonly("expecting", &Reducer::expecting)
+      .def_property_readonly("iteration", &Reducer::iteration)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def("bucket_bounds", &Reducer::bucket_bounds)
+      .def("ready_order", &Reducer::ready_order)
+      .def("unready_params", &Reducer::unready_params)
+      .def("last_comm_ms", &Reducer::last_comm_ms);
+}

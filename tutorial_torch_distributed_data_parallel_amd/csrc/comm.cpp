@@ -1,0 +1,86 @@
+#include "comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace tdp {
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void check_nccl(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+
+std::vector<uint8_t> Communicator::unique_id() {
+  ncclUniqueId id;
+  check_nccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  std::vector<uint8_t> out(sizeof(id.internal));
+  std::memcpy(out.data(), id.internal, sizeof(id.internal));
+  return out;
+}
+
+Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world, int device)
+    : rank_(rank), world_(world), device_(device) {
+  ncclUniqueId id;
+  if (uid.size() != sizeof(id.internal))
+    throw std::runtime_error("RCCL unique id must be " + std::to_string(sizeof(id.internal)) +
+                             " bytes");
+  std::memcpy(id.internal, uid.data(), sizeof(id.internal));
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  // Highest priority for the comm stream: bucket all-reduces should not queue behind backward
+  // GEMMs on the hardware queues (GPU_MAX_HW_QUEUES=4 per process on this pool).
+  int lo = 0, hi = 0;
+  check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+  check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi),
+            "hipStreamCreateWithPriority");
+  check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+Communicator::~Communicator() {
+  if (comm_) ncclCommDestroy(comm_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Communicator::abort() {
+  if (comm_) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
+void Communicator::all_reduce(const void* send, void* recv, size_t count, ncclDataType_t dt,
+                              ncclRedOp_t op, hipStream_t s) {
+  check_nccl(ncclAllReduce(send, recv, count, dt, op, comm_, s), "ncclAllReduce");
+}
+
+void Communicator::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+  check_nccl(ncclBroadcast(buf, buf, count, dt, root, comm_, s), "ncclBroadcast");
+}
+
+void Communicator::all_gather(const void* send, void* recv, size_t send_count, ncclDataType_t dt,
+                              hipStream_t s) {
+  check_nccl(ncclAllGather(send, recv, send_count, dt, comm_, s), "ncclAllGather");
+}
+
+void Communicator::reduce_scatter(const void* send, void* recv, size_t recv_count,
+                                  ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  check_nccl(ncclReduceScatter(send, recv, recv_count, dt, op, comm_, s), "ncclReduceScatter");
+}
+
+void Communicator::send(const void* buf, size_t count, ncclDataType_t dt, int peer,
+                        hipStream_t s) {
+  check_nccl(ncclSend(buf, count, dt, peer, comm_, s), "ncclSend");
+}
+
+void Communicator::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s) {
+  check_nccl(ncclRecv(buf, count, dt, peer, comm_, s), "ncclRecv");
+}
+
+void Communicator::group_start() { check_nccl(ncclGroupStart(), "ncclGroupStart"); }
+void Communicator::group_end() { check_nccl(ncclGroupEnd(), "ncclGroupEnd"); }
+
+}  // namespace tdp

@@ -1,0 +1,157 @@
+// Host-side launch API of the hand-written gfx950 kernels.
+//
+// These functions take raw device pointers plus the HIP stream to launch on; they never allocate,
+// copy or synchronise (workspaces are passed in), so bindings.cpp can wrap them for PyTorch
+// tensors and every launch stays hipGraph-capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdp {
+
+// ------------------------------------------------------------------------------------------------
+// fp32 GEMM on v_mfma_f32_32x32x2_f32 (exact f32, the dtype of the reference's nn.Linear).
+//   C[M,N] = op(A)[M,K] . op(B)[K,N]  (+ bias[N]) (+ beta*C) (ReLU)
+//   a_kcontig: A stored [M][K] (else [K][M]);  b_kcontig: B stored [N][K] (else [K][N]).
+//   mask (optional, A's layout, leading dim ldmask): A is replaced by 0 where mask <= 0 -- the
+//   ReLU backward of the layer that produced `mask`, fused into the operand load.
+//   rowsum (optional, [M]): rowsum = rowsum_beta*rowsum + sum_k A[m,k] (bias gradient).
+// ------------------------------------------------------------------------------------------------
+struct GemmF32Args {
+  const float* A = nullptr;
+  const float* B = nullptr;
+  float* C = nullptr;
+  const float* mask = nullptr;
+  const float* bias = nullptr;
+  float* rowsum = nullptr;
+  long lda = 0, ldb = 0, ldc = 0, ldmask = 0;
+  int M = 0, N = 0, K = 0;
+  bool a_kcontig = true, b_kcontig = true;
+  float beta = 0.f, rowsum_beta = 0.f;
+  bool relu = false;
+};
+
+struct GemmPlan {
+  int tile = 0;         // index into the tile table of gemm_f32.hip
+  int bm = 128, bn = 64;
+  int splits = 1;
+  int k_per_split = 0;
+  long ws_floats = 0;   // split-K workspace needed (0 when splits == 1)
+};
+
+GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
+void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
+
+// bf16-operand GEMM (AMP path): same contract, A/B bf16 (uint16 storage), C fp32 or bf16.
+struct GemmBF16Args {
+  const uint16_t* A = nullptr;
+  const uint16_t* B = nullptr;
+  void* C = nullptr;
+  bool c_bf16 = false;
+  const uint16_t* mask = nullptr;
+  const float* bias = nullptr;
+  float* rowsum = nullptr;
+  long lda = 0, ldb = 0, ldc = 0, ldmask = 0;
+  int M = 0, N = 0, K = 0;
+  bool a_kcontig = true, b_kcontig = true;
+  float beta = 0.f, rowsum_beta = 0.f;
+  bool relu = false;
+};
+GemmPlan gemm_bf16_plan(const GemmBF16Args& a, int num_cus);
+void gemm_bf16_run(const GemmBF16Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
+
+// split-K combine + epilogue: C = epi(sum_z ws[z]) ; C fp32 or bf16
+void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf16, long ldc,
+                   const float* bias, float beta, bool relu, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------------
+// Loss / metrics
+// ------------------------------------------------------------------------------------------------
+// Fused cross-entropy forward over logits[B,C] (fp32), int64 labels.
+//   out_loss[0] = mean (or sum) loss over non-ignored rows; also optional device accumulators:
+//   acc[0] += sum loss, acc[1] += #correct (argmax == label), acc[2] += #counted rows.
+//   lse_out[B] (optional) saves log-sum-exp per row for the backward.
+void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, long ld,
+                       int ignore_index, float label_smoothing, bool mean, float* out_loss,
+                       float* lse_out, float* acc, hipStream_t s);
+// dlogits = gout[0] * d(loss)/d(logits)
+void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* lse,
+                       const float* gout, int B, int C, long ld, int ignore_index,
+                       float label_smoothing, bool mean, float* dlogits, hipStream_t s);
+// argmax/correct counting only (eval): acc[1] += correct, acc[2] += rows
+void count_correct(const float* logits, const int64_t* labels, int B, int C, long ld, float* acc,
+                   hipStream_t s);
+
+// ------------------------------------------------------------------------------------------------
+// Optimizers: fused single-pass updates over a flat arena or a multi-tensor chunk table.
+// ------------------------------------------------------------------------------------------------
+struct SgdHyper {
+  float lr, momentum, dampening, weight_decay;
+  bool nesterov, maximize, first_step;
+  float grad_scale;  // grads are multiplied by this first (1/world for sum-reduced grads)
+};
+void sgd_flat(float* p, const float* g, float* buf, long n, const SgdHyper& h, hipStream_t s);
+
+struct AdamHyper {
+  float lr, beta1, beta2, eps, weight_decay;
+  bool amsgrad, maximize, decoupled;  // decoupled = AdamW
+  float bc1, bc2_sqrt;                // 1-beta1^t, sqrt(1-beta2^t)
+  float grad_scale;
+};
+void adam_flat(float* p, const float* g, float* m, float* v, float* vmax, long n,
+               const AdamHyper& h, hipStream_t s);
+
+// Multi-tensor form: `table` is a device array of TensorChunk records.
+struct TensorChunk {
+  float* p;
+  const float* g;
+  float* s0;  // momentum buf / exp_avg
+  float* s1;  // exp_avg_sq
+  float* s2;  // max_exp_avg_sq
+  long n;
+};
+void sgd_multi(const TensorChunk* table, int count, const SgdHyper& h, hipStream_t s);
+void adam_multi(const TensorChunk* table, int count, const AdamHyper& h, hipStream_t s);
+
+// elementwise helpers
+void scale_inplace(float* x, long n, float a, hipStream_t s);
+void fill_f32(float* x, long n, float v, hipStream_t s);
+void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
+void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);
+// sum of squares of x into out[0] (+= when accumulate), for grad-norm clipping
+void sumsq(const float* x, long n, float* out, bool accumulate, hipStream_t s);
+// x *= min(1, max_norm / (sqrt(total[0]) + eps))
+void clip_scale(float* x, long n, const float* total_sumsq, float max_norm, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------------
+// Batch norm (BatchNorm1d/2d and SyncBatchNorm). x is viewed as [N][C][HW] (HW = 1 for 1d).
+// Reductions that need more parallelism than C workgroups split the N*HW axis into `splits`
+// parts whose partials go to `ws` (bn_ws_floats tells how many floats it needs).
+// ------------------------------------------------------------------------------------------------
+int bn_splits(int N, int C, int HW, int num_cus);
+long bn_ws_floats(int C, int splits);  // >= max(3C, 2C) * splits
+// per-channel mean and biased variance (Welford per lane, Chan merges across lanes/blocks)
+void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, float* mean,
+                float* var, hipStream_t s);
+// merge R ranks' rows [mean(C) | var(C) | count(1)] (row stride 2C+1) -> mean, invstd, with the
+// total count written at invstd[C] (callers pass invstd = mean + C of one [2C+1] stats buffer);
+// running stats (optional) updated with momentum and the unbiased variance.
+void bn_merge(const float* gathered, int R, int C, float eps, float momentum, float* mean,
+              float* invstd, float* running_mean, float* running_var, hipStream_t s);
+// y = (x - mean) * invstd * w + b (optional ReLU). w/b may be null (affine=False).
+void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
+              const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s);
+// eval: y = (x - rmean) * rsqrt(rvar + eps) * w + b (optional ReLU)
+void bn_eval(const float* x, const float* rmean, const float* rvar, const float* w,
+             const float* b, int N, int C, int HW, float eps, bool relu, float* y, hipStream_t s);
+// sums[0:C] = sum dy, sums[C:2C] = sum dy*(x-mean), with dy masked by (y > 0) when y != null
+// (fused ReLU). dw/db (optional, accumulate when beta != 0): dw = sum_dy_xmu*invstd, db = sum_dy.
+void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const float* invstd,
+                   const float* y_relu, int N, int C, int HW, int splits, float* ws, float* sums,
+                   float* dw, float* db, float grad_beta, hipStream_t s);
+// dx = w*invstd*(dy - sum_dy/cnt - (x-mean)*invstd^2*sum_dy_xmu/cnt), sums possibly all-reduced.
+void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
+                  const float* w, const float* sums, const float* y_relu, const float* count,
+                  int N, int C, int HW, float* dx, hipStream_t s);
+
+}  // namespace tdp

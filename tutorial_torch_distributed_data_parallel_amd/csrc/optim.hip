@@ -1,0 +1,258 @@
+// Fused optimizer steps and small elementwise utilities.
+//
+// The reference steps torch.optim.Adam (REF/multi-GPU-training-torch.py:249), which on the GPU runs
+// _multi_tensor_adam: ~7 _foreach passes over p/g/m/v (TORCH/optim/adam.py:
+// 683-800). Here each optimizer is ONE pass: every element of p, g and the state is read once and
+// p and the state written once (SGD+momentum 20 B/elem, Adam 28 B/elem), f32x4-vectorised and
+// grid-strided. The "flat" form runs over the whole parameter arena of a DDP model (params and
+// grads are views into two equally laid out flat buffers, see parallel/arena.py); the "multi"
+// form walks a device-side chunk table for arbitrary parameter lists.
+//
+// `grad_scale` folds the 1/world_size gradient averaging into the update when the reducer used a
+// SUM all-reduce, so no separate div_ pass over the gradients is needed (K24).
+#include "common.h"
+#include "kernels.h"
+
+namespace tdp {
+namespace {
+
+__device__ __forceinline__ void sgd_elem(float& p, float g, float& b, const SgdHyper& h) {
+  g *= h.grad_scale;
+  if (h.maximize) g = -g;
+  if (h.weight_decay != 0.f) g = fmaf(h.weight_decay, p, g);
+  if (h.momentum != 0.f) {
+    b = h.first_step ? g : fmaf(b, h.momentum, (1.f - h.dampening) * g);
+    g = h.nesterov ? fmaf(h.momentum, b, g) : b;
+  }
+  p = fmaf(-h.lr, g, p);
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float* vmax,
+                                          const AdamHyper& h) {
+  g *= h.grad_scale;
+  if (h.maximize) g = -g;
+  if (h.weight_decay != 0.f) {
+    if (h.decoupled) p *= (1.f - h.lr * h.weight_decay);
+    else g = fmaf(h.weight_decay, p, g);
+  }
+  m = fmaf(1.f - h.beta1, g - m, m);  // lerp(m, g, 1-beta1)
+  v = fmaf(v, h.beta2, (1.f - h.beta2) * g * g);
+  float vv = v;
+  if (h.amsgrad) {
+    vv = fmaxf(*vmax, v);
+    *vmax = vv;
+  }
+  const float denom = sqrtf(vv) / h.bc2_sqrt + h.eps;
+  p = fmaf(-(h.lr / h.bc1), m / denom, p);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ buf, long n,
+                                                       SgdHyper h) {
+  const long n4 = VEC ? n / 4 : 0;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool mom = h.momentum != 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (mom && !h.first_step) bv = reinterpret_cast<f32x4*>(buf)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], be = bv[e];
+      sgd_elem(pe, gv[e], be, h);
+      pv[e] = pe;
+      bv[e] = be;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    if (mom) reinterpret_cast<f32x4*>(buf)[i] = bv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pe = p[i], be = (mom && !h.first_step) ? buf[i] : 0.f;
+    sgd_elem(pe, g[i], be, h);
+    p[i] = pe;
+    if (mom) buf[i] = be;
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p,
+                                                        const float* __restrict__ g,
+                                                        float* __restrict__ m,
+                                                        float* __restrict__ v,
+                                                        float* __restrict__ vmax, long n,
+                                                        AdamHyper h) {
+  const long n4 = VEC ? n / 4 : 0;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+    f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+    if (h.amsgrad) xv = reinterpret_cast<f32x4*>(vmax)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], me = mv[e], ve = vv[e], xe = xv[e];
+      adam_elem(pe, gv[e], me, ve, &xe, h);
+      pv[e] = pe; mv[e] = me; vv[e] = ve; xv[e] = xe;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+    if (h.amsgrad) reinterpret_cast<f32x4*>(vmax)[i] = xv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pe = p[i], me = m[i], ve = v[i];
+    float xe = h.amsgrad ? vmax[i] : 0.f;
+    adam_elem(pe, g[i], me, ve, &xe, h);
+    p[i] = pe; m[i] = me; v[i] = ve;
+    if (h.amsgrad) vmax[i] = xe;
+  }
+}
+
+// One workgroup per chunk-table entry (chunks are <= 64K elements, built on the host).
+__global__ __launch_bounds__(256) void sgd_multi_kernel(const TensorChunk* __restrict__ table,
+                                                        SgdHyper h) {
+  const TensorChunk c = table[blockIdx.x];
+  const bool mom = h.momentum != 0.f;
+  for (long i = threadIdx.x; i < c.n; i += blockDim.x) {
+    float pe = c.p[i], be = (mom && !h.first_step) ? c.s0[i] : 0.f;
+    sgd_elem(pe, c.g[i], be, h);
+    c.p[i] = pe;
+    if (mom) c.s0[i] = be;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(const TensorChunk* __restrict__ table,
+                                                         AdamHyper h) {
+  const TensorChunk c = table[blockIdx.x];
+  for (long i = threadIdx.x; i < c.n; i += blockDim.x) {
+    float pe = c.p[i], me = c.s0[i], ve = c.s1[i];
+    float xe = h.amsgrad ? c.s2[i] : 0.f;
+    adam_elem(pe, c.g[i], me, ve, &xe, h);
+    c.p[i] = pe; c.s0[i] = me; c.s1[i] = ve;
+    if (h.amsgrad) c.s2[i] = xe;
+  }
+}
+
+__global__ void scale_kernel(float* x, long n, float a) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    x[i] *= a;
+}
+
+__global__ void fill_kernel(float* x, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+
+__global__ void f2bf_kernel(const float* __restrict__ x, unsigned short* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = f32_to_bf16(x[i]);
+}
+
+__global__ void bf2f_kernel(const unsigned short* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = bf16_to_f32(x[i]);
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n,
+                                                    float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    s = fmaf(x[i], x[i], s);
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+__global__ void clip_kernel(float* x, long n, const float* total, float max_norm) {
+  const float norm = sqrtf(total[0]);
+  const float coef = max_norm / (norm + 1e-6f);
+  if (coef >= 1.f) return;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    x[i] *= coef;
+}
+
+inline int grid_for(long work, int cap = 2048) {
+  long g = (work + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+void sgd_flat(float* p, const float* g, float* buf, long n, const SgdHyper& h, hipStream_t s) {
+  if (n <= 0) return;
+  // grid capped at 2048 workgroups (8 per CU) and grid-strided (Guideline 11)
+  if (al16(p) && al16(g) && (buf == nullptr || al16(buf)))
+    hipLaunchKernelGGL(sgd_flat_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf,
+                       n, h);
+  else
+    hipLaunchKernelGGL(sgd_flat_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, p, g, buf, n,
+                       h);
+}
+
+void adam_flat(float* p, const float* g, float* m, float* v, float* vmax, long n,
+               const AdamHyper& h, hipStream_t s) {
+  if (n <= 0) return;
+  if (al16(p) && al16(g) && al16(m) && al16(v) && (vmax == nullptr || al16(vmax)))
+    hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, m,
+                       v, vmax, n, h);
+  else
+    hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v,
+                       vmax, n, h);
+}
+
+void sgd_multi(const TensorChunk* table, int count, const SgdHyper& h, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(sgd_multi_kernel, dim3(count), dim3(256), 0, s, table, h);
+}
+
+void adam_multi(const TensorChunk* table, int count, const AdamHyper& h, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3(count), dim3(256), 0, s, table, h);
+}
+
+void scale_inplace(float* x, long n, float a, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, a);
+}
+
+void fill_f32(float* x, long n, float v, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, v);
+}
+
+void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(f2bf_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, (unsigned short*)y, n);
+}
+
+void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(bf2f_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const unsigned short*)x,
+                       y, n);
+}
+
+void sumsq(const float* x, long n, float* out, bool accumulate, hipStream_t s) {
+  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float), s);
+  if (n > 0) hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 1024)), dim3(256), 0, s, x, n, out);
+}
+
+void clip_scale(float* x, long n, const float* total_sumsq, float max_norm, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(clip_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, total_sumsq,
+                       max_norm);
+}
+
+}  // namespace tdp

@@ -1,0 +1,233 @@
+#include "reducer.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace tdp {
+
+// ------------------------------------------------------------------------------------------------
+// RcclBackend
+// ------------------------------------------------------------------------------------------------
+RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_t numel,
+                         int elem_size, int num_buckets, Compression compression, bool timing,
+                         bool skip_single_rank)
+    : comm_(std::move(comm)),
+      arena_(static_cast<char*>(arena)),
+      numel_(numel),
+      elem_size_(elem_size),
+      compression_(compression),
+      timing_(timing),
+      skip_single_rank_(skip_single_rank) {
+  if (compression_ == Compression::BF16 && elem_size_ != 4)
+    throw std::runtime_error("bf16 gradient compression needs an fp32 arena");
+  ready_.resize(num_buckets);
+  for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+  check_hip(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
+  if (timing_) {
+    check_hip(hipEventCreate(&t0_), "event");
+    check_hip(hipEventCreate(&t1_), "event");
+  }
+  if (compression_ == Compression::BF16)
+    check_hip(hipMalloc(&wire_, sizeof(uint16_t) * (size_t)numel_), "hipMalloc(wire)");
+}
+
+RcclBackend::~RcclBackend() {
+  for (auto& e : ready_) (void)hipEventDestroy(e);
+  if (done_) (void)hipEventDestroy(done_);
+  if (t0_) (void)hipEventDestroy(t0_);
+  if (t1_) (void)hipEventDestroy(t1_);
+  if (wire_) (void)hipFree(wire_);
+}
+
+static ncclDataType_t nccl_dtype(int elem_size) {
+  switch (elem_size) {
+    case 4: return ncclFloat32;
+    case 2: return ncclBfloat16;
+    case 8: return ncclFloat64;
+    default: throw std::runtime_error("unsupported arena element size");
+  }
+}
+
+void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
+  hipStream_t cs = comm_->comm_stream();
+  check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
+  check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+  if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
+  launched_any_ = true;
+  const int64_t n = end - begin;
+  if (n > 0 && !(skip_single_rank_ && comm_->world() == 1)) {
+    char* ptr = arena_ + begin * elem_size_;
+    if (compression_ == Compression::BF16) {
+      uint16_t* w = wire_ + begin;
+      f32_to_bf16_copy(reinterpret_cast<float*>(ptr), w, n, cs);
+      comm_->all_reduce(w, w, (size_t)n, ncclBfloat16, ncclAvg, cs);
+      bf16_to_f32_copy(w, reinterpret_cast<float*>(ptr), n, cs);
+    } else {
+      comm_->all_reduce(ptr, ptr, (size_t)n, nccl_dtype(elem_size_), ncclAvg, cs);
+    }
+  }
+  if (post_bucket) post_bucket(bucket, begin, end, cs);
+}
+
+void RcclBackend::wait_all(hipStream_t compute) {
+  if (!launched_any_) return;
+  hipStream_t cs = comm_->comm_stream();
+  if (timing_) {
+    check_hip(hipEventRecord(t1_, cs), "hipEventRecord");
+    timed_pending_ = true;
+  }
+  check_hip(hipEventRecord(done_, cs), "hipEventRecord");
+  check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
+  launched_any_ = false;
+}
+
+void RcclBackend::zero(int64_t begin, int64_t end, hipStream_t compute) {
+  if (end > begin)
+    check_hip(hipMemsetAsync(arena_ + begin * elem_size_, 0, (size_t)(end - begin) * elem_size_,
+                             compute),
+              "hipMemsetAsync");
+}
+
+double RcclBackend::last_comm_ms() {
+  if (!timing_ || !timed_pending_) return -1.0;
+  if (hipEventQuery(t1_) != hipSuccess) return -1.0;  // not finished yet: never block here
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, t0_, t1_) != hipSuccess) return -1.0;
+  return ms;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reducer
+// ------------------------------------------------------------------------------------------------
+std::vector<int64_t> Reducer::compute_bucket_bounds(const std::vector<int64_t>& offsets,
+                                                    const std::vector<int64_t>& numels,
+                                                    int64_t arena_numel, int elem_size,
+                                                    int64_t first_cap_bytes, int64_t cap_bytes,
+                                                    int64_t split_bytes) {
+  std::vector<int64_t> b{0};
+  int64_t cur_bytes = 0;
+  const int64_t split = split_bytes > 0 ? std::max<int64_t>(split_bytes / elem_size, 1) : 0;
+  for (size_t i = 0; i < offsets.size(); ++i) {
+    const int64_t cap = (b.size() == 1 ? first_cap_bytes : cap_bytes);
+    const int64_t bytes = numels[i] * elem_size;
+    if (cur_bytes > 0 && cur_bytes + bytes > cap) {
+      b.push_back(offsets[i]);
+      cur_bytes = 0;
+    }
+    if (split > 0 && numels[i] > split) {
+      // a large parameter gets its own buckets, cut every `split` elements
+      if (b.back() != offsets[i]) b.push_back(offsets[i]);
+      for (int64_t s = split; s < numels[i]; s += split) b.push_back(offsets[i] + s);
+      const int64_t tail = offsets[i] + numels[i];
+      if (i + 1 < offsets.size()) b.push_back(tail);
+      cur_bytes = 0;
+      continue;
+    }
+    cur_bytes += bytes;
+  }
+  if (b.back() != arena_numel) b.push_back(arena_numel);
+  // drop empty ranges (can appear with zero-sized params or padding)
+  std::vector<int64_t> out{b[0]};
+  for (size_t i = 1; i < b.size(); ++i)
+    if (b[i] > out.back()) out.push_back(b[i]);
+  if (out.size() == 1) out.push_back(std::max<int64_t>(arena_numel, 0));
+  return out;
+}
+
+Reducer::Reducer(std::vector<int64_t> offsets, std::vector<int64_t> numels,
+                 std::vector<int64_t> bucket_bounds, std::shared_ptr<ReducerBackend> backend)
+    : offsets_(std::move(offsets)),
+      numels_(std::move(numels)),
+      bounds_(std::move(bucket_bounds)),
+      backend_(std::move(backend)) {
+  if (offsets_.size() != numels_.size()) throw std::runtime_error("offsets/numels mismatch");
+  if (bounds_.size() < 2) throw std::runtime_error("need at least one bucket");
+  const int nb = num_buckets();
+  param_buckets_.resize(offsets_.size());
+  bucket_nparams_.assign(nb, 0);
+  for (size_t p = 0; p < offsets_.size(); ++p) {
+    const int64_t a = offsets_[p], e = offsets_[p] + numels_[p];
+    if (numels_[p] == 0) continue;
+    // first bucket whose end is > a
+    int b = (int)(std::upper_bound(bounds_.begin(), bounds_.end(), a) - bounds_.begin()) - 1;
+    for (; b < nb && bounds_[b] < e; ++b) {
+      param_buckets_[p].push_back(b);
+      bucket_nparams_[b]++;
+    }
+  }
+  pending_ = bucket_nparams_;
+  param_ready_.assign(offsets_.size(), 0);
+  bucket_ready_.assign(nb, 0);
+}
+
+void Reducer::prepare_for_backward() {
+  pending_ = bucket_nparams_;
+  std::fill(param_ready_.begin(), param_ready_.end(), 0);
+  for (int b = 0; b < num_buckets(); ++b) bucket_ready_[b] = (bucket_nparams_[b] == 0);
+  next_bucket_ = 0;
+  expecting_ = true;
+}
+
+void Reducer::mark_ready(int p, hipStream_t compute) {
+  if (!expecting_) return;
+  if (p < 0 || p >= (int)offsets_.size()) throw std::runtime_error("bad parameter index");
+  if (param_ready_[p])
+    throw std::runtime_error(
+        "Expected to mark a variable ready only once (parameter " + std::to_string(p) +
+        " produced a gradient twice in one backward; reentrant backward or a parameter used in "
+        "two autograd graphs is not supported)");
+  param_ready_[p] = 1;
+  if (iteration_ == 0) first_ready_order_.push_back(p);
+  for (int b : param_buckets_[p])
+    if (--pending_[b] == 0) bucket_ready_[b] = 1;
+  launch_ready(compute);
+}
+
+void Reducer::launch_ready(hipStream_t compute) {
+  const int nb = num_buckets();
+  while (next_bucket_ < nb && bucket_ready_[next_bucket_]) {
+    backend_->launch(next_bucket_, bounds_[next_bucket_], bounds_[next_bucket_ + 1], compute);
+    ++next_bucket_;
+  }
+}
+
+std::vector<int> Reducer::unready_params() const {
+  std::vector<int> out;
+  for (size_t p = 0; p < param_ready_.size(); ++p)
+    if (!param_ready_[p] && numels_[p] > 0) out.push_back((int)p);
+  return out;
+}
+
+void Reducer::finalize(hipStream_t compute, bool allow_unused) {
+  if (!expecting_) return;
+  const auto unready = unready_params();
+  if (!unready.empty()) {
+    if (!allow_unused) {
+      std::string idx;
+      for (size_t i = 0; i < unready.size() && i < 16; ++i)
+        idx += (i ? ", " : "") + std::to_string(unready[i]);
+      throw std::runtime_error(
+          "Expected to have finished reduction in the prior iteration before starting a new "
+          "one: parameters [" + idx + "] received no gradient. Pass find_unused_parameters=True "
+          "if some parameters do not take part in the loss.");
+    }
+    for (int p : unready) {
+      // an unused parameter contributes a zero gradient (the slot may hold last step's values)
+      backend_->zero(offsets_[p], offsets_[p] + numels_[p], compute);
+      param_ready_[p] = 1;
+      if (iteration_ == 0) first_ready_order_.push_back(p);
+      for (int b : param_buckets_[p])
+        if (--pending_[b] == 0) bucket_ready_[b] = 1;
+    }
+    launch_ready(compute);
+  }
+  if (next_bucket_ != num_buckets())
+    throw std::runtime_error("reducer: not every bucket became ready");
+  backend_->wait_all(compute);
+  expecting_ = false;
+  ++iteration_;
+}
+
+}  // namespace tdp

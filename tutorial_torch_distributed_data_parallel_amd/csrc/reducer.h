@@ -1,0 +1,113 @@
+// Gradient reducer: DDP's C++ Reducer re-designed around a flat gradient arena.
+//
+// torch DDP (TORCH/nn/parallel/distributed.py:1163-1275) copies every
+// gradient into a bucket, divides by world size, all-reduces, and copies back (K24: 2 x 217 MiB of
+// copies per AlexNet step), starts from one all-parameter bucket and rebuilds buckets after
+// iteration 0. Here:
+//   * every parameter's .grad IS a view of one flat arena laid out in backward order, so a bucket
+//     is just a contiguous [begin, end) element range: no copy-in, no copy-out;
+//   * a bucket boundary may fall inside a large parameter (fc1's 144 MiB weight can be split);
+//   * averaging is ncclAvg inside the all-reduce (no div_ pass);
+//   * buckets launch strictly in index order as soon as every parameter overlapping them is
+//     ready (identical collective order on every rank), on the communicator's high-priority
+//     stream after an event recorded on the compute stream; finalize() makes the compute stream
+//     wait on the last bucket, so the optimizer step is ordered after the reduction without a
+//     host sync.
+// The backend is abstract so that the same bucketing/readiness logic runs over RCCL on MI355X
+// and over torch.distributed (gloo) in the CPU tests.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "comm.h"
+
+namespace tdp {
+
+struct ReducerBackend {
+  virtual ~ReducerBackend() = default;
+  // average arena elements [begin, end) across ranks, ordered after work already on `compute`
+  virtual void launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) = 0;
+  // make `compute` wait for every bucket launched so far in this iteration
+  virtual void wait_all(hipStream_t compute) = 0;
+  // zero arena elements [begin, end) (gradients of parameters unused in this iteration)
+  virtual void zero(int64_t begin, int64_t end, hipStream_t compute) = 0;
+  // device-side comm time of the last finished iteration in ms (-1 when unknown)
+  virtual double last_comm_ms() { return -1.0; }
+};
+
+// Gradient compression for the wire: NONE sends the arena dtype (fp32), BF16 casts each bucket to
+// bf16 on the comm stream, all-reduces that and casts back (torch's bf16_compress_hook).
+enum class Compression : int { NONE = 0, BF16 = 1 };
+
+class RcclBackend : public ReducerBackend {
+ public:
+  RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_t numel, int elem_size,
+              int num_buckets, Compression compression, bool timing, bool skip_single_rank);
+  ~RcclBackend() override;
+  void launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) override;
+  void wait_all(hipStream_t compute) override;
+  void zero(int64_t begin, int64_t end, hipStream_t compute) override;
+  double last_comm_ms() override;
+  // called after a bucket's all-reduce is enqueued, with the comm stream (fused optimizer hook)
+  std::function<void(int, int64_t, int64_t, hipStream_t)> post_bucket;
+
+ private:
+  std::shared_ptr<Communicator> comm_;
+  char* arena_;
+  int64_t numel_;
+  int elem_size_;
+  Compression compression_;
+  bool timing_, skip_single_rank_;
+  std::vector<hipEvent_t> ready_;
+  hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
+  bool launched_any_ = false, timed_pending_ = false;
+  uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
+};
+
+class Reducer {
+ public:
+  Reducer(std::vector<int64_t> offsets, std::vector<int64_t> numels,
+          std::vector<int64_t> bucket_bounds, std::shared_ptr<ReducerBackend> backend);
+
+  // Boundaries (element offsets, first 0, last = arena numel) for parameters laid out at
+  // `offsets` (ascending). Small parameters are grouped up to cap_bytes (first_cap_bytes for the
+  // first bucket); a parameter larger than split_bytes (> 0) is cut into split_bytes pieces.
+  static std::vector<int64_t> compute_bucket_bounds(const std::vector<int64_t>& offsets,
+                                                    const std::vector<int64_t>& numels,
+                                                    int64_t arena_numel, int elem_size,
+                                                    int64_t first_cap_bytes, int64_t cap_bytes,
+                                                    int64_t split_bytes);
+
+  void prepare_for_backward();
+  void mark_ready(int param, hipStream_t compute);
+  // launch whatever is left, zero never-ready params when allowed, make `compute` wait
+  void finalize(hipStream_t compute, bool allow_unused);
+
+  bool expecting() const { return expecting_; }
+  int64_t iteration() const { return iteration_; }
+  std::vector<int64_t> bucket_bounds() const { return bounds_; }
+  std::vector<int> ready_order() const { return first_ready_order_; }
+  std::vector<int> unready_params() const;
+  int num_buckets() const { return (int)bounds_.size() - 1; }
+  double last_comm_ms() { return backend_->last_comm_ms(); }
+
+ private:
+  void launch_ready(hipStream_t compute);
+
+  std::vector<int64_t> offsets_, numels_, bounds_;
+  std::vector<std::vector<int>> param_buckets_;
+  std::vector<int> bucket_nparams_, pending_;
+  std::vector<char> param_ready_, bucket_ready_;
+  std::vector<int> first_ready_order_;
+  std::shared_ptr<ReducerBackend> backend_;
+  int next_bucket_ = 0;
+  bool expecting_ = false;
+  int64_t iteration_ = 0;
+};
+
+}  // namespace tdp

@@ -1,0 +1,95 @@
+"""Synthetic datasets resident in device memory, plus a device-side loader.
+
+The reference trains on CIFAR-10 resized to 224x224 through torchvision, downloaded concurrently
+by every rank (REF/data_and_toy_model.py:8-38; SURVEY.md §5.2 download race) and decoded by 2
+worker processes per rank (REF/multi-GPU-training-torch.py:85-99). There is no network here and
+the benchmark is defined on synthetic data, so a dataset is a tensor already in HBM (288 GB per
+MI355X) and a batch is a gather by the sampler's indices: no host decode, no pinned H2D copy
+per step. Labels are a fixed random linear function of the input so a
+model can actually learn (loss curves are meaningful in tests).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class SyntheticDataset(torch.utils.data.Dataset):
+    """`n` samples of `shape` (float32) with labels in [0, num_classes), built from `seed`."""
+
+    def __init__(self, n: int, shape, num_classes: int = 10, seed: int = 0, device="cpu",
+                 learnable: bool = True, dtype=torch.float32):
+        self.n = int(n)
+        self.shape = tuple(shape)
+        self.num_classes = num_classes
+        device = torch.device(device)
+        g = torch.Generator(device=device if device.type == "cuda" else "cpu")
+        g.manual_seed(seed)
+        self.x = torch.randn((self.n,) + self.shape, generator=g, device=device, dtype=dtype)
+        if learnable:
+            feat = self.x.reshape(self.n, -1)
+            proj = torch.randn(feat.shape[1], num_classes, generator=g, device=device,
+                               dtype=dtype)
+            self.y = (feat @ proj).argmax(dim=1)
+        else:
+            self.y = torch.randint(0, num_classes, (self.n,), generator=g, device=device)
+        self.device = device
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return self.x[i], self.y[i]
+
+
+class DeviceLoader:
+    """Iterates (inputs, labels) batches of a tensor dataset by sampler order, on device.
+
+    ``sampler`` is any iterable of indices (e.g. DistributedSampler) and is re-iterated every
+    epoch, so ``sampler.set_epoch(e)`` takes effect exactly as with torch's DataLoader. The index
+    list of an epoch goes to the device once; each batch is one ``index_select`` per tensor.
+    """
+
+    def __init__(self, dataset, batch_size: int, sampler=None, drop_last: bool = False,
+                 device=None, batch_sampler=None):
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.sampler = sampler
+        self.batch_sampler = batch_sampler
+        self.drop_last = drop_last
+        self.device = torch.device(device) if device is not None else dataset.device
+
+    def _index_batches(self):
+        if self.batch_sampler is not None:
+            for b in self.batch_sampler:
+                yield torch.as_tensor(b, dtype=torch.long)
+            return
+        order = list(self.sampler) if self.sampler is not None else list(range(len(self.dataset)))
+        idx = torch.as_tensor(order, dtype=torch.long)
+        n = len(idx)
+        stop = n - (n % self.batch_size) if self.drop_last else n
+        for s in range(0, stop, self.batch_size):
+            yield idx[s: s + self.batch_size]
+
+    def __iter__(self):
+        x, y = self.dataset.x, self.dataset.y
+        for b in self._index_batches():
+            b = b.to(x.device, non_blocking=True)
+            xb = x.index_select(0, b)
+            yb = y.index_select(0, b)
+            if xb.device != self.device:
+                xb = xb.to(self.device, non_blocking=True)
+                yb = yb.to(self.device, non_blocking=True)
+            yield xb, yb
+
+    def __len__(self):
+        if self.batch_sampler is not None:
+            return len(self.batch_sampler)
+        n = len(self.sampler) if self.sampler is not None else len(self.dataset)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+
+def cifar_like(n_train: int = 50000, n_test: int = 10000, shape=(3, 224, 224), device="cpu",
+               seed: int = 0):
+    """Train/test sets with the reference's tensor shapes (CIFAR-10 resized to 224)."""
+    return (SyntheticDataset(n_train, shape, 10, seed, device),
+            SyntheticDataset(n_test, shape, 10, seed + 1, device))

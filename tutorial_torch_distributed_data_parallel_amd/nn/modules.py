@@ -1,0 +1,118 @@
+"""nn.Module front-ends over the native ops (drop-in for the torch modules the reference uses).
+
+Each subclasses its torch counterpart, so parameter names, initialisation, ``state_dict`` keys and
+``repr`` are identical to torch's -- checkpoints stay interchangeable with stock PyTorch -- and
+only ``forward`` is replaced. ReLU can be fused into the producing layer (``relu=True``), which is
+how the models in ``models/`` express torchvision's ``Linear -> ReLU`` pairs.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..parallel import runtime as rt
+
+
+class Linear(nn.Linear):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True,
+                 relu: bool = False, device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        self.relu = relu
+
+    def forward(self, x):
+        return ops.linear(x, self.weight, self.bias, relu=self.relu)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+class _NativeBN(nn.modules.batchnorm._BatchNorm):
+    """Shared forward for BatchNorm{1,2}d / SyncBatchNorm."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True,
+                 track_running_stats=True, relu: bool = False, device=None, dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats,
+                         device=device, dtype=dtype)
+        self.relu = relu
+        self._nbt = 0  # host mirror of num_batches_tracked: no device->host sync per step
+
+    def _group(self):
+        return None
+
+    def forward(self, x):
+        self._check_input_dim(x)
+        use_batch = self.training or not self.track_running_stats
+        factor = 0.0
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            self._nbt += 1
+            factor = (1.0 / self._nbt) if self.momentum is None else self.momentum
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        return ops.batch_norm(x, rm, rv, self.weight, self.bias, training=use_batch,
+                              momentum=factor, eps=self.eps, relu=self.relu,
+                              group=self._group() if use_batch else None)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+class BatchNorm1d(_NativeBN):
+    def _check_input_dim(self, x):
+        if x.dim() not in (2, 3):
+            raise ValueError(f"expected 2D or 3D input (got {x.dim()}D input)")
+
+
+class BatchNorm2d(_NativeBN):
+    def _check_input_dim(self, x):
+        if x.dim() != 4:
+            raise ValueError(f"expected 4D input (got {x.dim()}D input)")
+
+
+class SyncBatchNorm(_NativeBN):
+    """Batch statistics over the whole job (README pitfall, REF/README.md:79-81).
+
+    Synchronises only in training mode with world_size > 1 (torch semantics,
+    TORCH/nn/modules/batchnorm.py:744-839); otherwise it is a plain batch norm.
+    """
+
+    def _check_input_dim(self, x):
+        if x.dim() < 2:
+            raise ValueError(f"expected at least 2D input (got {x.dim()}D input)")
+
+    def _group(self):
+        if self.training and rt.is_initialized() and rt.get_world_size() > 1:
+            return rt.SyncGroup()
+        return None
+
+    @classmethod
+    def convert_sync_batchnorm(cls, module: nn.Module, process_group=None) -> nn.Module:
+        """Recursively replace every BatchNorm*D (torch's or ours) with SyncBatchNorm."""
+        out = module
+        if isinstance(module, nn.modules.batchnorm._BatchNorm) and not isinstance(module, cls):
+            out = cls(module.num_features, module.eps, module.momentum, module.affine,
+                      module.track_running_stats, relu=getattr(module, "relu", False))
+            if module.affine:
+                with torch.no_grad():
+                    out.weight = module.weight
+                    out.bias = module.bias
+            out.running_mean = module.running_mean
+            out.running_var = module.running_var
+            out.num_batches_tracked = module.num_batches_tracked
+            out._nbt = getattr(module, "_nbt", 0)
+            out.training = module.training
+        for name, child in module.named_children():
+            out.add_module(name, cls.convert_sync_batchnorm(child, process_group))
+        return out
+
+
+class CrossEntropyLoss(nn.CrossEntropyLoss):
+    def forward(self, input, target):
+        if self.weight is not None:
+            raise NotImplementedError("class weights are not supported by the native loss")
+        return ops.cross_entropy(input, target, ignore_index=self.ignore_index,
+                                 label_smoothing=self.label_smoothing, reduction=self.reduction)
+
+
+convert_sync_batchnorm = SyncBatchNorm.convert_sync_batchnorm

@@ -1,0 +1,71 @@
+"""Linear (+ fused ReLU) on the native fp32 MFMA GEMM.
+
+Forward, input-gradient and weight-gradient are each ONE kernel (plus a split-K combine when the
+tile grid alone cannot fill 256 CUs):
+  * forward  ``y = relu(x W^T + b)``: bias and ReLU in the GEMM epilogue;
+  * backward: the ReLU mask ``y > 0`` is applied while the kernels stage ``dy`` (K18), the bias
+    gradient is the row sum of that staged tile inside the weight-gradient kernel (K17), and the
+    weight gradient lands directly in the DDP gradient arena (K23, see ``_grad.py``).
+On CPU the same math runs through ``torch.nn.functional`` (the reference implementation used by
+the gloo/CPU tests). Reference behaviour: torchvision AlexNet's classifier Linear/ReLU layers
+(REF/data_and_toy_model.py:41-45).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native
+from ._grad import grad_dest, needs
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2, weight, bias, relu: bool):
+        C = native()
+        y = torch.empty((x2.shape[0], weight.shape[0]), device=x2.device, dtype=torch.float32)
+        C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
+        ctx.relu = relu
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, weight, y = ctx.saved_tensors
+        w_param, b_param = ctx.params
+        if dy.dim() != 2 or dy.stride(1) != 1:
+            dy = dy.contiguous()
+        mask = y if ctx.relu else None
+        dx = dw = db = None
+        if needs(ctx, 1):
+            dw = grad_dest(w_param)
+            db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
+            # dW[out, in] = dy^T . x : A = dy stored [K=batch][M=out], B = x stored [K][N=in]
+            C.gemm_f32(dy, x2, dw, False, False, mask=mask, rowsum=db)
+        elif b_param is not None and needs(ctx, 2):
+            db = grad_dest(b_param)
+            m = dy if mask is None else dy * (mask > 0)
+            torch.sum(m, dim=0, out=db)
+        if needs(ctx, 0):
+            dx = torch.empty_like(x2)
+            # dx[B, in] = dy . W : A = dy [M=B][K=out], B = W stored [K=out][N=in]
+            C.gemm_f32(dy, weight, dx, True, False, mask=mask)
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
+           relu: bool = False) -> torch.Tensor:
+    """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
+    if not x.is_cuda:
+        y = F.linear(x, weight, bias)
+        return F.relu(y) if relu else y
+    if x.dtype != torch.float32:
+        raise TypeError(f"native linear expects float32 activations, got {x.dtype}")
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    y = _LinearFn.apply(x2, weight, bias, relu)
+    return y.reshape(*lead, weight.shape[0])

@@ -1,0 +1,65 @@
+"""Cross-entropy on the fused native kernels.
+
+``acc`` is an optional device accumulator ``[loss_sum, correct, count]`` updated inside the
+forward kernel, which is how the training/eval loops keep the reference's per-epoch metric sums
+(REF/multi-GPU-training-torch.py:131,147-151) without a host sync per step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native
+
+
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index: int, smoothing: float, mean: bool, acc):
+        C = native()
+        loss, lse = C.ce_fwd(logits, target, ignore_index, smoothing, mean, acc)
+        ctx.save_for_backward(logits, target, lse)
+        ctx.cfg = (ignore_index, smoothing, mean)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, target, lse = ctx.saved_tensors
+        ignore_index, smoothing, mean = ctx.cfg
+        d = native().ce_bwd(logits, target, lse, gout.reshape(1).float(), ignore_index, smoothing,
+                            mean)
+        return d, None, None, None, None, None
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                  label_smoothing: float = 0.0, reduction: str = "mean",
+                  acc: torch.Tensor | None = None) -> torch.Tensor:
+    if not logits.is_cuda:
+        loss = F.cross_entropy(logits, target, ignore_index=ignore_index,
+                               label_smoothing=label_smoothing, reduction=reduction)
+        if acc is not None:
+            with torch.no_grad():
+                valid = target != ignore_index
+                per = F.cross_entropy(logits.detach(), target, ignore_index=ignore_index,
+                                      label_smoothing=label_smoothing, reduction="sum")
+                acc[0] += per
+                acc[1] += ((logits.argmax(1) == target) & valid).sum()
+                acc[2] += valid.sum()
+        return loss
+    if reduction not in ("mean", "sum"):
+        raise NotImplementedError("native cross_entropy supports reduction='mean'|'sum'")
+    if logits.dim() != 2:
+        raise ValueError("native cross_entropy expects [batch, classes] logits")
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    return _CrossEntropyFn.apply(logits, target.contiguous().long(), int(ignore_index),
+                                 float(label_smoothing), reduction == "mean", acc)
+
+
+@torch.no_grad()
+def count_correct(logits: torch.Tensor, target: torch.Tensor, acc: torch.Tensor) -> None:
+    """acc[1] += #(argmax == target), acc[2] += #rows (fused argmax+compare+count)."""
+    if not logits.is_cuda:
+        acc[1] += (logits.argmax(1) == target).sum()
+        acc[2] += target.numel()
+        return
+    native().count_correct(logits.contiguous(), target.contiguous().long(), acc)

@@ -1,0 +1,143 @@
+"""Batch norm / SyncBatchNorm autograd function over the native kernels (``csrc/norm.hip``).
+
+Protocol (same as torch's SyncBatchNorm, TORCH/nn/modules/_functions.py:7-209):
+  forward : local [mean | var | count]  --all_gather-->  count-weighted merge (+ running stats)
+            --> normalise (optionally with a fused ReLU)
+  backward: local [sum_dy | sum_dy_xmu] (+ local dW, dB straight into the grad arena)
+            --all_reduce(sum)--> dx
+With ``group=None`` the same kernels implement plain BatchNorm (one "rank").
+On CPU the identical protocol runs on torch ops (``_TorchKernels``), which is what the gloo
+multi-process tests exercise.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native
+from ._grad import grad_dest, needs
+
+
+class _TorchKernels:
+    """CPU reference of the five native batch-norm kernels (same tensor contracts)."""
+
+    @staticmethod
+    def _view(x):
+        N, C = x.shape[0], x.shape[1]
+        return x.reshape(N, C, -1)
+
+    def bn_moments(self, x):
+        v = self._view(x)
+        C = v.shape[1]
+        mean = v.mean(dim=(0, 2))
+        var = v.var(dim=(0, 2), unbiased=False)
+        cnt = torch.tensor([float(v.shape[0] * v.shape[2])], dtype=x.dtype)
+        return [torch.cat([mean, var, cnt])[: 2 * C + 1]]
+
+    def bn_merge(self, gathered, C, eps, momentum, rmean, rvar):
+        g = gathered.reshape(-1, 2 * C + 1)
+        g = g[g[:, 2 * C] > 0]
+        n = g[:, 2 * C: 2 * C + 1]
+        total = n.sum()
+        mean = (g[:, :C] * n).sum(0) / total
+        m2 = (g[:, C: 2 * C] * n + n * (g[:, :C] - mean) ** 2).sum(0)
+        var = m2 / total
+        if rmean is not None:
+            unbiased = m2 / (total - 1) if total > 1 else var
+            rmean.mul_(1 - momentum).add_(mean, alpha=momentum)
+            rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+        return torch.cat([mean, torch.rsqrt(var + eps), total.reshape(1)])
+
+    def bn_elemt(self, x, stats, w, b, relu):
+        C = x.shape[1]
+        shape = (1, C) + (1,) * (x.dim() - 2)
+        y = (x - stats[:C].view(shape)) * stats[C: 2 * C].view(shape)
+        if w is not None:
+            y = y * w.view(shape)
+        if b is not None:
+            y = y + b.view(shape)
+        return F.relu(y) if relu else y
+
+    def bn_bwd_reduce(self, dy, x, stats, y, dw, db, beta):
+        C = x.shape[1]
+        if y is not None:
+            dy = dy * (y > 0)
+        dv, xv = self._view(dy), self._view(x)
+        s_dy = dv.sum(dim=(0, 2))
+        s_dyx = (dv * (xv - stats[:C].view(1, C, 1))).sum(dim=(0, 2))
+        if dw is not None:
+            dw.copy_(s_dyx * stats[C: 2 * C])
+        if db is not None:
+            db.copy_(s_dy)
+        return torch.cat([s_dy, s_dyx])
+
+    def bn_bwd_elemt(self, dy, x, stats, w, sums, y):
+        C = x.shape[1]
+        shape = (1, C) + (1,) * (x.dim() - 2)
+        if y is not None:
+            dy = dy * (y > 0)
+        cnt = stats[2 * C]
+        inv = stats[C: 2 * C].view(shape)
+        mdy = (sums[:C] / cnt).view(shape)
+        mdyx = (sums[C:] / cnt).view(shape)
+        dx = (dy - mdy - (x - stats[:C].view(shape)) * inv * inv * mdyx) * inv
+        if w is not None:
+            dx = dx * w.view(shape)
+        return dx
+
+
+_TORCH_K = _TorchKernels()
+
+
+def _kernels(x):
+    return native() if x.is_cuda else _TORCH_K
+
+
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group):
+        K = _kernels(x)
+        x = x.contiguous()
+        C = x.shape[1]
+        st = K.bn_moments(x)[0]
+        gathered = group.all_gather_flat(st) if group is not None else st
+        stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var)
+        y = K.bn_elemt(x, stats, weight, bias, relu)
+        ctx.params = (weight, bias)
+        ctx.relu = relu
+        ctx.group = group
+        ctx.save_for_backward(x, weight, stats, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, stats, y = ctx.saved_tensors
+        K = _kernels(x)
+        dy = dy.contiguous()
+        w_param, b_param = ctx.params
+        dw = grad_dest(w_param) if (w_param is not None and needs(ctx, 1)) else None
+        db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
+        sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0)
+        dx = None
+        if needs(ctx, 0):
+            if ctx.group is not None:
+                ctx.group.all_reduce_sum_(sums)
+            dx = K.bn_bwd_elemt(dy, x, stats, weight, sums, y)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
+               running_var: torch.Tensor | None, weight: torch.Tensor | None = None,
+               bias: torch.Tensor | None = None, training: bool = True, momentum: float = 0.1,
+               eps: float = 1e-5, relu: bool = False, group=None) -> torch.Tensor:
+    """Batch norm over dim 1 of x ([N, C] or [N, C, *]); ``group`` makes it synchronous."""
+    if training:
+        return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, float(momentum),
+                                  float(eps), bool(relu), group)
+    if x.is_cuda and not (torch.is_grad_enabled() and (x.requires_grad or (
+            weight is not None and weight.requires_grad))):
+        return native().bn_eval(x.contiguous(), running_mean, running_var, weight, bias,
+                                float(eps), bool(relu))
+    # inference-mode BN that must be differentiated (frozen-BN fine-tuning): ATen formula
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, False, 0.0, eps)
+    return F.relu(y) if relu else y

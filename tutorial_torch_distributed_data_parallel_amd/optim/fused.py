@@ -1,0 +1,280 @@
+"""Fused SGD / Adam / AdamW (torch.optim-compatible).
+
+The reference steps ``torch.optim.Adam(ddp_model.parameters(), lr=0.001)``
+(REF/multi-GPU-training-torch.py:249, REF/multi-GPU-training-accelerate.py:126); the north star
+adds a fused SGD. Both are ``torch.optim.Optimizer`` subclasses (param_groups, state_dict,
+load_state_dict, LR schedulers all work) whose ``step`` is:
+  * FLAT  -- when the group's parameters are exactly one ParamArena (every DDP model, or any model
+             passed through ``flatten_module``) and each .grad is its arena view: ONE kernel over
+             the whole arena, optimizer state kept in arena-shaped flat buffers
+             (state[p][...] are views into them);
+  * MULTI -- otherwise: one launch over a device-side chunk table of the individual tensors;
+  * CPU   -- torch's own single-tensor implementation (reference path for the CPU tests).
+Semantics are torch's (TORCH/optim/sgd.py, TORCH/optim/adam.py): momentum buffer initialised to
+the first gradient, dampening, nesterov, maximize, L2 vs decoupled weight decay, amsgrad,
+bias-corrected Adam with a per-parameter step counter.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from .._native import native
+from ..parallel.arena import arena_of
+
+
+def _flat_arena(group):
+    params = group["params"]
+    a = arena_of(params)
+    if a is None:
+        return None
+    for i in range(len(a.params)):
+        if not a.is_arena_grad(i):
+            return None
+    return a
+
+
+class _FusedBase(Optimizer):
+    _state_keys: tuple = ()
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self._flat_bufs = {}  # id(arena) -> {key: flat tensor}
+        self._flat_step = {}  # id(arena) -> int step shared by every arena parameter (Adam)
+
+    def _flat_state(self, arena, keys):
+        """Arena-shaped state buffers; adopts values already in self.state (load_state_dict)."""
+        bufs = self._flat_bufs.get(id(arena))
+        if bufs is not None and all(k in bufs for k in keys):
+            return bufs, False  # steady state: no per-parameter Python work
+        fresh = False
+        if bufs is None:
+            bufs = {k: arena.new_state() for k in keys}
+            self._flat_bufs[id(arena)] = bufs
+            fresh = True
+        for i, p in enumerate(arena.params):
+            st = self.state[p]
+            for k in keys:
+                view = arena.state_view(bufs[k], i)
+                cur = st.get(k)
+                if cur is None:
+                    st[k] = view
+                elif cur.data_ptr() != view.data_ptr():
+                    view.copy_(cur)
+                    st[k] = view
+                    fresh = False
+        return bufs, fresh
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._flat_bufs = {}  # re-adopted into flat buffers on the next step
+        self._flat_step = {}
+
+    def state_dict(self):
+        # materialise the shared flat step counter into torch's per-parameter "step" entries
+        for g in self.param_groups:
+            a = arena_of(g["params"])
+            if a is not None and id(a) in self._flat_step:
+                t = torch.tensor(float(self._flat_step[id(a)]))
+                for p in a.params:
+                    self.state[p]["step"] = t.clone()
+        return super().state_dict()
+
+
+class SGD(_FusedBase):
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, *, maximize: bool = False,
+                 grad_scale: float = 1.0):
+        if lr < 0 or momentum < 0 or weight_decay < 0:
+            raise ValueError("invalid SGD hyper-parameter")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
+                                      weight_decay=weight_decay, nesterov=nesterov,
+                                      maximize=maximize, grad_scale=grad_scale))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for g in self.param_groups:
+            ps = [p for p in g["params"] if p.grad is not None]
+            if not ps:
+                continue
+            hyper = (g["lr"], g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"],
+                     g["maximize"])
+            if not ps[0].is_cuda:
+                self._cpu_step(g, ps)
+                continue
+            C = native()
+            mom = g["momentum"] != 0
+            arena = _flat_arena(g) if len(ps) == len(g["params"]) else None
+            if arena is not None:
+                if mom:
+                    # fresh == the buffers were just created (torch: buf = clone(grad))
+                    bufs, fresh = self._flat_state(arena, ("momentum_buffer",))
+                    C.sgd_flat(arena.data, arena.grad, bufs["momentum_buffer"], *hyper[:5],
+                               hyper[5], fresh, g["grad_scale"])
+                else:
+                    C.sgd_flat(arena.data, arena.grad, None, *hyper[:5], hyper[5], False,
+                               g["grad_scale"])
+                continue
+            new, old = [], []
+            for p in ps:
+                st = self.state[p]
+                if mom and st.get("momentum_buffer") is None:
+                    st["momentum_buffer"] = torch.empty_like(p)
+                    new.append(p)
+                else:
+                    old.append(p)
+            for lst, first in ((new, True), (old, False)):
+                if lst:
+                    bufs = [self.state[p]["momentum_buffer"] for p in lst] if mom else []
+                    C.sgd_multi([p.data for p in lst], [p.grad.contiguous() for p in lst], bufs,
+                                *hyper[:5], hyper[5], first, g["grad_scale"])
+        return loss
+
+    def _cpu_step(self, g, ps):
+        for p in ps:
+            d = p.grad * g["grad_scale"]
+            if g["maximize"]:
+                d = -d
+            if g["weight_decay"]:
+                d = d.add(p, alpha=g["weight_decay"])
+            if g["momentum"]:
+                st = self.state[p]
+                buf = st.get("momentum_buffer")
+                if buf is None:
+                    buf = d.clone()
+                    st["momentum_buffer"] = buf
+                else:
+                    buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+                d = d.add(buf, alpha=g["momentum"]) if g["nesterov"] else buf
+            p.add_(d, alpha=-g["lr"])
+
+
+class Adam(_FusedBase):
+    _decoupled = False
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False,
+                 grad_scale: float = 1.0):
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"invalid betas {betas}")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps,
+                                      weight_decay=weight_decay, amsgrad=amsgrad,
+                                      maximize=maximize, grad_scale=grad_scale))
+
+    def _keys(self, g):
+        return ("exp_avg", "exp_avg_sq") + (("max_exp_avg_sq",) if g["amsgrad"] else ())
+
+    def _bump_step(self, ps):
+        steps = set()
+        for p in ps:
+            st = self.state[p]
+            s = st.get("step")
+            s = torch.tensor(0.0) if s is None else s
+            s = s + 1 if torch.is_tensor(s) else torch.tensor(float(s) + 1)
+            st["step"] = s
+            steps.add(int(s.item()) if torch.is_tensor(s) else int(s))
+        return steps
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for g in self.param_groups:
+            ps = [p for p in g["params"] if p.grad is not None]
+            if not ps:
+                continue
+            b1, b2 = g["betas"]
+            if not ps[0].is_cuda:
+                self._cpu_step(g, ps)
+                continue
+            C = native()
+            keys = self._keys(g)
+            args = (g["lr"], b1, b2, g["eps"], g["weight_decay"], g["amsgrad"], g["maximize"],
+                    self._decoupled)
+            arena = _flat_arena(g) if len(ps) == len(g["params"]) else None
+            if arena is not None:
+                key = id(arena)
+                if key not in self._flat_step:
+                    prev = {int(self.state[p]["step"].item()) if torch.is_tensor(
+                        self.state[p].get("step")) else int(self.state[p].get("step") or 0)
+                        for p in arena.params}
+                    if len(prev) == 1:
+                        self._flat_step[key] = prev.pop()
+                if key in self._flat_step:
+                    bufs, _ = self._flat_state(arena, keys)
+                    self._flat_step[key] += 1
+                    C.adam_flat(arena.data, arena.grad, bufs["exp_avg"], bufs["exp_avg_sq"],
+                                bufs.get("max_exp_avg_sq"), *args, self._flat_step[key],
+                                g["grad_scale"])
+                    continue
+            for k2 in list(self._flat_step):  # leaving the flat path: write the counter back
+                a2 = arena_of(g["params"])
+                if a2 is not None and id(a2) == k2:
+                    t = torch.tensor(float(self._flat_step.pop(k2)))
+                    for p in a2.params:
+                        self.state[p]["step"] = t.clone()
+            by_step = {}
+            for p in ps:
+                st = self.state[p]
+                for k in keys:
+                    if st.get(k) is None:
+                        st[k] = torch.zeros_like(p)
+            self._bump_step(ps)
+            for p in ps:
+                by_step.setdefault(int(self.state[p]["step"].item()), []).append(p)
+            for step, lst in by_step.items():
+                st = [self.state[p] for p in lst]
+                C.adam_multi([p.data for p in lst], [p.grad.contiguous() for p in lst],
+                             [s["exp_avg"] for s in st], [s["exp_avg_sq"] for s in st],
+                             [s["max_exp_avg_sq"] for s in st] if g["amsgrad"] else [],
+                             *args, step, g["grad_scale"])
+        return loss
+
+    def _cpu_step(self, g, ps):
+        b1, b2 = g["betas"]
+        for p in ps:
+            st = self.state[p]
+            if st.get("exp_avg") is None:
+                st["exp_avg"] = torch.zeros_like(p)
+                st["exp_avg_sq"] = torch.zeros_like(p)
+                if g["amsgrad"]:
+                    st["max_exp_avg_sq"] = torch.zeros_like(p)
+            self._bump_step([p])
+            t = int(st["step"].item())
+            grad = p.grad * g["grad_scale"]
+            if g["maximize"]:
+                grad = -grad
+            if g["weight_decay"]:
+                if self._decoupled:
+                    p.mul_(1 - g["lr"] * g["weight_decay"])
+                else:
+                    grad = grad.add(p, alpha=g["weight_decay"])
+            m, v = st["exp_avg"], st["exp_avg_sq"]
+            m.lerp_(grad, 1 - b1)
+            v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+            bc1 = 1 - b1 ** t
+            bc2s = (1 - b2 ** t) ** 0.5
+            vv = v
+            if g["amsgrad"]:
+                torch.maximum(st["max_exp_avg_sq"], v, out=st["max_exp_avg_sq"])
+                vv = st["max_exp_avg_sq"]
+            denom = (vv.sqrt() / bc2s).add_(g["eps"])
+            p.addcdiv_(m, denom, value=-g["lr"] / bc1)
+
+
+class AdamW(Adam):
+    _decoupled = True
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
+                 grad_scale: float = 1.0):
+        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, maximize=maximize,
+                         grad_scale=grad_scale)

@@ -1,0 +1,350 @@
+"""DistributedDataParallel on the flat gradient arena + native reducer.
+
+API-compatible with the way the reference uses torch DDP (``DDP(model, device_ids=[rank])``,
+REF/multi-GPU-training-torch.py:245; Accelerate's ``prepare_model``, ACC/accelerator.py:1882-1896)
+and with the rest of torch's constructor surface (bucket_cap_mb, broadcast_buffers,
+find_unused_parameters, no_sync, state_dict with ``module.`` prefix, register_comm_hook for
+gradient compression). Behaviour matched (SURVEY.md §4.3 oracles):
+  1. after construction every rank holds rank 0's parameters and buffers (one broadcast of the
+     flat arena, M3; buffers re-broadcast each forward when broadcast_buffers, M6);
+  2. after backward ``param.grad == mean over ranks of the local gradients`` (ncclAvg);
+  3. inside ``no_sync()`` gradients stay local and accumulate;
+  4. parameter shapes are verified across ranks at construction (M2).
+What differs by design (MI355X-first): gradients are bucket views from the start (no copies),
+buckets follow backward order from iteration 0 (no 217 MiB first-iteration bucket, no rebuild),
+a bucket may split a large tensor, all-reduces run on a dedicated high-priority HIP stream.
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .._native import native
+from . import runtime as rt
+from .arena import BufferArena, flatten_module
+
+_MB = 1024 * 1024
+
+
+def _param_signature(params) -> str:
+    h = hashlib.sha1()
+    for p in params:
+        h.update(f"{tuple(p.shape)}:{p.dtype};".encode())
+    return h.hexdigest()
+
+
+def _verify_param_shapes(params):
+    if rt.get_world_size() == 1:
+        return
+    sig = _param_signature(params)
+    sigs = [None] * rt.get_world_size()
+    dist.all_gather_object(sigs, (len(params), sig))
+    if any(s != sigs[0] for s in sigs):
+        raise RuntimeError(
+            "DDP expects the same model on every rank: parameter count/shape/dtype signatures "
+            f"differ across ranks: {sigs}")
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
+                 broadcast_buffers: bool = True, process_group=None,
+                 bucket_cap_mb: float | None = None, find_unused_parameters: bool = False,
+                 check_reduction: bool = False, gradient_as_bucket_view: bool = True,
+                 static_graph: bool = False, first_bucket_cap_mb: float | None = None,
+                 split_bucket_mb: float | None = None, grad_compression: str | None = None,
+                 timing: bool = False):
+        super().__init__()
+        if process_group is not None:
+            raise NotImplementedError("sub-groups are not supported: DDP uses the world group")
+        if not rt.is_initialized():
+            raise RuntimeError("call init_process_group() before wrapping a model in DDP")
+        self.module = module
+        self.device_ids = device_ids
+        self.output_device = output_device
+        self.dim = dim
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.static_graph = static_graph
+        self.gradient_as_bucket_view = True  # always: gradients live in the bucket arena
+        self.require_backward_grad_sync = True
+        self.world_size = rt.get_world_size()
+        self.rank = rt.get_rank()
+
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise RuntimeError("DDP: module has no parameter that requires grad")
+        devs = {p.device for p in params}
+        if len(devs) != 1:
+            raise ValueError(f"DDP expects all parameters on one device, got {devs}")
+        self.device = next(iter(devs))
+        if self.device.type == "cuda" and device_ids:
+            want = torch.device("cuda", device_ids[0]) if isinstance(device_ids[0], int) \
+                else torch.device(device_ids[0])
+            if want != self.device:
+                raise ValueError(f"module is on {self.device} but device_ids={device_ids}")
+        self._gpu = self.device.type == "cuda"
+
+        _verify_param_shapes(params)
+        self.arena = flatten_module(module)
+        self.buffers_arena = BufferArena(module)
+        # M3: every rank starts from rank 0's weights -- one broadcast of the flat arena
+        with torch.no_grad():
+            rt.broadcast(self.arena.data, 0)
+            self._sync_buffers()
+
+        cap = (bucket_cap_mb if bucket_cap_mb is not None else 25.0) * _MB
+        first = (first_bucket_cap_mb if first_bucket_cap_mb is not None else 1.0) * _MB
+        split = (split_bucket_mb or 0.0) * _MB
+        C = native() if self._gpu else None
+        esize = self.arena.data.element_size()
+        if C is not None:
+            bounds = C.Reducer.compute_bucket_bounds(self.arena.offsets, self.arena.numels,
+                                                     self.arena.numel, esize, int(first),
+                                                     int(cap), int(split))
+        else:
+            bounds = _bucket_bounds_py(self.arena.offsets, self.arena.numels, self.arena.numel,
+                                       esize, int(first), int(cap), int(split))
+        self._bounds = bounds
+        self._compression = grad_compression
+        self._timing = timing
+        self._build_reducer()
+        self._hooks = []
+        for i, p in enumerate(self.arena.params):
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self._callback_queued = False
+        self._iter = 0
+
+    # --------------------------------------------------------------------------- reducer
+    def _build_reducer(self):
+        nb = len(self._bounds) - 1
+        if self._gpu:
+            C = native()
+            comp = {None: 0, "none": 0, "fp32": 0, "bf16": 1}[self._compression]
+            comm = rt.comm()
+            if comm is None:
+                raise RuntimeError("GPU DDP needs the RCCL backend (init_process_group('nccl'))")
+            self._backend = C.RcclBackend(comm, self.arena.grad, nb, compression=comp,
+                                          timing=self._timing, skip_single_rank=True)
+            self.reducer = C.Reducer(self.arena.offsets, self.arena.numels, self._bounds,
+                                     self._backend)
+        else:
+            self._works = []
+            self._backend = None
+            self.reducer = _make_py_reducer(self)
+
+    def _make_hook(self, idx):
+        arena = self.arena
+
+        def hook(p):
+            if not arena.is_arena_grad(idx):
+                # a gradient produced outside the native ops: move it into its bucket slot
+                slot = arena.grad_view(idx)
+                slot.copy_(p.grad)
+                p.grad = slot
+            if self.require_backward_grad_sync and self.reducer.expecting:
+                if not self._callback_queued:
+                    torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+                    self._callback_queued = True
+                self.reducer.mark_ready(idx, self._gpu)
+        return hook
+
+    def _finalize(self):
+        self._callback_queued = False
+        self.reducer.finalize(self._gpu, self.find_unused_parameters)
+        self._iter += 1
+
+    def _sync_buffers(self):
+        if self.world_size == 1:
+            return
+        ba = self.buffers_arena
+        if ba.data is not None:
+            rt.broadcast(ba.data, 0)
+        for b in ba.others:
+            rt.broadcast(b, 0)
+
+    # --------------------------------------------------------------------------- nn.Module
+    def forward(self, *inputs, **kwargs):
+        if torch.is_grad_enabled() and self.require_backward_grad_sync:
+            self.reducer.prepare_for_backward()
+        if self.broadcast_buffers and self.world_size > 1 and self.module.training:
+            with torch.no_grad():
+                self._sync_buffers()
+        return self.module(*inputs, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def register_comm_hook(self, state, hook):
+        """Gradient compression hooks: torch's bf16_compress_hook (or the string "bf16")."""
+        name = hook if isinstance(hook, str) else getattr(hook, "__name__", "")
+        if name in ("bf16", "bf16_compress_hook"):
+            self._compression = "bf16"
+        elif name in ("allreduce_hook", "none", "fp32"):
+            self._compression = None
+        else:
+            raise NotImplementedError(f"comm hook {name!r} is not supported (bf16 | fp32)")
+        if self._gpu:
+            self._build_reducer()
+
+    # --------------------------------------------------------------------------- logging
+    def _get_ddp_logging_data(self) -> dict:
+        b = self._bounds
+        esize = self.arena.data.element_size()
+        return {
+            "world_size": self.world_size,
+            "backend_name": rt.get_backend(),
+            "bucket_cap_bytes": None,
+            "bucket_sizes": [(b[i + 1] - b[i]) * esize for i in range(len(b) - 1)],
+            "num_buckets": len(b) - 1,
+            "has_rebuilt_buckets": 0,
+            "iterations": self._iter,
+            "gradient_as_bucket_view": True,
+            "find_unused_parameters": self.find_unused_parameters,
+            "first_iteration_ready_order": list(self.reducer.ready_order()),
+            "avg_backward_comm_time_ms": self.reducer.last_comm_ms(),
+            "grad_compression": self._compression or "none",
+        }
+
+
+def _bucket_bounds_py(offsets, numels, arena_numel, esize, first_cap, cap, split):
+    """Python twin of Reducer::compute_bucket_bounds (used when no native module: CPU)."""
+    b = [0]
+    cur = 0
+    split_el = max(split // esize, 1) if split > 0 else 0
+    for i, (o, n) in enumerate(zip(offsets, numels)):
+        c = first_cap if len(b) == 1 else cap
+        nbytes = n * esize
+        if cur > 0 and cur + nbytes > c:
+            b.append(o)
+            cur = 0
+        if split_el and n > split_el:
+            if b[-1] != o:
+                b.append(o)
+            b.extend(o + s for s in range(split_el, n, split_el))
+            if i + 1 < len(offsets):
+                b.append(o + n)
+            cur = 0
+            continue
+        cur += nbytes
+    if b[-1] != arena_numel:
+        b.append(arena_numel)
+    out = [b[0]]
+    for x in b[1:]:
+        if x > out[-1]:
+            out.append(x)
+    if len(out) == 1:
+        out.append(arena_numel)
+    return out
+
+
+def _make_py_reducer(ddp: DistributedDataParallel):
+    """Reducer over torch.distributed (gloo) for CPU runs. Uses the native C++ Reducer logic
+    when the extension is importable (it is, on every supported machine), else a Python twin."""
+    arena = ddp.arena
+    world = ddp.world_size
+
+    def launch(bucket, begin, end):
+        t = arena.grad[begin:end]
+        if world > 1:
+            t.div_(world)  # DDP semantics: divide, then SUM (gloo has no AVG)
+            ddp._works.append(dist.all_reduce(t, async_op=True))
+
+    def wait():
+        for w in ddp._works:
+            w.wait()
+        ddp._works.clear()
+
+    def zero(begin, end):
+        arena.grad[begin:end].zero_()
+
+    try:
+        C = native()
+        backend = C.PyBackend(launch, wait, zero)
+        return C.Reducer(arena.offsets, arena.numels, ddp._bounds, backend)
+    except Exception:  # pragma: no cover - extension missing on a CPU-only box
+        return _PyReducer(arena.offsets, arena.numels, ddp._bounds, launch, wait, zero)
+
+
+class _PyReducer:
+    def __init__(self, offsets, numels, bounds, launch, wait, zero):
+        self.offsets, self.numels, self.bounds = offsets, numels, bounds
+        self._launch, self._wait, self._zero = launch, wait, zero
+        nb = len(bounds) - 1
+        self.param_buckets = []
+        self.nparams = [0] * nb
+        for o, n in zip(offsets, numels):
+            bs = [b for b in range(nb) if n and bounds[b] < o + n and bounds[b + 1] > o]
+            self.param_buckets.append(bs)
+            for b in bs:
+                self.nparams[b] += 1
+        self.expecting = False
+        self.iteration = 0
+        self.num_buckets = nb
+        self._order = []
+
+    def prepare_for_backward(self):
+        self.pending = list(self.nparams)
+        self.ready = [n == 0 for n in self.nparams]
+        self.pready = [False] * len(self.offsets)
+        self.next = 0
+        self.expecting = True
+
+    def mark_ready(self, p, gpu=False):
+        if not self.expecting:
+            return
+        if self.pready[p]:
+            raise RuntimeError("Expected to mark a variable ready only once")
+        self.pready[p] = True
+        if self.iteration == 0:
+            self._order.append(p)
+        for b in self.param_buckets[p]:
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self.ready[b] = True
+        self._launch_ready()
+
+    def _launch_ready(self):
+        while self.next < self.num_buckets and self.ready[self.next]:
+            self._launch(self.next, self.bounds[self.next], self.bounds[self.next + 1])
+            self.next += 1
+
+    def finalize(self, gpu=False, allow_unused=False):
+        if not self.expecting:
+            return
+        unready = [i for i, r in enumerate(self.pready) if not r and self.numels[i]]
+        if unready and not allow_unused:
+            raise RuntimeError(f"parameters {unready} received no gradient; pass "
+                               "find_unused_parameters=True")
+        for p in unready:
+            self._zero(self.offsets[p], self.offsets[p] + self.numels[p])
+            self.pready[p] = True
+            for b in self.param_buckets[p]:
+                self.pending[b] -= 1
+                if self.pending[b] == 0:
+                    self.ready[b] = True
+        self._launch_ready()
+        self._wait()
+        self.expecting = False
+        self.iteration += 1
+
+    def bucket_bounds(self):
+        return list(self.bounds)
+
+    def ready_order(self):
+        return list(self._order)
+
+    def last_comm_ms(self):
+        return -1.0
+
+
+DDP = DistributedDataParallel
