@@ -75,8 +75,11 @@ def test_ddp_step_matches_torch(pg, opt_name, bn):
     # gradients live in the arena (zero-copy buckets)
     for i, p in enumerate(ddp.arena.params):
         assert ddp.arena.is_arena_grad(i)
+    # A Linear bias feeding a BatchNorm has an exactly-zero true gradient, so its computed
+    # gradient is pure summation-order noise; Adam normalises that noise to +-lr per step.
+    atol = 3.5e-3 if (bn and opt_name == "adam") else 2e-4
     for p, r in zip(model.parameters(), ref.parameters()):
-        torch.testing.assert_close(p, r, atol=2e-4, rtol=1e-3)
+        torch.testing.assert_close(p, r, atol=atol, rtol=1e-3)
 
 
 def test_no_sync_accumulates(pg):
