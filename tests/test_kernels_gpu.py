@@ -24,12 +24,14 @@ def _ref_gemm(A, B, a_k, b_k, mask=None):
 
 
 SHAPES = [(128, 4096, 9216), (128, 10, 4096), (128, 4096, 10), (4096, 4096, 128),
-          (10, 4096, 128), (37, 53, 71), (1, 1, 1), (256, 320, 96), (130, 66, 257)]
+          (10, 4096, 128), (37, 53, 71), (1, 1, 1), (256, 320, 96), (130, 66, 257),
+          (132, 196, 100), (260, 136, 44), (64, 8, 4)]
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, False), (False, True)])
-def test_gemm_layouts(C, M, N, K, a_k, b_k):
+def test_gemm_layouts(C, M, N, K, a_k, b_k, mode):
     if M * N * K > 128 * 4096 * 9216 // 4 and not (a_k and b_k):
         pytest.skip("large shape covered in the forward layout")
     torch.manual_seed(M + N + K)
@@ -37,7 +39,11 @@ def test_gemm_layouts(C, M, N, K, a_k, b_k):
     A = torch.randn((M, K) if a_k else (K, M), device=d)
     B = torch.randn((N, K) if b_k else (K, N), device=d)
     out = torch.empty(M, N, device=d)
-    C.gemm_f32(A, B, out, a_k, b_k)
+    C.gemm_f32_set_mode(mode)  # 0: auto (LDS-DMA fast kernel when aligned), 1: generic
+    try:
+        C.gemm_f32(A, B, out, a_k, b_k)
+    finally:
+        C.gemm_f32_set_mode(0)
     ref = _ref_gemm(A, B, a_k, b_k)
     tol = 2e-4 * max(1.0, K ** 0.5)
     _close(out, ref, rtol=1e-4, atol=tol)
@@ -208,3 +214,31 @@ def test_linear_autograd_matches_torch():
         _close(gx, rgx.float(), atol=2e-3)
         _close(gw, rgw.float(), atol=2e-3)
         _close(gb, rgb.float(), atol=2e-3)
+
+
+def test_gemm_fast_epilogue_and_split(C):
+    torch.manual_seed(9)
+    for (M, N, K) in [(128, 4096, 4096), (96, 200, 300), (200, 260, 1024)]:
+        A = torch.randn(M, K, device="cuda")
+        W = torch.randn(N, K, device="cuda")
+        b = torch.randn(N, device="cuda")
+        out = torch.empty(M, N, device="cuda")
+        C.gemm_f32(A, W, out, True, True, bias=b, relu=True)
+        ref = torch.relu(_ref_gemm(A, W, True, True) + b)
+        _close(out, ref, atol=2e-4 * K ** 0.5)
+
+
+def test_relu_bias_bwd(C):
+    torch.manual_seed(10)
+    for B, N in [(128, 4096), (37, 130), (5, 3)]:
+        dy = torch.randn(B, N, device="cuda")
+        y = torch.relu(torch.randn(B, N, device="cuda"))
+        db = torch.empty(N, device="cuda")
+        g = C.relu_bias_bwd(dy, y, db)
+        ref = dy * (y > 0)
+        _close(g, ref, atol=0, rtol=0)
+        _close(db, ref.sum(0), atol=1e-4)
+        db2 = torch.empty(N, device="cuda")
+        g2 = C.relu_bias_bwd(dy, None, db2)
+        assert g2.data_ptr() == dy.data_ptr()
+        _close(db2, dy.sum(0), atol=1e-4)

@@ -1,0 +1,250 @@
+"""Accelerate-style facade over the native runtime (the reference's second entry point).
+
+Covers the Accelerator surface the reference uses (REF/multi-GPU-training-accelerate.py:39-141,
+SURVEY.md §2.2 B16-B21): ``Accelerator()``, ``.device``, ``.is_main_process``,
+``.is_local_main_process``, ``.num_processes``, ``.process_index``, ``.prepare(model, optimizer,
+dataloader)``, ``.backward(loss)``, ``.wait_for_everyone()``, ``.save_model(model, dir)`` (->
+``model.safetensors`` with unwrapped keys, main process only), ``.unwrap_model``, ``.print``,
+plus ``gather`` / ``reduce`` / ``save_state`` / ``load_state`` / ``end_training``.
+
+State comes from the environment like Accelerate's PartialState (ACC/state.py:177-328,769-791):
+with LOCAL_RANK / WORLD_SIZE set (our launcher or torchrun) the process joins a multi-rank job
+(RCCL on GPUs); under plain ``python`` it is a single process. ``prepare`` places the model on the
+device and wraps it in the native DDP when there is more than one process (ACC/accelerator.py:
+1882-1896); data loaders are sharded by whole batches (BatchSamplerShard semantics) and moved to
+the device per batch (DataLoaderShard); optimizers are passed through (gradient accumulation
+gating as AcceleratedOptimizer does).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..data.sampler import BatchShardSampler
+from ..data.synthetic import DeviceLoader
+from ..parallel import runtime as rt
+from ..parallel.arena import flatten_module
+from ..parallel.ddp import DistributedDataParallel
+from ..utils import checkpoint as ckpt
+
+
+class AcceleratedOptimizer:
+    def __init__(self, optimizer, accelerator):
+        self.optimizer = optimizer
+        self._acc = accelerator
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self._acc.sync_gradients:
+            self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    def step(self, closure=None):
+        if self._acc.sync_gradients:
+            return self.optimizer.step(closure)
+        return None
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        return self.optimizer.load_state_dict(sd)
+
+
+class ShardedLoader:
+    """Batches of a base loader dealt to ranks round-robin, moved to the device."""
+
+    def __init__(self, base, accelerator, even_batches: bool = True):
+        self.base = base
+        self.acc = accelerator
+        self.even = even_batches
+        self.sampler = getattr(base, "sampler", None)
+
+    def set_epoch(self, epoch: int):
+        if self.sampler is not None and hasattr(self.sampler, "set_epoch"):
+            self.sampler.set_epoch(epoch)
+
+    def _device_loader(self):
+        b = self.base
+        order = list(b.sampler) if b.sampler is not None else list(range(len(b.dataset)))
+        bs = BatchShardSampler(len(order), b.batch_size, self.acc.num_processes,
+                               self.acc.process_index, drop_last=b.drop_last,
+                               even_batches=self.even, order=order)
+        return DeviceLoader(b.dataset, b.batch_size, batch_sampler=bs, device=self.acc.device)
+
+    def __iter__(self):
+        if isinstance(self.base, DeviceLoader):
+            yield from self._device_loader()
+            return
+        W, r = self.acc.num_processes, self.acc.process_index
+        dev = self.acc.device
+        batches = []
+        for i, batch in enumerate(self.base):
+            batches.append(batch)
+            if len(batches) == W:
+                yield _to_device(batches[r], dev)
+                batches = []
+        if batches and self.even:
+            # complete the last round with batches from the start, like even_batches=True
+            head = iter(self.base)
+            while len(batches) < W:
+                batches.append(next(head))
+            yield _to_device(batches[r], dev)
+
+    def __len__(self):
+        n = len(self.base)
+        W = self.acc.num_processes
+        return -(-n // W) if self.even else len(range(self.acc.process_index, n, W))
+
+
+def _to_device(batch, dev):
+    if torch.is_tensor(batch):
+        return batch.to(dev, non_blocking=True)
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(_to_device(b, dev) for b in batch)
+    if isinstance(batch, dict):
+        return {k: _to_device(v, dev) for k, v in batch.items()}
+    return batch
+
+
+class Accelerator:
+    def __init__(self, cpu: bool = False, gradient_accumulation_steps: int = 1,
+                 even_batches: bool = True, ddp_kwargs: dict | None = None):
+        if not rt.is_initialized():
+            multi = int(os.environ.get("WORLD_SIZE", "1")) > 1 or "LOCAL_RANK" in os.environ
+            backend = "gloo" if (cpu or not torch.cuda.is_available()) else "nccl"
+            if multi:
+                rt.init_process_group(backend)
+            else:
+                rt.init_process_group(backend, rank=0, world_size=1, local_rank=0)
+        self.device = rt.device()
+        self.gradient_accumulation_steps = max(1, int(gradient_accumulation_steps))
+        self.even_batches = even_batches
+        self.ddp_kwargs = ddp_kwargs or {}
+        self._step = 0
+        self.sync_gradients = True
+        self._models = []
+
+    # ------------------------------------------------------------------ process state
+    @property
+    def num_processes(self) -> int:
+        return rt.get_world_size()
+
+    @property
+    def process_index(self) -> int:
+        return rt.get_rank()
+
+    @property
+    def local_process_index(self) -> int:
+        return rt.get_local_rank()
+
+    @property
+    def is_main_process(self) -> bool:
+        return rt.get_rank() == 0
+
+    @property
+    def is_local_main_process(self) -> bool:
+        return rt.get_local_rank() == 0
+
+    @property
+    def distributed_type(self) -> str:
+        return "MULTI_GPU" if (self.num_processes > 1 and self.device.type == "cuda") else (
+            "MULTI_CPU" if self.num_processes > 1 else "NO")
+
+    def print(self, *a, **k):
+        if self.is_local_main_process:
+            print(*a, **k)
+
+    # ------------------------------------------------------------------ prepare
+    def prepare_model(self, model):
+        model = model.to(self.device)
+        if self.num_processes > 1:
+            dev_ids = [self.device.index] if self.device.type == "cuda" else None
+            model = DistributedDataParallel(model, device_ids=dev_ids, **self.ddp_kwargs)
+        else:
+            flatten_module(model)  # single process: still one flat arena for the fused step
+        self._models.append(model)
+        return model
+
+    def prepare_optimizer(self, opt):
+        return AcceleratedOptimizer(opt, self)
+
+    def prepare_data_loader(self, loader):
+        return ShardedLoader(loader, self, even_batches=self.even_batches)
+
+    def _prepare_one(self, obj):
+        if isinstance(obj, torch.nn.Module):
+            return self.prepare_model(obj)
+        if isinstance(obj, torch.optim.Optimizer):
+            return self.prepare_optimizer(obj)
+        if isinstance(obj, (torch.utils.data.DataLoader, DeviceLoader)):
+            return self.prepare_data_loader(obj)
+        return obj
+
+    def prepare(self, *objs):
+        # models first (parameters move into the arena before optimizers are wrapped)
+        out = [None] * len(objs)
+        for i, o in enumerate(objs):
+            if isinstance(o, torch.nn.Module):
+                out[i] = self._prepare_one(o)
+        for i, o in enumerate(objs):
+            if out[i] is None:
+                out[i] = self._prepare_one(o)
+        return out[0] if len(out) == 1 else tuple(out)
+
+    # ------------------------------------------------------------------ training
+    def backward(self, loss, **kwargs):
+        self._step += 1
+        self.sync_gradients = (self._step % self.gradient_accumulation_steps) == 0
+        (loss / self.gradient_accumulation_steps).backward(**kwargs)
+
+    def clip_grad_norm_(self, parameters, max_norm: float, norm_type: float = 2.0):
+        return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type)
+
+    def wait_for_everyone(self):
+        rt.barrier()
+
+    def gather(self, t: torch.Tensor) -> torch.Tensor:
+        return rt.all_gather_flat(t).reshape(self.num_processes * t.shape[0], *t.shape[1:]) \
+            if t.dim() > 0 else rt.all_gather_flat(t.reshape(1))
+
+    def reduce(self, t: torch.Tensor, reduction: str = "sum") -> torch.Tensor:
+        t = t.clone()
+        rt.all_reduce(t, "sum")
+        if reduction == "mean":
+            t /= self.num_processes
+        return t
+
+    def unwrap_model(self, model):
+        return ckpt.unwrap_model(model)
+
+    def save_model(self, model, save_directory: str, safe_serialization: bool = True):
+        if not safe_serialization:
+            path = os.path.join(save_directory, "pytorch_model.bin")
+            if self.is_main_process:
+                os.makedirs(save_directory, exist_ok=True)
+                torch.save({k: v.detach().cpu().clone()
+                            for k, v in self.unwrap_model(model).state_dict().items()}, path)
+            return path
+        return ckpt.save_model_safetensors(model, save_directory)
+
+    def save_state(self, output_dir: str, model=None, optimizer=None):
+        model = model if model is not None else (self._models[0] if self._models else None)
+        opt = optimizer.optimizer if isinstance(optimizer, AcceleratedOptimizer) else optimizer
+        ckpt.save_training_state(os.path.join(output_dir, "state.pt"), model, opt)
+
+    def load_state(self, input_dir: str, model=None, optimizer=None):
+        model = model if model is not None else (self._models[0] if self._models else None)
+        opt = optimizer.optimizer if isinstance(optimizer, AcceleratedOptimizer) else optimizer
+        return ckpt.load_training_state(os.path.join(input_dir, "state.pt"), model, opt,
+                                        map_location=self.device)
+
+    def end_training(self):
+        rt.destroy_process_group()

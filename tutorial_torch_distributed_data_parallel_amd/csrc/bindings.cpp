@@ -95,8 +95,11 @@ std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus)
   GemmF32Args a;
   a.M = M; a.N = N; a.K = K;
   a.rowsum = rowsum ? reinterpret_cast<float*>(16) : nullptr;
+  a.a_kcontig = true; a.b_kcontig = true;
+  a.A = reinterpret_cast<const float*>(256); a.B = reinterpret_cast<const float*>(256);
+  a.lda = K; a.ldb = K;
   const GemmPlan p = gemm_f32_plan(a, cus);
-  return {p.tile, p.bm, p.bn, p.splits, p.k_per_split, p.ws_floats};
+  return {p.fast ? 1 : 0, p.tile, p.bm, p.bn, p.stages, p.splits, p.k_per_split, p.ws_floats};
 }
 
 // ----------------------------------------------------------------------------------------- loss
@@ -223,6 +226,29 @@ void adam_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
               decoupled, (float)(1.0 - std::pow(b1, (double)step)),
               (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale};
   adam_multi(reinterpret_cast<const TensorChunk*>(tab.data_ptr()), count, h, cur_stream());
+}
+
+// g = dy*(y>0) (new tensor; dy itself when y is None), db (optional) = sum over rows of g
+Tensor relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
+                        const c10::optional<Tensor>& db, double beta_db) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_ROWMAJOR(dy);
+  const int B = (int)dy.size(0), N = (int)dy.size(1);
+  const bool has_y = y.has_value() && y->defined();
+  Tensor g = dy;
+  if (has_y) {
+    CHECK_ROWMAJOR(*y);
+    TORCH_CHECK(y->sizes() == dy.sizes() && y->stride(0) == dy.stride(0), "relu mask layout");
+    g = at::empty({B, N}, dy.options());
+  }
+  float* dbp = fptr(db);
+  if (!has_y && dbp == nullptr) return g;
+  const int slices = relu_bias_slices(B, N, num_cus(dy.get_device()));
+  Tensor part;
+  if (dbp) part = at::empty({(int64_t)slices * N}, dy.options());
+  relu_bias_bwd_ws(dy.data_ptr<float>(), has_y ? y->data_ptr<float>() : nullptr, B, N,
+                   dy.stride(0), g.data_ptr<float>(), dbp, (float)beta_db,
+                   dbp ? part.data_ptr<float>() : nullptr, slices, cur_stream());
+  return g;
 }
 
 // ------------------------------------------------------------------------------------ misc ops
@@ -402,6 +428,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none(), py::arg("beta") = 0.0,
         py::arg("rowsum_beta") = 0.0, py::arg("relu") = false);
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
+  m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
+  m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
+        py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
   m.def("ce_fwd", &ce_fwd_op);
   m.def("ce_bwd", &ce_bwd_op);
   m.def("count_correct", &count_correct_op);

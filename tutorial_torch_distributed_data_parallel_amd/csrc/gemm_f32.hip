@@ -221,6 +221,7 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(Params p) {
     }
 }
 
+// grid: (ceil(N4 / 64), ceil(M / 4)); a 256-thread block covers 4 rows x 64 column groups
 template <bool VEC>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws,
                                                             int splits, int M, int N, void* Cv,
@@ -228,55 +229,36 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             const float* __restrict__ bias,
                                                             float beta, int relu) {
   const long plane = (long)M * N;
+  const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  constexpr int W = VEC ? 4 : 1;
+  const int col = (blockIdx.x * 64 + (threadIdx.x & 63)) * W;
+  if (col >= N) return;
+  const long base = (long)row * N + col;
+  float v[W];
   if (VEC) {
-    const int n4 = N / 4;
-    const long total = (long)M * n4;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-         i += (long)gridDim.x * blockDim.x) {
-      const int row = (int)(i / n4), col = (int)(i % n4) * 4;
-      f32x4 v = *reinterpret_cast<const f32x4*>(ws + (long)row * N + col);
-      for (int z = 1; z < splits; ++z) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(ws + z * plane + (long)row * N + col);
-        v += t;
-      }
-      if (bias) v += *reinterpret_cast<const f32x4*>(bias + col);
-      if (c_bf16) {
-        unsigned short* C = reinterpret_cast<unsigned short*>(Cv) + (long)row * ldc + col;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = v[e];
-          if (beta != 0.f) x += beta * bf16_to_f32(C[e]);
-          if (relu) x = fmaxf(x, 0.f);
-          C[e] = f32_to_bf16(x);
-        }
-      } else {
-        float* C = reinterpret_cast<float*>(Cv) + (long)row * ldc + col;
-        if (beta != 0.f) v += beta * *reinterpret_cast<const f32x4*>(C);
-        if (relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *reinterpret_cast<f32x4*>(C) = v;
-      }
-    }
+    f32x4 t = *reinterpret_cast<const f32x4*>(ws + base);
+    for (int z = 1; z < splits; ++z) t += *reinterpret_cast<const f32x4*>(ws + z * plane + base);
+    for (int e = 0; e < 4; ++e) v[e] = t[e];
   } else {
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < plane;
-         i += (long)gridDim.x * blockDim.x) {
-      const int row = (int)(i / N), col = (int)(i % N);
-      float v = 0.f;
-      for (int z = 0; z < splits; ++z) v += ws[z * plane + i];
-      if (bias) v += bias[col];
-      if (c_bf16) {
-        unsigned short* C = reinterpret_cast<unsigned short*>(Cv) + (long)row * ldc + col;
-        if (beta != 0.f) v += beta * bf16_to_f32(*C);
-        if (relu) v = fmaxf(v, 0.f);
-        *C = f32_to_bf16(v);
-      } else {
-        float* C = reinterpret_cast<float*>(Cv) + (long)row * ldc + col;
-        if (beta != 0.f) v += beta * *C;
-        if (relu) v = fmaxf(v, 0.f);
-        *C = v;
-      }
+    float t = 0.f;
+    for (int z = 0; z < splits; ++z) t += ws[z * plane + base];
+    v[0] = t;
+  }
+#pragma unroll
+  for (int e = 0; e < W; ++e) {
+    float x = v[e];
+    if (bias) x += bias[col + e];
+    if (c_bf16) {
+      unsigned short* C = reinterpret_cast<unsigned short*>(Cv) + (long)row * ldc + col + e;
+      if (beta != 0.f) x += beta * bf16_to_f32(*C);
+      if (relu) x = fmaxf(x, 0.f);
+      *C = f32_to_bf16(x);
+    } else {
+      float* C = reinterpret_cast<float*>(Cv) + (long)row * ldc + col + e;
+      if (beta != 0.f) x += beta * *C;
+      if (relu) x = fmaxf(x, 0.f);
+      *C = x;
     }
   }
 }
@@ -312,8 +294,15 @@ inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 }  // namespace
 
+static int g_mode = 0;
+void gemm_f32_set_mode(int mode) { g_mode = mode; }
+
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus) {
   GemmPlan plan;
+  if (g_mode != 1 && gemm_f32_fast_ok(a)) {
+    gemm_f32_fast_plan(a, num_cus, plan);
+    return plan;
+  }
   if (a.M >= 512 && a.N >= 512) plan.tile = 0;
   else if (a.M <= 64) plan.tile = 2;
   else plan.tile = 1;
@@ -339,6 +328,10 @@ GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus) {
 
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
+  if (plan.fast) {
+    gemm_f32_fast_run(a, plan, ws, s);
+    return;
+  }
   Params p;
   p.A = a.A; p.B = a.B; p.C = a.C; p.mask = a.mask; p.bias = a.bias; p.rowsum = a.rowsum;
   p.ws = ws; p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldmask = a.ldmask;
@@ -358,16 +351,14 @@ void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf
                    const float* bias, float beta, bool relu, hipStream_t s) {
   const bool vec = (N % 4 == 0) && (ldc % 4 == 0) && aligned16(C) &&
                    (bias == nullptr || aligned16(bias));
-  const long work = vec ? (long)M * N / 4 : (long)M * N;
-  int grid = (int)((work + 255) / 256);
-  if (grid > 4096) grid = 4096;
-  if (grid < 1) grid = 1;
+  const int cols = vec ? N / 4 : N;
+  dim3 grid((cols + 63) / 64, (M + 3) / 4);
   if (vec)
-    hipLaunchKernelGGL(splitk_reduce_kernel<true>, dim3(grid), dim3(256), 0, s, ws, splits, M, N,
-                       C, c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
+    hipLaunchKernelGGL(splitk_reduce_kernel<true>, grid, dim3(256), 0, s, ws, splits, M, N, C,
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
   else
-    hipLaunchKernelGGL(splitk_reduce_kernel<false>, dim3(grid), dim3(256), 0, s, ws, splits, M,
-                       N, C, c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
+    hipLaunchKernelGGL(splitk_reduce_kernel<false>, grid, dim3(256), 0, s, ws, splits, M, N, C,
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
 }
 
 }  // namespace tdp

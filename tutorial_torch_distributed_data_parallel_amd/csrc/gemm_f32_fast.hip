@@ -1,0 +1,379 @@
+// Fast fp32 GEMM for gfx950: v_mfma_f32_32x32x2_f32 fed by a multi-stage LDS-DMA pipeline.
+//
+// Used for every aligned shape (contiguous dims % 4 == 0, 16-B aligned operands); gemm_f32.hip
+// keeps a register-staged generic kernel for the rest. Structure (MI355X-specific choices):
+//   * 256 threads = 4 waves (2x2); a wave owns 64 x 32*FN outputs as FM=2 x FN 32x32 MFMA tiles;
+//     block tile 128 x 64*FN, K step BK = 32.
+//   * Global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no ds_write): S stages in flight,
+//     one counted `s_waitcnt vmcnt` + one raw s_barrier per K step (guide §5 "Pipelining across
+//     barriers"; __syncthreads would drain the DMA queue). All LDS lives in one dynamic array.
+//   * K-contiguous tiles ([rows][32 floats], 128-B rows) are XOR-swizzled through the SOURCE
+//     address (chunk c of row r lands in slot c ^ (r & 7)) since the DMA image is lane-linear;
+//     fragments are read with ds_read_b128: lane half h of k-step (q, s) consumes k = 8q+4h+s,
+//     so one b128 read feeds 4 MFMAs.
+//   * MN-contiguous tiles ([32 k][cols], 512-B rows, conflict-free as is) are read with
+//     ds_read_b64 covering two 32x32 tiles at once: tile f takes the interleaved rows/cols
+//     2*i + f, so a lane's two operands are adjacent in memory. The epilogue undoes the
+//     interleave (and stores float2 when the output columns are interleaved).
+//   * Fragments for q+1 are read while the 16 MFMAs of q issue (register double-buffer), so one
+//     wave per SIMD keeps the matrix pipe busy.
+//   * Out-of-range rows/cols are clamped to valid addresses (they only feed discarded outputs);
+//     the K tail is zeroed on the fragment read of the last tile.
+//   * Block ids are remapped so the workgroups of one XCD share one split-K slice / row panel of
+//     the operand every tile re-reads (L2 locality, guide §5.5 T1; bijective form).
+#include "common.h"
+#include "kernels.h"
+
+namespace tdp {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kBK = 32;
+
+struct FastParams {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  float* ws;
+  long lda, ldb, ldc;
+  int M, N, K;
+  int k_per_split, splits;
+  int tiles_n, tiles_m;
+  float beta;
+  int relu;
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef char lds_char;  // generic pointer into the dynamic LDS array (reads infer ds_read)
+
+__device__ __forceinline__ void glds16(const float* src, lds_char* dst) {
+  __builtin_amdgcn_global_load_lds(
+      (const void*)src, (void __attribute__((address_space(3)))*)(
+          (__attribute__((address_space(3))) char*)dst), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Issue this wave's share of one K tile: a K-contiguous [R][32] tile or an MN-contiguous
+// [32][C] tile; `chunks` 1-KiB pieces split over the 4 waves.
+template <int R>
+__device__ __forceinline__ void issue_kc(const float* g, long ld, int r0, int rlim, int k0,
+                                         int klim, lds_char* dst, int wid, int lane) {
+  constexpr int CH = R / 8;  // 1-KiB chunks (8 rows of 128 B)
+#pragma unroll
+  for (int i = 0; i < CH / 4; ++i) {
+    const int j = wid * (CH / 4) + i;
+    const int row = j * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ (row & 7);
+    int gr = r0 + row;
+    gr = gr < rlim ? gr : rlim - 1;
+    int gk = k0 + kc * 4;
+    gk = gk < klim ? gk : klim - 4;
+    glds16(g + (long)gr * ld + gk, dst + j * 1024);
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void issue_mn(const float* g, long ld, int c0, int clim, int k0,
+                                         int klim, lds_char* dst, int wid, int lane) {
+  constexpr int ROWS_PER = 1024 / (C * 4);  // rows per 1-KiB chunk
+  constexpr int CH = kBK / ROWS_PER;
+  constexpr int LPR = C / 4;                // lanes per row
+#pragma unroll
+  for (int i = 0; i < CH / 4; ++i) {
+    const int j = wid * (CH / 4) + i;
+    const int row = j * ROWS_PER + lane / LPR;
+    int gk = k0 + row;
+    gk = gk < klim ? gk : klim - 1;
+    int gc = c0 + (lane % LPR) * 4;
+    gc = gc < clim ? gc : clim - 4;
+    glds16(g + (long)gk * ld + gc, dst + j * 1024);
+  }
+}
+
+template <int FN, bool AK, bool BKC, int S>
+__global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
+  constexpr int FM = 2;
+  constexpr int BM = 128, BN = 64 * FN;
+  constexpr int A_BYTES = BM * kBK * 4, B_BYTES = BN * kBK * 4;
+  constexpr int STG = A_BYTES + B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 4, GB = B_BYTES / 1024 / 4;  // glds per wave per tile
+  constexpr int G = GA + GB;
+  static_assert(BKC || FN == 2, "an MN-contiguous B operand needs FN == 2 (interleaved tiles)");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = smem_raw;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // XCD-aware remap (bijective): hardware ids b and b+8 share an XCD; give each XCD a
+  // contiguous range of logical tiles, ordered split-major so an XCD shares one K slice.
+  const int nwg = gridDim.x;
+  const int b = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  const int tiles_mn = p.tiles_n * p.tiles_m;
+  const int z = lid / tiles_mn;
+  const int t_mn = lid % tiles_mn;
+  const int tm = t_mn / p.tiles_n, tn = t_mn % p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int kb = z * p.k_per_split;
+  const int ke = min(p.K, kb + p.k_per_split);
+  const int nk = (ke - kb + kBK - 1) / kBK;
+
+  auto issue = [&](int t) {
+    lds_char* st = smem + (t % S) * STG;
+    const int k0 = kb + t * kBK;
+    if (AK) issue_kc<BM>(p.A, p.lda, m0, p.M, k0, ke, st, wid, lane);
+    else issue_mn<BM>(p.A, p.lda, m0, p.M, k0, ke, st, wid, lane);
+    if (BKC) issue_kc<BN>(p.B, p.ldb, n0, p.N, k0, ke, st + A_BYTES, wid, lane);
+    else issue_mn<BN>(p.B, p.ldb, n0, p.N, k0, ke, st + A_BYTES, wid, lane);
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t) issue(t);
+
+  const int h = lane >> 5, l31 = lane & 31;
+  // per-lane LDS byte offsets of the fragment reads (within a stage)
+  int a_off[FM], b_off[FN];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    const int row = wm * 64 + f * 32 + l31;
+    a_off[f] = AK ? row * 128 : (wm * 64 + 2 * l31) * 4;
+  }
+#pragma unroll
+  for (int g = 0; g < FN; ++g) {
+    const int row = wn * (32 * FN) + g * 32 + l31;
+    b_off[g] = BKC ? A_BYTES + row * 128 : A_BYTES + (wn * 64 + 2 * l31) * 4;
+  }
+
+  // fragment registers: value of tile f at k-step s of one q
+  float av[2][FM][4], bv[2][FN][4];
+  auto read_frag = [&](const lds_char* st, int q, float (&a)[FM][4], float (&bb)[FN][4]) {
+    if (AK) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int row = wm * 64 + f * 32 + l31;
+        const int slot = (2 * q + h) ^ (row & 7);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(st + a_off[f] + slot * 16);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[f][s] = v[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 8 * q + 4 * h + s;
+        const f32x2 v = *reinterpret_cast<const f32x2*>(st + k * (BM * 4) + a_off[0]);
+        a[0][s] = v[0];
+        a[1][s] = v[1];
+      }
+    }
+    if (BKC) {
+#pragma unroll
+      for (int g = 0; g < FN; ++g) {
+        const int row = wn * (32 * FN) + g * 32 + l31;
+        const int slot = (2 * q + h) ^ (row & 7);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(st + b_off[g] + slot * 16);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bb[g][s] = v[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 8 * q + 4 * h + s;
+        const f32x2 v = *reinterpret_cast<const f32x2*>(st + k * (BN * 4) + b_off[0]);
+        bb[0][s] = v[0];
+        bb[1][s] = v[1];
+      }
+    }
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt<(S - 2) * G>();
+    __builtin_amdgcn_s_barrier();
+    issue(kt + S - 1);  // refill the stage every wave finished reading (kt - 1)
+    const lds_char* st = smem + (kt % S) * STG;
+    const int kvalid = ke - (kb + kt * kBK);  // < 32 only on the K tail
+    read_frag(st, 0, av[0], bv[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 3) read_frag(st, q + 1, av[(q + 1) & 1], bv[(q + 1) & 1]);
+      float (&a)[FM][4] = av[q & 1];
+      float (&bb)[FN][4] = bv[q & 1];
+      if (kvalid < kBK) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (8 * q + 4 * h + s >= kvalid) {
+#pragma unroll
+            for (int f = 0; f < FM; ++f) a[f][s] = 0.f;
+#pragma unroll
+            for (int g = 0; g < FN; ++g) bb[g][s] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int g = 0; g < FN; ++g)
+            acc[f][g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[f][s], bb[g][s], acc[f][g], 0, 0,
+                                                             0);
+    }
+  }
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  // epilogue
+  const bool split = p.splits > 1;
+  float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
+  const long ldo = split ? p.N : p.ldc;
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+      if (row >= p.M) continue;
+      float* orow = out + (long)row * ldo;
+      if (BKC) {
+#pragma unroll
+        for (int g = 0; g < FN; ++g) {
+          const int col = n0 + wn * (32 * FN) + g * 32 + l31;
+          if (col >= p.N) continue;
+          float v = acc[f][g][r];
+          if (!split) {
+            if (p.bias) v += p.bias[col];
+            if (p.beta != 0.f) v += p.beta * orow[col];
+            if (p.relu) v = fmaxf(v, 0.f);
+          }
+          orow[col] = v;
+        }
+      } else {
+        const int col = n0 + wn * 64 + 2 * l31;  // (g=0, g=1) are adjacent columns
+        f32x2 v = {acc[f][0][r], acc[f][1][r]};
+        if (col + 1 < p.N) {
+          if (!split) {
+            if (p.bias) { v[0] += p.bias[col]; v[1] += p.bias[col + 1]; }
+            if (p.beta != 0.f) {
+              const f32x2 o = *reinterpret_cast<const f32x2*>(orow + col);
+              v[0] += p.beta * o[0];
+              v[1] += p.beta * o[1];
+            }
+            if (p.relu) { v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); }
+          }
+          *reinterpret_cast<f32x2*>(orow + col) = v;
+        } else if (col < p.N) {
+          float x = v[0];
+          if (!split) {
+            if (p.bias) x += p.bias[col];
+            if (p.beta != 0.f) x += p.beta * orow[col];
+            if (p.relu) x = fmaxf(x, 0.f);
+          }
+          orow[col] = x;
+        }
+      }
+    }
+  }
+}
+
+template <int FN, bool AK, bool BKC, int S>
+void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
+  constexpr int STG = 128 * kBK * 4 + 64 * FN * kBK * 4;
+  const size_t lds = (size_t)S * STG;
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AK, BKC, S>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    configured = true;
+  }
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AK, BKC, S>), dim3(nblocks), dim3(kT), lds, s, p);
+}
+
+}  // namespace
+
+bool gemm_f32_fast_ok(const GemmF32Args& a) {
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (a.mask || a.rowsum) return false;
+  if (!al(a.A) || !al(a.B) || a.lda % 4 || a.ldb % 4) return false;
+  if (a.K < 4 || a.K % 4) return false;
+  if (!a.a_kcontig && a.M % 4) return false;
+  if (!a.b_kcontig && a.N % 4) return false;
+  if (a.a_kcontig && !a.b_kcontig) return true;
+  return true;
+}
+
+// Plan: FN (tile width), stages and split-K so that the grid covers the chip.
+void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
+  const bool b_mn = !a.b_kcontig;
+  int fn = b_mn ? 2 : (a.N >= 2048 && a.M >= 512 ? 2 : 1);
+  const int bn = 64 * fn;
+  const long tiles = (long)ceil_div(a.M, 128) * ceil_div(a.N, bn);
+  int splits = 1;
+  if (tiles < num_cus) {
+    const int want = (int)((num_cus + tiles - 1) / tiles);
+    const int kmax = a.K / (kBK * 8);  // keep >= 8 K steps per split
+    splits = want < kmax ? want : kmax;
+    if (splits < 1) splits = 1;
+  }
+  int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
+  plan.fast = true;
+  plan.bm = 128;
+  plan.bn = bn;
+  plan.tile = fn;
+  plan.k_per_split = kps;
+  plan.splits = ceil_div(a.K, kps);
+  plan.ws_floats = plan.splits > 1 ? (long)plan.splits * a.M * a.N : 0;
+  // short K (few tiles per block): 2 stages -> 2 workgroups per CU hide prologue/epilogue;
+  // long K: deeper pipeline at one workgroup per CU.
+  const int nk = ceil_div(kps, kBK);
+  plan.stages = (nk <= 8) ? 2 : 4;
+}
+
+void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+  FastParams p;
+  p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
+  p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
+  p.M = a.M; p.N = a.N; p.K = a.K;
+  p.k_per_split = plan.k_per_split;
+  p.splits = plan.splits;
+  p.tiles_m = ceil_div(a.M, 128);
+  p.tiles_n = ceil_div(a.N, plan.bn);
+  p.beta = plan.splits > 1 ? 0.f : a.beta;
+  p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
+  const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
+  const bool ak = a.a_kcontig, bk = a.b_kcontig;
+  const int fn = plan.tile;
+#define TDP_L(FN, AK, BK, S) launch_fast<FN, AK, BK, S>(p, nblocks, s)
+#define TDP_S(FN, AK, BK) \
+  do { if (plan.stages == 2) TDP_L(FN, AK, BK, 2); else TDP_L(FN, AK, BK, 4); } while (0)
+  if (ak && bk) {
+    if (fn == 1) TDP_S(1, true, true); else TDP_S(2, true, true);
+  } else if (ak && !bk) {
+    TDP_S(2, true, false);
+  } else if (!ak && !bk) {
+    TDP_S(2, false, false);
+  } else {
+    if (fn == 1) TDP_S(1, false, true); else TDP_S(2, false, true);
+  }
+#undef TDP_S
+#undef TDP_L
+  if (plan.splits > 1)
+    splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+}
+
+}  // namespace tdp

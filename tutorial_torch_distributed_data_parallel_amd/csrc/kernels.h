@@ -32,8 +32,10 @@ struct GemmF32Args {
 };
 
 struct GemmPlan {
-  int tile = 0;         // index into the tile table of gemm_f32.hip
+  bool fast = false;    // LDS-DMA pipelined kernel (gemm_f32_fast.hip) vs generic
+  int tile = 0;         // generic: tile-table index; fast: FN (block tile 128 x 64*FN)
   int bm = 128, bn = 64;
+  int stages = 2;       // fast kernel pipeline depth
   int splits = 1;
   int k_per_split = 0;
   long ws_floats = 0;   // split-K workspace needed (0 when splits == 1)
@@ -41,6 +43,11 @@ struct GemmPlan {
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
+bool gemm_f32_fast_ok(const GemmF32Args& a);
+void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
+void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
+// set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel
+void gemm_f32_set_mode(int mode);
 
 // bf16-operand GEMM (AMP path): same contract, A/B bf16 (uint16 storage), C fp32 or bf16.
 struct GemmBF16Args {
@@ -115,6 +122,12 @@ void adam_multi(const TensorChunk* table, int count, const AdamHyper& h, hipStre
 
 // elementwise helpers
 void scale_inplace(float* x, long n, float a, hipStream_t s);
+// ReLU backward + bias gradient in one pass over dy[B][N] (row stride ld):
+//   g[B][N] = dy * (y > 0) (written only when y != null), db = beta_db*db + sum_rows(g).
+//   `part` holds slices*N floats of column partial sums (slices from relu_bias_slices).
+int relu_bias_slices(int B, int N, int num_cus);
+void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, float* g,
+                      float* db, float beta_db, float* part, int slices, hipStream_t s);
 void fill_f32(float* x, long n, float v, hipStream_t s);
 void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
 void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);

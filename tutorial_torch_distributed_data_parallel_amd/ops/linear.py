@@ -3,9 +3,10 @@
 Forward, input-gradient and weight-gradient are each ONE kernel (plus a split-K combine when the
 tile grid alone cannot fill 256 CUs):
   * forward  ``y = relu(x W^T + b)``: bias and ReLU in the GEMM epilogue (SURVEY.md §2.5 K12/K2);
-  * backward: the ReLU mask ``y > 0`` is applied while the kernels stage ``dy`` (K18), the bias
-    gradient is the row sum of that staged tile inside the weight-gradient kernel (K17), and the
-    weight gradient lands directly in the DDP gradient arena (K23, see ``_grad.py``).
+  * backward: one pass applies the ReLU mask ``y > 0`` to ``dy`` and reduces the bias gradient
+    (K17/K18, ``relu_bias_bwd``); the weight- and input-gradient GEMMs then read that masked
+    gradient through their LDS-DMA pipelines, and the weight gradient lands directly in the DDP
+    gradient arena (K23, see ``_grad.py``).
 On CPU the same math runs through ``torch.nn.functional`` (the reference implementation used by
 the gloo/CPU tests). Reference behaviour: torchvision AlexNet's classifier Linear/ReLU layers
 (REF/data_and_toy_model.py:41-45).
@@ -37,21 +38,19 @@ class _LinearFn(torch.autograd.Function):
         w_param, b_param = ctx.params
         if dy.dim() != 2 or dy.stride(1) != 1:
             dy = dy.contiguous()
-        mask = y if ctx.relu else None
         dx = dw = db = None
+        want_db = b_param is not None and needs(ctx, 2)
+        db = grad_dest(b_param) if want_db else None
+        # g = dy * (y > 0) and db = sum_rows(g) in one pass (g is dy itself without ReLU)
+        g = C.relu_bias_bwd(dy, y if ctx.relu else None, db) if (ctx.relu or want_db) else dy
         if needs(ctx, 1):
             dw = grad_dest(w_param)
-            db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
-            # dW[out, in] = dy^T . x : A = dy stored [K=batch][M=out], B = x stored [K][N=in]
-            C.gemm_f32(dy, x2, dw, False, False, mask=mask, rowsum=db)
-        elif b_param is not None and needs(ctx, 2):
-            db = grad_dest(b_param)
-            m = dy if mask is None else dy * (mask > 0)
-            torch.sum(m, dim=0, out=db)
+            # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in]
+            C.gemm_f32(g, x2, dw, False, False)
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
-            # dx[B, in] = dy . W : A = dy [M=B][K=out], B = W stored [K=out][N=in]
-            C.gemm_f32(dy, weight, dx, True, False, mask=mask)
+            # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
+            C.gemm_f32(g, weight, dx, True, False)
         return dx, dw, db, None
 
 
