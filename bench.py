@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--dataset", type=int, default=8192, help="synthetic samples per rank")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
+    ap.add_argument("--eager", action="store_true",
+                    help="tdp: run the step eagerly instead of replaying a captured hipGraph")
     return ap.parse_args()
 
 
@@ -98,6 +100,27 @@ def main():
 
         def loss_fn(out, y):
             return tdp.ops.cross_entropy(out, y, acc=acc)
+
+        # batches are gathered on the device by the sampler's indices (one H2D copy per epoch)
+        idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
+        cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices()}
+
+        def advance():
+            if cur["pos"] + a.batch > len(cur["idx"]):
+                cur["epoch"] += 1
+                sampler.set_epoch(cur["epoch"])
+                cur["idx"], cur["pos"] = loader.epoch_indices(), 0
+            idx_static.copy_(cur["idx"][cur["pos"]: cur["pos"] + a.batch])
+            cur["pos"] += a.batch
+
+        def tdp_step():
+            x = data.x.index_select(0, idx_static)
+            y = data.y.index_select(0, idx_static)
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(ddp(x), y)
+            loss.backward()
+            opt.step()
+            return loss
     else:
         import torch.distributed as dist
         import torch.nn as nn
@@ -175,14 +198,27 @@ def main():
             it[0] = iter(loader)
             return next(it[0])
 
-    def step():
-        x, y = next_batch()
-        opt.zero_grad(set_to_none=True)
-        out = ddp(x)
-        loss = loss_fn(out, y)
-        loss.backward()
-        opt.step()
-        return loss
+    if a.impl == "tdp":
+        advance()
+        run = tdp_step
+        if use_gpu and not a.eager:
+            from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
+
+            run = try_capture(tdp_step, warmup=3,
+                              log=lambda m: print(m, file=sys.stderr, flush=True))
+
+        def step():
+            advance()
+            return run()
+    else:
+        def step():
+            x, y = next_batch()
+            opt.zero_grad(set_to_none=True)
+            out = ddp(x)
+            loss = loss_fn(out, y)
+            loss.backward()
+            opt.step()
+            return loss
 
     for _ in range(a.warmup):
         step()
@@ -227,8 +263,9 @@ def main():
                 "global_batch": a.batch * world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "impl": "tdp (native gfx950 kernels + RCCL reducer)" if a.impl == "tdp"
-                        else "stock torch DDP + torch.optim",
+                "impl": ("tdp (native gfx950 kernels + RCCL reducer" +
+                         (", eager)" if (a.eager or not use_gpu) else ", hipGraph step)"))
+                        if a.impl == "tdp" else "stock torch DDP + torch.optim",
                 "optimizer": a.optim,
                 "final_loss": round(float(loss.item()), 5),
             },

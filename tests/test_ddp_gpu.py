@@ -97,3 +97,47 @@ def test_no_sync_accumulates(pg):
     tdp.ops.cross_entropy(ddp(x), y).backward()
     for p, g in zip(model.parameters(), g1):
         torch.testing.assert_close(p.grad, 2 * g, atol=1e-5, rtol=1e-5)
+
+
+def test_captured_step_matches_eager(pg):
+    """A hipGraph-replayed DDP step (train/graph.py) produces the eager step's results."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    def build():
+        torch.manual_seed(3)
+        m = ToyMLP(in_features=256, hidden=(128, 128), num_classes=10, device="cuda")
+        d = tdp.DDP(m, device_ids=[0])
+        return m, d, tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+
+    X = torch.randn(512, 256, device="cuda")
+    Y = torch.randint(0, 10, (512,), device="cuda")
+    idx = torch.zeros(64, dtype=torch.long, device="cuda")
+
+    def make_step(d, opt):
+        def step():
+            x, y = X.index_select(0, idx), Y.index_select(0, idx)
+            opt.zero_grad(set_to_none=True)
+            loss = tdp.ops.cross_entropy(d(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    m1, d1, o1 = build()
+    m2, d2, o2 = build()
+    eager = make_step(d1, o1)
+    orders = [torch.randperm(512, device="cuda")[:64] for _ in range(8)]
+    # CapturedStep runs 3 warm-up steps + 1 capture step on the current idx
+    idx.copy_(orders[0])
+    for _ in range(4):
+        eager()
+    graph = CapturedStep(make_step(d2, o2), warmup=3)
+    for o in orders[1:]:
+        idx.copy_(o)
+        le = eager()
+        lg = graph.replay()
+        torch.testing.assert_close(lg, le, atol=1e-5, rtol=1e-5)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)

@@ -51,13 +51,18 @@ static ncclDataType_t nccl_dtype(int elem_size) {
 }
 
 void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
+  if (skip_single_rank_ && comm_->world() == 1) {
+    // one rank: the average over ranks is the local gradient -- no collective, no stream hop
+    if (post_bucket) post_bucket(bucket, begin, end, compute);
+    return;
+  }
   hipStream_t cs = comm_->comm_stream();
   check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
   check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
   const int64_t n = end - begin;
-  if (n > 0 && !(skip_single_rank_ && comm_->world() == 1)) {
+  if (n > 0) {
     char* ptr = arena_ + begin * elem_size_;
     if (compression_ == Compression::BF16) {
       uint16_t* w = wire_ + begin;

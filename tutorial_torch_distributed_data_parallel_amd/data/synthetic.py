@@ -58,13 +58,28 @@ class DeviceLoader:
         self.drop_last = drop_last
         self.device = torch.device(device) if device is not None else dataset.device
 
-    def _index_batches(self):
+    def epoch_indices(self) -> torch.Tensor:
+        """The whole epoch's index order as ONE device tensor (one host->device copy per epoch,
+        never a pageable copy per step, which would serialise the CPU with the GPU queue)."""
         if self.batch_sampler is not None:
+            flat = [i for b in self.batch_sampler for i in b]
+        else:
+            flat = list(self.sampler) if self.sampler is not None else \
+                list(range(len(self.dataset)))
+        idx = torch.as_tensor(flat, dtype=torch.long)
+        dev = self.dataset.x.device
+        if dev.type == "cuda":
+            idx = idx.pin_memory().to(dev, non_blocking=True)
+        return idx
+
+    def _index_batches(self):
+        idx = self.epoch_indices()
+        if self.batch_sampler is not None:
+            s = 0
             for b in self.batch_sampler:
-                yield torch.as_tensor(b, dtype=torch.long)
+                yield idx[s: s + len(b)]
+                s += len(b)
             return
-        order = list(self.sampler) if self.sampler is not None else list(range(len(self.dataset)))
-        idx = torch.as_tensor(order, dtype=torch.long)
         n = len(idx)
         stop = n - (n % self.batch_size) if self.drop_last else n
         for s in range(0, stop, self.batch_size):
@@ -73,7 +88,6 @@ class DeviceLoader:
     def __iter__(self):
         x, y = self.dataset.x, self.dataset.y
         for b in self._index_batches():
-            b = b.to(x.device, non_blocking=True)
             xb = x.index_select(0, b)
             yb = y.index_select(0, b)
             if xb.device != self.device:
