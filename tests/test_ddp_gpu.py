@@ -129,9 +129,9 @@ def test_captured_step_matches_eager(pg):
     m2, d2, o2 = build()
     eager = make_step(d1, o1)
     orders = [torch.randperm(512, device="cuda")[:64] for _ in range(8)]
-    # CapturedStep runs 3 warm-up steps + 1 capture step on the current idx
+    # CapturedStep runs 3 real warm-up steps; the capture itself records without executing
     idx.copy_(orders[0])
-    for _ in range(4):
+    for _ in range(3):
         eager()
     graph = CapturedStep(make_step(d2, o2), warmup=3)
     for o in orders[1:]:

@@ -10,7 +10,9 @@ optimizer update -- into a hipGraph once, then each iteration is one graph launc
 Contract (as for torch.cuda.graphs): the captured function reads its varying inputs from static
 tensors the caller refreshes before ``replay`` (here: a device index tensor for the batch);
 hyper-parameters are baked in at capture (re-capture after an LR change); optimizer state and
-gradients live in fixed buffers (the flat arenas), so replay updates them in place.
+gradients live in fixed buffers (the flat arenas), so replay updates them in place. The
+``warmup`` steps really execute; the capturing call only records (it does not advance the
+model), so after construction the model has taken exactly ``warmup`` steps.
 """
 from __future__ import annotations
 
