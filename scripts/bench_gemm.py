@@ -42,6 +42,14 @@ def timeit(fn, reps=20):
     return ev[0].elapsed_time(ev[1]) / reps * 1000.0  # us
 
 
+SWEEP = {  # (fn, splits, stages) variants of the fast kernel to compare per shape
+    "fc1_fwd": [(1, 4, 3), (1, 8, 3), (1, 8, 2), (2, 8, 2), (2, 16, 2), (1, 16, 3)],
+    "fc2_fwd": [(1, 4, 3), (1, 8, 3), (2, 8, 2), (1, 16, 2)],
+    "fc2_dgrad": [(1, 4, 3), (1, 8, 3), (2, 8, 2), (2, 16, 2)],
+    "fc1_wgrad": [(2, 1, 2), (2, 1, 3), (1, 1, 2)],
+    "fc2_wgrad": [(2, 1, 2), (1, 1, 2)],
+}
+
 res = {}
 for name, M, N, K, ak, bk in SHAPES:
     A, B, out = mk(M, N, K, ak, bk)
@@ -59,6 +67,14 @@ for name, M, N, K, ak, bk in SHAPES:
                     C.gemm_f32_set_mode(0)
             us = timeit(f)
             row.setdefault(impl, []).append(us)
+    for v in SWEEP.get(name, []):
+        A2, B2, out2 = A, B, out
+        C.gemm_f32_set_override(*v)
+        try:
+            us = min(timeit(lambda: C.gemm_f32(A2, B2, out2, ak, bk)) for _ in range(3))
+        finally:
+            C.gemm_f32_set_override(0, 0, 0)
+        row[f"fn{v[0]}_s{v[1]}_st{v[2]}_us"] = round(us, 1)
     for impl in ("fast", "generic", "torch"):
         us = min(row[impl])
         row[impl + "_us"] = round(us, 1)

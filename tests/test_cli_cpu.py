@@ -1,0 +1,63 @@
+"""Entry points end to end on CPU/gloo: YAML handling, spawn, checkpoints, HTCondor writer."""
+import os
+import subprocess
+import sys
+
+import torch
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _settings(tmp_path, **train):
+    s = {"script_path": os.path.join(ROOT, "scripts", "train_ddp.py"),
+         "out_dir": str(tmp_path / "out"),
+         "optional_args": {"set_epoch": True, "print_rand": True},
+         "local": {"device": "cuda", "condor": {"bid": 50, "num_cpus": 2, "memory_cpus": 1000,
+                                                "num_gpus": 2, "memory_gpus": 60000}},
+         "train": dict(model="toy_mlp", n_train=64, n_test=20, train_batch_size=8,
+                       test_batch_size=10, num_epochs=2, checkpoint_epoch=1, lr=1e-3,
+                       max_steps_per_epoch=2, **train)}
+    p = tmp_path / "local_settings.yaml"
+    p.write_text(yaml.safe_dump(s))
+    return p, s
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, *args], capture_output=True, text=True, env=env,
+                          timeout=timeout, cwd=ROOT)
+
+
+def test_train_ddp_two_ranks(tmp_path):
+    p, s = _settings(tmp_path)
+    r = _run([os.path.join(ROOT, "scripts", "train_ddp.py"), "--settings_file", str(p)])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = s["out_dir"]
+    assert os.path.exists(os.path.join(out, "local_settings.yaml"))  # YAML copied (R10)
+    assert os.path.exists(os.path.join(out, "ckpt_0.pt")) and os.path.exists(
+        os.path.join(out, "ckpt_1.pt"))
+    sd = torch.load(os.path.join(out, "ckpt_1.pt"), map_location="cpu", weights_only=True)
+    assert all(k.startswith("module.") for k in sd)
+    assert "Epoch 2/2, Train Loss:" in r.stdout
+    assert r.stdout.count("Epoch 2/2, Train Loss:") == 1  # rank 0 only
+    assert "Python random state" in r.stdout  # print_rand
+
+
+def test_train_accelerate_single_process(tmp_path):
+    p, s = _settings(tmp_path)
+    r = _run([os.path.join(ROOT, "scripts", "train_accelerate.py"), "--settings_file", str(p)])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert os.path.exists(os.path.join(s["out_dir"], "model.safetensors"))
+    assert "Finished Training." in r.stdout
+
+
+def test_launch_writes_condor_file(tmp_path):
+    p, s = _settings(tmp_path)
+    r = _run([os.path.join(ROOT, "scripts", "launch.py"), "--settings_file", str(p),
+              "--write-condor"])
+    assert r.returncode == 0, r.stderr
+    sub = open(os.path.join(s["out_dir"], "submission_file.sub")).read()
+    assert "request_gpus = 2" in sub and "TARGET.CUDAGlobalMemoryMb > 60000" in sub
+    assert sub.strip().endswith("queue")

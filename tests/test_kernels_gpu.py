@@ -242,3 +242,16 @@ def test_relu_bias_bwd(C):
         g2 = C.relu_bias_bwd(dy, None, db2)
         assert g2.data_ptr() == dy.data_ptr()
         _close(db2, dy.sum(0), atol=1e-4)
+
+
+def test_gemm_fast_wgrad_rowsum(C):
+    """Bias gradient reduced inside the LDS-DMA wgrad kernel (A = g^T, MN-contiguous)."""
+    torch.manual_seed(11)
+    for B, out_f, in_f in [(128, 256, 384), (64, 132, 200), (128, 4096, 256)]:
+        g = torch.randn(B, out_f, device="cuda")
+        x = torch.randn(B, in_f, device="cuda")
+        dw = torch.empty(out_f, in_f, device="cuda")
+        db = torch.full((out_f,), 7.0, device="cuda")
+        C.gemm_f32(g, x, dw, False, False, rowsum=db)
+        _close(dw, (g.t().double() @ x.double()).float(), atol=2e-3)
+        _close(db, g.sum(0), atol=1e-3)

@@ -35,12 +35,13 @@ struct FastParams {
   const float* B;
   float* C;
   const float* bias;
+  float* rowsum;  // optional [M]: sum over K of A (bias gradient), only with an MN-contig A
   float* ws;
   long lda, ldb, ldc;
   int M, N, K;
   int k_per_split, splits;
   int tiles_n, tiles_m;
-  float beta;
+  float beta, rowsum_beta;
   int relu;
 };
 
@@ -59,42 +60,64 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Issue this wave's share of one K tile: a K-contiguous [R][32] tile or an MN-contiguous
-// [32][C] tile; `chunks` 1-KiB pieces split over the 4 waves.
-template <int R>
-__device__ __forceinline__ void issue_kc(const float* g, long ld, int r0, int rlim, int k0,
-                                         int klim, lds_char* dst, int wid, int lane) {
-  constexpr int CH = R / 8;  // 1-KiB chunks (8 rows of 128 B)
-#pragma unroll
-  for (int i = 0; i < CH / 4; ++i) {
-    const int j = wid * (CH / 4) + i;
-    const int row = j * 8 + (lane >> 3);
-    const int kc = (lane & 7) ^ (row & 7);
-    int gr = r0 + row;
-    gr = gr < rlim ? gr : rlim - 1;
-    int gk = k0 + kc * 4;
-    gk = gk < klim ? gk : klim - 4;
-    glds16(g + (long)gr * ld + gk, dst + j * 1024);
-  }
-}
+// Row swizzle of K-contiguous tiles: slot(row, chunk) = chunk ^ swz(row). XOR-ing in row bits 3-5
+// makes every 16-lane group of a ds_read_b128 (rows r..r+31 of one fragment) hit 16 distinct
+// (row parity, slot) pairs = all 64 banks: conflict-free (plain `row & 7` left a 2-way conflict,
+// SQ_LDS_BANK_CONFLICT = 4 cycles per read in the first profile).
+__device__ __forceinline__ int swz(int row) { return (row ^ (row >> 3)) & 7; }
 
-template <int C>
-__device__ __forceinline__ void issue_mn(const float* g, long ld, int c0, int clim, int k0,
-                                         int klim, lds_char* dst, int wid, int lane) {
-  constexpr int ROWS_PER = 1024 / (C * 4);  // rows per 1-KiB chunk
-  constexpr int CH = kBK / ROWS_PER;
-  constexpr int LPR = C / 4;                // lanes per row
+// Per-lane source pointers of one operand's share of a K tile, computed once per workgroup:
+// only the k offset changes from tile to tile (clamped on the K tail).
+template <int R, bool KC>
+struct TileSrc {
+  // K-contiguous [R][32] tile: CH = R/8 1-KiB chunks, CH/4 per wave
+  // MN-contiguous [32][R] tile: CH = 32*R*4/1024 chunks, CH/4 per wave
+  static constexpr int CH = KC ? R / 8 : (32 * R * 4) / 1024;
+  static constexpr int NPW = CH / 4;
+  const float* base[NPW];
+  int koff[NPW];  // K-contig: k offset of the lane's 16-B chunk; MN: row (k) within the tile
+  long ld;
+
+  __device__ __forceinline__ void init(const float* g, long ld_, int r0, int rlim, int wid,
+                                       int lane) {
+    ld = ld_;
 #pragma unroll
-  for (int i = 0; i < CH / 4; ++i) {
-    const int j = wid * (CH / 4) + i;
-    const int row = j * ROWS_PER + lane / LPR;
-    int gk = k0 + row;
-    gk = gk < klim ? gk : klim - 1;
-    int gc = c0 + (lane % LPR) * 4;
-    gc = gc < clim ? gc : clim - 4;
-    glds16(g + (long)gk * ld + gc, dst + j * 1024);
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      if (KC) {
+        const int row = j * 8 + (lane >> 3);
+        int gr = r0 + row;
+        gr = gr < rlim ? gr : rlim - 1;
+        base[i] = g + (long)gr * ld;
+        koff[i] = ((lane & 7) ^ swz(row)) * 4;
+      } else {
+        constexpr int LPR = R / 4;                 // lanes per 512-B row
+        constexpr int RPC = 1024 / (R * 4);        // rows per chunk
+        const int row = j * RPC + lane / LPR;
+        int gc = r0 + (lane % LPR) * 4;
+        gc = gc < rlim ? gc : rlim - 4;
+        base[i] = g + gc;
+        koff[i] = row;
+      }
+    }
   }
-}
+
+  __device__ __forceinline__ void issue(int k0, int klim, char* dst, int wid) const {
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      if (KC) {
+        int gk = k0 + koff[i];
+        gk = gk < klim ? gk : klim - 4;
+        glds16(base[i] + gk, dst + j * 1024);
+      } else {
+        int gk = k0 + koff[i];
+        gk = gk < klim ? gk : klim - 1;
+        glds16(base[i] + (long)gk * ld, dst + j * 1024);
+      }
+    }
+  }
+};
 
 template <int FN, bool AK, bool BKC, int S>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
@@ -104,7 +127,6 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   constexpr int STG = A_BYTES + B_BYTES;
   constexpr int GA = A_BYTES / 1024 / 4, GB = B_BYTES / 1024 / 4;  // glds per wave per tile
   constexpr int G = GA + GB;
-  static_assert(BKC || FN == 2, "an MN-contiguous B operand needs FN == 2 (interleaved tiles)");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
 
@@ -128,13 +150,15 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   const int ke = min(p.K, kb + p.k_per_split);
   const int nk = (ke - kb + kBK - 1) / kBK;
 
+  TileSrc<BM, AK> srcA;
+  TileSrc<BN, BKC> srcB;
+  srcA.init(p.A, p.lda, m0, p.M, wid, lane);
+  srcB.init(p.B, p.ldb, n0, p.N, wid, lane);
   auto issue = [&](int t) {
     lds_char* st = smem + (t % S) * STG;
     const int k0 = kb + t * kBK;
-    if (AK) issue_kc<BM>(p.A, p.lda, m0, p.M, k0, ke, st, wid, lane);
-    else issue_mn<BM>(p.A, p.lda, m0, p.M, k0, ke, st, wid, lane);
-    if (BKC) issue_kc<BN>(p.B, p.ldb, n0, p.N, k0, ke, st + A_BYTES, wid, lane);
-    else issue_mn<BN>(p.B, p.ldb, n0, p.N, k0, ke, st + A_BYTES, wid, lane);
+    srcA.issue(k0, ke, st, wid);
+    srcB.issue(k0, ke, st + A_BYTES, wid);
   };
 
   f32x16 acc[FM][FN];
@@ -159,7 +183,10 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
 #pragma unroll
   for (int g = 0; g < FN; ++g) {
     const int row = wn * (32 * FN) + g * 32 + l31;
-    b_off[g] = BKC ? A_BYTES + row * 128 : A_BYTES + (wn * 64 + 2 * l31) * 4;
+    // MN-contiguous B: FN == 2 interleaves the two tiles' columns (ds_read_b64), FN == 1 reads
+    // the wave's 32 columns directly (ds_read_b32)
+    b_off[g] = BKC ? A_BYTES + row * 128
+                   : A_BYTES + (FN == 2 ? (wn * 64 + 2 * l31) * 4 : (wn * 32 + l31) * 4);
   }
 
   // fragment registers: value of tile f at k-step s of one q
@@ -169,7 +196,7 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int row = wm * 64 + f * 32 + l31;
-        const int slot = (2 * q + h) ^ (row & 7);
+        const int slot = (2 * q + h) ^ swz(row);
         const f32x4 v = *reinterpret_cast<const f32x4*>(st + a_off[f] + slot * 16);
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[f][s] = v[s];
@@ -187,28 +214,42 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
 #pragma unroll
       for (int g = 0; g < FN; ++g) {
         const int row = wn * (32 * FN) + g * 32 + l31;
-        const int slot = (2 * q + h) ^ (row & 7);
+        const int slot = (2 * q + h) ^ swz(row);
         const f32x4 v = *reinterpret_cast<const f32x4*>(st + b_off[g] + slot * 16);
 #pragma unroll
         for (int s = 0; s < 4; ++s) bb[g][s] = v[s];
       }
-    } else {
+    } else if (FN == 2) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int k = 8 * q + 4 * h + s;
         const f32x2 v = *reinterpret_cast<const f32x2*>(st + k * (BN * 4) + b_off[0]);
         bb[0][s] = v[0];
-        bb[1][s] = v[1];
+        bb[FN - 1][s] = v[1];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 8 * q + 4 * h + s;
+        bb[0][s] = *reinterpret_cast<const float*>(st + k * (BN * 4) + b_off[0]);
       }
     }
   };
 
+  // bias gradient: the workgroups of the first column tile also sum their A tiles over K
+  const bool do_rs = !AK && p.rowsum != nullptr && tn == 0;
+  float rs = 0.f;
   for (int kt = 0; kt < nk; ++kt) {
     wait_vmcnt<(S - 2) * G>();
     __builtin_amdgcn_s_barrier();
     issue(kt + S - 1);  // refill the stage every wave finished reading (kt - 1)
     const lds_char* st = smem + (kt % S) * STG;
     const int kvalid = ke - (kb + kt * kBK);  // < 32 only on the K tail
+    if (do_rs && threadIdx.x < BM) {
+      const int kmax = kvalid < kBK ? kvalid : kBK;
+      for (int k = 0; k < kmax; ++k)
+        rs += *reinterpret_cast<const float*>(st + k * (BM * 4) + threadIdx.x * 4);
+    }
     read_frag(st, 0, av[0], bv[0]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -237,6 +278,10 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
     }
   }
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+  if (do_rs && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
+    float* d = p.rowsum + m0 + threadIdx.x;
+    *d = (p.rowsum_beta != 0.f ? p.rowsum_beta * *d : 0.f) + rs;
+  }
 
   // epilogue
   const bool split = p.splits > 1;
@@ -250,7 +295,7 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
       const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
       if (row >= p.M) continue;
       float* orow = out + (long)row * ldo;
-      if (BKC) {
+      if (BKC || FN == 1) {
 #pragma unroll
         for (int g = 0; g < FN; ++g) {
           const int col = n0 + wn * (32 * FN) + g * 32 + l31;
@@ -265,7 +310,7 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
         }
       } else {
         const int col = n0 + wn * 64 + 2 * l31;  // (g=0, g=1) are adjacent columns
-        f32x2 v = {acc[f][0][r], acc[f][1][r]};
+        f32x2 v = {acc[f][0][r], acc[f][FN - 1][r]};
         if (col + 1 < p.N) {
           if (!split) {
             if (p.bias) { v[0] += p.bias[col]; v[1] += p.bias[col + 1]; }
@@ -308,7 +353,8 @@ void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
 
 bool gemm_f32_fast_ok(const GemmF32Args& a) {
   auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-  if (a.mask || a.rowsum) return false;
+  if (a.mask) return false;
+  if (a.rowsum && a.a_kcontig) return false;  // row sums are taken from the [k][m] A tile
   if (!al(a.A) || !al(a.B) || a.lda % 4 || a.ldb % 4) return false;
   if (a.K < 4 || a.K % 4) return false;
   if (!a.a_kcontig && a.M % 4) return false;
@@ -317,19 +363,30 @@ bool gemm_f32_fast_ok(const GemmF32Args& a) {
   return true;
 }
 
-// Plan: FN (tile width), stages and split-K so that the grid covers the chip.
+// Plan: tile width (FN), split-K and pipeline depth so that every CU runs TWO workgroups (two
+// waves per SIMD: one wave's barrier / LDS latency hides behind the other's MFMAs -- the first
+// PMC profile showed 53 % MFMA-busy at one workgroup per CU) while keeping >= 8 K steps per split.
+// LDS per workgroup must stay <= 80 KiB for two per CU: FN=1 (24 KiB/stage) allows 3 stages,
+// FN=2 (32 KiB/stage) 2 stages.
+static int o_fn = 0, o_splits = 0, o_stages = 0;
+void gemm_f32_set_override(int fn, int splits, int stages) {
+  o_fn = fn; o_splits = splits; o_stages = stages;
+}
+
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
-  const bool b_mn = !a.b_kcontig;
-  int fn = b_mn ? 2 : (a.N >= 2048 && a.M >= 512 ? 2 : 1);
+  int fn = (a.M >= 512 && a.N >= 512) ? 2 : 1;
+  if (o_fn == 1 || o_fn == 2) fn = o_fn;
   const int bn = 64 * fn;
   const long tiles = (long)ceil_div(a.M, 128) * ceil_div(a.N, bn);
+  const long target = 2L * num_cus;
   int splits = 1;
-  if (tiles < num_cus) {
-    const int want = (int)((num_cus + tiles - 1) / tiles);
-    const int kmax = a.K / (kBK * 8);  // keep >= 8 K steps per split
+  if (tiles < target && a.rowsum == nullptr) {
+    const int want = (int)((target + tiles - 1) / tiles);
+    const int kmax = a.K / (kBK * 8);
     splits = want < kmax ? want : kmax;
     if (splits < 1) splits = 1;
   }
+  if (o_splits > 0 && a.rowsum == nullptr) splits = o_splits;
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
   plan.bm = 128;
@@ -338,15 +395,15 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   plan.k_per_split = kps;
   plan.splits = ceil_div(a.K, kps);
   plan.ws_floats = plan.splits > 1 ? (long)plan.splits * a.M * a.N : 0;
-  // short K (few tiles per block): 2 stages -> 2 workgroups per CU hide prologue/epilogue;
-  // long K: deeper pipeline at one workgroup per CU.
   const int nk = ceil_div(kps, kBK);
-  plan.stages = (nk <= 8) ? 2 : 4;
+  plan.stages = (fn == 1 && nk > 4) ? 3 : 2;
+  if (o_stages == 2 || o_stages == 3) plan.stages = o_stages;
 }
 
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   FastParams p;
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
+  p.rowsum = a.rowsum; p.rowsum_beta = a.rowsum_beta;
   p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
   p.M = a.M; p.N = a.N; p.K = a.K;
   p.k_per_split = plan.k_per_split;
@@ -360,16 +417,14 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   const int fn = plan.tile;
 #define TDP_L(FN, AK, BK, S) launch_fast<FN, AK, BK, S>(p, nblocks, s)
 #define TDP_S(FN, AK, BK) \
-  do { if (plan.stages == 2) TDP_L(FN, AK, BK, 2); else TDP_L(FN, AK, BK, 4); } while (0)
-  if (ak && bk) {
-    if (fn == 1) TDP_S(1, true, true); else TDP_S(2, true, true);
-  } else if (ak && !bk) {
-    TDP_S(2, true, false);
-  } else if (!ak && !bk) {
-    TDP_S(2, false, false);
-  } else {
-    if (fn == 1) TDP_S(1, false, true); else TDP_S(2, false, true);
-  }
+  do { if (plan.stages == 3) TDP_L(FN, AK, BK, 3); else TDP_L(FN, AK, BK, 2); } while (0)
+#define TDP_F(AK, BK) \
+  do { if (fn == 1) TDP_S(1, AK, BK); else TDP_S(2, AK, BK); } while (0)
+  if (ak && bk) TDP_F(true, true);
+  else if (ak && !bk) TDP_F(true, false);
+  else if (!ak && !bk) TDP_F(false, false);
+  else TDP_F(false, true);
+#undef TDP_F
 #undef TDP_S
 #undef TDP_L
   if (plan.splits > 1)

@@ -48,6 +48,8 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
 // set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel
 void gemm_f32_set_mode(int mode);
+// benchmarking knob: force the fast kernel's tile width / split-K / stages (0 = planner's choice)
+void gemm_f32_set_override(int fn, int splits, int stages);
 
 // bf16-operand GEMM (AMP path): same contract, A/B bf16 (uint16 storage), C fp32 or bf16.
 struct GemmBF16Args {

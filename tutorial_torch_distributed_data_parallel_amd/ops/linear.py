@@ -3,10 +3,10 @@
 Forward, input-gradient and weight-gradient are each ONE kernel (plus a split-K combine when the
 tile grid alone cannot fill 256 CUs):
   * forward  ``y = relu(x W^T + b)``: bias and ReLU in the GEMM epilogue (SURVEY.md §2.5 K12/K2);
-  * backward: one pass applies the ReLU mask ``y > 0`` to ``dy`` and reduces the bias gradient
-    (K17/K18, ``relu_bias_bwd``); the weight- and input-gradient GEMMs then read that masked
-    gradient through their LDS-DMA pipelines, and the weight gradient lands directly in the DDP
-    gradient arena (K23, see ``_grad.py``).
+  * backward: one pass applies the ReLU mask ``y > 0`` to ``dy`` (K18, ``relu_bias_bwd``); the
+    weight-gradient GEMM also reduces the bias gradient from its staged A tiles (K17), both
+    GEMMs read the masked gradient through their LDS-DMA pipelines, and the weight gradient lands
+    directly in the DDP gradient arena (K23, see ``_grad.py``).
 On CPU the same math runs through ``torch.nn.functional`` (the reference implementation used by
 the gloo/CPU tests). Reference behaviour: torchvision AlexNet's classifier Linear/ReLU layers
 (REF/data_and_toy_model.py:41-45).
@@ -41,12 +41,15 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
-        # g = dy * (y > 0) and db = sum_rows(g) in one pass (g is dy itself without ReLU)
-        g = C.relu_bias_bwd(dy, y if ctx.relu else None, db) if (ctx.relu or want_db) else dy
+        # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU)
+        g = C.relu_bias_bwd(dy, y) if ctx.relu else dy
         if needs(ctx, 1):
             dw = grad_dest(w_param)
-            # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in]
-            C.gemm_f32(g, x2, dw, False, False)
+            # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];
+            # the bias gradient (sum over the batch of g) is reduced inside the same kernel
+            C.gemm_f32(g, x2, dw, False, False, rowsum=db)
+        elif want_db:
+            C.relu_bias_bwd(g, None, db)
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
