@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--eager", action="store_true",
                     help="tdp: run the step eagerly instead of replaying a captured hipGraph")
+    ap.add_argument("--no-fused-opt", action="store_true",
+                    help="tdp: run optimizer.step() after backward instead of applying the "
+                         "optimizer per gradient bucket inside the reduction")
     return ap.parse_args()
 
 
@@ -91,6 +94,9 @@ def main():
             opt = tdp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
         else:
             opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
+        fused = False
+        if use_gpu and not a.no_fused_opt:
+            fused = ddp.register_fused_optimizer(opt)
         data = SyntheticDataset(a.dataset, (9216,), 10, seed=rank, device=dev)
         sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
         loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
@@ -266,7 +272,9 @@ def main():
                 "impl": ("tdp (native gfx950 kernels + RCCL reducer" +
                          (", eager)" if (a.eager or not use_gpu) else ", hipGraph step)"))
                         if a.impl == "tdp" else "stock torch DDP + torch.optim",
-                "optimizer": a.optim,
+                "optimizer": a.optim + (" (fused into the bucket reduction)"
+                                        if a.impl == "tdp" and use_gpu and not a.no_fused_opt
+                                        else ""),
                 "final_loss": round(float(loss.item()), 5),
             },
         }

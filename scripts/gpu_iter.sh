@@ -1,14 +1,15 @@
 #!/bin/bash
-# Iteration call: GPU tests, GEMM microbench, flagship bench + kernel profile of our path.
+# Iteration call: GPU tests, GEMM microbench, flagship bench variants + kernel profile.
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-100}
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps $STEPS --warmup 20 > gpurun_out/bench_tdp.json 2> gpurun_out/bench_tdp.err && \
+timeout -k 10 300 python bench.py --steps $STEPS --warmup 20 --no-fused-opt > gpurun_out/bench_tdp_nofuse.json 2> gpurun_out/bench_tdp_nofuse.err && \
+timeout -k 10 300 python bench.py --steps $STEPS --warmup 20 --eager > gpurun_out/bench_tdp_eager.json 2> gpurun_out/bench_tdp_eager.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_tdp -o run -- python3 bench.py --steps 30 --warmup 10 > gpurun_out/prof_tdp.log 2>&1
 rc=$?
-tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/bench_gemm.log gpurun_out/bench_tdp.json 2>/dev/null
+tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/bench_tdp*.json 2>/dev/null
 exit $rc

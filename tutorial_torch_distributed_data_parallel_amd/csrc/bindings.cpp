@@ -510,7 +510,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            }),
            py::arg("comm"), py::arg("arena"), py::arg("num_buckets"),
            py::arg("compression") = 0, py::arg("timing") = false,
-           py::arg("skip_single_rank") = true);
+           py::arg("skip_single_rank") = true)
+      // fused optimizer: kind 1 = SGD(p, momentum_buf), 2 = Adam(p, exp_avg, exp_avg_sq[, max])
+      .def("set_fused_sgd",
+           [](RcclBackend& b, Tensor p, c10::optional<Tensor> buf, double lr, double momentum,
+              double dampening, double wd, bool nesterov, bool maximize, bool fresh) {
+             CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
+             b.fused.kind = 1;
+             b.fused.p = p.data_ptr<float>();
+             b.fused.s0 = fptr(buf);
+             b.fused.sgd = SgdHyper{(float)lr, (float)momentum, (float)dampening, (float)wd,
+                                    nesterov, maximize, false, 1.f};
+             if (fresh) b.fused.fresh.assign(1 << 16, 1);
+           })
+      .def("set_fused_adam",
+           [](RcclBackend& b, Tensor p, Tensor m, Tensor v, c10::optional<Tensor> vmax,
+              double lr, double b1, double b2, double eps, double wd, bool amsgrad,
+              bool maximize, bool decoupled, int64_t step) {
+             CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
+             b.fused.kind = 2;
+             b.fused.p = p.data_ptr<float>();
+             b.fused.s0 = m.data_ptr<float>();
+             b.fused.s1 = v.data_ptr<float>();
+             b.fused.s2 = fptr(vmax);
+             b.fused.adam = AdamHyper{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                                      amsgrad, maximize, decoupled, 1.f, 1.f, 1.f};
+             b.fused.adam_beta1 = (float)b1;
+             b.fused.adam_beta2 = (float)b2;
+             b.fused.adam_step = step;
+           })
+      .def("clear_fused", [](RcclBackend& b) { b.fused = FusedOptimizer{}; })
+      .def_property_readonly("fused_adam_step",
+                             [](RcclBackend& b) { return b.fused.adam_step; });
   py::class_<PyBackend, ReducerBackend, std::shared_ptr<PyBackend>>(m, "PyBackend")
       .def(py::init<py::function, py::function, py::function>());
 

@@ -1,6 +1,7 @@
 #include "reducer.h"
 
 #include <algorithm>
+#include <cmath>
 #include <stdexcept>
 
 #include "kernels.h"
@@ -51,7 +52,8 @@ static ncclDataType_t nccl_dtype(int elem_size) {
 }
 
 void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
-  if (skip_single_rank_ && comm_->world() == 1) {
+  const bool collective = !(skip_single_rank_ && comm_->world() == 1);
+  if (!collective && fused.kind == 0) {
     // one rank: the average over ranks is the local gradient -- no collective, no stream hop
     if (post_bucket) post_bucket(bucket, begin, end, compute);
     return;
@@ -62,7 +64,7 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
   const int64_t n = end - begin;
-  if (n > 0) {
+  if (n > 0 && collective) {
     char* ptr = arena_ + begin * elem_size_;
     if (compression_ == Compression::BF16) {
       uint16_t* w = wire_ + begin;
@@ -72,6 +74,21 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
     } else {
       comm_->all_reduce(ptr, ptr, (size_t)n, nccl_dtype(elem_size_), ncclAvg, cs);
     }
+  }
+  if (n > 0 && fused.kind == 1) {
+    SgdHyper h = fused.sgd;
+    h.first_step = fused.fresh.empty() ? false : (bool)fused.fresh[bucket];
+    if (!fused.fresh.empty()) fused.fresh[bucket] = 0;
+    sgd_flat(fused.p + begin, reinterpret_cast<float*>(arena_) + begin,
+             fused.s0 ? fused.s0 + begin : nullptr, n, h, cs);
+  } else if (n > 0 && fused.kind == 2) {
+    if (bucket == 0) ++fused.adam_step;
+    AdamHyper h = fused.adam;
+    const double t = (double)(fused.adam_step > 0 ? fused.adam_step : 1);
+    h.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
+    h.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
+    adam_flat(fused.p + begin, reinterpret_cast<float*>(arena_) + begin, fused.s0 + begin,
+              fused.s1 + begin, fused.s2 ? fused.s2 + begin : nullptr, n, h, cs);
   }
   if (post_bucket) post_bucket(bucket, begin, end, cs);
 }

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "comm.h"
+#include "kernels.h"
 
 namespace tdp {
 
@@ -44,6 +45,24 @@ struct ReducerBackend {
 // bf16 on the comm stream, all-reduces that and casts back (torch's bf16_compress_hook).
 enum class Compression : int { NONE = 0, BF16 = 1 };
 
+// Optimizer update fused into the reduction (torch's DDP._register_fused_optim idea): as soon as a
+// bucket's averaged gradient exists, its slice of the parameter arena is updated on the comm
+// stream, overlapping the update of early buckets with the backward compute / all-reduce of
+// later ones. Parameters, gradients and optimizer state share the arena layout, so a bucket's
+// update is the flat kernel on [begin, end) of every buffer.
+struct FusedOptimizer {
+  int kind = 0;  // 0 none, 1 SGD, 2 Adam
+  float* p = nullptr;
+  float* s0 = nullptr;  // momentum buffer / exp_avg
+  float* s1 = nullptr;  // exp_avg_sq
+  float* s2 = nullptr;  // max_exp_avg_sq
+  SgdHyper sgd{};
+  AdamHyper adam{};
+  float adam_beta1 = 0.9f, adam_beta2 = 0.999f;
+  int64_t adam_step = 0;       // incremented when the first bucket of an iteration updates
+  std::vector<char> fresh;     // per bucket: SGD momentum not yet initialised
+};
+
 class RcclBackend : public ReducerBackend {
  public:
   RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_t numel, int elem_size,
@@ -55,6 +74,7 @@ class RcclBackend : public ReducerBackend {
   double last_comm_ms() override;
   // called after a bucket's all-reduce is enqueued, with the comm stream (fused optimizer hook)
   std::function<void(int, int64_t, int64_t, hipStream_t)> post_bucket;
+  FusedOptimizer fused;
 
  private:
   std::shared_ptr<Communicator> comm_;

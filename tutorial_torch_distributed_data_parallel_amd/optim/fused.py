@@ -69,9 +69,31 @@ class _FusedBase(Optimizer):
         super().load_state_dict(state_dict)
         self._flat_bufs = {}  # re-adopted into flat buffers on the next step
         self._flat_step = {}
+        ddp = getattr(self, "_fused_ddp", None)
+        if ddp is not None:
+            ddp.push_fused_hyper(self, initial=True)
+
+    def _fused_step(self) -> bool:
+        """When a DDP model applies this optimizer inside its reduction, step() only refreshes
+        the hyper-parameters (e.g. after an LR-scheduler change) for the next iteration."""
+        ddp = getattr(self, "_fused_ddp", None)
+        if ddp is None:
+            return False
+        ddp.push_fused_hyper(self)
+        return True
+
+    def _current_flat_step(self, arena) -> int:
+        if id(arena) in self._flat_step:
+            return self._flat_step[id(arena)]
+        steps = {int(self.state[p]["step"].item()) if torch.is_tensor(self.state[p].get("step"))
+                 else int(self.state[p].get("step") or 0) for p in arena.params}
+        return max(steps) if steps else 0
 
     def state_dict(self):
         # materialise the shared flat step counter into torch's per-parameter "step" entries
+        ddp = getattr(self, "_fused_ddp", None)
+        if ddp is not None and self.__class__.__name__ != "SGD":
+            self._flat_step[id(ddp.arena)] = int(ddp._backend.fused_adam_step)
         for g in self.param_groups:
             a = arena_of(g["params"])
             if a is not None and id(a) in self._flat_step:
@@ -99,6 +121,8 @@ class SGD(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._fused_step():
+            return loss
         for g in self.param_groups:
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:
@@ -187,6 +211,8 @@ class Adam(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._fused_step():
+            return loss
         for g in self.param_groups:
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:

@@ -117,6 +117,7 @@ class DistributedDataParallel(nn.Module):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self._callback_queued = False
         self._iter = 0
+        self._fused_opt = None
 
     # --------------------------------------------------------------------------- reducer
     def _build_reducer(self):
@@ -184,6 +185,58 @@ class DistributedDataParallel(nn.Module):
         finally:
             self.require_backward_grad_sync = old
 
+    # --------------------------------------------------------------------------- fused optimizer
+    def register_fused_optimizer(self, optimizer) -> bool:
+        """Apply ``optimizer`` bucket by bucket inside the reduction (torch's
+        ``DDP._register_fused_optim``): each bucket's parameters are updated on the comm stream
+        right after its gradient is averaged, overlapping the update with the rest of backward
+        and with later buckets' all-reduces. ``optimizer.step()`` then only refreshes the
+        hyper-parameters for the next iteration. Requires a tdp SGD/Adam over exactly this DDP's
+        parameters (one param group). Returns False (optimizer left unfused) on CPU.
+        """
+        from ..optim.fused import SGD, Adam
+
+        if not self._gpu:
+            return False
+        if self.find_unused_parameters:
+            raise ValueError("a fused optimizer needs every parameter to get a gradient")
+        if len(optimizer.param_groups) != 1:
+            raise ValueError("fused optimizer: exactly one parameter group is supported")
+        params = optimizer.param_groups[0]["params"]
+        if {id(p) for p in params} != {id(p) for p in self.arena.params}:
+            raise ValueError("fused optimizer must own exactly the DDP model's parameters")
+        if not isinstance(optimizer, (SGD, Adam)):
+            raise TypeError("fused optimizer must be tdp.optim.SGD / Adam / AdamW")
+        self._fused_opt = optimizer
+        optimizer._fused_ddp = self
+        self.push_fused_hyper(optimizer, initial=True)
+        return True
+
+    def push_fused_hyper(self, opt, initial: bool = False):
+        from ..optim.fused import SGD
+
+        g = opt.param_groups[0]
+        a = self.arena
+        if isinstance(opt, SGD):
+            buf, fresh = None, False
+            if g["momentum"] != 0:
+                # fresh == the momentum buffers were just created: each bucket's first update
+                # initialises them with the gradient (torch: buf = clone(grad))
+                bufs, fresh = opt._flat_state(a, ("momentum_buffer",))
+                buf = bufs["momentum_buffer"]
+            self._backend.set_fused_sgd(a.data, buf, g["lr"], g["momentum"], g["dampening"],
+                                        g["weight_decay"], g["nesterov"], g["maximize"],
+                                        bool(fresh) and initial)
+        else:
+            keys = opt._keys(g)
+            bufs, _ = opt._flat_state(a, keys)
+            step = opt._current_flat_step(a) if initial else self._backend.fused_adam_step
+            b1, b2 = g["betas"]
+            self._backend.set_fused_adam(a.data, bufs["exp_avg"], bufs["exp_avg_sq"],
+                                         bufs.get("max_exp_avg_sq"), g["lr"], b1, b2, g["eps"],
+                                         g["weight_decay"], g["amsgrad"], g["maximize"],
+                                         opt._decoupled, int(step))
+
     def register_comm_hook(self, state, hook):
         """Gradient compression hooks: torch's bf16_compress_hook (or the string "bf16")."""
         name = hook if isinstance(hook, str) else getattr(hook, "__name__", "")
@@ -195,6 +248,8 @@ class DistributedDataParallel(nn.Module):
             raise NotImplementedError(f"comm hook {name!r} is not supported (bf16 | fp32)")
         if self._gpu:
             self._build_reducer()
+            if self._fused_opt is not None:
+                self.push_fused_hyper(self._fused_opt, initial=False)
 
     # --------------------------------------------------------------------------- logging
     def _get_ddp_logging_data(self) -> dict:
