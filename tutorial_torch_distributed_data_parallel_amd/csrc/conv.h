@@ -1,0 +1,33 @@
+// Implicit-GEMM convolution API (see conv.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tdp {
+
+constexpr int kConvFwd = 0, kConvDgrad = 1, kConvWgrad = 2;
+
+// x: [N][C][H][W], w: [Cout][C][R][S], y: [N][Cout][P][Q]
+struct ConvGeom {
+  int N, C, H, W, Cout, R, S, P, Q, sh, sw, ph, pw;
+};
+
+struct ConvPlan {
+  int mode = 0;
+  int M = 0, N = 0, K = 0;
+  int fm = 2, fn = 2;
+  int splits = 1, k_per_split = 0;
+  long ws_floats = 0;
+};
+
+ConvPlan conv_plan(int mode, const ConvGeom& g, int num_cus);
+// FWD: A = w, B = x, C = y (bias/relu epilogue); DGRAD: A = w, B = dy, C = dx;
+// WGRAD: A = dy, B = x, C = dw (C += beta * old when beta != 0).
+void conv_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B, float* C,
+              const float* bias, bool relu, float beta, float* ws, hipStream_t s);
+
+// NCHW ReLU backward + per-channel bias gradient: g = dy*(y>0) (if y), db = sum over n,hw.
+int chan_splits(int N, int C, int HW, int num_cus);
+void chan_relu_bias_bwd(const float* dy, const float* y, int N, int C, int HW, float* g,
+                        float* db, float beta, float* part, int splits, hipStream_t s);
+
+}  // namespace tdp

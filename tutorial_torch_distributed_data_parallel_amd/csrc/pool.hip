@@ -1,0 +1,193 @@
+// Pooling, dropout and residual elementwise kernels for the CNN models (AlexNet, ResNet-50).
+//
+// K3/K5/K9 max_pool2d_with_indices (+K20 backward), K10/K21 adaptive_avg_pool2d
+// (+ backward; identity fast path handled by the caller), K11/K19 dropout (+ backward), plus the
+// residual add+ReLU of ResNet bottlenecks. Max-pool backward is a GATHER over the (at most
+// ceil(k/s)^2) windows that contain an input element, checking the saved argmax -- deterministic,
+// no atomics. Dropout masks come from a counter-based hash of (seed, element index), so the
+// backward regenerates the mask instead of storing it.
+#include "common.h"
+#include "kernels.h"
+#include "pool.h"
+
+namespace tdp {
+namespace {
+
+inline int ew_grid(long n) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return g < 1 ? 1 : (int)g;
+}
+
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, int NC, int H, int W, int P,
+                                   int Q, int k, int s, int pad, float* __restrict__ y,
+                                   int* __restrict__ idx) {
+  const long total = (long)NC * P * Q;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % Q);
+    const long t = i / Q;
+    const int p = (int)(t % P);
+    const long nc = t / P;
+    const float* xp = x + nc * H * W;
+    const int h0 = p * s - pad, w0 = q * s - pad;
+    float best = -INFINITY;
+    int bi = -1;
+    for (int r = 0; r < k; ++r) {
+      const int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      for (int c = 0; c < k; ++c) {
+        const int w = w0 + c;
+        if (w < 0 || w >= W) continue;
+        const float v = xp[h * W + w];
+        // first maximum wins; a NaN wins and then sticks (torch's max_pool2d propagates NaN)
+        if (bi < 0 || (v > best && best == best) || (v != v && best == best)) {
+          best = v;
+          bi = h * W + w;
+        }
+      }
+    }
+    y[i] = best;
+    if (idx) idx[i] = bi;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int* __restrict__ idx,
+                                   int NC, int H, int W, int P, int Q, int k, int s, int pad,
+                                   float* __restrict__ dx) {
+  const long total = (long)NC * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const long t = i / W;
+    const int h = (int)(t % H);
+    const long nc = t / H;
+    const int me = h * W + w;
+    // windows p with p*s - pad <= h <= p*s - pad + k - 1
+    const int plo = max(0, (h + pad - k + s) / s), phi = min(P - 1, (h + pad) / s);
+    const int qlo = max(0, (w + pad - k + s) / s), qhi = min(Q - 1, (w + pad) / s);
+    float acc = 0.f;
+    for (int p = plo; p <= phi; ++p)
+      for (int q = qlo; q <= qhi; ++q) {
+        const long o = (nc * P + p) * Q + q;
+        if (idx[o] == me) acc += dy[o];
+      }
+    dx[i] = acc;
+  }
+}
+
+__global__ void avgpool_fwd_kernel(const float* __restrict__ x, int NC, int H, int W, int P,
+                                   int Q, float* __restrict__ y) {
+  const long total = (long)NC * P * Q;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % Q);
+    const long t = i / Q;
+    const int p = (int)(t % P);
+    const long nc = t / P;
+    const int h0 = (p * H) / P, h1 = ((p + 1) * H + P - 1) / P;
+    const int w0 = (q * W) / Q, w1 = ((q + 1) * W + Q - 1) / Q;
+    const float* xp = x + nc * H * W;
+    float acc = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) acc += xp[h * W + w];
+    y[i] = acc / (float)((h1 - h0) * (w1 - w0));
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int NC, int H, int W, int P,
+                                   int Q, float* __restrict__ dx) {
+  const long total = (long)NC * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const long t = i / W;
+    const int h = (int)(t % H);
+    const long nc = t / H;
+    float acc = 0.f;
+    // output cells whose adaptive window contains (h, w)
+    for (int p = (h * P) / H; p < P && (p * H) / P <= h; ++p) {
+      const int h0 = (p * H) / P, h1 = ((p + 1) * H + P - 1) / P;
+      if (h < h0 || h >= h1) continue;
+      for (int q = (w * Q) / W; q < Q && (q * W) / Q <= w; ++q) {
+        const int w0 = (q * W) / Q, w1 = ((q + 1) * W + Q - 1) / Q;
+        if (w < w0 || w >= w1) continue;
+        acc += dy[(nc * P + p) * Q + q] / (float)((h1 - h0) * (w1 - w0));
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
+__device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, long n, float p, uint64_t seed,
+                               float* __restrict__ y) {
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = hash32(seed, i) >= thr ? x[i] * scale : 0.f;
+}
+
+__global__ void add_relu_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                long n, int relu, float* __restrict__ y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float v = a[i] + b[i];
+    y[i] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+__global__ void relu_mask_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                 long n, float* __restrict__ g) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    g[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+}  // namespace
+
+void maxpool2d_fwd(const float* x, int NC, int H, int W, int P, int Q, int k, int s, int pad,
+                   float* y, int* idx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid((long)NC * P * Q)), dim3(256), 0, st, x, NC,
+                     H, W, P, Q, k, s, pad, y, idx);
+}
+
+void maxpool2d_bwd(const float* dy, const int* idx, int NC, int H, int W, int P, int Q, int k,
+                   int s, int pad, float* dx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid((long)NC * H * W)), dim3(256), 0, st, dy,
+                     idx, NC, H, W, P, Q, k, s, pad, dx);
+}
+
+void avgpool2d_adaptive_fwd(const float* x, int NC, int H, int W, int P, int Q, float* y,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_grid((long)NC * P * Q)), dim3(256), 0, st, x, NC,
+                     H, W, P, Q, y);
+}
+
+void avgpool2d_adaptive_bwd(const float* dy, int NC, int H, int W, int P, int Q, float* dx,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_grid((long)NC * H * W)), dim3(256), 0, st, dy,
+                     NC, H, W, P, Q, dx);
+}
+
+void dropout_apply(const float* x, long n, float p, uint64_t seed, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(dropout_kernel, dim3(ew_grid(n)), dim3(256), 0, st, x, n, p, seed, y);
+}
+
+void add_relu(const float* a, const float* b, long n, bool relu, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(add_relu_kernel, dim3(ew_grid(n)), dim3(256), 0, st, a, b, n, relu ? 1 : 0,
+                     y);
+}
+
+void relu_mask(const float* dy, const float* y, long n, float* g, hipStream_t st) {
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(ew_grid(n)), dim3(256), 0, st, dy, y, n, g);
+}
+
+}  // namespace tdp

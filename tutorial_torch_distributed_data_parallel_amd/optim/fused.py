@@ -74,13 +74,10 @@ class _FusedBase(Optimizer):
             ddp.push_fused_hyper(self, initial=True)
 
     def _fused_step(self) -> bool:
-        """When a DDP model applies this optimizer inside its reduction, step() only refreshes
-        the hyper-parameters (e.g. after an LR-scheduler change) for the next iteration."""
-        ddp = getattr(self, "_fused_ddp", None)
-        if ddp is None:
-            return False
-        ddp.push_fused_hyper(self)
-        return True
+        """When a DDP model applies this optimizer inside its reduction the update already
+        happened during backward, so step() has nothing left to do (the DDP forward hands the
+        current hyper-parameters, e.g. after an LR-scheduler step, to the fused update)."""
+        return getattr(self, "_fused_ddp", None) is not None
 
     def _current_flat_step(self, arena) -> int:
         if id(arena) in self._flat_step:

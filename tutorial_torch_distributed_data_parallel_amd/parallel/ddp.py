@@ -171,6 +171,10 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *inputs, **kwargs):
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.reducer.prepare_for_backward()
+            if self._fused_opt is not None:
+                # hyper-parameters as they are NOW (after any LR-scheduler step) drive this
+                # iteration's in-reduction update
+                self.push_fused_hyper(self._fused_opt)
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._sync_buffers()
