@@ -40,33 +40,51 @@ def parse():
     ap.add_argument("--optim", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
-    ap.add_argument("--dataset", type=int, default=8192, help="synthetic samples per rank")
+    ap.add_argument("--model", choices=["toy_mlp", "alexnet", "resnet50"], default="toy_mlp",
+                    help="toy_mlp = the headline config; alexnet / resnet50 = the CNN configs")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--dataset", type=int, default=None,
+                    help="synthetic samples per rank (default 8192 MLP, 512 CNN)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--eager", action="store_true",
                     help="tdp: run the step eagerly instead of replaying a captured hipGraph")
-    ap.add_argument("--no-fused-opt", action="store_true",
-                    help="tdp: run optimizer.step() after backward instead of applying the "
-                         "optimizer per gradient bucket inside the reduction")
+    ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
+                    help="tdp: apply the optimizer per gradient bucket inside the reduction "
+                         "(auto: when world_size > 1, where it overlaps the all-reduce; on one "
+                         "GPU a single flat optimizer step after backward is faster)")
+    ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
     return ap.parse_args()
 
 
-def baseline_for(n_gpus: int, impl: str, syncbn: bool):
+def baseline_for(n_gpus: int, impl: str, syncbn: bool, model: str = "toy_mlp"):
     """Stock torch DDP number on MI355X for the same config (bench_baseline.json), if measured."""
     f = ROOT / "bench_baseline.json"
     if impl != "tdp" or not f.exists():
         return None
     try:
         tab = json.loads(f.read_text())
-        key = f"{'mlp_syncbn' if syncbn else 'mlp'}_dp{n_gpus}"
+        name = {"toy_mlp": "mlp"}.get(model, model)
+        key = f"{name}{'_syncbn' if syncbn else ''}_dp{n_gpus}"
         v = tab.get(key)
         return float(v) if v else None
     except Exception:
         return None
 
 
+MODEL_DESC = {
+    "toy_mlp": "toy-MLP 9216-4096-4096-10 (Linear+ReLU{bn})",
+    "alexnet": "AlexNet (torchvision topology, 10 classes, 3x{s}x{s}{bn})",
+    "resnet50": "ResNet-50 (torchvision v1.5 topology, 10 classes, 3x{s}x{s}{bn})",
+}
+
+
 def main():
     a = parse()
+    if a.dataset is None:
+        a.dataset = 8192 if a.model == "toy_mlp" else 512
+    metric = METRIC if a.model == "toy_mlp" else \
+        f"samples/sec (whole node) {a.model} DDP at 1/2/4/8 MI355X"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -78,12 +96,17 @@ def main():
                                                                         DistributedSampler,
                                                                         SyntheticDataset)
         from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+        from tutorial_torch_distributed_data_parallel_amd.models.registry import (build_model,
+                                                                                  input_shape)
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
 
         tdp.init_process_group("nccl" if use_gpu else "gloo")
         rank, world, dev = rt.get_rank(), rt.get_world_size(), rt.device()
         torch.manual_seed(1234 + rank)
-        model = ToyMLP(batchnorm=a.syncbn, device=dev)
+        if a.model == "toy_mlp":
+            model = ToyMLP(batchnorm=a.syncbn, device=dev)
+        else:
+            model = build_model(a.model, device=dev)
         if a.syncbn:
             model = tdp.nn.convert_sync_batchnorm(model)
         ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
@@ -95,9 +118,11 @@ def main():
         else:
             opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
         fused = False
-        if use_gpu and not a.no_fused_opt:
+        want_fused = a.fused_opt == "on" or (a.fused_opt == "auto" and world > 1)
+        if use_gpu and want_fused and not a.no_fused_opt:
             fused = ddp.register_fused_optimizer(opt)
-        data = SyntheticDataset(a.dataset, (9216,), 10, seed=rank, device=dev)
+        data = SyntheticDataset(a.dataset, input_shape(a.model, a.image_size), 10, seed=rank,
+                                device=dev)
         sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
         loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
         barrier = rt.barrier
@@ -149,16 +174,10 @@ def main():
             os.environ["MASTER_PORT"] = str(29600 + os.getpid() % 300)
             dist.init_process_group("nccl" if use_gpu else "gloo", rank=0, world_size=1)
         torch.manual_seed(1234 + rank)
-        layers = [nn.Linear(9216, 4096)]
-        if a.syncbn:
-            layers.append(nn.BatchNorm1d(4096))
-        layers += [nn.ReLU(inplace=True), nn.Linear(4096, 4096)]
-        if a.syncbn:
-            layers.append(nn.BatchNorm1d(4096))
-        layers += [nn.ReLU(inplace=True), nn.Linear(4096, 10)]
-        model = nn.Sequential(*layers).to(dev)
-        if a.syncbn:
-            model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        sys.path.insert(0, str(ROOT / "scripts"))
+        from stock_models import stock_model
+
+        model = stock_model(a.model, a.syncbn).to(dev)
         ddp = TorchDDP(model, device_ids=[local] if use_gpu else None,
                        bucket_cap_mb=a.bucket_mb if a.bucket_mb else 25)
         crit = nn.CrossEntropyLoss()
@@ -166,7 +185,8 @@ def main():
                else torch.optim.Adam(ddp.parameters(), lr=1e-3))
         g = torch.Generator(device=dev)
         g.manual_seed(rank)
-        X = torch.randn(a.dataset, 9216, generator=g, device=dev)
+        shape = (9216,) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
+        X = torch.randn(a.dataset, *shape, generator=g, device=dev)
         Y = torch.randint(0, 10, (a.dataset,), generator=g, device=dev)
 
         class _DS:
@@ -248,10 +268,10 @@ def main():
     dt = float(t.item())
     ms = dt * 1000.0 / a.steps
     value = a.batch * world * a.steps / dt
-    base = baseline_for(world, a.impl, a.syncbn)
+    base = baseline_for(world, a.impl, a.syncbn, a.model)
     if rank == 0:
         rec = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": world if use_gpu else 0,
@@ -264,8 +284,8 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (on-device random features, random-init weights)",
             "config": {
-                "model": "toy-MLP 9216-4096-4096-10 (Linear+ReLU" +
-                         (", +SyncBatchNorm" if a.syncbn else "") + ")",
+                "model": MODEL_DESC[a.model].format(
+                    s=a.image_size, bn=", +SyncBatchNorm" if a.syncbn else ""),
                 "global_batch": a.batch * world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
@@ -273,8 +293,7 @@ def main():
                          (", eager)" if (a.eager or not use_gpu) else ", hipGraph step)"))
                         if a.impl == "tdp" else "stock torch DDP + torch.optim",
                 "optimizer": a.optim + (" (fused into the bucket reduction)"
-                                        if a.impl == "tdp" and use_gpu and not a.no_fused_opt
-                                        else ""),
+                                        if a.impl == "tdp" and fused else ""),
                 "final_loss": round(float(loss.item()), 5),
             },
         }

@@ -1,0 +1,154 @@
+"""Conv / pooling / dropout / residual kernels and the CNN models vs a float64 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CONVS = [
+    # N, C, H, W, Cout, R, stride, pad
+    (2, 3, 63, 63, 64, 11, 4, 2),     # AlexNet conv1 (scaled input)
+    (2, 64, 15, 15, 192, 5, 1, 2),    # AlexNet conv2
+    (2, 192, 13, 13, 384, 3, 1, 1),   # AlexNet conv3
+    (3, 64, 14, 14, 256, 1, 1, 0),    # ResNet 1x1 expand
+    (2, 256, 14, 14, 512, 1, 2, 0),   # ResNet downsample projection
+    (2, 128, 15, 15, 128, 3, 2, 1),   # ResNet v1.5 strided 3x3
+    (2, 3, 40, 40, 64, 7, 2, 3),      # ResNet stem
+    (1, 5, 9, 11, 7, 3, 1, 1),        # odd everything
+    (2, 7, 10, 9, 33, 2, 3, 0),       # stride > kernel
+]
+
+
+def _ref(x, w, b, s, p, relu):
+    y = F.conv2d(x.double().cpu(), w.double().cpu(), None if b is None else b.double().cpu(),
+                 s, p)
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("N,C,H,W,Co,R,s,p", CONVS)
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv2d_fwd_bwd(N, C, H, W, Co, R, s, p, relu):
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(N * 1000 + C * 10 + R)
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = (torch.randn(Co, C, R, R, device="cuda") / (C * R * R) ** 0.5).requires_grad_()
+    b = torch.randn(Co, device="cuda", requires_grad=True)
+    y = ops.conv2d(x, w, b, s, p, relu=relu)
+    xr = x.detach().double().cpu().requires_grad_()
+    wr = w.detach().double().cpu().requires_grad_()
+    br = b.detach().double().cpu().requires_grad_()
+    yr = F.conv2d(xr, wr, br, s, p)
+    if relu:
+        yr = F.relu(yr)
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.double().cpu())
+    K = Co * R * R
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-4,
+                               atol=2e-4 * max(1.0, K ** 0.5))
+    P = N * y.shape[2] * y.shape[3]
+    torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4,
+                               atol=2e-4 * max(1.0, P ** 0.5))
+    torch.testing.assert_close(b.grad.double().cpu(), br.grad, rtol=1e-4,
+                               atol=2e-4 * max(1.0, P ** 0.5))
+
+
+def test_conv2d_no_bias_wgrad_only():
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(3)
+    x = torch.randn(4, 64, 28, 28, device="cuda")
+    w = torch.randn(128, 64, 3, 3, device="cuda", requires_grad=True)
+    y = ops.conv2d(x, w, None, 1, 1)
+    y.sum().backward()
+    wr = w.detach().double().cpu().requires_grad_()
+    F.conv2d(x.double().cpu(), wr, None, 1, 1).sum().backward()
+    torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=5e-2)
+
+
+@pytest.mark.parametrize("k,s,p,H", [(3, 2, 0, 55), (3, 2, 0, 13), (3, 2, 1, 112), (2, 2, 0, 8)])
+def test_maxpool(k, s, p, H):
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(H)
+    x = torch.randn(2, 5, H, H + 1, device="cuda", requires_grad=True)
+    y = ops.max_pool2d(x, k, s, p)
+    xr = x.detach().clone().requires_grad_()
+    yr = F.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y, yr, rtol=0, atol=0)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("H,W,P,Q", [(13, 13, 6, 6), (7, 7, 1, 1), (10, 7, 3, 4), (5, 5, 6, 6)])
+def test_adaptive_avgpool(H, W, P, Q):
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    x = torch.randn(2, 3, H, W, device="cuda", requires_grad=True)
+    y = ops.adaptive_avg_pool2d(x, (P, Q))
+    xr = x.detach().clone().requires_grad_()
+    yr = F.adaptive_avg_pool2d(xr, (P, Q))
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_dropout_statistics_and_backward():
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(0)
+    x = torch.ones(1 << 20, device="cuda", requires_grad=True)
+    y = ops.dropout(x, 0.5, True)
+    kept = (y != 0)
+    frac = kept.float().mean().item()
+    assert abs(frac - 0.5) < 0.005
+    torch.testing.assert_close(y[kept], torch.full_like(y[kept], 2.0))
+    y.backward(torch.ones_like(y))
+    torch.testing.assert_close(x.grad, y.detach())  # same mask and scale
+    y2 = ops.dropout(x, 0.5, True)
+    assert not torch.equal(y2, y)  # fresh seed per call
+    assert ops.dropout(x, 0.5, False) is x
+
+
+def test_add_relu():
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    a = torch.randn(3, 8, 5, 5, device="cuda", requires_grad=True)
+    b = torch.randn(3, 8, 5, 5, device="cuda", requires_grad=True)
+    y = ops.add_relu(a, b)
+    torch.testing.assert_close(y, F.relu(a + b))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = dy * ((a + b) > 0)
+    torch.testing.assert_close(a.grad, ref)
+    torch.testing.assert_close(b.grad, ref)
+
+
+@pytest.mark.parametrize("name,hw", [("alexnet", 224), ("resnet50", 64)])
+def test_model_matches_cpu_reference(name, hw):
+    """Whole model on GPU (native kernels) vs the same weights on CPU (ATen), fwd + grads."""
+    from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
+
+    torch.manual_seed(0)
+    m_cpu = build_model(name)
+    m_gpu = build_model(name)
+    m_gpu.load_state_dict(m_cpu.state_dict())
+    m_gpu.cuda()
+    for m in (m_cpu, m_gpu):
+        m.eval() if name == "alexnet" else m.train()  # AlexNet: no dropout randomness
+    x = torch.randn(2, 3, hw, hw)
+    y_cpu = m_cpu(x)
+    y_gpu = m_gpu(x.cuda())
+    torch.testing.assert_close(y_gpu.cpu(), y_cpu, rtol=2e-3, atol=2e-3)
+    y_cpu.square().sum().backward()
+    y_gpu.square().sum().backward()
+    for (n, pc), (_, pg) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
+        scale = pc.grad.abs().max().item() + 1e-6
+        err = (pg.grad.cpu() - pc.grad).abs().max().item()
+        assert err <= 2e-3 * scale + 1e-5, (n, err, scale)

@@ -13,7 +13,9 @@
 #include <mutex>
 
 #include "comm.h"
+#include "conv.h"
 #include "kernels.h"
+#include "pool.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -368,6 +370,144 @@ Tensor bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
   return dx;
 }
 
+// ---------------------------------------------------------------------------------- conv / pool
+ConvGeom conv_geom(const std::vector<int64_t>& xs, const std::vector<int64_t>& ws,
+                   int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  TORCH_CHECK(xs.size() == 4 && ws.size() == 4, "conv2d: 4-D input and weight expected");
+  TORCH_CHECK(xs[1] == ws[1], "conv2d: input channels ", xs[1], " != weight channels ", ws[1],
+              " (groups are not supported)");
+  ConvGeom g;
+  g.N = (int)xs[0]; g.C = (int)xs[1]; g.H = (int)xs[2]; g.W = (int)xs[3];
+  g.Cout = (int)ws[0]; g.R = (int)ws[2]; g.S = (int)ws[3];
+  g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw;
+  g.P = (g.H + 2 * g.ph - g.R) / g.sh + 1;
+  g.Q = (g.W + 2 * g.pw - g.S) / g.sw + 1;
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "conv2d: empty output");
+  TORCH_CHECK((long)g.N * g.C * g.H * g.W < (1L << 31) && (long)g.N * g.Cout * g.P * g.Q < (1L << 31),
+              "conv2d: tensors must have < 2^31 elements");
+  return g;
+}
+
+Tensor conv_exec(int mode, const ConvGeom& g, const Tensor& A, const Tensor& B, Tensor C,
+                 const c10::optional<Tensor>& bias, bool relu, double beta) {
+  const ConvPlan pl = conv_plan(mode, g, num_cus(C.get_device()));
+  Tensor ws;
+  if (pl.ws_floats > 0) ws = at::empty({pl.ws_floats}, C.options());
+  conv_run(pl, g, A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(), fptr(bias),
+           relu, (float)beta, pl.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  return C;
+}
+
+Tensor conv2d_fwd_op(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                     int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool relu) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_GPU(w); CHECK_F32(w); CHECK_CONTIG(w);
+  const ConvGeom g = conv_geom(x.sizes().vec(), w.sizes().vec(), sh, sw, ph, pw);
+  auto y = at::empty({g.N, g.Cout, g.P, g.Q}, x.options());
+  return conv_exec(kConvFwd, g, w, x, y, bias, relu, 0.0);
+}
+
+Tensor conv2d_dgrad_op(const Tensor& dy, const Tensor& w, std::vector<int64_t> x_shape,
+                       int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(w);
+  const ConvGeom g = conv_geom(x_shape, w.sizes().vec(), sh, sw, ph, pw);
+  TORCH_CHECK(dy.size(2) == g.P && dy.size(3) == g.Q, "conv2d dgrad: dy shape mismatch");
+  auto dx = at::empty(x_shape, dy.options());
+  return conv_exec(kConvDgrad, g, w, dy, dx, c10::nullopt, false, 0.0);
+}
+
+void conv2d_wgrad_op(const Tensor& dy, const Tensor& x, Tensor& dw, int64_t sh, int64_t sw,
+                     int64_t ph, int64_t pw, double beta) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_CONTIG(dw);
+  const ConvGeom g = conv_geom(x.sizes().vec(), dw.sizes().vec(), sh, sw, ph, pw);
+  conv_exec(kConvWgrad, g, dy, x, dw, c10::nullopt, false, beta);
+}
+
+// NCHW: g = dy*(y>0) (new tensor, or dy itself when y is None); db (optional) = per-channel sum
+Tensor chan_relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
+                             const c10::optional<Tensor>& db, double beta) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy);
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  const int HW = (int)(dy.numel() / ((int64_t)N * C));
+  const bool has_y = y.has_value() && y->defined();
+  Tensor g = has_y ? at::empty_like(dy) : dy;
+  float* dbp = fptr(db);
+  if (!has_y && !dbp) return g;
+  const int sp = chan_splits(N, C, HW, num_cus(dy.get_device()));
+  Tensor part = at::empty({(int64_t)sp * C}, dy.options());
+  chan_relu_bias_bwd(dy.data_ptr<float>(), has_y ? y->data_ptr<float>() : nullptr, N, C, HW,
+                     g.data_ptr<float>(), dbp, (float)beta, part.data_ptr<float>(), sp,
+                     cur_stream());
+  return g;
+}
+
+std::vector<Tensor> maxpool2d_fwd_op(const Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4, "max_pool2d: 4-D input expected");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int P = (H + 2 * (int)pad - (int)k) / (int)s + 1, Q = (W + 2 * (int)pad - (int)k) / (int)s + 1;
+  auto y = at::empty({N, C, P, Q}, x.options());
+  auto idx = at::empty({N, C, P, Q}, x.options().dtype(at::kInt));
+  maxpool2d_fwd(x.data_ptr<float>(), N * C, H, W, P, Q, (int)k, (int)s, (int)pad,
+                y.data_ptr<float>(), idx.data_ptr<int>(), cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool2d_bwd_op(const Tensor& dy, const Tensor& idx, std::vector<int64_t> x_shape,
+                        int64_t k, int64_t s, int64_t pad) {
+  CHECK_GPU(dy); CHECK_CONTIG(dy); CHECK_CONTIG(idx);
+  auto dx = at::empty(x_shape, dy.options());
+  maxpool2d_bwd(dy.contiguous().data_ptr<float>(), idx.data_ptr<int>(),
+                (int)(x_shape[0] * x_shape[1]), (int)x_shape[2], (int)x_shape[3],
+                (int)dy.size(2), (int)dy.size(3), (int)k, (int)s, (int)pad, dx.data_ptr<float>(),
+                cur_stream());
+  return dx;
+}
+
+Tensor avgpool_fwd_op(const Tensor& x, int64_t P, int64_t Q) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  auto y = at::empty({N, C, P, Q}, x.options());
+  avgpool2d_adaptive_fwd(x.data_ptr<float>(), N * C, H, W, (int)P, (int)Q, y.data_ptr<float>(),
+                         cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd_op(const Tensor& dy, std::vector<int64_t> x_shape) {
+  CHECK_GPU(dy); CHECK_F32(dy);
+  auto d = dy.contiguous();
+  auto dx = at::empty(x_shape, dy.options());
+  avgpool2d_adaptive_bwd(d.data_ptr<float>(), (int)(x_shape[0] * x_shape[1]), (int)x_shape[2],
+                         (int)x_shape[3], (int)dy.size(2), (int)dy.size(3), dx.data_ptr<float>(),
+                         cur_stream());
+  return dx;
+}
+
+Tensor dropout_op(const Tensor& x, double p, int64_t seed) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  auto y = at::empty_like(x);
+  dropout_apply(x.data_ptr<float>(), x.numel(), (float)p, (uint64_t)seed, y.data_ptr<float>(),
+                cur_stream());
+  return y;
+}
+
+Tensor add_relu_op(const Tensor& a, const Tensor& b, bool relu) {
+  CHECK_GPU(a); CHECK_F32(a); CHECK_CONTIG(a); CHECK_CONTIG(b);
+  TORCH_CHECK(a.sizes() == b.sizes(), "add_relu: shape mismatch");
+  auto y = at::empty_like(a);
+  add_relu(a.data_ptr<float>(), b.data_ptr<float>(), a.numel(), relu, y.data_ptr<float>(),
+           cur_stream());
+  return y;
+}
+
+Tensor relu_mask_op(const Tensor& dy, const Tensor& y) {
+  CHECK_GPU(dy); CHECK_F32(dy);
+  auto d = dy.contiguous();
+  auto g = at::empty_like(d);
+  relu_mask(d.data_ptr<float>(), y.data_ptr<float>(), d.numel(), g.data_ptr<float>(),
+            cur_stream());
+  return g;
+}
+
 // ---------------------------------------------------------------------------------------- comm
 ncclDataType_t nccl_dt(const Tensor& t) {
   switch (t.scalar_type()) {
@@ -443,6 +583,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &sumsq_op, py::arg("x"), py::arg("into") = py::none());
   m.def("clip_", &clip_op);
   m.def("cast_f32_bf16", &cast_f32_bf16_op);
+  m.def("conv2d_fwd", &conv2d_fwd_op);
+  m.def("conv2d_dgrad", &conv2d_dgrad_op);
+  m.def("conv2d_wgrad", &conv2d_wgrad_op);
+  m.def("chan_relu_bias_bwd", &chan_relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
+        py::arg("db") = py::none(), py::arg("beta") = 0.0);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd_op);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd_op);
+  m.def("avgpool_fwd", &avgpool_fwd_op);
+  m.def("avgpool_bwd", &avgpool_bwd_op);
+  m.def("dropout", &dropout_op);
+  m.def("add_relu", &add_relu_op);
+  m.def("relu_mask", &relu_mask_op);
   m.def("bn_moments", &bn_moments_op);
   m.def("bn_merge", &bn_merge_op);
   m.def("bn_elemt", &bn_elemt_op);

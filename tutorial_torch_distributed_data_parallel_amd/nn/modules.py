@@ -27,6 +27,45 @@ class Linear(nn.Linear):
         return super().extra_repr() + (", relu=True" if self.relu else "")
 
 
+class Conv2d(nn.Conv2d):
+    """``nn.Conv2d`` (groups=1, dilation=1, zero padding) on the implicit-GEMM kernels, with an
+    optional fused ReLU."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0,
+                 bias: bool = True, relu: bool = False, device=None, dtype=None):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
+                         bias=bias, device=device, dtype=dtype)
+        self.relu = relu
+
+    def forward(self, x):
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, relu=self.relu)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+class ReLU(nn.ReLU):
+    """Standalone ReLU (models fuse it into the producer where possible)."""
+
+    def forward(self, x):
+        return torch.relu(x)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    def forward(self, x):
+        return ops.max_pool2d(x, self.kernel_size, self.stride, self.padding)
+
+
+class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
+    def forward(self, x):
+        return ops.adaptive_avg_pool2d(x, self.output_size)
+
+
+class Dropout(nn.Dropout):
+    def forward(self, x):
+        return ops.dropout(x, self.p, self.training)
+
+
 class _NativeBN(nn.modules.batchnorm._BatchNorm):
     """Shared forward for BatchNorm{1,2}d / SyncBatchNorm."""
 

@@ -1,0 +1,113 @@
+"""Pooling, dropout and residual add+ReLU over the native kernels (``csrc/pool.hip``).
+
+SURVEY.md §2.5: K3/K5/K9 ``max_pool2d_with_indices`` and K20 its backward (a deterministic gather,
+no atomics), K10/K21 ``adaptive_avg_pool2d`` (identity when the input already has the output size,
+as for 224x224 AlexNet where the features end at 6x6), K11/K19 dropout (mask regenerated from a
+counter-based hash in the backward instead of being stored) and the residual add+ReLU of ResNet
+bottlenecks. CPU tensors run the ``torch.nn.functional`` reference.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import native
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = native().maxpool2d_fwd(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.cfg = (list(x.shape), k, s, p)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        shape, k, s, p = ctx.cfg
+        return native().maxpool2d_bwd(dy.contiguous(), idx, shape, k, s, p), None, None, None
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0):
+    """Square-window max pooling (``ceil_mode=False``, no dilation)."""
+    k = _pair(kernel_size)
+    s = _pair(stride if stride is not None else kernel_size)
+    p = _pair(padding)
+    if not x.is_cuda:
+        return F.max_pool2d(x, k, s, p)
+    if k[0] != k[1] or s[0] != s[1] or p[0] != p[1]:
+        raise NotImplementedError("native max_pool2d supports square windows only")
+    return _MaxPoolFn.apply(x.contiguous(), k[0], s[0], p[0])
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, P, Q):
+        ctx.shape = list(x.shape)
+        return native().avgpool_fwd(x, P, Q)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return native().avgpool_bwd(dy, ctx.shape), None, None
+
+
+def adaptive_avg_pool2d(x, output_size):
+    P, Q = _pair(output_size)
+    if x.shape[-2] == P and x.shape[-1] == Q:
+        return x  # identity (torch launches a copy kernel here)
+    if not x.is_cuda:
+        return F.adaptive_avg_pool2d(x, (P, Q))
+    return _AvgPoolFn.apply(x.contiguous(), P, Q)
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.cfg = (p, seed)
+        return native().dropout(x, p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.cfg
+        # same (seed, index) hash -> same mask, same 1/(1-p) scale
+        return native().dropout(dy.contiguous(), p, seed), None, None
+
+
+def dropout(x, p: float = 0.5, training: bool = True, generator=None):
+    """Inverted dropout. The per-call seed comes from torch's CPU generator (reproducible under
+    ``torch.manual_seed``); inside a captured hipGraph the seed is fixed at capture."""
+    if not training or p == 0.0:
+        return x
+    if p >= 1.0:
+        return x * 0.0
+    if not x.is_cuda:
+        return F.dropout(x, p, True)
+    seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item())
+    return _DropoutFn.apply(x.contiguous(), float(p), seed)
+
+
+class _AddReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        y = native().add_relu(a, b, True)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        g = native().relu_mask(dy, y)
+        return g, g
+
+
+def add_relu(a, b):
+    """``relu(a + b)`` -- the residual join of a ResNet block."""
+    if not a.is_cuda:
+        return F.relu(a + b)
+    return _AddReluFn.apply(a.contiguous(), b.contiguous())
