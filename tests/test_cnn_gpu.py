@@ -130,25 +130,40 @@ def test_add_relu():
     torch.testing.assert_close(b.grad, ref)
 
 
-@pytest.mark.parametrize("name,hw", [("alexnet", 224), ("resnet50", 64)])
-def test_model_matches_cpu_reference(name, hw):
-    """Whole model on GPU (native kernels) vs the same weights on CPU (ATen), fwd + grads."""
+@pytest.mark.parametrize("name,hw,n", [("alexnet", 224, 2), ("resnet50", 64, 8)])
+def test_model_matches_cpu_reference(name, hw, n):
+    """Whole model on GPU (native fp32 kernels) vs the same weights in float64 on CPU (ATen).
+
+    Gradients are compared in eval mode: train-mode batch norm over ResNet's 2x2 layer4 maps
+    (32 values per channel here) is so ill-conditioned that even CPU fp32 differs from fp64 by
+    ~25% in layer4's weight gradients; the train-mode forward is still compared."""
     from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
 
     torch.manual_seed(0)
-    m_cpu = build_model(name)
+    m_cpu = build_model(name).double()
     m_gpu = build_model(name)
     m_gpu.load_state_dict(m_cpu.state_dict())
     m_gpu.cuda()
-    for m in (m_cpu, m_gpu):
-        m.eval() if name == "alexnet" else m.train()  # AlexNet: no dropout randomness
-    x = torch.randn(2, 3, hw, hw)
+    x = torch.randn(n, 3, hw, hw, dtype=torch.float64)
+    if name == "resnet50":
+        with torch.no_grad():
+            y_cpu = m_cpu.train()(x)
+            y_gpu = m_gpu.train()(x.float().cuda())
+        torch.testing.assert_close(y_gpu.double().cpu(), y_cpu, rtol=2e-3, atol=2e-3)
+        torch.testing.assert_close(m_gpu.bn1.running_var.double().cpu(), m_cpu.bn1.running_var,
+                                   rtol=1e-4, atol=1e-5)
+    m_cpu.eval()
+    m_gpu.eval()
     y_cpu = m_cpu(x)
-    y_gpu = m_gpu(x.cuda())
-    torch.testing.assert_close(y_gpu.cpu(), y_cpu, rtol=2e-3, atol=2e-3)
+    y_gpu = m_gpu(x.float().cuda())
+    torch.testing.assert_close(y_gpu.double().cpu(), y_cpu, rtol=2e-3, atol=2e-3)
     y_cpu.square().sum().backward()
     y_gpu.square().sum().backward()
-    for (n, pc), (_, pg) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
-        scale = pc.grad.abs().max().item() + 1e-6
-        err = (pg.grad.cpu() - pc.grad).abs().max().item()
-        assert err <= 2e-3 * scale + 1e-5, (n, err, scale)
+    # relative L2 error per parameter: a ReLU whose pre-activation rounds to the other side of 0
+    # in fp32 vs fp64 (it happens ~1 in 1e5 elements) legitimately flips single gradient entries
+    worst = []
+    for (pn, pc), (_, pg) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
+        err = (pg.grad.double().cpu() - pc.grad).norm().item() / (pc.grad.norm().item() + 1e-12)
+        worst.append((err, pn))
+    worst.sort(reverse=True)
+    assert worst[0][0] <= 2e-3, worst[:5]

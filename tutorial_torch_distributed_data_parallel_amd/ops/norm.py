@@ -138,6 +138,14 @@ def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
             weight is not None and weight.requires_grad))):
         return native().bn_eval(x.contiguous(), running_mean, running_var, weight, bias,
                                 float(eps), bool(relu))
-    # inference-mode BN that must be differentiated (frozen-BN fine-tuning): ATen formula
-    y = F.batch_norm(x, running_mean, running_var, weight, bias, False, 0.0, eps)
+    # inference-mode BN that must be differentiated (frozen-BN fine-tuning): a per-channel affine
+    # map y = x * scale + shift, differentiated by autograd through plain elementwise ops
+    shape = (1, x.shape[1]) + (1,) * (x.dim() - 2)
+    scale = torch.rsqrt(running_var + eps)
+    if weight is not None:
+        scale = scale * weight
+    shift = -running_mean * scale
+    if bias is not None:
+        shift = shift + bias
+    y = x * scale.view(shape) + shift.view(shape)
     return F.relu(y) if relu else y
