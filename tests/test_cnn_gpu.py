@@ -25,9 +25,18 @@ def _ref(x, w, b, s, p, relu):
     return F.relu(y) if relu else y
 
 
+@pytest.fixture(params=["nhwc", "nchw"])
+def conv_path(request):
+    from tutorial_torch_distributed_data_parallel_amd.ops import conv as conv_mod
+
+    conv_mod.FORCE_NCHW = request.param == "nchw"
+    yield request.param
+    conv_mod.FORCE_NCHW = False
+
+
 @pytest.mark.parametrize("N,C,H,W,Co,R,s,p", CONVS)
 @pytest.mark.parametrize("relu", [False, True])
-def test_conv2d_fwd_bwd(N, C, H, W, Co, R, s, p, relu):
+def test_conv2d_fwd_bwd(N, C, H, W, Co, R, s, p, relu, conv_path):
     from tutorial_torch_distributed_data_parallel_amd import ops
 
     torch.manual_seed(N * 1000 + C * 10 + R)
@@ -55,6 +64,52 @@ def test_conv2d_fwd_bwd(N, C, H, W, Co, R, s, p, relu):
                                atol=2e-4 * max(1.0, P ** 0.5))
 
 
+def test_conv2d_nhwc_layouts():
+    """channels_last in -> channels_last out; NCHW inputs are accepted and converted."""
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(5)
+    w = torch.randn(32, 16, 3, 3, device="cuda")
+    for fmt in (torch.contiguous_format, torch.channels_last):
+        x = torch.randn(2, 16, 9, 9, device="cuda").contiguous(memory_format=fmt)
+        y = ops.conv2d(x, w, None, 1, 1)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(y.double().cpu(),
+                                   F.conv2d(x.double().cpu(), w.double().cpu(), None, 1, 1),
+                                   rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14), (8, 256, 7, 7), (2, 3, 5, 5)])
+def test_batchnorm_channels_last(shape):
+    """BatchNorm2d on NHWC activations runs the [pixels, C] kernels; compare with torch."""
+    from tutorial_torch_distributed_data_parallel_amd import nn as tnn
+
+    torch.manual_seed(1)
+    bn = tnn.BatchNorm2d(shape[1], relu=True).cuda()
+    ref = torch.nn.BatchNorm2d(shape[1]).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    x = (torch.randn(shape, device="cuda") * 2 + 0.5).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    y = bn(x)
+    yr = torch.relu(ref(xr))
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
+    bn.eval()
+    ref.eval()
+    torch.testing.assert_close(bn(x.detach()), torch.relu(ref(x.detach())), rtol=1e-4, atol=1e-4)
+
+
 def test_conv2d_no_bias_wgrad_only():
     from tutorial_torch_distributed_data_parallel_amd import ops
 
@@ -68,12 +123,17 @@ def test_conv2d_no_bias_wgrad_only():
     torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=5e-2)
 
 
+FMTS = [torch.contiguous_format, torch.channels_last]
+
+
+@pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("k,s,p,H", [(3, 2, 0, 55), (3, 2, 0, 13), (3, 2, 1, 112), (2, 2, 0, 8)])
-def test_maxpool(k, s, p, H):
+def test_maxpool(k, s, p, H, fmt):
     from tutorial_torch_distributed_data_parallel_amd import ops
 
     torch.manual_seed(H)
-    x = torch.randn(2, 5, H, H + 1, device="cuda", requires_grad=True)
+    x = torch.randn(2, 5, H, H + 1, device="cuda").contiguous(memory_format=fmt)
+    x.requires_grad_()
     y = ops.max_pool2d(x, k, s, p)
     xr = x.detach().clone().requires_grad_()
     yr = F.max_pool2d(xr, k, s, p)
@@ -84,11 +144,13 @@ def test_maxpool(k, s, p, H):
     torch.testing.assert_close(x.grad, xr.grad, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("H,W,P,Q", [(13, 13, 6, 6), (7, 7, 1, 1), (10, 7, 3, 4), (5, 5, 6, 6)])
-def test_adaptive_avgpool(H, W, P, Q):
+def test_adaptive_avgpool(H, W, P, Q, fmt):
     from tutorial_torch_distributed_data_parallel_amd import ops
 
-    x = torch.randn(2, 3, H, W, device="cuda", requires_grad=True)
+    x = torch.randn(2, 3, H, W, device="cuda").contiguous(memory_format=fmt)
+    x.requires_grad_()
     y = ops.adaptive_avg_pool2d(x, (P, Q))
     xr = x.detach().clone().requires_grad_()
     yr = F.adaptive_avg_pool2d(xr, (P, Q))
@@ -116,11 +178,12 @@ def test_dropout_statistics_and_backward():
     assert ops.dropout(x, 0.5, False) is x
 
 
-def test_add_relu():
+@pytest.mark.parametrize("fmt", FMTS)
+def test_add_relu(fmt):
     from tutorial_torch_distributed_data_parallel_amd import ops
 
-    a = torch.randn(3, 8, 5, 5, device="cuda", requires_grad=True)
-    b = torch.randn(3, 8, 5, 5, device="cuda", requires_grad=True)
+    a = torch.randn(3, 8, 5, 5, device="cuda").contiguous(memory_format=fmt).requires_grad_()
+    b = torch.randn(3, 8, 5, 5, device="cuda").requires_grad_()  # NCHW: converted to a's layout
     y = ops.add_relu(a, b)
     torch.testing.assert_close(y, F.relu(a + b))
     dy = torch.randn_like(y)

@@ -422,6 +422,106 @@ void conv2d_wgrad_op(const Tensor& dy, const Tensor& x, Tensor& dw, int64_t sh, 
   conv_exec(kConvWgrad, g, dy, x, dw, c10::nullopt, false, beta);
 }
 
+// ------------------------------------------------------------- NHWC (channels_last) conv path
+#define CHECK_CL(x)                                                                      \
+  TORCH_CHECK((x).dim() == 4 && (x).is_contiguous(at::MemoryFormat::ChannelsLast),       \
+              #x " must be a channels_last 4-D tensor")
+
+ConvGeom nhwc_geom(const std::vector<int64_t>& xs, int64_t cout, int64_t R, int64_t S,
+                   int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  return conv_geom(xs, {cout, xs[1], R, S}, sh, sw, ph, pw);
+}
+
+Tensor conv_nhwc_exec(int mode, const ConvGeom& g, const Tensor& A, const Tensor& B, Tensor C,
+                      const c10::optional<Tensor>& bias, bool relu, double beta) {
+  TORCH_CHECK(conv_nhwc_ok(mode, g), "conv (NHWC): channels must be multiples of 4 and "
+              "input-gradient strides powers of two");
+  const ConvPlan pl = conv_nhwc_plan(mode, g, num_cus(C.get_device()));
+  Tensor ws;
+  if (pl.ws_floats > 0) ws = at::empty({pl.ws_floats}, C.options());
+  conv_nhwc_run(pl, g, A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
+                fptr(bias), relu, (float)beta, pl.ws_floats > 0 ? ws.data_ptr<float>() : nullptr,
+                cur_stream());
+  return C;
+}
+
+// x channels_last [N,C,H,W]; wt [Cout, R*S*C] (k = (r, s, c)) -> y channels_last
+Tensor conv_nhwc_fwd_op(const Tensor& x, const Tensor& wt, const c10::optional<Tensor>& bias,
+                        int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                        bool relu) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CL(x); CHECK_GPU(wt); CHECK_CONTIG(wt);
+  const ConvGeom g = nhwc_geom(x.sizes().vec(), wt.size(0), R, S, sh, sw, ph, pw);
+  TORCH_CHECK(wt.numel() == (int64_t)g.Cout * R * S * g.C, "conv (NHWC): weight size mismatch");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.Cout, "bias size");
+  auto y = at::empty({g.N, g.Cout, g.P, g.Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  return conv_nhwc_exec(kConvFwd, g, x, wt, y, bias, relu, 0.0);
+}
+
+// dy channels_last [N,Cout,P,Q]; w2 [R*S*Cout, C] -> dx channels_last x_shape
+Tensor conv_nhwc_dgrad_op(const Tensor& dy, const Tensor& w2, std::vector<int64_t> x_shape,
+                          int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy); CHECK_CONTIG(w2);
+  const ConvGeom g = nhwc_geom(x_shape, dy.size(1), R, S, sh, sw, ph, pw);
+  TORCH_CHECK(dy.size(2) == g.P && dy.size(3) == g.Q && dy.size(0) == g.N, "dgrad: dy shape");
+  TORCH_CHECK(w2.numel() == (int64_t)g.Cout * R * S * g.C, "dgrad: weight size mismatch");
+  auto dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  return conv_nhwc_exec(kConvDgrad, g, dy, w2, dx, c10::nullopt, false, 0.0);
+}
+
+// dy channels_last, x channels_last -> dwt [Cout, R*S*C] (dwt = beta*dwt + grad)
+void conv_nhwc_wgrad_op(const Tensor& dy, const Tensor& x, Tensor& dwt, int64_t R, int64_t S,
+                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, double beta) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy); CHECK_CL(x); CHECK_CONTIG(dwt);
+  const ConvGeom g = nhwc_geom(x.sizes().vec(), dy.size(1), R, S, sh, sw, ph, pw);
+  TORCH_CHECK(dy.size(2) == g.P && dy.size(3) == g.Q, "wgrad: dy shape");
+  TORCH_CHECK(dwt.numel() == (int64_t)g.Cout * R * S * g.C, "wgrad: dw size mismatch");
+  conv_nhwc_exec(kConvWgrad, g, dy, x, dwt, c10::nullopt, false, beta);
+}
+
+// NHWC pooling: x channels_last -> y channels_last
+std::vector<Tensor> maxpool_nhwc_fwd_op(const Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CL(x);
+  TORCH_CHECK(x.numel() < (1L << 31), "max_pool2d: < 2^31 elements");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int P = (H + 2 * (int)pad - (int)k) / (int)s + 1, Q = (W + 2 * (int)pad - (int)k) / (int)s + 1;
+  auto y = at::empty({N, C, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, C, P, Q},
+                       x.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool2d_nhwc_fwd(x.data_ptr<float>(), N, H, W, C, P, Q, (int)k, (int)s, (int)pad,
+                     y.data_ptr<float>(), idx.data_ptr<int>(), cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_nhwc_bwd_op(const Tensor& dy, const Tensor& idx, std::vector<int64_t> x_shape,
+                           int64_t k, int64_t s, int64_t pad) {
+  CHECK_GPU(dy); CHECK_CL(dy); CHECK_CL(idx);
+  auto dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  maxpool2d_nhwc_bwd(dy.data_ptr<float>(), idx.data_ptr<int>(), (int)x_shape[0],
+                     (int)x_shape[2], (int)x_shape[3], (int)x_shape[1], (int)dy.size(2),
+                     (int)dy.size(3), (int)k, (int)s, (int)pad, dx.data_ptr<float>(),
+                     cur_stream());
+  return dx;
+}
+
+Tensor avgpool_nhwc_fwd_op(const Tensor& x, int64_t P, int64_t Q) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CL(x);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  auto y = at::empty({N, C, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  avgpool2d_nhwc_fwd(x.data_ptr<float>(), N, H, W, C, (int)P, (int)Q, y.data_ptr<float>(),
+                     cur_stream());
+  return y;
+}
+
+Tensor avgpool_nhwc_bwd_op(const Tensor& dy, std::vector<int64_t> x_shape) {
+  CHECK_GPU(dy); CHECK_F32(dy);
+  auto d = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  auto dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  avgpool2d_nhwc_bwd(d.data_ptr<float>(), (int)x_shape[0], (int)x_shape[2], (int)x_shape[3],
+                     (int)x_shape[1], (int)dy.size(2), (int)dy.size(3), dx.data_ptr<float>(),
+                     cur_stream());
+  return dx;
+}
+
 // NCHW: g = dy*(y>0) (new tensor, or dy itself when y is None); db (optional) = per-channel sum
 Tensor chan_relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
                              const c10::optional<Tensor>& db, double beta) {
@@ -483,16 +583,22 @@ Tensor avgpool_bwd_op(const Tensor& dy, std::vector<int64_t> x_shape) {
 }
 
 Tensor dropout_op(const Tensor& x, double p, int64_t seed) {
-  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  CHECK_GPU(x); CHECK_F32(x);
+  TORCH_CHECK(x.is_non_overlapping_and_dense(), "dropout: dense input expected");
   auto y = at::empty_like(x);
   dropout_apply(x.data_ptr<float>(), x.numel(), (float)p, (uint64_t)seed, y.data_ptr<float>(),
                 cur_stream());
   return y;
 }
 
+// elementwise ops work on any dense layout; operands must share it (callers make them match)
+#define CHECK_SAME_DENSE(a, b)                                                             \
+  TORCH_CHECK((a).is_non_overlapping_and_dense() && (a).sizes() == (b).sizes() &&          \
+                  (a).strides() == (b).strides(),                                          \
+              #a " and " #b " must be dense tensors of the same shape and layout")
+
 Tensor add_relu_op(const Tensor& a, const Tensor& b, bool relu) {
-  CHECK_GPU(a); CHECK_F32(a); CHECK_CONTIG(a); CHECK_CONTIG(b);
-  TORCH_CHECK(a.sizes() == b.sizes(), "add_relu: shape mismatch");
+  CHECK_GPU(a); CHECK_F32(a); CHECK_F32(b); CHECK_SAME_DENSE(a, b);
   auto y = at::empty_like(a);
   add_relu(a.data_ptr<float>(), b.data_ptr<float>(), a.numel(), relu, y.data_ptr<float>(),
            cur_stream());
@@ -500,10 +606,9 @@ Tensor add_relu_op(const Tensor& a, const Tensor& b, bool relu) {
 }
 
 Tensor relu_mask_op(const Tensor& dy, const Tensor& y) {
-  CHECK_GPU(dy); CHECK_F32(dy);
-  auto d = dy.contiguous();
-  auto g = at::empty_like(d);
-  relu_mask(d.data_ptr<float>(), y.data_ptr<float>(), d.numel(), g.data_ptr<float>(),
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_SAME_DENSE(dy, y);
+  auto g = at::empty_like(dy);
+  relu_mask(dy.data_ptr<float>(), y.data_ptr<float>(), dy.numel(), g.data_ptr<float>(),
             cur_stream());
   return g;
 }
@@ -584,11 +689,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_", &clip_op);
   m.def("cast_f32_bf16", &cast_f32_bf16_op);
   m.def("conv2d_fwd", &conv2d_fwd_op);
+  m.def("conv_nhwc_fwd", &conv_nhwc_fwd_op);
+  m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
+  m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
   m.def("conv2d_dgrad", &conv2d_dgrad_op);
   m.def("conv2d_wgrad", &conv2d_wgrad_op);
   m.def("chan_relu_bias_bwd", &chan_relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta") = 0.0);
   m.def("maxpool2d_fwd", &maxpool2d_fwd_op);
+  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd_op);
+  m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd_op);
+  m.def("avgpool_nhwc_fwd", &avgpool_nhwc_fwd_op);
+  m.def("avgpool_nhwc_bwd", &avgpool_nhwc_bwd_op);
   m.def("maxpool2d_bwd", &maxpool2d_bwd_op);
   m.def("avgpool_fwd", &avgpool_fwd_op);
   m.def("avgpool_bwd", &avgpool_bwd_op);

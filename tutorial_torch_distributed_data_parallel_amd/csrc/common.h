@@ -55,4 +55,25 @@ __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Division by a runtime-constant divisor as multiply-high + add + shift (no integer divide in
+// kernel loops); exact for numerators < 2^31.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << s) - d)) / d + 1);
+  if (d == 1) { f.m = 0; f.s = 0; }
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
 }  // namespace tdp

@@ -25,6 +25,14 @@ ConvPlan conv_plan(int mode, const ConvGeom& g, int num_cus);
 void conv_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B, float* C,
               const float* bias, bool relu, float beta, float* ws, hipStream_t s);
 
+// NHWC implicit GEMM on the LDS-DMA MFMA pipeline (gemm_f32_fast.hip). Requires C % 4 == 0,
+// Cout % 4 == 0 and (for DGRAD) power-of-two strides; plan.fm holds the pipeline depth.
+bool conv_nhwc_ok(int mode, const ConvGeom& g);
+ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
+void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
+                   float* C, const float* bias, bool relu, float beta, float* ws,
+                   hipStream_t s);
+
 // NCHW ReLU backward + per-channel bias gradient: g = dy*(y>0) (if y), db = sum over n,hw.
 int chan_splits(int N, int C, int HW, int num_cus);
 void chan_relu_bias_bwd(const float* dy, const float* y, int N, int C, int HW, float* g,

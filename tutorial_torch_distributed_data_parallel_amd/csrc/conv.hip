@@ -25,25 +25,6 @@ namespace {
 constexpr int kCT = 256;
 constexpr int kCBK = 32;
 
-struct FastDiv {
-  uint32_t d, m, s;
-};
-
-FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t s = 0;
-  while ((1u << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << s) - d)) / d + 1);
-  if (d == 1) { f.m = 0; f.s = 0; }
-  return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (__umulhi(n, f.m) + n) >> f.s;  // valid for n < 2^31
-}
-
 struct ConvParams {
   const float* A;    // FWD/DGRAD: weights; WGRAD: dy (gradient of the conv output)
   const float* B;    // FWD/WGRAD: x; DGRAD: dy

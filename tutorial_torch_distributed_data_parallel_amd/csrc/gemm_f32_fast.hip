@@ -21,7 +21,14 @@
 //     the K tail is zeroed on the fragment read of the last tile.
 //   * Block ids are remapped so the workgroups of one XCD share one split-K slice / row panel of
 //     the operand every tile re-reads (L2 locality, guide §5.5 T1; bijective form).
+//   * Implicit-GEMM convolution (NHWC activations) runs through the SAME pipeline: only the
+//     per-lane DMA source addresses change. An "implicit" operand computes, per 16-B chunk, the
+//     activation pixel + channel that GEMM element (row, k) reads (im2col for the forward pass,
+//     its transpose-stride form for the input gradient, shifted pixels for the weight gradient);
+//     taps that fall into the zero padding read a 16-B zero page. With C % 32 == 0 a K tile
+//     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
 #include "common.h"
+#include "conv.h"
 #include "kernels.h"
 
 namespace tdp {
@@ -30,7 +37,20 @@ namespace {
 constexpr int kT = 256;
 constexpr int kBK = 32;
 
+// Geometry of an implicit (convolution) operand; the "row grid" is the pixel grid GEMM rows
+// (FWD/DGRAD A) or GEMM k (WGRAD B) walk over, the source is the NHWC tensor being gathered.
+struct ConvInfo {
+  const float* zero;        // >= 16 B of zeros (padding taps)
+  int Hs, Ws, Cs;           // source tensor dims
+  int S, sh, sw, ph, pw;
+  int shl, swl;             // log2 of the strides (DGRAD)
+  int grid_pq, grid_q;      // row-grid pixels per image / per row
+  int uniform;              // Cs % 32 == 0: one filter tap per K tile
+  FastDiv dC, dS, dPQ, dQ;
+};
+
 struct FastParams {
+  ConvInfo cv;
   const float* A;
   const float* B;
   float* C;
@@ -119,8 +139,167 @@ struct TileSrc {
   }
 };
 
-template <int FN, bool AK, bool BKC, int S>
+// Operand source kinds
+constexpr int kDenseK = 0, kDenseMN = 1, kImFwd = 2, kImDgrad = 3, kImWgrad = 4;
+
+// Implicit K-contiguous A (rows = pixels of the row grid, k = (r, s, c) with c fastest):
+//   FWD   : source x,  pixel (n, p, q), tap reads x[n][p*sh-ph+r][q*sw-pw+s][c]
+//   DGRAD : source dy, pixel (n, h, w) of dx, tap reads dy[n][(h+ph-r)/sh][(w+pw-s)/sw][c]
+//           (only when both divisions are exact; strides are powers of two)
+template <int R, int MODE>
+struct ImSrcA {
+  static constexpr int NPW = R / 8 / 4;
+  const float* img[NPW];
+  int hb[NPW], wb[NPW], koff[NPW];
+
+  __device__ __forceinline__ void init(const FastParams& p, int r0, int rlim, int wid,
+                                       int lane) {
+    const ConvInfo& cv = p.cv;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      const int row = j * 8 + (lane >> 3);
+      int gr = r0 + row;
+      gr = gr < rlim ? gr : rlim - 1;
+      const uint32_t n = fdiv(gr, cv.dPQ);
+      const uint32_t pq = gr - n * cv.grid_pq;
+      const uint32_t y = fdiv(pq, cv.dQ);
+      const uint32_t x = pq - y * cv.grid_q;
+      img[i] = p.A + (long)n * cv.Hs * cv.Ws * cv.Cs;
+      if (MODE == kImFwd) {
+        hb[i] = (int)y * cv.sh - cv.ph;
+        wb[i] = (int)x * cv.sw - cv.pw;
+      } else {
+        hb[i] = (int)y + cv.ph;
+        wb[i] = (int)x + cv.pw;
+      }
+      koff[i] = ((lane & 7) ^ swz(row)) * 4;
+    }
+  }
+
+  __device__ __forceinline__ void issue(const FastParams& p, int k0, int klim, char* dst,
+                                        int wid) const {
+    const ConvInfo& cv = p.cv;
+    int ur = 0, us = 0, uc = 0;
+    if (cv.uniform) {  // k0 is wave-uniform: scalar decomposition, one tap for the whole tile
+      const uint32_t rs = fdiv(k0, cv.dC);
+      uc = k0 - rs * cv.Cs;
+      ur = fdiv(rs, cv.dS);
+      us = rs - ur * cv.S;
+    }
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      const int k = k0 + koff[i];
+      int r, s, c;
+      if (cv.uniform) {
+        r = ur; s = us; c = uc + koff[i];
+      } else {
+        const uint32_t rs = fdiv(k, cv.dC);
+        c = k - rs * cv.Cs;
+        r = fdiv(rs, cv.dS);
+        s = rs - r * cv.S;
+      }
+      bool ok = k < klim;
+      int h, w;
+      if (MODE == kImFwd) {
+        h = hb[i] + r;
+        w = wb[i] + s;
+      } else {
+        const int hh = hb[i] - r, ww = wb[i] - s;
+        ok = ok && hh >= 0 && ww >= 0 && !(hh & ((1 << cv.shl) - 1)) &&
+             !(ww & ((1 << cv.swl) - 1));
+        h = hh >> cv.shl;
+        w = ww >> cv.swl;
+      }
+      ok = ok && (unsigned)h < (unsigned)cv.Hs && (unsigned)w < (unsigned)cv.Ws;
+      const float* src = ok ? img[i] + ((long)h * cv.Ws + w) * cv.Cs + c : cv.zero;
+      glds16(src, dst + j * 1024);
+    }
+  }
+};
+
+// Implicit MN-contiguous B of the weight gradient: k = dy pixel (n, p, q), columns
+// (r, s, c) with c fastest; element = x[n][p*sh-ph+r][q*sw-pw+s][c]. A lane's 4 columns share
+// one tap (Cs % 4 == 0), fixed for the whole kernel; only the pixel changes per tile.
+template <int R>
+struct ImSrcB {
+  static constexpr int CH = (32 * R * 4) / 1024, NPW = CH / 4;
+  static constexpr int LPR = R / 4, RPC = 1024 / (R * 4);
+  int th, tw, coff;
+  int koff[NPW];
+
+  __device__ __forceinline__ void init(const FastParams& p, int r0, int rlim, int wid,
+                                       int lane) {
+    const ConvInfo& cv = p.cv;
+    int gc = r0 + (lane % LPR) * 4;
+    gc = gc < rlim ? gc : rlim - 4;
+    const uint32_t rs = fdiv(gc, cv.dC);
+    coff = gc - rs * cv.Cs;
+    const int r = fdiv(rs, cv.dS);
+    const int s = rs - r * cv.S;
+    th = r - cv.ph;
+    tw = s - cv.pw;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) koff[i] = (wid * NPW + i) * RPC + lane / LPR;
+  }
+
+  __device__ __forceinline__ void issue(const FastParams& p, int k0, int klim, char* dst,
+                                        int wid) const {
+    const ConvInfo& cv = p.cv;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      int gk = k0 + koff[i];
+      gk = gk < klim ? gk : klim - 1;
+      const uint32_t n = fdiv(gk, cv.dPQ);
+      const uint32_t pq = gk - n * cv.grid_pq;
+      const uint32_t y = fdiv(pq, cv.dQ);
+      const uint32_t x = pq - y * cv.grid_q;
+      const int h = (int)y * cv.sh + th, w = (int)x * cv.sw + tw;
+      const bool ok = (unsigned)h < (unsigned)cv.Hs && (unsigned)w < (unsigned)cv.Ws;
+      const float* src =
+          ok ? p.B + (((long)n * cv.Hs + h) * cv.Ws + w) * cv.Cs + coff : cv.zero;
+      glds16(src, dst + j * 1024);
+    }
+  }
+};
+
+template <int R, int KIND, bool IS_A>
+struct SrcOf;
+template <int R, bool IS_A>
+struct SrcOf<R, kDenseK, IS_A> {
+  TileSrc<R, true> t;
+  __device__ __forceinline__ void init(const FastParams& p, int r0, int rlim, int wid, int lane) {
+    t.init(IS_A ? p.A : p.B, IS_A ? p.lda : p.ldb, r0, rlim, wid, lane);
+  }
+  __device__ __forceinline__ void issue(const FastParams&, int k0, int klim, char* dst,
+                                        int wid) const {
+    t.issue(k0, klim, dst, wid);
+  }
+};
+template <int R, bool IS_A>
+struct SrcOf<R, kDenseMN, IS_A> {
+  TileSrc<R, false> t;
+  __device__ __forceinline__ void init(const FastParams& p, int r0, int rlim, int wid, int lane) {
+    t.init(IS_A ? p.A : p.B, IS_A ? p.lda : p.ldb, r0, rlim, wid, lane);
+  }
+  __device__ __forceinline__ void issue(const FastParams&, int k0, int klim, char* dst,
+                                        int wid) const {
+    t.issue(k0, klim, dst, wid);
+  }
+};
+template <int R>
+struct SrcOf<R, kImFwd, true> : ImSrcA<R, kImFwd> {};
+template <int R>
+struct SrcOf<R, kImDgrad, true> : ImSrcA<R, kImDgrad> {};
+template <int R>
+struct SrcOf<R, kImWgrad, false> : ImSrcB<R> {};
+
+template <int FN, int AKIND, int BKIND, int S>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
+  constexpr bool AK = AKIND != kDenseMN;
+  constexpr bool BKC = BKIND == kDenseK;
   constexpr int FM = 2;
   constexpr int BM = 128, BN = 64 * FN;
   constexpr int A_BYTES = BM * kBK * 4, B_BYTES = BN * kBK * 4;
@@ -150,15 +329,15 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   const int ke = min(p.K, kb + p.k_per_split);
   const int nk = (ke - kb + kBK - 1) / kBK;
 
-  TileSrc<BM, AK> srcA;
-  TileSrc<BN, BKC> srcB;
-  srcA.init(p.A, p.lda, m0, p.M, wid, lane);
-  srcB.init(p.B, p.ldb, n0, p.N, wid, lane);
+  SrcOf<BM, AKIND, true> srcA;
+  SrcOf<BN, BKIND, false> srcB;
+  srcA.init(p, m0, p.M, wid, lane);
+  srcB.init(p, n0, p.N, wid, lane);
   auto issue = [&](int t) {
     lds_char* st = smem + (t % S) * STG;
     const int k0 = kb + t * kBK;
-    srcA.issue(k0, ke, st, wid);
-    srcB.issue(k0, ke, st + A_BYTES, wid);
+    srcA.issue(p, k0, ke, st, wid);
+    srcB.issue(p, k0, ke, st + A_BYTES, wid);
   };
 
   f32x16 acc[FM][FN];
@@ -336,17 +515,29 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   }
 }
 
-template <int FN, bool AK, bool BKC, int S>
+template <int FN, int AKIND, int BKIND, int S>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
   constexpr int STG = 128 * kBK * 4 + 64 * FN * kBK * 4;
   const size_t lds = (size_t)S * STG;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AK, BKC, S>,
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AK, BKC, S>), dim3(nblocks), dim3(kT), lds, s, p);
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S>), dim3(nblocks), dim3(kT), lds,
+                     s, p);
+}
+
+template <int AKIND, int BKIND>
+void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s) {
+  if (fn == 1) {
+    if (stages == 3) launch_fast<1, AKIND, BKIND, 3>(p, nblocks, s);
+    else launch_fast<1, AKIND, BKIND, 2>(p, nblocks, s);
+  } else {
+    if (stages == 3) launch_fast<2, AKIND, BKIND, 3>(p, nblocks, s);
+    else launch_fast<2, AKIND, BKIND, 2>(p, nblocks, s);
+  }
 }
 
 }  // namespace
@@ -414,21 +605,98 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
   const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
   const bool ak = a.a_kcontig, bk = a.b_kcontig;
-  const int fn = plan.tile;
-#define TDP_L(FN, AK, BK, S) launch_fast<FN, AK, BK, S>(p, nblocks, s)
-#define TDP_S(FN, AK, BK) \
-  do { if (plan.stages == 3) TDP_L(FN, AK, BK, 3); else TDP_L(FN, AK, BK, 2); } while (0)
-#define TDP_F(AK, BK) \
-  do { if (fn == 1) TDP_S(1, AK, BK); else TDP_S(2, AK, BK); } while (0)
-  if (ak && bk) TDP_F(true, true);
-  else if (ak && !bk) TDP_F(true, false);
-  else if (!ak && !bk) TDP_F(false, false);
-  else TDP_F(false, true);
-#undef TDP_F
-#undef TDP_S
-#undef TDP_L
+  const int fn = plan.tile, st = plan.stages;
+  if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nblocks, s);
+  else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nblocks, s);
+  else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nblocks, s);
+  else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nblocks, s);
   if (plan.splits > 1)
     splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+}
+
+// ------------------------------------------------------------------ implicit-GEMM convolution
+static const float* zero_page() {
+  static float* z = nullptr;
+  if (!z) {
+    (void)hipMalloc(&z, 256);
+    (void)hipMemset(z, 0, 256);
+  }
+  return z;
+}
+
+static int ilog2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+bool conv_nhwc_ok(int mode, const ConvGeom& g) {
+  if (g.C % 4 || g.Cout % 4) return false;
+  if (mode == kConvDgrad && (ilog2_exact(g.sh) < 0 || ilog2_exact(g.sw) < 0)) return false;
+  return true;
+}
+
+ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
+  ConvPlan pl;
+  pl.mode = mode;
+  if (mode == kConvFwd) { pl.M = g.N * g.P * g.Q; pl.N = g.Cout; pl.K = g.R * g.S * g.C; }
+  else if (mode == kConvDgrad) { pl.M = g.N * g.H * g.W; pl.N = g.C; pl.K = g.R * g.S * g.Cout; }
+  else { pl.M = g.Cout; pl.N = g.R * g.S * g.C; pl.K = g.N * g.P * g.Q; }
+  GemmF32Args a{};
+  a.M = pl.M; a.N = pl.N; a.K = pl.K;
+  GemmPlan gp;
+  gemm_f32_fast_plan(a, num_cus, gp);
+  pl.fn = gp.tile;
+  pl.fm = gp.stages;  // pipeline depth (the NHWC path always uses BM = 128)
+  pl.splits = gp.splits;
+  pl.k_per_split = gp.k_per_split;
+  pl.ws_floats = gp.ws_floats;
+  return pl;
+}
+
+// FWD  : A = x (NHWC), B = Wt [Cout][R*S*C],  C = y  [N*P*Q][Cout] (+bias, relu)
+// DGRAD: A = dy (NHWC), B = W2 [R*S*Cout][C], C = dx [N*H*W][C]
+// WGRAD: A = dy [N*P*Q][Cout], B = x (NHWC),  C = dWt [Cout][R*S*C] (beta: accumulate)
+void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
+                   float* C, const float* bias, bool relu, float beta, float* ws,
+                   hipStream_t s) {
+  FastParams p{};
+  ConvInfo& cv = p.cv;
+  cv.zero = zero_page();
+  cv.S = g.S; cv.sh = g.sh; cv.sw = g.sw; cv.ph = g.ph; cv.pw = g.pw;
+  cv.shl = ilog2_exact(g.sh) < 0 ? 0 : ilog2_exact(g.sh);
+  cv.swl = ilog2_exact(g.sw) < 0 ? 0 : ilog2_exact(g.sw);
+  if (pl.mode == kConvDgrad) {
+    cv.Hs = g.P; cv.Ws = g.Q; cv.Cs = g.Cout;
+    cv.grid_pq = g.H * g.W; cv.grid_q = g.W;
+  } else {
+    cv.Hs = g.H; cv.Ws = g.W; cv.Cs = g.C;
+    cv.grid_pq = g.P * g.Q; cv.grid_q = g.Q;
+  }
+  cv.uniform = (cv.Cs % 32 == 0) ? 1 : 0;
+  cv.dC = make_fastdiv(cv.Cs);
+  cv.dS = make_fastdiv(g.S);
+  cv.dPQ = make_fastdiv(cv.grid_pq);
+  cv.dQ = make_fastdiv(cv.grid_q);
+  p.A = A; p.B = B; p.C = C; p.bias = bias; p.ws = ws;
+  p.rowsum = nullptr; p.rowsum_beta = 0.f;
+  p.M = pl.M; p.N = pl.N; p.K = pl.K;
+  if (pl.mode == kConvFwd) { p.lda = 0; p.ldb = pl.K; p.ldc = pl.N; }
+  else if (pl.mode == kConvDgrad) { p.lda = 0; p.ldb = pl.N; p.ldc = pl.N; }
+  else { p.lda = pl.M; p.ldb = 0; p.ldc = pl.N; }
+  p.k_per_split = pl.k_per_split;
+  p.splits = pl.splits;
+  p.tiles_m = ceil_div(pl.M, 128);
+  p.tiles_n = ceil_div(pl.N, 64 * pl.fn);
+  p.beta = pl.splits > 1 ? 0.f : beta;
+  p.relu = (pl.splits > 1 ? false : relu) ? 1 : 0;
+  const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
+  const int fn = pl.fn, st = pl.fm;
+  if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s);
+  else if (pl.mode == kConvDgrad) launch_kinds<kImDgrad, kDenseMN>(p, fn, st, nblocks, s);
+  else launch_kinds<kDenseMN, kImWgrad>(p, fn, st, nblocks, s);
+  if (pl.splits > 1)
+    splitk_reduce(ws, pl.splits, pl.M, pl.N, C, false, pl.N, bias, beta, relu, s);
 }
 
 }  // namespace tdp

@@ -151,6 +151,107 @@ __global__ void relu_mask_kernel(const float* __restrict__ dy, const float* __re
     g[i] = y[i] > 0.f ? dy[i] : 0.f;
 }
 
+// ---- NHWC (channels_last) variants: consecutive threads walk the channel dimension, so every
+// access is coalesced; index math is 32-bit (host checks numel < 2^31).
+__global__ void maxpool_nhwc_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C,
+                                        int P, int Q, int k, int s, int pad,
+                                        float* __restrict__ y, int* __restrict__ idx) {
+  const unsigned total = (unsigned)N * P * Q * C;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const unsigned c = i % C, t = i / C;
+    const unsigned q = t % Q, t2 = t / Q;
+    const unsigned p = t2 % P, n = t2 / P;
+    const int h0 = (int)p * s - pad, w0 = (int)q * s - pad;
+    const float* xp = x + (size_t)n * H * W * C + c;
+    float best = -INFINITY;
+    int bi = -1;
+    for (int r = 0; r < k; ++r) {
+      const int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      for (int cc = 0; cc < k; ++cc) {
+        const int w = w0 + cc;
+        if (w < 0 || w >= W) continue;
+        const float v = xp[(size_t)(h * W + w) * C];
+        if (bi < 0 || (v > best && best == best) || (v != v && best == best)) {
+          best = v;
+          bi = h * W + w;
+        }
+      }
+    }
+    y[i] = best;
+    idx[i] = bi;
+  }
+}
+
+__global__ void maxpool_nhwc_bwd_kernel(const float* __restrict__ dy, const int* __restrict__ idx,
+                                        int N, int H, int W, int C, int P, int Q, int k, int s,
+                                        int pad, float* __restrict__ dx) {
+  const unsigned total = (unsigned)N * H * W * C;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const unsigned c = i % C, t = i / C;
+    const int w = (int)(t % W);
+    const unsigned t2 = t / W;
+    const int h = (int)(t2 % H);
+    const unsigned n = t2 / H;
+    const int me = h * W + w;
+    const int plo = max(0, (h + pad - k + s) / s), phi = min(P - 1, (h + pad) / s);
+    const int qlo = max(0, (w + pad - k + s) / s), qhi = min(Q - 1, (w + pad) / s);
+    float acc = 0.f;
+    for (int p = plo; p <= phi; ++p)
+      for (int q = qlo; q <= qhi; ++q) {
+        const size_t o = (((size_t)n * P + p) * Q + q) * C + c;
+        if (idx[o] == me) acc += dy[o];
+      }
+    dx[i] = acc;
+  }
+}
+
+__global__ void avgpool_nhwc_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C,
+                                        int P, int Q, float* __restrict__ y) {
+  const unsigned total = (unsigned)N * P * Q * C;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const unsigned c = i % C, t = i / C;
+    const int q = (int)(t % Q);
+    const unsigned t2 = t / Q;
+    const int p = (int)(t2 % P);
+    const unsigned n = t2 / P;
+    const int h0 = (p * H) / P, h1 = ((p + 1) * H + P - 1) / P;
+    const int w0 = (q * W) / Q, w1 = ((q + 1) * W + Q - 1) / Q;
+    const float* xp = x + (size_t)n * H * W * C + c;
+    float acc = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) acc += xp[(size_t)(h * W + w) * C];
+    y[i] = acc / (float)((h1 - h0) * (w1 - w0));
+  }
+}
+
+__global__ void avgpool_nhwc_bwd_kernel(const float* __restrict__ dy, int N, int H, int W, int C,
+                                        int P, int Q, float* __restrict__ dx) {
+  const unsigned total = (unsigned)N * H * W * C;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const unsigned c = i % C, t = i / C;
+    const int w = (int)(t % W);
+    const unsigned t2 = t / W;
+    const int h = (int)(t2 % H);
+    const unsigned n = t2 / H;
+    float acc = 0.f;
+    for (int p = (h * P) / H; p < P && (p * H) / P <= h; ++p) {
+      const int h0 = (p * H) / P, h1 = ((p + 1) * H + P - 1) / P;
+      if (h < h0 || h >= h1) continue;
+      for (int q = (w * Q) / W; q < Q && (q * W) / Q <= w; ++q) {
+        const int w0 = (q * W) / Q, w1 = ((q + 1) * W + Q - 1) / Q;
+        if (w < w0 || w >= w1) continue;
+        acc += dy[(((size_t)n * P + p) * Q + q) * C + c] / (float)((h1 - h0) * (w1 - w0));
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
 }  // namespace
 
 void maxpool2d_fwd(const float* x, int NC, int H, int W, int P, int Q, int k, int s, int pad,
@@ -184,6 +285,30 @@ void dropout_apply(const float* x, long n, float p, uint64_t seed, float* y, hip
 void add_relu(const float* a, const float* b, long n, bool relu, float* y, hipStream_t st) {
   hipLaunchKernelGGL(add_relu_kernel, dim3(ew_grid(n)), dim3(256), 0, st, a, b, n, relu ? 1 : 0,
                      y);
+}
+
+void maxpool2d_nhwc_fwd(const float* x, int N, int H, int W, int C, int P, int Q, int k, int s,
+                        int pad, float* y, int* idx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_nhwc_fwd_kernel, dim3(ew_grid((long)N * P * Q * C)), dim3(256), 0,
+                     st, x, N, H, W, C, P, Q, k, s, pad, y, idx);
+}
+
+void maxpool2d_nhwc_bwd(const float* dy, const int* idx, int N, int H, int W, int C, int P, int Q,
+                        int k, int s, int pad, float* dx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel, dim3(ew_grid((long)N * H * W * C)), dim3(256), 0,
+                     st, dy, idx, N, H, W, C, P, Q, k, s, pad, dx);
+}
+
+void avgpool2d_nhwc_fwd(const float* x, int N, int H, int W, int C, int P, int Q, float* y,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_nhwc_fwd_kernel, dim3(ew_grid((long)N * P * Q * C)), dim3(256), 0,
+                     st, x, N, H, W, C, P, Q, y);
+}
+
+void avgpool2d_nhwc_bwd(const float* dy, int N, int H, int W, int C, int P, int Q, float* dx,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_nhwc_bwd_kernel, dim3(ew_grid((long)N * H * W * C)), dim3(256), 0,
+                     st, dy, N, H, W, C, P, Q, dx);
 }
 
 void relu_mask(const float* dy, const float* y, long n, float* g, hipStream_t st) {

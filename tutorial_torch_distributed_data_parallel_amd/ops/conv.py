@@ -2,12 +2,21 @@
 
 Replaces MIOpen for the CNN models (SURVEY.md §2.3 N4; §2.5 K1/K4/K6-K8 forward, K22 backward;
 torchvision AlexNet features, REF/data_and_toy_model.py:41-45; ResNet-50 for the "ResNet-50-sized
-CNN" config). Three kernels, none of which materialises an im2col buffer (``csrc/conv.hip``):
-  * forward  ``y = relu?(conv(x, W) + b)`` -- bias and ReLU in the epilogue (K2 disappears);
-  * input gradient (dgrad) -- strided convs handled by the divisibility test in the gather;
-  * weight gradient (wgrad) -- split-K over the N*P*Q pixel reduction, written straight into the
-    DDP gradient arena (``_grad.grad_dest``).
-The ReLU mask and the per-channel bias gradient are one pass over ``dy`` (``chan_relu_bias_bwd``).
+CNN" config). No im2col buffer is ever materialised.
+
+Main path -- channels_last (NHWC) activations on the LDS-DMA MFMA GEMM pipeline
+(``csrc/gemm_f32_fast.hip``, implicit operand sources):
+  * forward  ``y[(n,p,q)][co] = relu?(sum_(r,s,c) x[n][p*sh-ph+r][q*sw-pw+s][c] * W[co][c][r][s] + b)``
+    -- K is ordered (r, s, c) so every 16-B DMA chunk is 4 contiguous channels of one pixel;
+  * input gradient -- the same gather on ``dy`` with the transpose-stride test;
+  * weight gradient -- ``dy^T`` (a plain [pixels][Cout] matrix) times shifted-pixel rows of ``x``,
+    split-K over the N*P*Q reduction.
+  Outputs are channels_last, so a 1x1 convolution IS a GEMM ([N*H*W, C] x [C, Cout]); batch norm
+  and the ReLU/bias backward treat NHWC tensors as [pixels, C] matrices. Weights keep torch's
+  [Cout][C][R][S] layout (checkpoint compatible); R x S > 1 convs use a transposed copy per step.
+  Input channels that are not a multiple of 4 (the RGB stem) are zero-padded to 4.
+Fallback -- NCHW register-staged implicit GEMM (``csrc/conv.hip``) for shapes the NHWC path does
+not take (channel counts not a multiple of 4 beyond the stem, non power-of-two strides in dgrad).
 CPU tensors run ``torch.nn.functional.conv2d`` (the oracle of the CPU tests).
 Groups and dilation are not supported (no model here uses them).
 """
@@ -61,15 +70,100 @@ class _Conv2dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+_CL = torch.channels_last
+
+
+def _rows(t):
+    """[N, C, H, W] channels_last tensor -> its [N*H*W, C] storage as a 2-D view."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+class _ConvNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, relu: bool):
+        C = native()
+        N, Cin, H, W = x.shape
+        Cout, _, R, S = weight.shape
+        Cp = (Cin + 3) // 4 * 4
+        sh, sw = stride
+        ph, pw = padding
+        if Cp != Cin:  # zero-pad the channels (RGB stem) so every DMA chunk is 4 channels
+            xp = torch.zeros((N, Cp, H, W), device=x.device, dtype=x.dtype, memory_format=_CL)
+            xp[:, :Cin].copy_(x)
+        else:
+            xp = x.contiguous(memory_format=_CL)
+        wt = weight.permute(0, 2, 3, 1)  # [Cout, R, S, C]: k = (r, s, c)
+        if Cp != Cin:
+            wt = F.pad(wt, (0, Cp - Cin))
+        wt = wt.contiguous()
+        y = C.conv_nhwc_fwd(xp, wt, bias, R, S, sh, sw, ph, pw, relu)
+        ctx.geom = (R, S, sh, sw, ph, pw, Cin, Cp)
+        ctx.relu = relu
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(xp, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        xp, weight, y = ctx.saved_tensors
+        w_param, b_param = ctx.params
+        R, S, sh, sw, ph, pw, Cin, Cp = ctx.geom
+        Cout = weight.shape[0]
+        dy = dy.contiguous(memory_format=_CL)
+        want_db = b_param is not None and needs(ctx, 2)
+        db = grad_dest(b_param) if want_db else None
+        # ReLU mask + bias gradient: one pass over dy viewed as [pixels, Cout]
+        if ctx.relu or want_db:
+            g2 = C.relu_bias_bwd(_rows(dy), _rows(y) if ctx.relu else None, db)
+            g = g2.view(dy.shape[0], dy.shape[2], dy.shape[3], Cout).permute(0, 3, 1, 2)
+        else:
+            g = dy
+        dx = dw = None
+        if needs(ctx, 1):
+            dw = grad_dest(w_param)
+            if R == 1 and S == 1 and Cp == Cin:
+                C.conv_nhwc_wgrad(g, xp, dw, R, S, sh, sw, ph, pw, 0.0)  # [Cout][C] already
+            else:
+                dwt = torch.empty((Cout, R, S, Cp), device=dy.device, dtype=dy.dtype)
+                C.conv_nhwc_wgrad(g, xp, dwt, R, S, sh, sw, ph, pw, 0.0)
+                dw.copy_(dwt[..., :Cin].permute(0, 3, 1, 2))
+        if needs(ctx, 0):
+            w2 = weight.permute(2, 3, 0, 1)  # [R, S, Cout, C]: k = (r, s, co), n = c
+            if Cp != Cin:
+                w2 = F.pad(w2, (0, Cp - Cin))
+            w2 = w2.contiguous()
+            dx = C.conv_nhwc_dgrad(g, w2, list(xp.shape), R, S, sh, sw, ph, pw)
+            if Cp != Cin:
+                dx = dx[:, :Cin]
+        return dx, dw, db, None, None, None
+
+
+FORCE_NCHW = False  # tests: route every conv through the NCHW fallback kernels
+
+
+def _nhwc_ok(x, weight, stride):
+    if FORCE_NCHW:
+        return False
+    Cin, Cout = weight.shape[1], weight.shape[0]
+    pow2 = all(s > 0 and (s & (s - 1)) == 0 for s in stride)
+    return (Cin % 4 == 0 or Cin < 4) and Cout % 4 == 0 and (pow2 or not x.requires_grad)
+
+
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            stride=1, padding=0, relu: bool = False) -> torch.Tensor:
-    """``relu?(conv2d(x, weight, bias, stride, padding))`` for NCHW float32 tensors."""
+    """``relu?(conv2d(x, weight, bias, stride, padding))`` for float32 [N, C, H, W] tensors.
+
+    On the GPU the result is channels_last (NHWC memory, logical NCHW shape, as torch does for
+    channels_last inputs)."""
     stride, padding = _pair(stride), _pair(padding)
     if not x.is_cuda:
         y = F.conv2d(x, weight, bias, stride, padding)
         return F.relu(y) if relu else y
     if x.dtype != torch.float32:
         raise TypeError(f"native conv2d expects float32 activations, got {x.dtype}")
+    if _nhwc_ok(x, weight, stride):
+        return _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu)
     return _Conv2dFn.apply(x.contiguous(), weight.contiguous(), bias, stride, padding, relu)
 
 

@@ -89,6 +89,20 @@ class _TorchKernels:
 _TORCH_K = _TorchKernels()
 
 
+def _is_nhwc(x) -> bool:
+    return x.dim() == 4 and not x.is_contiguous() and \
+        x.is_contiguous(memory_format=torch.channels_last)
+
+
+def _rows(x):
+    return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
+
+def _unrows(y2, shape4):
+    N, C, H, W = shape4
+    return y2.view(N, H, W, C).permute(0, 3, 1, 2)
+
+
 def _kernels(x):
     return native() if x.is_cuda else _TORCH_K
 
@@ -97,8 +111,12 @@ class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group):
         K = _kernels(x)
-        x = x.contiguous()
         C = x.shape[1]
+        # channels_last (NHWC) activations are a [pixels, C] matrix: the BatchNorm1d kernels
+        # (64 adjacent channels per workgroup, coalesced) apply unchanged
+        ctx.nhwc = x.is_cuda and _is_nhwc(x)
+        ctx.shape4 = tuple(x.shape)
+        x = _rows(x) if ctx.nhwc else x.contiguous()
         st = K.bn_moments(x)[0]
         gathered = group.all_gather_flat(st) if group is not None else st
         stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var)
@@ -107,13 +125,14 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.group = group
         ctx.save_for_backward(x, weight, stats, y if relu else None)
-        return y
+        return _unrows(y, ctx.shape4) if ctx.nhwc else y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, stats, y = ctx.saved_tensors
         K = _kernels(x)
-        dy = dy.contiguous()
+        dy = _rows(dy.contiguous(memory_format=torch.channels_last)) if ctx.nhwc \
+            else dy.contiguous()
         w_param, b_param = ctx.params
         dw = grad_dest(w_param) if (w_param is not None and needs(ctx, 1)) else None
         db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
@@ -123,6 +142,8 @@ class _BatchNormFn(torch.autograd.Function):
             if ctx.group is not None:
                 ctx.group.all_reduce_sum_(sums)
             dx = K.bn_bwd_elemt(dy, x, stats, weight, sums, y)
+            if ctx.nhwc:
+                dx = _unrows(dx, ctx.shape4)
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -136,6 +157,10 @@ def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
                                   float(eps), bool(relu), group)
     if x.is_cuda and not (torch.is_grad_enabled() and (x.requires_grad or (
             weight is not None and weight.requires_grad))):
+        if _is_nhwc(x):
+            y2 = native().bn_eval(_rows(x), running_mean, running_var, weight, bias, float(eps),
+                                  bool(relu))
+            return _unrows(y2, tuple(x.shape))
         return native().bn_eval(x.contiguous(), running_mean, running_var, weight, bias,
                                 float(eps), bool(relu))
     # inference-mode BN that must be differentiated (frozen-BN fine-tuning): a per-channel affine

@@ -18,10 +18,26 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
+_CL = torch.channels_last
+
+
+def is_nhwc(x) -> bool:
+    """channels_last memory that is not also plain-contiguous (1x1 spatial maps are both)."""
+    return x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=_CL)
+
+
+def _fmt(x):
+    return _CL if is_nhwc(x) else torch.contiguous_format
+
+
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):
-        y, idx = native().maxpool2d_fwd(x, k, s, p)
+        ctx.nhwc = is_nhwc(x)
+        if ctx.nhwc:
+            y, idx = native().maxpool_nhwc_fwd(x, k, s, p)
+        else:
+            y, idx = native().maxpool2d_fwd(x, k, s, p)
         ctx.save_for_backward(idx)
         ctx.cfg = (list(x.shape), k, s, p)
         ctx.mark_non_differentiable(idx)
@@ -31,7 +47,11 @@ class _MaxPoolFn(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         shape, k, s, p = ctx.cfg
-        return native().maxpool2d_bwd(dy.contiguous(), idx, shape, k, s, p), None, None, None
+        if ctx.nhwc:
+            dx = native().maxpool_nhwc_bwd(dy.contiguous(memory_format=_CL), idx, shape, k, s, p)
+        else:
+            dx = native().maxpool2d_bwd(dy.contiguous(), idx, shape, k, s, p)
+        return dx, None, None, None
 
 
 def max_pool2d(x, kernel_size, stride=None, padding=0):
@@ -43,17 +63,22 @@ def max_pool2d(x, kernel_size, stride=None, padding=0):
         return F.max_pool2d(x, k, s, p)
     if k[0] != k[1] or s[0] != s[1] or p[0] != p[1]:
         raise NotImplementedError("native max_pool2d supports square windows only")
-    return _MaxPoolFn.apply(x.contiguous(), k[0], s[0], p[0])
+    return _MaxPoolFn.apply(x.contiguous(memory_format=_fmt(x)), k[0], s[0], p[0])
 
 
 class _AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, P, Q):
         ctx.shape = list(x.shape)
+        ctx.nhwc = is_nhwc(x)
+        if ctx.nhwc:
+            return native().avgpool_nhwc_fwd(x, P, Q)
         return native().avgpool_fwd(x, P, Q)
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.nhwc:
+            return native().avgpool_nhwc_bwd(dy, ctx.shape), None, None
         return native().avgpool_bwd(dy, ctx.shape), None, None
 
 
@@ -63,20 +88,20 @@ def adaptive_avg_pool2d(x, output_size):
         return x  # identity (torch launches a copy kernel here)
     if not x.is_cuda:
         return F.adaptive_avg_pool2d(x, (P, Q))
-    return _AvgPoolFn.apply(x.contiguous(), P, Q)
+    return _AvgPoolFn.apply(x.contiguous(memory_format=_fmt(x)), P, Q)
 
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p, seed):
-        ctx.cfg = (p, seed)
+        ctx.cfg = (p, seed, _fmt(x))
         return native().dropout(x, p, seed)
 
     @staticmethod
     def backward(ctx, dy):
-        p, seed = ctx.cfg
-        # same (seed, index) hash -> same mask, same 1/(1-p) scale
-        return native().dropout(dy.contiguous(), p, seed), None, None
+        p, seed, fmt = ctx.cfg
+        # same (seed, memory index) hash -> same mask, same 1/(1-p) scale
+        return native().dropout(dy.contiguous(memory_format=fmt), p, seed), None, None
 
 
 def dropout(x, p: float = 0.5, training: bool = True, generator=None):
@@ -89,20 +114,21 @@ def dropout(x, p: float = 0.5, training: bool = True, generator=None):
     if not x.is_cuda:
         return F.dropout(x, p, True)
     seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item())
-    return _DropoutFn.apply(x.contiguous(), float(p), seed)
+    return _DropoutFn.apply(x.contiguous(memory_format=_fmt(x)), float(p), seed)
 
 
 class _AddReluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b):
         y = native().add_relu(a, b, True)
+        ctx.fmt = _fmt(a)
         ctx.save_for_backward(y)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        g = native().relu_mask(dy, y)
+        g = native().relu_mask(dy.contiguous(memory_format=ctx.fmt), y)
         return g, g
 
 
@@ -110,4 +136,5 @@ def add_relu(a, b):
     """``relu(a + b)`` -- the residual join of a ResNet block."""
     if not a.is_cuda:
         return F.relu(a + b)
-    return _AddReluFn.apply(a.contiguous(), b.contiguous())
+    fmt = _fmt(a)
+    return _AddReluFn.apply(a.contiguous(memory_format=fmt), b.contiguous(memory_format=fmt))
