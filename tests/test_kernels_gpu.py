@@ -162,7 +162,8 @@ def test_multi_tensor_sgd_adam(C):
         _close(p, r.detach(), atol=1e-6)
 
 
-@pytest.mark.parametrize("shape", [(128, 4096), (32, 64, 7, 7), (5, 3), (8, 16, 33)])
+@pytest.mark.parametrize("shape", [(128, 4096), (32, 64, 7, 7), (5, 3), (8, 16, 33), (1000, 64),
+                                   (300, 2048), (77, 12), (6000, 256)])
 def test_batchnorm_kernels(C, shape):
     torch.manual_seed(6)
     x = torch.randn(shape, device="cuda") * 3 + 1

@@ -13,6 +13,8 @@
 // channels (one per lane, coalesced across the wave) and its 4 waves split the rows; for HW > 1 a
 // workgroup owns one channel (coalesced along HW). Either way the N*HW axis can additionally be
 // split over blockIdx.y so that a small-C layer still puts >= 1 workgroup on every CU.
+#include <initializer_list>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -275,6 +277,223 @@ __global__ __launch_bounds__(256) void bwd_elemt_kernel(
   }
 }
 
+// ------------------------------------------------------------------ [rows, C] with C % 4 == 0
+// BatchNorm1d and channels_last BatchNorm2d (NHWC activations are a [pixels, C] matrix). A
+// workgroup owns CB = min(C, 1024) channels; a thread owns 4 adjacent channels (one 16-B load
+// per row, rows coalesced across lanes) and walks rows with stride RPW = 256 / (CB / 4); the
+// RPW row groups are merged through LDS. One reciprocal per row serves 4 Welford updates.
+__device__ __forceinline__ void rows4_layout(int C, int& CB, int& LPR, int& RPW) {
+  CB = C < 1024 ? C : 1024;
+  LPR = CB / 4;
+  RPW = 256 / LPR;
+}
+
+__global__ __launch_bounds__(256) void moments_rows4(const float* __restrict__ x, int N, int C,
+                                                     int splits, float* __restrict__ ws,
+                                                     float* __restrict__ mean,
+                                                     float* __restrict__ var) {
+  __shared__ float sh[3][1024];
+  int CB, LPR, RPW;
+  rows4_layout(C, CB, LPR, RPW);
+  const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
+  const int c = blockIdx.x * CB + 4 * cq;
+  const bool act = rg < RPW && c < C;
+  long b, e;
+  range_of(N, splits, blockIdx.y, b, e);
+  float n = 0.f, mu[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+#pragma unroll 4
+    for (long r = b + rg; r < e; r += RPW) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + c);
+      n += 1.f;
+      const float inv = 1.f / n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[j] - mu[j];
+        mu[j] = fmaf(d, inv, mu[j]);
+        m2[j] = fmaf(d, v[j] - mu[j], m2[j]);
+      }
+    }
+  }
+  if (rg < RPW) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = rg * CB + 4 * cq + j;
+      sh[0][s] = n;
+      sh[1][s] = mu[j];
+      sh[2][s] = m2[j];
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < CB; k += 256) {
+    const int ch = blockIdx.x * CB + k;
+    if (ch >= C) continue;
+    Wf w{0.f, 0.f, 0.f};
+    for (int g = 0; g < RPW; ++g)
+      w = wf_merge(w, Wf{sh[0][g * CB + k], sh[1][g * CB + k], sh[2][g * CB + k]});
+    if (splits == 1) {
+      mean[ch] = w.mean;
+      var[ch] = w.n > 0.f ? w.m2 / w.n : 0.f;
+    } else {
+      float* o = ws + (long)blockIdx.y * 3 * C;
+      o[ch] = w.n; o[C + ch] = w.mean; o[2 * C + ch] = w.m2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bwd_reduce_rows4(const float* __restrict__ dy,
+                                                        const float* __restrict__ x,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ yr, int N,
+                                                        int C, int splits,
+                                                        float* __restrict__ part) {
+  __shared__ float sh[2][1024];
+  int CB, LPR, RPW;
+  rows4_layout(C, CB, LPR, RPW);
+  const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
+  const int c = blockIdx.x * CB + 4 * cq;
+  const bool act = rg < RPW && c < C;
+  long b, e;
+  range_of(N, splits, blockIdx.y, b, e);
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
+#pragma unroll 4
+    for (long r = b + rg; r < e; r += RPW) {
+      const long off = r * C + c;
+      f32x4 d = *reinterpret_cast<const f32x4*>(dy + off);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + off);
+      if (yr) {
+        const f32x4 yv = *reinterpret_cast<const f32x4*>(yr + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] += d[j];
+        m[j] = fmaf(d[j], xv[j] - mu[j], m[j]);
+      }
+    }
+  }
+  if (rg < RPW) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sh[0][rg * CB + 4 * cq + j] = a[j];
+      sh[1][rg * CB + 4 * cq + j] = m[j];
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < CB; k += 256) {
+    const int ch = blockIdx.x * CB + k;
+    if (ch >= C) continue;
+    float sa = 0.f, sm = 0.f;
+    for (int g = 0; g < RPW; ++g) {
+      sa += sh[0][g * CB + k];
+      sm += sh[1][g * CB + k];
+    }
+    float* o = part + (long)blockIdx.y * 2 * C;
+    o[ch] = sa;
+    o[C + ch] = sm;
+  }
+}
+
+// y = relu?(x * sc + sh) with per-channel sc/sh computed once per thread
+__global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
+                                                   const float* __restrict__ mean,
+                                                   const float* __restrict__ invstd,
+                                                   const float* __restrict__ w,
+                                                   const float* __restrict__ bb, int N, int C,
+                                                   int splits, int relu, int eval, float eps,
+                                                   float* __restrict__ y) {
+  int CB, LPR, RPW;
+  rows4_layout(C, CB, LPR, RPW);
+  const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
+  const int c = blockIdx.x * CB + 4 * cq;
+  if (rg >= RPW || c >= C) return;
+  long b, e;
+  range_of(N, splits, blockIdx.y, b, e);
+  float sc[4], sf[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float is = eval ? rsqrtf(invstd[c + j] + eps) : invstd[c + j];
+    sc[j] = is * (w ? w[c + j] : 1.f);
+    sf[j] = (bb ? bb[c + j] : 0.f) - mean[c + j] * sc[j];
+  }
+#pragma unroll 4
+  for (long r = b + rg; r < e; r += RPW) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float q = fmaf(v[j], sc[j], sf[j]);
+      o[j] = relu ? fmaxf(q, 0.f) : q;
+    }
+    *reinterpret_cast<f32x4*>(y + r * C + c) = o;
+  }
+}
+
+// dx = d*k1 + x*k2 + k3 (d = dy masked by y > 0), constants per channel
+__global__ __launch_bounds__(256) void bwd_elemt_rows4(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ w,
+    const float* __restrict__ sums, const float* __restrict__ yr, const float* __restrict__ cnt,
+    int N, int C, int splits, float* __restrict__ dx) {
+  int CB, LPR, RPW;
+  rows4_layout(C, CB, LPR, RPW);
+  const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
+  const int c = blockIdx.x * CB + 4 * cq;
+  if (rg >= RPW || c >= C) return;
+  long b, e;
+  range_of(N, splits, blockIdx.y, b, e);
+  const float inv_count = 1.f / cnt[0];
+  float k1[4], k2[4], k3[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float is = invstd[c + j];
+    const float mdy = sums[c + j] * inv_count;
+    const float mdyx = sums[C + c + j] * inv_count;
+    const float sw = is * (w ? w[c + j] : 1.f);
+    const float q = is * is * mdyx;
+    k1[j] = sw;
+    k2[j] = -q * sw;
+    k3[j] = (mean[c + j] * q - mdy) * sw;
+  }
+#pragma unroll 4
+  for (long r = b + rg; r < e; r += RPW) {
+    const long off = r * C + c;
+    f32x4 d = *reinterpret_cast<const f32x4*>(dy + off);
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + off);
+    if (yr) {
+      const f32x4 yv = *reinterpret_cast<const f32x4*>(yr + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaf(d[j], k1[j], fmaf(xv[j], k2[j], k3[j]));
+    *reinterpret_cast<f32x4*>(dx + off) = o;
+  }
+}
+
+inline bool rows4_ok(int C, int HW, std::initializer_list<const void*> ptrs) {
+  if (HW != 1 || C % 4) return false;
+  for (const void* q : ptrs)
+    if (q && ((uintptr_t)q & 15)) return false;
+  return true;
+}
+
+inline int rows4_nblk(int C) { return (C + 1023) / 1024; }
+
+// row splits for the streaming (elementwise) rows4 kernels: ~4 workgroups per CU
+inline int rows4_ew_splits(int N, int C) {
+  const int CB = C < 1024 ? C : 1024, RPW = 256 / (CB / 4);
+  const int nblk = rows4_nblk(C);
+  long s = (1024 + nblk - 1) / nblk;
+  const long cap = (N + 4L * RPW - 1) / (4L * RPW);  // >= 4 row iterations per thread
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : (int)s;
+}
+
 inline int ew_grid(long total) {
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
@@ -284,6 +503,14 @@ inline int ew_grid(long total) {
 }  // namespace
 
 int bn_splits(int N, int C, int HW, int num_cus) {
+  if (HW == 1 && C % 4 == 0) {  // rows4 kernels: ~4 workgroups per CU, >= 8 row iterations
+    const int CB = C < 1024 ? C : 1024, RPW = 256 / (CB / 4);
+    const int nblk = rows4_nblk(C);
+    long s = (4L * num_cus + nblk - 1) / nblk;
+    const long cap = (N + 8L * RPW - 1) / (8L * RPW);
+    if (s > cap) s = cap;
+    return s < 1 ? 1 : (int)s;
+  }
   if (HW == 1) {
     const int blocks = (C + 63) / 64;
     int s = (num_cus + blocks - 1) / blocks;
@@ -301,7 +528,10 @@ long bn_ws_floats(int C, int splits) { return 3L * C * (splits > 0 ? splits : 1)
 
 void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, float* mean,
                 float* var, hipStream_t s) {
-  if (HW == 1)
+  if (rows4_ok(C, HW, {x}))
+    hipLaunchKernelGGL(moments_rows4, dim3(rows4_nblk(C), splits), dim3(256), 0, s, x, N, C,
+                       splits, ws, mean, var);
+  else if (HW == 1)
     hipLaunchKernelGGL(moments_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, x, N, C, splits,
                        ws, mean, var);
   else
@@ -320,6 +550,12 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
 
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s) {
+  if (rows4_ok(C, HW, {x, y, mean, invstd, w, b})) {
+    const int sp = rows4_ew_splits(N, C);
+    hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, mean, invstd, w,
+                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, y);
+    return;
+  }
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, mean, invstd, w, b,
                      total, C, HW, relu ? 1 : 0, 0, 0.f, y);
@@ -327,6 +563,12 @@ void bn_elemt(const float* x, const float* mean, const float* invstd, const floa
 
 void bn_eval(const float* x, const float* rmean, const float* rvar, const float* w,
              const float* b, int N, int C, int HW, float eps, bool relu, float* y, hipStream_t s) {
+  if (rows4_ok(C, HW, {x, y})) {
+    const int sp = rows4_ew_splits(N, C);
+    hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, rmean, rvar, w,
+                       b, N, C, sp, relu ? 1 : 0, 1, eps, y);
+    return;
+  }
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, rmean, rvar, w, b,
                      total, C, HW, relu ? 1 : 0, 1, eps, y);
@@ -336,7 +578,10 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
                    const float* y_relu, int N, int C, int HW, int splits, float* ws, float* sums,
                    float* dw, float* db, float grad_beta, hipStream_t s) {
   // partials always go through ws (2*C*splits floats); the final kernel also writes dw/db
-  if (HW == 1)
+  if (rows4_ok(C, HW, {dy, x, y_relu, mean}))
+    hipLaunchKernelGGL(bwd_reduce_rows4, dim3(rows4_nblk(C), splits), dim3(256), 0, s, dy, x,
+                       mean, y_relu, N, C, splits, ws);
+  else if (HW == 1)
     hipLaunchKernelGGL(bwd_reduce_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, dy, x, mean,
                        y_relu, N, C, splits, ws);
   else
@@ -349,6 +594,12 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
                   int N, int C, int HW, float* dx, hipStream_t s) {
+  if (rows4_ok(C, HW, {dy, x, y_relu, dx})) {
+    const int sp = rows4_ew_splits(N, C);
+    hipLaunchKernelGGL(bwd_elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, dy, x, mean,
+                       invstd, w, sums, y_relu, count, N, C, sp, dx);
+    return;
+  }
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(bwd_elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, dy, x, mean, invstd,
                      w, sums, y_relu, count, total, C, HW, dx);

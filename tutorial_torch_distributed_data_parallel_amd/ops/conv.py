@@ -88,7 +88,8 @@ class _ConvNHWCFn(torch.autograd.Function):
         sh, sw = stride
         ph, pw = padding
         if Cp != Cin:  # zero-pad the channels (RGB stem) so every DMA chunk is 4 channels
-            xp = torch.zeros((N, Cp, H, W), device=x.device, dtype=x.dtype, memory_format=_CL)
+            xp = torch.empty((N, Cp, H, W), device=x.device, dtype=x.dtype, memory_format=_CL)
+            xp[:, Cin:].zero_()
             xp[:, :Cin].copy_(x)
         else:
             xp = x.contiguous(memory_format=_CL)
