@@ -1,5 +1,8 @@
 #include "comm.h"
 
+#include <cstdlib>
+#include <string>
+
 #include <cstring>
 #include <stdexcept>
 
@@ -33,9 +36,12 @@ Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world,
   check_hip(hipSetDevice(device), "hipSetDevice");
   // Highest priority for the comm stream: bucket all-reduces should not queue behind backward
   // GEMMs on the hardware queues (GPU_MAX_HW_QUEUES=4 per process on this pool).
+  // TDP_COMM_PRIORITY=normal selects a default-priority stream instead (measurement knob).
   int lo = 0, hi = 0;
   check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-  check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi),
+  const char* pr = std::getenv("TDP_COMM_PRIORITY");
+  const bool normal = pr && std::string(pr) == "normal";
+  check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, normal ? lo : hi),
             "hipStreamCreateWithPriority");
   check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
 }

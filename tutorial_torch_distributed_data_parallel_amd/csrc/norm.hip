@@ -117,17 +117,29 @@ __global__ __launch_bounds__(256) void moments_2d(const float* __restrict__ x, i
   }
 }
 
-__global__ void moments_final(const float* __restrict__ ws, int C, int splits,
-                              float* __restrict__ mean, float* __restrict__ var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Split partials -> final: a workgroup owns 64 channels (one per lane, coalesced) and its 4 waves
+// take every 4th split; the four partial results merge through LDS.
+__global__ __launch_bounds__(256) void moments_final(const float* __restrict__ ws, int C,
+                                                     int splits, float* __restrict__ mean,
+                                                     float* __restrict__ var) {
+  __shared__ Wf sh[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   Wf w{0.f, 0.f, 0.f};
-  for (int z = 0; z < splits; ++z) {
-    const float* o = ws + (long)z * 3 * C;
-    w = wf_merge(w, Wf{o[c], o[C + c], o[2 * C + c]});
+  if (c < C) {
+#pragma unroll 4
+    for (int z = g; z < splits; z += 4) {
+      const float* o = ws + (long)z * 3 * C;
+      w = wf_merge(w, Wf{o[c], o[C + c], o[2 * C + c]});
+    }
   }
-  mean[c] = w.mean;
-  var[c] = w.n > 0.f ? w.m2 / w.n : 0.f;
+  sh[g][lane] = w;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    w = wf_merge(wf_merge(sh[0][lane], sh[1][lane]), wf_merge(sh[2][lane], sh[3][lane]));
+    mean[c] = w.mean;
+    var[c] = w.n > 0.f ? w.m2 / w.n : 0.f;
+  }
 }
 
 // Rows of `g`: [mean(C) | var(C) | count], stride 2C+1. Zero-count ranks drop out, as in
@@ -243,16 +255,29 @@ __global__ __launch_bounds__(256) void bwd_reduce_2d(const float* __restrict__ d
   }
 }
 
-__global__ void bwd_reduce_final(const float* __restrict__ part, int C, int splits,
-                                 const float* __restrict__ invstd, float* __restrict__ sums,
-                                 float* __restrict__ dw, float* __restrict__ db, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void bwd_reduce_final(const float* __restrict__ part, int C,
+                                                        int splits,
+                                                        const float* __restrict__ invstd,
+                                                        float* __restrict__ sums,
+                                                        float* __restrict__ dw,
+                                                        float* __restrict__ db, float beta) {
+  __shared__ float s0[4][64], s1[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float a = 0.f, m = 0.f;
-  for (int z = 0; z < splits; ++z) {
-    a += part[(long)z * 2 * C + c];
-    m += part[(long)z * 2 * C + C + c];
+  if (c < C) {
+#pragma unroll 4
+    for (int z = g; z < splits; z += 4) {
+      a += part[(long)z * 2 * C + c];
+      m += part[(long)z * 2 * C + C + c];
+    }
   }
+  s0[g][lane] = a;
+  s1[g][lane] = m;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  a = (s0[0][lane] + s0[1][lane]) + (s0[2][lane] + s0[3][lane]);
+  m = (s1[0][lane] + s1[1][lane]) + (s1[2][lane] + s1[3][lane]);
   sums[c] = a;
   sums[C + c] = m;
   if (dw) dw[c] = (beta != 0.f ? beta * dw[c] : 0.f) + m * invstd[c];
@@ -503,10 +528,10 @@ inline int ew_grid(long total) {
 }  // namespace
 
 int bn_splits(int N, int C, int HW, int num_cus) {
-  if (HW == 1 && C % 4 == 0) {  // rows4 kernels: ~4 workgroups per CU, >= 8 row iterations
+  if (HW == 1 && C % 4 == 0) {  // rows4 kernels: ~1 workgroup per CU, >= 8 row iterations
     const int CB = C < 1024 ? C : 1024, RPW = 256 / (CB / 4);
     const int nblk = rows4_nblk(C);
-    long s = (4L * num_cus + nblk - 1) / nblk;
+    long s = ((long)num_cus + nblk - 1) / nblk;
     const long cap = (N + 8L * RPW - 1) / (8L * RPW);
     if (s > cap) s = cap;
     return s < 1 ? 1 : (int)s;
@@ -538,7 +563,7 @@ void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, flo
     hipLaunchKernelGGL(moments_2d, dim3(C, splits), dim3(256), 0, s, x, N, C, HW, splits, ws,
                        mean, var);
   if (splits > 1)
-    hipLaunchKernelGGL(moments_final, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, splits, mean,
+    hipLaunchKernelGGL(moments_final, dim3((C + 63) / 64), dim3(256), 0, s, ws, C, splits, mean,
                        var);
 }
 
@@ -587,7 +612,7 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
   else
     hipLaunchKernelGGL(bwd_reduce_2d, dim3(C, splits), dim3(256), 0, s, dy, x, mean, y_relu, N, C,
                        HW, splits, ws);
-  hipLaunchKernelGGL(bwd_reduce_final, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, splits,
+  hipLaunchKernelGGL(bwd_reduce_final, dim3((C + 63) / 64), dim3(256), 0, s, ws, C, splits,
                      invstd, sums, dw, db, grad_beta);
 }
 

@@ -1,6 +1,8 @@
 #include "reducer.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <cmath>
 #include <stdexcept>
 
@@ -32,6 +34,8 @@ RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_
   }
   if (compression_ == Compression::BF16)
     check_hip(hipMalloc(&wire_, sizeof(uint16_t) * (size_t)numel_), "hipMalloc(wire)");
+  const char* mode = std::getenv("TDP_COMM_STREAM");
+  inline_ = mode && std::string(mode) == "compute";
 }
 
 RcclBackend::~RcclBackend() {
@@ -58,9 +62,13 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
     if (post_bucket) post_bucket(bucket, begin, end, compute);
     return;
   }
-  hipStream_t cs = comm_->comm_stream();
-  check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
-  check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+  // inline_: collectives and fused updates go on the compute stream itself (no cross-stream
+  // dependency; no overlap with the rest of backward)
+  hipStream_t cs = inline_ ? compute : comm_->comm_stream();
+  if (!inline_) {
+    check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+  }
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
   const int64_t n = end - begin;
@@ -95,6 +103,10 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
 
 void RcclBackend::wait_all(hipStream_t compute) {
   if (!launched_any_) return;
+  if (inline_) {
+    launched_any_ = false;
+    return;
+  }
   hipStream_t cs = comm_->comm_stream();
   if (timing_) {
     check_hip(hipEventRecord(t1_, cs), "hipEventRecord");

@@ -86,6 +86,7 @@ class RcclBackend : public ReducerBackend {
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false;
+  bool inline_ = false;  // TDP_COMM_STREAM=compute: no side stream
   uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
 };
 

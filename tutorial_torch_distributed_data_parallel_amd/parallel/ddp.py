@@ -16,6 +16,8 @@ a bucket may split a large tensor, all-reduces run on a dedicated high-priority 
 """
 from __future__ import annotations
 
+import os
+
 import contextlib
 import hashlib
 
@@ -128,8 +130,11 @@ class DistributedDataParallel(nn.Module):
             comm = rt.comm()
             if comm is None:
                 raise RuntimeError("GPU DDP needs the RCCL backend (init_process_group('nccl'))")
+            # TDP_FORCE_COLLECTIVE=1 keeps the all-reduce (and its stream hop) at world size 1:
+            # the single-GPU rehearsal of the multi-GPU schedule
+            skip = os.environ.get("TDP_FORCE_COLLECTIVE", "0") != "1"
             self._backend = C.RcclBackend(comm, self.arena.grad, nb, compression=comp,
-                                          timing=self._timing, skip_single_rank=True)
+                                          timing=self._timing, skip_single_rank=skip)
             self.reducer = C.Reducer(self.arena.offsets, self.arena.numels, self._bounds,
                                      self._backend)
         else:
