@@ -12,6 +12,9 @@ bucketed RCCL all-reduce -> optimizer step. Weak scaling: per-GPU work is fixed.
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
   python bench.py --impl torch                      # stock torch DDP + torch.optim (comparison)
 
+Execution: eager by default (GPU-bound with the native kernels); ``--graph`` replays a captured
+hipGraph of the whole step instead.
+
 Timing: W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
 both sides; the max over ranks is reported; rank 0 prints one JSON line.
 """
@@ -47,12 +50,18 @@ def parse():
                     help="synthetic samples per rank (default 8192 MLP, 512 CNN)")
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
-    ap.add_argument("--eager", action="store_true",
-                    help="tdp: run the step eagerly instead of replaying a captured hipGraph")
-    ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
-                    help="tdp: apply the optimizer per gradient bucket inside the reduction "
-                         "(auto: when world_size > 1, where it overlaps the all-reduce; on one "
-                         "GPU a single flat optimizer step after backward is faster)")
+    ap.add_argument("--graph", action="store_true",
+                    help="tdp: capture the whole step into a hipGraph and replay it (bucket "
+                         "all-reduces then overlap backward on a side stream). Off by default: "
+                         "with the native kernels the eager step is GPU-bound and measured as "
+                         "fast on one GPU (profiles/bench/mode*.json), and eager keeps RCCL out "
+                         "of stream capture on multi-GPU runs")
+    ap.add_argument("--eager", action="store_true", help="tdp: run eagerly (the default)")
+    ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="off",
+                    help="tdp: apply the optimizer per gradient bucket inside the reduction. "
+                         "Measured on MI355X (profiles/bench/mode*.json) the single flat "
+                         "optimizer step after backward is faster on this model, so it is off "
+                         "by default (auto = on when world_size > 1)")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
     return ap.parse_args()
 
@@ -227,7 +236,7 @@ def main():
     if a.impl == "tdp":
         advance()
         run = tdp_step
-        if use_gpu and not a.eager:
+        if use_gpu and a.graph and not a.eager:
             from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
 
             run = try_capture(tdp_step, warmup=3,
@@ -290,7 +299,8 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "impl": ("tdp (native gfx950 kernels + RCCL reducer" +
-                         (", eager)" if (a.eager or not use_gpu) else ", hipGraph step)"))
+                         (", hipGraph step)" if (use_gpu and a.graph and not a.eager)
+                          else ", eager)"))
                         if a.impl == "tdp" else "stock torch DDP + torch.optim",
                 "optimizer": a.optim + (" (fused into the bucket reduction)"
                                         if a.impl == "tdp" and fused else ""),

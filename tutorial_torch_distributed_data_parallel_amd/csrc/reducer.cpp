@@ -35,7 +35,11 @@ RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_
   if (compression_ == Compression::BF16)
     check_hip(hipMalloc(&wire_, sizeof(uint16_t) * (size_t)numel_), "hipMalloc(wire)");
   const char* mode = std::getenv("TDP_COMM_STREAM");
-  inline_ = mode && std::string(mode) == "compute";
+  const std::string m = mode ? mode : "auto";
+  stream_mode_ = m == "side" ? kStreamSide
+                 : m == "compute" ? kStreamCompute
+                 : m == "hostsync" ? kStreamHostSync
+                                   : kStreamAuto;
 }
 
 RcclBackend::~RcclBackend() {
@@ -62,12 +66,29 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
     if (post_bucket) post_bucket(bucket, begin, end, compute);
     return;
   }
-  // inline_: collectives and fused updates go on the compute stream itself (no cross-stream
-  // dependency; no overlap with the rest of backward)
-  hipStream_t cs = inline_ ? compute : comm_->comm_stream();
-  if (!inline_) {
+  // Stream choice (measured on MI355X, profiles/bench/mode*.json): in EAGER execution a side
+  // stream costs 1.5-3x step time -- a hipStreamWaitEvent barrier left pending on one hardware
+  // queue while the host runs ahead slows every kernel dispatched on the other queue (ResNet-50:
+  // 95 ms vs 65 ms). Inside a hipGraph the same dependency is free and the all-reduce overlaps
+  // backward. So: side stream while capturing, the compute stream itself otherwise
+  // (TDP_COMM_STREAM=side|compute|hostsync overrides for measurements).
+  bool side = true;
+  if (stream_mode_ == kStreamAuto) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(compute, &cap), "hipStreamIsCapturing");
+    side = cap == hipStreamCaptureStatusActive;
+  } else {
+    side = stream_mode_ != kStreamCompute;
+  }
+  if (!side && launched_side_) side = true;  // never switch streams within one iteration
+  hipStream_t cs = side ? comm_->comm_stream() : compute;
+  if (side) {
+    launched_side_ = true;
     check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
-    check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+    if (stream_mode_ == kStreamHostSync)
+      check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
+    else
+      check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
   }
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
@@ -103,10 +124,11 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
 
 void RcclBackend::wait_all(hipStream_t compute) {
   if (!launched_any_) return;
-  if (inline_) {
+  if (!launched_side_) {  // everything ran on the compute stream: already ordered
     launched_any_ = false;
     return;
   }
+  launched_side_ = false;
   hipStream_t cs = comm_->comm_stream();
   if (timing_) {
     check_hip(hipEventRecord(t1_, cs), "hipEventRecord");

@@ -9,10 +9,12 @@
 //   * a bucket boundary may fall inside a large parameter (fc1's 144 MiB weight can be split);
 //   * averaging is ncclAvg inside the all-reduce (no div_ pass);
 //   * buckets launch strictly in index order as soon as every parameter overlapping them is
-//     ready (identical collective order on every rank), on the communicator's high-priority
-//     stream after an event recorded on the compute stream; finalize() makes the compute stream
-//     wait on the last bucket, so the optimizer step is ordered after the reduction without a
-//     host sync.
+//     ready (identical collective order on every rank). While a hipGraph is being captured they
+//     go to the communicator's high-priority stream after an event recorded on the compute
+//     stream (overlapping backward) and finalize() makes the compute stream wait on the last
+//     bucket; in eager execution they are issued on the compute stream itself, because a
+//     cross-queue wait left pending while the host runs ahead was measured to slow every kernel
+//     on MI355X (see RcclBackend::launch). Either way no host sync is needed.
 // The backend is abstract so that the same bucketing/readiness logic runs over RCCL on MI355X
 // and over torch.distributed (gloo) in the CPU tests.
 #pragma once
@@ -86,7 +88,10 @@ class RcclBackend : public ReducerBackend {
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false;
-  bool inline_ = false;  // TDP_COMM_STREAM=compute: no side stream
+  // where bucket collectives run: auto = side stream only while capturing a hipGraph
+  enum { kStreamAuto = 0, kStreamSide = 1, kStreamCompute = 2, kStreamHostSync = 3 };
+  int stream_mode_ = kStreamAuto;
+  bool launched_side_ = false;
   uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
 };
 

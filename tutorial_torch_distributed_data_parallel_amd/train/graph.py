@@ -1,11 +1,17 @@
 """Whole-step HIP graph capture ("HIP graphs instead of a tracing compiler").
 
 A data-parallel training step of the toy MLP is ~25 kernel launches plus autograd, DDP hooks and
-optimizer bookkeeping in Python: on MI355X the GPU work is ~0.6 ms while eager host overhead is
-of the same order, so eager execution leaves the GPU idle between launches (the first rocprof
-timeline showed 50-175 us gaps). ``CapturedStep`` records one complete step -- on-device batch
+optimizer bookkeeping in Python. ``CapturedStep`` records one complete step -- on-device batch
 gather, forward, loss, backward with the reducer's bucketed RCCL all-reduces on the comm stream,
 optimizer update -- into a hipGraph once, then each iteration is one graph launch.
+
+When it pays (measured on MI355X, profiles/bench/mode*.json): the first eager implementation left
+50-175 us host gaps between kernels and capture cut the step from 1.67 to 0.64 ms; after the
+host path was trimmed (device-resident sampler indices, one flat optimizer kernel) the eager step
+is GPU-bound (0.62 ms) and replay brings nothing on one GPU. Capture still matters for the
+multi-GPU schedule: inside a graph the reducer's all-reduces run on a side stream and overlap
+backward for free, whereas eagerly a cross-queue wait left pending while the host runs ahead
+slows every kernel (the reducer therefore runs eager collectives on the compute stream).
 
 Contract (as for torch.cuda.graphs): the captured function reads its varying inputs from static
 tensors the caller refreshes before ``replay`` (here: a device index tensor for the batch);
