@@ -214,3 +214,30 @@ def accelerate_worker(rank, out_dir):
         assert all(not k.startswith("module.") for k in sd)
         assert set(sd) == set(acc.unwrap_model(model).state_dict())
     acc.end_training()
+
+
+def replica_check(rank, out_dir):
+    """SURVEY.md §5.2 debug mode: the replica checksum passes on healthy steps and names the
+    diverged rank after one rank's parameters are corrupted."""
+    import tutorial_torch_distributed_data_parallel_amd as tdp
+
+    _init()
+    torch.manual_seed(rank)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    ddp = tdp.DDP(model, check_replicas_every=1)
+    opt = tdp.optim.SGD(ddp.parameters(), lr=0.1)
+    for _ in range(3):
+        opt.zero_grad()
+        ddp(torch.randn(5, 8)).sum().backward()
+        opt.step()
+    ddp.check_replicas()
+    if rank == 1:
+        with torch.no_grad():
+            model[0].weight[0, 0] += 1e-3
+    try:
+        ddp(torch.randn(5, 8))
+    except RuntimeError as e:
+        assert "ranks [1]" in str(e), str(e)
+    else:
+        raise AssertionError("replica divergence not detected")
+    tdp.destroy_process_group()

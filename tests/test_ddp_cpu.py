@@ -45,3 +45,7 @@ def test_find_unused_parameters(tmp_path):
 
 def test_accelerate_facade_two_ranks(tmp_path):
     run(W.accelerate_worker, tmp_path)
+
+
+def test_replica_consistency_check(tmp_path):
+    run(W.replica_check, tmp_path)

@@ -58,7 +58,7 @@ class DistributedDataParallel(nn.Module):
                  check_reduction: bool = False, gradient_as_bucket_view: bool = True,
                  static_graph: bool = False, first_bucket_cap_mb: float | None = None,
                  split_bucket_mb: float | None = None, grad_compression: str | None = None,
-                 timing: bool = False):
+                 timing: bool = False, check_replicas_every: int | None = None):
         super().__init__()
         if process_group is not None:
             raise NotImplementedError("sub-groups are not supported: DDP uses the world group")
@@ -120,6 +120,11 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._iter = 0
         self._fused_opt = None
+        # SURVEY.md §5.2 debug mode: every N forwards, verify that all replicas hold bit-identical
+        # parameters (a checksum all-gather); TDP_CHECK_REPLICAS=N sets it from the environment
+        env_every = int(os.environ.get("TDP_CHECK_REPLICAS", "0") or 0)
+        self.check_replicas_every = check_replicas_every if check_replicas_every is not None \
+            else env_every
 
     # --------------------------------------------------------------------------- reducer
     def _build_reducer(self):
@@ -172,8 +177,32 @@ class DistributedDataParallel(nn.Module):
         for b in ba.others:
             rt.broadcast(b, 0)
 
+    # --------------------------------------------------------------------------- debug
+    def replica_checksum(self) -> torch.Tensor:
+        """Bit-exact checksum of the flat parameter arena: [sum of the int32 words, sum of the
+        words weighted by (index mod 65521) + 1] as int64 (order-sensitive, dtype-agnostic)."""
+        with torch.no_grad():
+            words = self.arena.data.view(torch.int32).to(torch.int64)
+            w = (torch.arange(words.numel(), device=words.device, dtype=torch.int64) % 65521) + 1
+            return torch.stack([words.sum(), (words * w).sum()])
+
+    def check_replicas(self) -> None:
+        """Raise if any rank's parameters differ from rank 0's (all-gather of the checksums)."""
+        local = self.replica_checksum()
+        if self.world_size == 1:
+            return
+        gathered = rt.all_gather_flat(local).view(self.world_size, 2)
+        bad = [r for r in range(self.world_size) if not torch.equal(gathered[r], gathered[0])]
+        if bad:
+            raise RuntimeError(f"DDP replicas diverged at iteration {self._iter}: ranks {bad} "
+                               f"hold different parameters than rank 0 "
+                               f"(checksums {gathered.tolist()})")
+
     # --------------------------------------------------------------------------- nn.Module
     def forward(self, *inputs, **kwargs):
+        if self.check_replicas_every and self._iter and \
+                self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled():
+            self.check_replicas()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.reducer.prepare_for_backward()
             if self._fused_opt is not None:
