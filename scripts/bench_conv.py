@@ -54,16 +54,20 @@ def main():
         flops = 2.0 * B * P * Q * Cout * Cin * R * S
         rec = {"layer": mn, "count": cnt, "x": [B, Cin, H, W], "w": list(ws), "stride": st[0],
                "gflop": round(flops / 1e9, 2)}
-        Cp = (Cin + 3) // 4 * 4
-        xcl = torch.zeros(B, Cp, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
-        xcl[:, :Cin].copy_(x)
-        wt = F.pad(w.permute(0, 2, 3, 1), (0, Cp - Cin)).contiguous()
-        w2 = F.pad(w.permute(2, 3, 0, 1), (0, Cp - Cin)).contiguous()
+        from tutorial_torch_distributed_data_parallel_amd import ops
+
+        xcl = x.contiguous(memory_format=torch.channels_last)
         dy = torch.randn(B, Cout, P, Q, device="cuda").contiguous(memory_format=torch.channels_last)
-        dwt = torch.empty(Cout, R, S, Cp, device="cuda")
-        t_f = timeit(lambda: C.conv_nhwc_fwd(xcl, wt, None, R, S, st[0], st[1], pd[0], pd[1], False))
-        t_d = timeit(lambda: C.conv_nhwc_dgrad(dy, w2, [B, Cp, H, W], R, S, st[0], st[1], pd[0], pd[1]))
-        t_w = timeit(lambda: C.conv_nhwc_wgrad(dy, xcl, dwt, R, S, st[0], st[1], pd[0], pd[1], 0.0))
+        with torch.no_grad():
+            t_f = timeit(lambda: ops.conv2d(xcl, w, None, st, pd))
+        # dgrad / wgrad through the autograd op (includes the weight re-layout copies, phase
+        # decomposition and transposed-wgrad paths exactly as training runs them)
+        xr = xcl.detach().clone().requires_grad_()
+        wr = w.detach().clone().requires_grad_()
+        y_x = ops.conv2d(xr, w, None, st, pd)
+        y_w = ops.conv2d(xcl, wr, None, st, pd)
+        t_d = timeit(lambda: torch.autograd.grad(y_x, xr, dy, retain_graph=True))
+        t_w = timeit(lambda: torch.autograd.grad(y_w, wr, dy, retain_graph=True))
         rec["ours_us"] = [round(t_f, 1), round(t_d, 1), round(t_w, 1)]
         for tag, fmt in (("miopen", torch.contiguous_format), ("miopen_cl", torch.channels_last)):
             xx = x.contiguous(memory_format=fmt)

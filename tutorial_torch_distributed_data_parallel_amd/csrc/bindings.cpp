@@ -468,6 +468,24 @@ Tensor conv_nhwc_dgrad_op(const Tensor& dy, const Tensor& w2, std::vector<int64_
   return conv_nhwc_exec(kConvDgrad, g, dy, w2, dx, c10::nullopt, false, 0.0);
 }
 
+// One stride phase of a strided input gradient, computed as a stride-1 implicit GEMM over the
+// phase's sub-grid: out[n][i][j][c] = sum_(t,u,co) dy[n][i+da-t][j+db-u][co] * w2p[t][u][co][c]
+// (w2p = the phase's taps of W2). Returns a channels_last [N, C, Hp, Wp] tensor.
+Tensor conv_nhwc_dgrad_phase_op(const Tensor& dy, const Tensor& w2p, int64_t C, int64_t Hp,
+                                int64_t Wp, int64_t Rp, int64_t Sp, int64_t da, int64_t db) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy); CHECK_CONTIG(w2p);
+  ConvGeom g;
+  g.N = (int)dy.size(0); g.Cout = (int)dy.size(1); g.P = (int)dy.size(2); g.Q = (int)dy.size(3);
+  g.C = (int)C; g.H = (int)Hp; g.W = (int)Wp; g.R = (int)Rp; g.S = (int)Sp;
+  g.sh = 1; g.sw = 1; g.ph = (int)da; g.pw = (int)db;
+  TORCH_CHECK(Rp > 0 && Sp > 0 && Hp > 0 && Wp > 0, "dgrad phase: empty phase");
+  TORCH_CHECK(w2p.numel() == Rp * Sp * g.Cout * C, "dgrad phase: weight size mismatch");
+  TORCH_CHECK((long)g.N * C * Hp * Wp < (1L << 31), "dgrad phase: < 2^31 elements");
+  auto out = at::empty({g.N, (int64_t)C, Hp, Wp},
+                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  return conv_nhwc_exec(kConvDgrad, g, dy, w2p, out, c10::nullopt, false, 0.0);
+}
+
 // dy channels_last, x channels_last -> dwt [Cout, R*S*C] (dwt = beta*dwt + grad)
 void conv_nhwc_wgrad_op(const Tensor& dy, const Tensor& x, Tensor& dwt, int64_t R, int64_t S,
                         int64_t sh, int64_t sw, int64_t ph, int64_t pw, double beta) {
@@ -692,6 +710,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd_op);
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
+  m.def("conv_nhwc_dgrad_phase", &conv_nhwc_dgrad_phase_op);
+  m.def("conv_wgrad_transposed", [](int64_t cout) {
+    ConvGeom g{};
+    g.Cout = (int)cout;
+    return conv_wgrad_transposed(g);
+  });
   m.def("conv2d_dgrad", &conv2d_dgrad_op);
   m.def("conv2d_wgrad", &conv2d_wgrad_op);
   m.def("chan_relu_bias_bwd", &chan_relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),

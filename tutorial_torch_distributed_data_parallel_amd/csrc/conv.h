@@ -28,6 +28,8 @@ void conv_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float
 // NHWC implicit GEMM on the LDS-DMA MFMA pipeline (gemm_f32_fast.hip). Requires C % 4 == 0,
 // Cout % 4 == 0 and (for DGRAD) power-of-two strides; plan.fm holds the pipeline depth.
 bool conv_nhwc_ok(int mode, const ConvGeom& g);
+// weight gradient computed as dW^T [R*S*C][Cout] (small Cout: keeps the 128-row tiles full)
+bool conv_wgrad_transposed(const ConvGeom& g);
 ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
 void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,

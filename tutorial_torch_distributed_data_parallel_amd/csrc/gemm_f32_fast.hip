@@ -140,7 +140,10 @@ struct TileSrc {
 };
 
 // Operand source kinds
-constexpr int kDenseK = 0, kDenseMN = 1, kImFwd = 2, kImDgrad = 3, kImWgrad = 4;
+// (kImWgradT: the same shifted-pixel operand as kImWgrad, used as A of the transposed weight
+// gradient dW^T[(r,s,c)][co] = x_shifted^T . dy when Cout is too small for a 128-row tile)
+constexpr int kDenseK = 0, kDenseMN = 1, kImFwd = 2, kImDgrad = 3, kImWgrad = 4,
+              kImWgradT = 5;
 
 // Implicit K-contiguous A (rows = pixels of the row grid, k = (r, s, c) with c fastest):
 //   FWD   : source x,  pixel (n, p, q), tap reads x[n][p*sh-ph+r][q*sw-pw+s][c]
@@ -222,7 +225,7 @@ struct ImSrcA {
 // Implicit MN-contiguous B of the weight gradient: k = dy pixel (n, p, q), columns
 // (r, s, c) with c fastest; element = x[n][p*sh-ph+r][q*sw-pw+s][c]. A lane's 4 columns share
 // one tap (Cs % 4 == 0), fixed for the whole kernel; only the pixel changes per tile.
-template <int R>
+template <int R, bool IS_A = false>
 struct ImSrcB {
   static constexpr int CH = (32 * R * 4) / 1024, NPW = CH / 4;
   static constexpr int LPR = R / 4, RPC = 1024 / (R * 4);
@@ -259,7 +262,7 @@ struct ImSrcB {
       const int h = (int)y * cv.sh + th, w = (int)x * cv.sw + tw;
       const bool ok = (unsigned)h < (unsigned)cv.Hs && (unsigned)w < (unsigned)cv.Ws;
       const float* src =
-          ok ? p.B + (((long)n * cv.Hs + h) * cv.Ws + w) * cv.Cs + coff : cv.zero;
+          ok ? (IS_A ? p.A : p.B) + (((long)n * cv.Hs + h) * cv.Ws + w) * cv.Cs + coff : cv.zero;
       glds16(src, dst + j * 1024);
     }
   }
@@ -294,11 +297,13 @@ struct SrcOf<R, kImFwd, true> : ImSrcA<R, kImFwd> {};
 template <int R>
 struct SrcOf<R, kImDgrad, true> : ImSrcA<R, kImDgrad> {};
 template <int R>
-struct SrcOf<R, kImWgrad, false> : ImSrcB<R> {};
+struct SrcOf<R, kImWgrad, false> : ImSrcB<R, false> {};
+template <int R>
+struct SrcOf<R, kImWgradT, true> : ImSrcB<R, true> {};
 
 template <int FN, int AKIND, int BKIND, int S>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
-  constexpr bool AK = AKIND != kDenseMN;
+  constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
   constexpr int FM = 2;
   constexpr int BM = 128, BN = 64 * FN;
@@ -630,6 +635,9 @@ static int ilog2_exact(int v) {
   return (1 << l) == v ? l : -1;
 }
 
+static bool wgrad_transposed(const ConvGeom& g) { return g.Cout < 128; }
+bool conv_wgrad_transposed(const ConvGeom& g) { return wgrad_transposed(g); }
+
 bool conv_nhwc_ok(int mode, const ConvGeom& g) {
   if (g.C % 4 || g.Cout % 4) return false;
   if (mode == kConvDgrad && (ilog2_exact(g.sh) < 0 || ilog2_exact(g.sw) < 0)) return false;
@@ -641,7 +649,8 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
   pl.mode = mode;
   if (mode == kConvFwd) { pl.M = g.N * g.P * g.Q; pl.N = g.Cout; pl.K = g.R * g.S * g.C; }
   else if (mode == kConvDgrad) { pl.M = g.N * g.H * g.W; pl.N = g.C; pl.K = g.R * g.S * g.Cout; }
-  else { pl.M = g.Cout; pl.N = g.R * g.S * g.C; pl.K = g.N * g.P * g.Q; }
+  else if (!wgrad_transposed(g)) { pl.M = g.Cout; pl.N = g.R * g.S * g.C; pl.K = g.N * g.P * g.Q; }
+  else { pl.M = g.R * g.S * g.C; pl.N = g.Cout; pl.K = g.N * g.P * g.Q; }
   GemmF32Args a{};
   a.M = pl.M; a.N = pl.N; a.K = pl.K;
   GemmPlan gp;
@@ -656,7 +665,8 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
 
 // FWD  : A = x (NHWC), B = Wt [Cout][R*S*C],  C = y  [N*P*Q][Cout] (+bias, relu)
 // DGRAD: A = dy (NHWC), B = W2 [R*S*Cout][C], C = dx [N*H*W][C]
-// WGRAD: A = dy [N*P*Q][Cout], B = x (NHWC),  C = dWt [Cout][R*S*C] (beta: accumulate)
+// WGRAD: A = dy [N*P*Q][Cout], B = x (NHWC),  C = dWt [Cout][R*S*C] (beta: accumulate);
+//        when conv_wgrad_transposed(g): C = dWt^T [R*S*C][Cout] (A/B arguments unchanged)
 void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,
                    hipStream_t s) {
@@ -681,9 +691,14 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   p.A = A; p.B = B; p.C = C; p.bias = bias; p.ws = ws;
   p.rowsum = nullptr; p.rowsum_beta = 0.f;
   p.M = pl.M; p.N = pl.N; p.K = pl.K;
+  const bool wt = pl.mode == kConvWgrad && wgrad_transposed(g);
+  if (wt) {  // A = implicit x^T, B = dy [K][Cout]
+    p.A = B; p.B = A;
+  }
   if (pl.mode == kConvFwd) { p.lda = 0; p.ldb = pl.K; p.ldc = pl.N; }
   else if (pl.mode == kConvDgrad) { p.lda = 0; p.ldb = pl.N; p.ldc = pl.N; }
-  else { p.lda = pl.M; p.ldb = 0; p.ldc = pl.N; }
+  else if (!wt) { p.lda = pl.M; p.ldb = 0; p.ldc = pl.N; }
+  else { p.lda = 0; p.ldb = pl.N; p.ldc = pl.N; }
   p.k_per_split = pl.k_per_split;
   p.splits = pl.splits;
   p.tiles_m = ceil_div(pl.M, 128);
@@ -694,7 +709,8 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   const int fn = pl.fn, st = pl.fm;
   if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s);
   else if (pl.mode == kConvDgrad) launch_kinds<kImDgrad, kDenseMN>(p, fn, st, nblocks, s);
-  else launch_kinds<kDenseMN, kImWgrad>(p, fn, st, nblocks, s);
+  else if (!wt) launch_kinds<kDenseMN, kImWgrad>(p, fn, st, nblocks, s);
+  else launch_kinds<kImWgradT, kDenseMN>(p, fn, st, nblocks, s);
   if (pl.splits > 1)
     splitk_reduce(ws, pl.splits, pl.M, pl.N, C, false, pl.N, bias, beta, relu, s);
 }
