@@ -57,11 +57,12 @@ def parse():
                          "fast on one GPU (profiles/bench/mode*.json), and eager keeps RCCL out "
                          "of stream capture on multi-GPU runs")
     ap.add_argument("--eager", action="store_true", help="tdp: run eagerly (the default)")
-    ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="off",
-                    help="tdp: apply the optimizer per gradient bucket inside the reduction. "
-                         "Measured on MI355X (profiles/bench/mode*.json) the single flat "
-                         "optimizer step after backward is faster on this model, so it is off "
-                         "by default (auto = on when world_size > 1)")
+    ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
+                    help="tdp: apply the optimizer per gradient bucket inside the reduction; "
+                         "with world_size > 1 it is sharded (reduce-scatter -> update 1/W -> "
+                         "all-gather: same wire bytes, 1/W of the optimizer's HBM traffic). "
+                         "auto = on when world_size > 1; on one GPU the single flat step after "
+                         "backward is faster (profiles/bench/mode*.json)")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
     return ap.parse_args()
 

@@ -828,6 +828,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.fused.adam_step = step;
            })
       .def("clear_fused", [](RcclBackend& b) { b.fused = FusedOptimizer{}; })
+      .def_property("fused_shard", [](RcclBackend& b) { return b.fused.shard; },
+                    [](RcclBackend& b, bool v) { b.fused.shard = v; })
       .def_property_readonly("fused_adam_step",
                              [](RcclBackend& b) { return b.fused.adam_step; });
   py::class_<PyBackend, ReducerBackend, std::shared_ptr<PyBackend>>(m, "PyBackend")

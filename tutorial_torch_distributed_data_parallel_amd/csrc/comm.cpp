@@ -41,7 +41,9 @@ Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world,
   check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
   const char* pr = std::getenv("TDP_COMM_PRIORITY");
   const bool normal = pr && std::string(pr) == "normal";
-  check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, normal ? lo : hi),
+  const bool blocking = pr && std::string(pr) == "blocking";
+  check_hip(hipStreamCreateWithPriority(&stream_, blocking ? hipStreamDefault : hipStreamNonBlocking,
+                                        (normal || blocking) ? lo : hi),
             "hipStreamCreateWithPriority");
   check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
 }

@@ -93,33 +93,66 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
   const int64_t n = end - begin;
-  if (n > 0 && collective) {
-    char* ptr = arena_ + begin * elem_size_;
-    if (compression_ == Compression::BF16) {
-      uint16_t* w = wire_ + begin;
-      f32_to_bf16_copy(reinterpret_cast<float*>(ptr), w, n, cs);
-      comm_->all_reduce(w, w, (size_t)n, ncclBfloat16, ncclAvg, cs);
-      bf16_to_f32_copy(w, reinterpret_cast<float*>(ptr), n, cs);
-    } else {
-      comm_->all_reduce(ptr, ptr, (size_t)n, nccl_dtype(elem_size_), ncclAvg, cs);
-    }
+  const int W = comm_->world();
+  bool first = false;
+  if (n > 0 && fused.kind == 1 && !fused.fresh.empty()) {
+    first = (bool)fused.fresh[bucket];
+    fused.fresh[bucket] = 0;
   }
-  if (n > 0 && fused.kind == 1) {
+  if (n > 0 && fused.kind == 2 && bucket == 0) ++fused.adam_step;
+  float* g = reinterpret_cast<float*>(arena_) + begin;
+  if (n > 0 && collective && fused.kind != 0 && fused.shard && W > 1 &&
+      compression_ == Compression::NONE && elem_size_ == 4) {
+    // Sharded update (ZeRO-1 inside DDP): reduce-scatter the averaged gradient so this rank owns
+    // 1/W of the bucket, update only that shard, all-gather the updated parameters. Same bytes
+    // on the wire as the all-reduce, 1/W of the optimizer's HBM traffic; the parameters end up
+    // identical on every rank, exactly as after all-reduce + replicated update. The < W-element
+    // tail that does not divide evenly is all-reduced and updated everywhere.
+    const int r = comm_->rank();
+    const int64_t cnt = n / W, body = cnt * W, tail = n - body;
+    if (cnt > 0) {
+      comm_->reduce_scatter(g, g + (int64_t)r * cnt, (size_t)cnt, ncclFloat32, ncclAvg, cs);
+      apply_fused(begin + (int64_t)r * cnt, cnt, first, cs);
+      comm_->all_gather(fused.p + begin + (int64_t)r * cnt, fused.p + begin, (size_t)cnt,
+                        ncclFloat32, cs);
+    }
+    if (tail > 0) {
+      comm_->all_reduce(g + body, g + body, (size_t)tail, ncclFloat32, ncclAvg, cs);
+      apply_fused(begin + body, tail, first, cs);
+    }
+  } else {
+    if (n > 0 && collective) {
+      char* ptr = arena_ + begin * elem_size_;
+      if (compression_ == Compression::BF16) {
+        uint16_t* w = wire_ + begin;
+        f32_to_bf16_copy(reinterpret_cast<float*>(ptr), w, n, cs);
+        comm_->all_reduce(w, w, (size_t)n, ncclBfloat16, ncclAvg, cs);
+        bf16_to_f32_copy(w, reinterpret_cast<float*>(ptr), n, cs);
+      } else {
+        comm_->all_reduce(ptr, ptr, (size_t)n, nccl_dtype(elem_size_), ncclAvg, cs);
+      }
+    }
+    if (n > 0) apply_fused(begin, n, first, cs);
+  }
+  if (post_bucket) post_bucket(bucket, begin, end, cs);
+}
+
+// optimizer update of arena elements [off, off + cnt) (no-op without a fused optimizer)
+void RcclBackend::apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs) {
+  if (cnt <= 0) return;
+  float* g = reinterpret_cast<float*>(arena_) + off;
+  if (fused.kind == 1) {
     SgdHyper h = fused.sgd;
-    h.first_step = fused.fresh.empty() ? false : (bool)fused.fresh[bucket];
-    if (!fused.fresh.empty()) fused.fresh[bucket] = 0;
-    sgd_flat(fused.p + begin, reinterpret_cast<float*>(arena_) + begin,
-             fused.s0 ? fused.s0 + begin : nullptr, n, h, cs);
-  } else if (n > 0 && fused.kind == 2) {
-    if (bucket == 0) ++fused.adam_step;
+    h.first_step = first;
+    sgd_flat(fused.p + off, g, fused.s0 ? fused.s0 + off : nullptr, cnt, h, cs);
+  } else if (fused.kind == 2) {
     AdamHyper h = fused.adam;
     const double t = (double)(fused.adam_step > 0 ? fused.adam_step : 1);
     h.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
     h.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
-    adam_flat(fused.p + begin, reinterpret_cast<float*>(arena_) + begin, fused.s0 + begin,
-              fused.s1 + begin, fused.s2 ? fused.s2 + begin : nullptr, n, h, cs);
+    adam_flat(fused.p + off, g, fused.s0 + off, fused.s1 + off,
+              fused.s2 ? fused.s2 + off : nullptr, cnt, h, cs);
   }
-  if (post_bucket) post_bucket(bucket, begin, end, cs);
 }
 
 void RcclBackend::wait_all(hipStream_t compute) {

@@ -63,6 +63,7 @@ struct FusedOptimizer {
   float adam_beta1 = 0.9f, adam_beta2 = 0.999f;
   int64_t adam_step = 0;       // incremented when the first bucket of an iteration updates
   std::vector<char> fresh;     // per bucket: SGD momentum not yet initialised
+  bool shard = false;          // reduce-scatter / update 1/W / all-gather (world > 1)
 };
 
 class RcclBackend : public ReducerBackend {
@@ -79,6 +80,7 @@ class RcclBackend : public ReducerBackend {
   FusedOptimizer fused;
 
  private:
+  void apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs);
   std::shared_ptr<Communicator> comm_;
   char* arena_;
   int64_t numel_;

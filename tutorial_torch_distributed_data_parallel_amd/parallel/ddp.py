@@ -224,13 +224,19 @@ class DistributedDataParallel(nn.Module):
             self.require_backward_grad_sync = old
 
     # --------------------------------------------------------------------------- fused optimizer
-    def register_fused_optimizer(self, optimizer) -> bool:
+    def register_fused_optimizer(self, optimizer, shard: bool | None = None) -> bool:
         """Apply ``optimizer`` bucket by bucket inside the reduction (torch's
-        ``DDP._register_fused_optim``): each bucket's parameters are updated on the comm stream
-        right after its gradient is averaged, overlapping the update with the rest of backward
-        and with later buckets' all-reduces. ``optimizer.step()`` then only refreshes the
-        hyper-parameters for the next iteration. Requires a tdp SGD/Adam over exactly this DDP's
+        ``DDP._register_fused_optim``): each bucket's parameters are updated right after its
+        gradient is averaged. ``optimizer.step()`` becomes a no-op; the DDP forward hands the
+        current hyper-parameters to the update. Requires a tdp SGD/Adam over exactly this DDP's
         parameters (one param group). Returns False (optimizer left unfused) on CPU.
+
+        ``shard`` (default: world_size > 1) turns each bucket's all-reduce into reduce-scatter ->
+        update of this rank's 1/W slice -> all-gather of the updated parameters (ZeRO stage 1
+        inside DDP, cf. torch's ZeroRedundancyOptimizer): the same bytes over xGMI, 1/W of the
+        optimizer's HBM traffic, identical parameters on every rank. Gradients are not averaged
+        outside the owned slice afterwards, and optimizer state is only current in the owned
+        slices until :meth:`consolidate_optimizer_state` (called by the checkpoint helpers).
         """
         from ..optim.fused import SGD, Adam
 
@@ -248,7 +254,29 @@ class DistributedDataParallel(nn.Module):
         self._fused_opt = optimizer
         optimizer._fused_ddp = self
         self.push_fused_hyper(optimizer, initial=True)
+        self._fused_shard = bool(self.world_size > 1 if shard is None else shard) and \
+            self.world_size > 1
+        self._backend.fused_shard = self._fused_shard
         return True
+
+    def consolidate_optimizer_state(self) -> None:
+        """Make every rank's fused-optimizer state complete after sharded updates: all-gather
+        each bucket's state slices in place (the tails are already replicated)."""
+        if not getattr(self, "_fused_shard", False) or self._fused_opt is None:
+            return
+        opt = self._fused_opt
+        bufs = opt._flat_bufs.get(id(self.arena), {})
+        comm = rt.comm()
+        W, r = self.world_size, self.rank
+        for name, buf in bufs.items():
+            if not torch.is_tensor(buf) or buf.numel() != self.arena.numel:
+                continue
+            for i in range(len(self._bounds) - 1):
+                begin, end = self._bounds[i], self._bounds[i + 1]
+                cnt = (end - begin) // W
+                if cnt > 0:
+                    comm.all_gather(buf[begin: begin + cnt * W],
+                                    buf[begin + r * cnt: begin + (r + 1) * cnt])
 
     def push_fused_hyper(self, opt, initial: bool = False):
         from ..optim.fused import SGD

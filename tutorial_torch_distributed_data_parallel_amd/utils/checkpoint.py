@@ -81,6 +81,9 @@ def save_training_state(path: str, model, optimizer=None, epoch: int | None = No
     obj = {"model": _detach_clone(unwrap_model(model).state_dict()), "epoch": epoch,
            "extra": extra or {}}
     if optimizer is not None:
+        ddp = getattr(optimizer, "_fused_ddp", None)
+        if ddp is not None:  # sharded in-reduction updates: gather the state slices first
+            ddp.consolidate_optimizer_state()
         obj["optimizer"] = optimizer.state_dict()
     save_on_main(obj if rt.get_rank() == 0 else None, path)
 
