@@ -19,6 +19,7 @@ from .. import ops
 from ..nn import CrossEntropyLoss
 from ..parallel import runtime as rt
 from ..utils import fault
+from ..utils import profiling as prof
 from ..utils.checkpoint import save_ddp_checkpoint
 from ..utils.metrics import EpochMeter, epoch_line
 from ..utils.seed import rng_report
@@ -59,10 +60,13 @@ def train(model, train_loader, criterion, optimizer, device, meter: EpochMeter |
             print(f"TRAIN: Device {device}, Batch {batch_idx}, Data {_sample_repr(inputs)}")
         fault.maybe_inject(rt.get_rank(), global_step + batch_idx)
         optimizer.zero_grad(set_to_none=True)
-        outputs = model(inputs)
-        loss = _loss(criterion, outputs, labels, meter.train)
-        loss.backward()
-        optimizer.step()
+        with prof.range("forward"):
+            outputs = model(inputs)
+            loss = _loss(criterion, outputs, labels, meter.train)
+        with prof.range("backward+reduce"):
+            loss.backward()
+        with prof.range("optimizer"):
+            optimizer.step()
         steps += 1
     meter.steps += steps
     return meter.train[0:1].clone(), meter.train[2:3].clone()
