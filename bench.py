@@ -58,11 +58,11 @@ def parse():
                          "of stream capture on multi-GPU runs")
     ap.add_argument("--eager", action="store_true", help="tdp: run eagerly (the default)")
     ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
-                    help="tdp: apply the optimizer per gradient bucket inside the reduction; "
-                         "with world_size > 1 it is sharded (reduce-scatter -> update 1/W -> "
-                         "all-gather: same wire bytes, 1/W of the optimizer's HBM traffic). "
-                         "auto = on when world_size > 1; on one GPU the single flat step after "
-                         "backward is faster (profiles/bench/mode*.json)")
+                    help="tdp: apply the optimizer inside the gradient reduction (DDP "
+                         "register_fused_optimizer): with world_size > 1 per bucket and sharded "
+                         "(reduce-scatter -> update 1/W -> all-gather: same wire bytes, 1/W of "
+                         "the optimizer's HBM traffic); with world_size 1 in the weight-gradient "
+                         "GEMM epilogues (no gradient write/re-read). auto = on")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
     return ap.parse_args()
 
@@ -128,7 +128,9 @@ def main():
         else:
             opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
         fused = False
-        want_fused = a.fused_opt == "on" or (a.fused_opt == "auto" and world > 1)
+        # auto = on: world > 1 shards the update inside the reduction; world 1 applies it in
+        # the weight-gradient GEMM epilogues (the local gradient is already the average)
+        want_fused = a.fused_opt in ("on", "auto")
         if use_gpu and want_fused and not a.no_fused_opt:
             fused = ddp.register_fused_optimizer(opt)
         data = SyntheticDataset(a.dataset, input_shape(a.model, a.image_size), 10, seed=rank,

@@ -177,3 +177,45 @@ def test_fused_optimizer_matches_unfused(pg, opt_name):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
     sd = o2.state_dict()
     assert len(sd["state"]) == len(list(m2.parameters()))
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam", "sgd_nesterov_wd"])
+def test_optimizer_epilogue_matches_bucket_update(pg, opt_name, monkeypatch):
+    """World size 1: the optimizer applied in the weight-gradient GEMM epilogue (gradient never
+    stored) == the per-bucket fused update == optimizer.step() after backward."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+
+    def build(mode):
+        monkeypatch.setenv("TDP_OPT_EPILOGUE", "1" if mode == "epilogue" else "0")
+        torch.manual_seed(5)
+        m = ToyMLP(in_features=512, hidden=(384, 256), num_classes=10, device="cuda")
+        d = tdp.DDP(m, device_ids=[0], bucket_cap_mb=0.5, first_bucket_cap_mb=0.02)
+        if opt_name == "sgd":
+            o = tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+        elif opt_name == "sgd_nesterov_wd":
+            o = tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9, nesterov=True,
+                              weight_decay=1e-3)
+        else:
+            o = tdp.optim.Adam(d.parameters(), lr=1e-3)
+        if mode != "plain":
+            assert d.register_fused_optimizer(o)
+        assert d._epi_on == (mode == "epilogue")
+        return m, d, o
+
+    runs = [build(mode) for mode in ("plain", "bucket", "epilogue")]
+    for i in range(4):
+        x = torch.randn(128, 512, device="cuda")
+        y = torch.randint(0, 10, (128,), device="cuda")
+        for m, d, o in runs:
+            o.zero_grad(set_to_none=True)
+            tdp.ops.cross_entropy(d(x), y).backward()
+            o.step()
+        if i == 1:
+            for _, _, o in runs:
+                o.param_groups[0]["lr"] *= 0.5
+    torch.cuda.synchronize()
+    ref = list(runs[0][0].parameters())
+    for m, _, _ in runs[1:]:
+        for a, b in zip(ref, m.parameters()):
+            torch.testing.assert_close(b, a, atol=2e-6, rtol=1e-5)

@@ -93,6 +93,41 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
   gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
 }
 
+// Weight-gradient GEMM whose epilogue applies the DDP's fused optimizer to arena elements
+// [offset, offset + M*N) instead of storing the gradient into C (world size 1, see
+// RcclBackend::epilogue_opt). C must be that contiguous arena slice (its contents are left as
+// they were: the gradient is never materialised).
+void gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
+                     RcclBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
+                     double rowsum_beta) {
+  CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
+  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
+  CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_CONTIG(C);
+  const int M = (int)C.size(0), N = (int)C.size(1);
+  const int K = (int)(a_kcontig ? A.size(1) : A.size(0));
+  TORCH_CHECK((a_kcontig ? A.size(0) : A.size(1)) == M, "gemm: A rows != C rows");
+  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm: B cols != C cols");
+  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm: inner dims differ");
+  TORCH_CHECK(backend.epilogue_allowed(), "optimizer epilogue: no fused optimizer at world 1");
+  GemmF32Args a;
+  a.A = A.data_ptr<float>(); a.B = B.data_ptr<float>(); a.C = C.data_ptr<float>();
+  a.lda = A.stride(0); a.ldb = B.stride(0); a.ldc = N;
+  a.M = M; a.N = N; a.K = K;
+  a.a_kcontig = a_kcontig; a.b_kcontig = b_kcontig;
+  if (rowsum.has_value() && rowsum->defined()) {
+    CHECK_GPU(*rowsum); CHECK_F32(*rowsum); CHECK_CONTIG(*rowsum);
+    TORCH_CHECK(rowsum->numel() == M, "gemm: rowsum must have M elements");
+    a.rowsum = rowsum->data_ptr<float>();
+    a.rowsum_beta = (float)rowsum_beta;
+  }
+  TORCH_CHECK((int64_t)M * N < (int64_t)1 << 31, "optimizer epilogue: parameter too large");
+  a.opt = backend.epilogue_opt(offset, (int64_t)M * N);
+  const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
+  gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+}
+
 std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus) {
   GemmF32Args a;
   a.M = M; a.N = N; a.K = K;
@@ -690,6 +725,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("mask") = py::none(),
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none(), py::arg("beta") = 0.0,
         py::arg("rowsum_beta") = 0.0, py::arg("relu") = false);
+  m.def("gemm_f32_opt", &gemm_f32_opt_op, py::arg("A"), py::arg("B"), py::arg("C"),
+        py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
+        py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0);
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);
@@ -809,7 +847,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.fused.s0 = fptr(buf);
              b.fused.sgd = SgdHyper{(float)lr, (float)momentum, (float)dampening, (float)wd,
                                     nesterov, maximize, false, 1.f};
-             if (fresh) b.fused.fresh.assign(1 << 16, 1);
+             if (fresh) {
+               b.fused.fresh.assign(1 << 16, 1);
+               b.set_epilogue_fresh(true);
+             }
            })
       .def("set_fused_adam",
            [](RcclBackend& b, Tensor p, Tensor m, Tensor v, c10::optional<Tensor> vmax,
@@ -828,6 +869,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.fused.adam_step = step;
            })
       .def("clear_fused", [](RcclBackend& b) { b.fused = FusedOptimizer{}; })
+      .def_property_readonly("epilogue_allowed", &RcclBackend::epilogue_allowed)
       .def_property("fused_shard", [](RcclBackend& b) { return b.fused.shard; },
                     [](RcclBackend& b, bool v) { b.fused.shard = v; })
       .def_property_readonly("fused_adam_step",

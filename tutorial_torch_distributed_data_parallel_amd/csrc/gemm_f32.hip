@@ -345,6 +345,15 @@ void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStre
   else launch_tile<false>(plan.tile, p, grid, a.a_kcontig, a.b_kcontig, s);
   if (plan.splits > 1)
     splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+  if (a.opt.kind != 0) gemm_opt_fallback(a, s);
+}
+
+// The generic kernel has no optimizer epilogue: C now holds the gradient, apply the flat update.
+void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s) {
+  const OptEpilogue& o = a.opt;
+  const long n = (long)a.M * a.N;
+  if (o.kind == 1) sgd_flat(o.p, a.C, o.s0, n, o.sgd, s);
+  else if (o.kind == 2) adam_flat(o.p, a.C, o.s0, o.s1, o.s2, n, o.adam, s);
 }
 
 void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf16, long ldc,

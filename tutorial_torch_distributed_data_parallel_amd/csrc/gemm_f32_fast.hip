@@ -30,6 +30,7 @@
 #include "common.h"
 #include "conv.h"
 #include "kernels.h"
+#include "optim_elem.h"
 
 namespace tdp {
 namespace {
@@ -63,6 +64,7 @@ struct FastParams {
   int tiles_n, tiles_m;
   float beta, rowsum_beta;
   int relu;
+  OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -301,7 +303,7 @@ struct SrcOf<R, kImWgrad, false> : ImSrcB<R, false> {};
 template <int R>
 struct SrcOf<R, kImWgradT, true> : ImSrcB<R, true> {};
 
-template <int FN, int AKIND, int BKIND, int S>
+template <int FN, int AKIND, int BKIND, int S, int OPTK>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
@@ -469,6 +471,104 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
 
   // epilogue
   const bool split = p.splits > 1;
+  if (OPTK != 0) {
+    // optimizer epilogue (no split-K by construction): C is a weight gradient; update the
+    // parameter and its optimizer state at C's index instead of storing C. The epilogue is
+    // latency-bound (each element is read, updated, written back), so every p / state load of a
+    // batch is issued before the first update: one HBM round trip per batch. A batch is the whole
+    // FM x 16 x FN accumulator set for FN == 1, one row tile (16 adjacent column pairs) for
+    // FN == 2. With interleaved MN-contiguous B (FN == 2) a lane owns two ADJACENT columns, read
+    // and written as float2 (two half-sector stores per line would force partial write-backs).
+    // Offsets are 32-bit (a parameter has < 2^31 elements; checked on the host).
+    constexpr bool SGD = OPTK == 1;
+    const OptEpilogue& o = p.opt;
+    const bool mom_rd = SGD && o.sgd.momentum != 0.f && !o.sgd.first_step;
+    const bool mom_wr = SGD && o.sgd.momentum != 0.f;
+    constexpr bool PAIR = !BKC && FN == 2;
+    constexpr int NG = PAIR ? 1 : FN;       // column groups per accumulator row
+    constexpr int NE = PAIR ? 2 : 1;        // elements per group
+    constexpr int FB = PAIR ? 1 : FM;       // row tiles per batch
+    constexpr int NB = FB * 16 * NG;        // groups per batch
+#pragma unroll
+    for (int f0 = 0; f0 < FM; f0 += FB) {
+      int idx[NB];
+      float pv[NB * NE], s0v[NB * NE], s1v[SGD ? 1 : NB * NE];
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int f = f0 + fb;
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            const int col = PAIR ? n0 + wn * 64 + 2 * l31 : n0 + wn * (32 * FN) + g * 32 + l31;
+            const int j = (fb * 16 + r) * NG + g;
+            // PAIR: N % 4 == 0 (fast-path precondition), so col + 1 < N whenever col < N;
+            // out-of-range lanes are marked by idx = -1 (and read element 0)
+            const bool ok = row < p.M && col < p.N;
+            idx[j] = ok ? row * (int)p.ldc + col : -1;
+            const int i = ok ? idx[j] : 0;
+            if (PAIR) {
+              const f32x2 v = *reinterpret_cast<const f32x2*>(o.p + i);
+              pv[2 * j] = v[0]; pv[2 * j + 1] = v[1];
+              if (!SGD || mom_rd) {
+                const f32x2 w = *reinterpret_cast<const f32x2*>(o.s0 + i);
+                s0v[2 * j] = w[0]; s0v[2 * j + 1] = w[1];
+              }
+              if (!SGD) {
+                const f32x2 u = *reinterpret_cast<const f32x2*>(o.s1 + i);
+                s1v[2 * j] = u[0]; s1v[2 * j + 1] = u[1];
+              }
+            } else {
+              pv[j] = o.p[i];
+              if (!SGD || mom_rd) s0v[j] = o.s0[i];
+              if (!SGD) s1v[j] = o.s1[i];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            const int j = (fb * 16 + r) * NG + g;
+            const int i = idx[j];
+            if (i < 0) continue;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const float gr = acc[f0 + fb][PAIR ? e : g][r];
+              float pe = pv[j * NE + e];
+              float b0 = (!SGD || mom_rd) ? s0v[j * NE + e] : 0.f;
+              if (SGD) {
+                sgd_elem(pe, gr, b0, o.sgd);
+              } else {
+                float b1 = s1v[j * NE + e];
+                adam_elem(pe, gr, b0, b1, o.s2 ? o.s2 + i + e : nullptr, o.adam);
+                s1v[j * NE + e] = b1;
+              }
+              pv[j * NE + e] = pe;
+              s0v[j * NE + e] = b0;
+            }
+            if (PAIR) {
+              *reinterpret_cast<f32x2*>(o.p + i) = f32x2{pv[2 * j], pv[2 * j + 1]};
+              if (!SGD || mom_wr)
+                *reinterpret_cast<f32x2*>(o.s0 + i) = f32x2{s0v[2 * j], s0v[2 * j + 1]};
+              if (!SGD)
+                *reinterpret_cast<f32x2*>(o.s1 + i) = f32x2{s1v[2 * j], s1v[2 * j + 1]};
+            } else {
+              o.p[i] = pv[j];
+              if (!SGD || mom_wr) o.s0[i] = s0v[j];
+              if (!SGD) o.s1[i] = s1v[j];
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
   float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
   const long ldo = split ? p.N : p.ldc;
 #pragma unroll
@@ -520,28 +620,28 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S>
+template <int FN, int AKIND, int BKIND, int S, int OPT = 0>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
   constexpr int STG = 128 * kBK * 4 + 64 * FN * kBK * 4;
   const size_t lds = (size_t)S * STG;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S>,
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S>), dim3(nblocks), dim3(kT), lds,
-                     s, p);
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT>), dim3(nblocks), dim3(kT),
+                     lds, s, p);
 }
 
-template <int AKIND, int BKIND>
+template <int AKIND, int BKIND, int OPT = 0>
 void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s) {
   if (fn == 1) {
-    if (stages == 3) launch_fast<1, AKIND, BKIND, 3>(p, nblocks, s);
-    else launch_fast<1, AKIND, BKIND, 2>(p, nblocks, s);
+    if (stages == 3) launch_fast<1, AKIND, BKIND, 3, OPT>(p, nblocks, s);
+    else launch_fast<1, AKIND, BKIND, 2, OPT>(p, nblocks, s);
   } else {
-    if (stages == 3) launch_fast<2, AKIND, BKIND, 3>(p, nblocks, s);
-    else launch_fast<2, AKIND, BKIND, 2>(p, nblocks, s);
+    if (stages == 3) launch_fast<2, AKIND, BKIND, 3, OPT>(p, nblocks, s);
+    else launch_fast<2, AKIND, BKIND, 2, OPT>(p, nblocks, s);
   }
 }
 
@@ -583,6 +683,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
     if (splits < 1) splits = 1;
   }
   if (o_splits > 0 && a.rowsum == nullptr) splits = o_splits;
+  if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
   plan.bm = 128;
@@ -608,15 +709,26 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.beta = plan.splits > 1 ? 0.f : a.beta;
   p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
+  p.opt = a.opt;
   const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
   const bool ak = a.a_kcontig, bk = a.b_kcontig;
   const int fn = plan.tile, st = plan.stages;
+  // the optimizer epilogue is instantiated for the weight-gradient layout only (A = dY^T and
+  // B = X both MN-contiguous); any other use stores C and applies the flat update afterwards
+  const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
+  if (opt) {
+    if (a.opt.kind == 1) launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nblocks, s);
+    else launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nblocks, s);
+    return;
+  }
+  p.opt.kind = 0;
   if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nblocks, s);
   else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nblocks, s);
   else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nblocks, s);
   else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nblocks, s);
   if (plan.splits > 1)
     splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+  if (a.opt.kind != 0) gemm_opt_fallback(a, s);
 }
 
 // ------------------------------------------------------------------ implicit-GEMM convolution

@@ -10,6 +10,37 @@
 namespace tdp {
 
 // ------------------------------------------------------------------------------------------------
+// Optimizer hyper-parameters (fused single-pass updates, csrc/optim.hip + optim_elem.h)
+// ------------------------------------------------------------------------------------------------
+struct SgdHyper {
+  float lr, momentum, dampening, weight_decay;
+  bool nesterov, maximize, first_step;
+  float grad_scale;  // grads are multiplied by this first (1/world for sum-reduced grads)
+};
+
+struct AdamHyper {
+  float lr, beta1, beta2, eps, weight_decay;
+  bool amsgrad, maximize, decoupled;  // decoupled = AdamW
+  float bc1, bc2_sqrt;                // 1-beta1^t, sqrt(1-beta2^t)
+  float grad_scale;
+};
+
+// Optimizer update applied by a GEMM epilogue in place of storing the result: when C is a weight
+// gradient, the epilogue reads p / state at C's element index (same layout and leading dimension
+// as C), updates them and never writes C. Used for the weight-gradient GEMMs when the gradient
+// needs no cross-rank reduction (world size 1): it removes the gradient's HBM write + re-read and
+// overlaps the update's memory traffic with the GEMM's MFMA work.
+struct OptEpilogue {
+  int kind = 0;  // 0 none, 1 SGD, 2 Adam
+  float* p = nullptr;
+  float* s0 = nullptr;  // momentum buffer / exp_avg
+  float* s1 = nullptr;  // exp_avg_sq
+  float* s2 = nullptr;  // max_exp_avg_sq
+  SgdHyper sgd{};
+  AdamHyper adam{};
+};
+
+// ------------------------------------------------------------------------------------------------
 // fp32 GEMM on v_mfma_f32_32x32x2_f32 (exact f32, the dtype of the reference's nn.Linear).
 //   C[M,N] = op(A)[M,K] . op(B)[K,N]  (+ bias[N]) (+ beta*C) (ReLU)
 //   a_kcontig: A stored [M][K] (else [K][M]);  b_kcontig: B stored [N][K] (else [K][N]).
@@ -29,6 +60,7 @@ struct GemmF32Args {
   bool a_kcontig = true, b_kcontig = true;
   float beta = 0.f, rowsum_beta = 0.f;
   bool relu = false;
+  OptEpilogue opt;  // kind != 0: apply the optimizer instead of storing C (needs splits == 1)
 };
 
 struct GemmPlan {
@@ -44,6 +76,8 @@ struct GemmPlan {
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
 bool gemm_f32_fast_ok(const GemmF32Args& a);
+// C (contiguous, ldc == N) holds a finished gradient: apply a.opt as a flat update over it
+void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s);
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
 // set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel
@@ -94,19 +128,8 @@ void count_correct(const float* logits, const int64_t* labels, int B, int C, lon
 // ------------------------------------------------------------------------------------------------
 // Optimizers: fused single-pass updates over a flat arena or a multi-tensor chunk table.
 // ------------------------------------------------------------------------------------------------
-struct SgdHyper {
-  float lr, momentum, dampening, weight_decay;
-  bool nesterov, maximize, first_step;
-  float grad_scale;  // grads are multiplied by this first (1/world for sum-reduced grads)
-};
 void sgd_flat(float* p, const float* g, float* buf, long n, const SgdHyper& h, hipStream_t s);
 
-struct AdamHyper {
-  float lr, beta1, beta2, eps, weight_decay;
-  bool amsgrad, maximize, decoupled;  // decoupled = AdamW
-  float bc1, bc2_sqrt;                // 1-beta1^t, sqrt(1-beta2^t)
-  float grad_scale;
-};
 void adam_flat(float* p, const float* g, float* m, float* v, float* vmax, long n,
                const AdamHyper& h, hipStream_t s);
 

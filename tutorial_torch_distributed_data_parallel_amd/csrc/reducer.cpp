@@ -99,7 +99,10 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
     first = (bool)fused.fresh[bucket];
     fused.fresh[bucket] = 0;
   }
-  if (n > 0 && fused.kind == 2 && bucket == 0) ++fused.adam_step;
+  if (n > 0 && fused.kind == 2 && bucket == 0 && !bucket0_launched_) {
+    ++fused.adam_step;
+    bucket0_launched_ = true;
+  }
   float* g = reinterpret_cast<float*>(arena_) + begin;
   if (n > 0 && collective && fused.kind != 0 && fused.shard && W > 1 &&
       compression_ == Compression::NONE && elem_size_ == 4) {
@@ -137,8 +140,50 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   if (post_bucket) post_bucket(bucket, begin, end, cs);
 }
 
-// optimizer update of arena elements [off, off + cnt) (no-op without a fused optimizer)
+// optimizer update of arena elements [off, off + cnt) minus the ranges a GEMM epilogue already
+// updated this iteration (no-op without a fused optimizer)
 void RcclBackend::apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs) {
+  if (cnt <= 0 || fused.kind == 0) return;
+  int64_t cur = off;
+  const int64_t end = off + cnt;
+  for (const auto& r : epi_done_) {  // sorted, disjoint
+    if (r.second <= cur || r.first >= end) continue;
+    if (r.first > cur) apply_fused_range(cur, r.first - cur, first, cs);
+    cur = std::max(cur, r.second);
+  }
+  if (cur < end) apply_fused_range(cur, end - cur, first, cs);
+}
+
+bool RcclBackend::epilogue_allowed() const {
+  return fused.kind != 0 && comm_->world() == 1 && skip_single_rank_ &&
+         compression_ == Compression::NONE && elem_size_ == 4;
+}
+
+OptEpilogue RcclBackend::epilogue_opt(int64_t off, int64_t n) {
+  if (!epilogue_allowed()) throw std::runtime_error("optimizer epilogue needs world size 1");
+  if (off < 0 || n <= 0 || off + n > numel_) throw std::runtime_error("epilogue range");
+  OptEpilogue o;
+  o.kind = fused.kind;
+  o.p = fused.p + off;
+  o.s0 = fused.s0 ? fused.s0 + off : nullptr;
+  o.s1 = fused.s1 ? fused.s1 + off : nullptr;
+  o.s2 = fused.s2 ? fused.s2 + off : nullptr;
+  if (fused.kind == 1) {
+    o.sgd = fused.sgd;
+    o.sgd.first_step = epi_fresh_;
+  } else {
+    // the step counter advances with this iteration's first bucket; an epilogue can run before it
+    const double t = (double)(fused.adam_step + (bucket0_launched_ ? 0 : 1));
+    o.adam = fused.adam;
+    o.adam.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
+    o.adam.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
+  }
+  auto it = std::lower_bound(epi_done_.begin(), epi_done_.end(), std::make_pair(off, off + n));
+  epi_done_.insert(it, {off, off + n});
+  return o;
+}
+
+void RcclBackend::apply_fused_range(int64_t off, int64_t cnt, bool first, hipStream_t cs) {
   if (cnt <= 0) return;
   float* g = reinterpret_cast<float*>(arena_) + off;
   if (fused.kind == 1) {
@@ -156,6 +201,10 @@ void RcclBackend::apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t 
 }
 
 void RcclBackend::wait_all(hipStream_t compute) {
+  // iteration boundary: epilogue bookkeeping restarts
+  epi_done_.clear();
+  if (fused.kind != 0) epi_fresh_ = false;
+  bucket0_launched_ = false;
   if (!launched_any_) return;
   if (!launched_side_) {  // everything ran on the compute stream: already ordered
     launched_any_ = false;

@@ -79,8 +79,20 @@ class RcclBackend : public ReducerBackend {
   std::function<void(int, int64_t, int64_t, hipStream_t)> post_bucket;
   FusedOptimizer fused;
 
+  // Optimizer-in-GEMM-epilogue (world size 1 only: the local gradient IS the averaged one): the
+  // weight-gradient GEMM of arena elements [off, off + n) applies the fused optimizer instead of
+  // storing the gradient. Returns the epilogue arguments (pointers offset to `off`, this
+  // iteration's hyper-parameters) and records the range so the bucket update skips it.
+  OptEpilogue epilogue_opt(int64_t off, int64_t n);
+  bool epilogue_allowed() const;
+  void set_epilogue_fresh(bool v) { epi_fresh_ = v; }
+
  private:
   void apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs);
+  void apply_fused_range(int64_t off, int64_t cnt, bool first, hipStream_t cs);
+  std::vector<std::pair<int64_t, int64_t>> epi_done_;  // ranges updated by GEMM epilogues
+  bool epi_fresh_ = false;        // SGD momentum of epilogue-updated ranges not yet initialised
+  bool bucket0_launched_ = false;  // this iteration's Adam step counter already advanced
   std::shared_ptr<Communicator> comm_;
   char* arena_;
   int64_t numel_;

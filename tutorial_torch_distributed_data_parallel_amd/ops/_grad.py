@@ -23,5 +23,17 @@ def grad_dest(p: torch.Tensor | None) -> torch.Tensor | None:
     return torch.empty_like(p)
 
 
+def epilogue_target(p: torch.Tensor | None):
+    """``(reducer_backend, arena_offset)`` when the weight-gradient GEMM of ``p`` should apply the
+    DDP's fused optimizer in its epilogue instead of storing the gradient (world size 1, fused
+    optimizer registered, gradient sync on, ``p.grad`` empty); else None. See
+    ``DistributedDataParallel.register_fused_optimizer``."""
+    ref = getattr(p, "_tdp_epi", None) if p is not None else None
+    if ref is None or p.grad is not None:
+        return None
+    ddp = ref()
+    return ddp.epilogue_slot(p) if ddp is not None else None
+
+
 def needs(ctx, i: int) -> bool:
     return bool(ctx.needs_input_grad[i])

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
-from ._grad import grad_dest, needs
+from ._grad import epilogue_target, grad_dest, needs
 
 
 class _LinearFn(torch.autograd.Function):
@@ -43,17 +43,24 @@ class _LinearFn(torch.autograd.Function):
         db = grad_dest(b_param) if want_db else None
         # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU)
         g = C.relu_bias_bwd(dy, y) if ctx.relu else dy
+        epi = epilogue_target(w_param) if needs(ctx, 1) else None
+        if needs(ctx, 0):
+            dx = torch.empty_like(x2)
+            # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
+            # (before the weight-gradient GEMM: with an optimizer epilogue that one updates W)
+            C.gemm_f32(g, weight, dx, True, False)
         if needs(ctx, 1):
             dw = grad_dest(w_param)
             # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];
             # the bias gradient (sum over the batch of g) is reduced inside the same kernel
-            C.gemm_f32(g, x2, dw, False, False, rowsum=db)
+            if epi is not None:
+                # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
+                # from the accumulators; the gradient itself is never written to HBM
+                C.gemm_f32_opt(g, x2, dw, False, False, epi[0], epi[1], rowsum=db)
+            else:
+                C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        if needs(ctx, 0):
-            dx = torch.empty_like(x2)
-            # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
-            C.gemm_f32(g, weight, dx, True, False)
         return dx, dw, db, None
 
 

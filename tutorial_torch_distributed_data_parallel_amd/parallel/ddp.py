@@ -20,6 +20,7 @@ import os
 
 import contextlib
 import hashlib
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -120,6 +121,8 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._iter = 0
         self._fused_opt = None
+        self._epi_on = False
+        self._epi_index = {}
         # SURVEY.md §5.2 debug mode: every N forwards, verify that all replicas hold bit-identical
         # parameters (a checksum all-gather); TDP_CHECK_REPLICAS=N sets it from the environment
         env_every = int(os.environ.get("TDP_CHECK_REPLICAS", "0") or 0)
@@ -257,7 +260,27 @@ class DistributedDataParallel(nn.Module):
         self._fused_shard = bool(self.world_size > 1 if shard is None else shard) and \
             self.world_size > 1
         self._backend.fused_shard = self._fused_shard
+        # world size 1: the local gradient is already the average, so weight-gradient GEMMs may
+        # apply the update in their epilogue (TDP_OPT_EPILOGUE=0 keeps the per-bucket update)
+        self._epi_index = {id(p): i for i, p in enumerate(self.arena.params)}
+        self._epi_on = (os.environ.get("TDP_OPT_EPILOGUE", "1") != "0" and
+                        bool(self._backend.epilogue_allowed))
+        if self._epi_on:
+            me = weakref.ref(self)
+            for p in self.arena.params:
+                p._tdp_epi = me
         return True
+
+    def epilogue_slot(self, p):
+        """(backend, arena offset) for an optimizer-epilogue weight-gradient GEMM of ``p`` in the
+        current backward, or None when the update must stay in the bucket path."""
+        if not (self._epi_on and self.require_backward_grad_sync and self.reducer.expecting and
+                self._backend.epilogue_allowed):
+            return None
+        i = self._epi_index.get(id(p))
+        if i is None or not self.arena.numels[i]:
+            return None
+        return self._backend, self.arena.offsets[i]
 
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
