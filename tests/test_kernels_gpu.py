@@ -256,3 +256,32 @@ def test_gemm_fast_wgrad_rowsum(C):
         C.gemm_f32(g, x, dw, False, False, rowsum=db)
         _close(dw, (g.t().double() @ x.double()).float(), atol=2e-3)
         _close(db, g.sum(0), atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,a_k,b_k", [(128, 10, 4096, True, True), (77, 13, 260, True, True),
+                                           (128, 4096, 10, True, False), (33, 64, 16, True, False),
+                                           (10, 4096, 128, False, False), (16, 100, 300, False, False),
+                                           (3, 7, 5, False, False)])
+def test_gemm_skinny_epilogues(C, M, N, K, a_k, b_k):
+    """Skinny kernels (one dimension <= 16): bias + ReLU + beta*C and the row-sum bias gradient."""
+    torch.manual_seed(M * 7 + N + K)
+    d = "cuda"
+    A = torch.randn((M, K) if a_k else (K, M), device=d)
+    B = torch.randn((N, K) if b_k else (K, N), device=d)
+    ref = _ref_gemm(A, B, a_k, b_k)
+    tol = 2e-4 * max(1.0, K ** 0.5)
+    bias = torch.randn(N, device=d)
+    out = torch.empty(M, N, device=d)
+    C.gemm_f32(A, B, out, a_k, b_k, bias=bias, relu=True)
+    _close(out, torch.relu(ref + bias), rtol=1e-4, atol=tol)
+    prev = torch.randn(M, N, device=d)
+    out = prev.clone()
+    C.gemm_f32(A, B, out, a_k, b_k, beta=1.0)
+    _close(out, ref + prev, rtol=1e-4, atol=tol)
+    if not a_k:
+        rs = torch.randn(M, device=d)
+        rs0 = rs.clone()
+        out = torch.empty(M, N, device=d)
+        C.gemm_f32(A, B, out, a_k, b_k, rowsum=rs, rowsum_beta=1.0)
+        _close(out, ref, rtol=1e-4, atol=tol)
+        _close(rs, rs0 + A.double().sum(0).float(), rtol=1e-4, atol=1e-3)

@@ -93,11 +93,11 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
   gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
 }
 
-// Weight-gradient GEMM whose epilogue applies the DDP's fused optimizer to arena elements
+// Returns whether the epilogue ran. Weight-gradient GEMM whose epilogue applies the DDP's fused optimizer to arena elements
 // [offset, offset + M*N) instead of storing the gradient into C (world size 1, see
 // RcclBackend::epilogue_opt). C must be that contiguous arena slice (its contents are left as
 // they were: the gradient is never materialised).
-void gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
+bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
                      RcclBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
                      double rowsum_beta) {
   CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
@@ -121,11 +121,18 @@ void gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
     a.rowsum_beta = (float)rowsum_beta;
   }
   TORCH_CHECK((int64_t)M * N < (int64_t)1 << 31, "optimizer epilogue: parameter too large");
-  a.opt = backend.epilogue_opt(offset, (int64_t)M * N);
+  // the epilogue exists on the fast kernel's weight-gradient layout without split-K; any other
+  // plan stores the gradient and leaves the update to the reducer's end-of-backward launch
+  GemmF32Args probe = a;
+  probe.opt.kind = 1;
+  const GemmPlan pp = gemm_f32_plan(probe, num_cus(C.get_device()));
+  const bool epi = pp.fast && !pp.skinny && pp.splits == 1 && !a_kcontig && !b_kcontig;
+  if (epi) a.opt = backend.epilogue_opt(offset, (int64_t)M * N);
   const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
   gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  return epi;
 }
 
 std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus) {

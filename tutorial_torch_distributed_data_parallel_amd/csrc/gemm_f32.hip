@@ -294,11 +294,15 @@ inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 }  // namespace
 
-static int g_mode = 0;
+static int g_mode = 0;  // 0 auto, 1 generic, 2 fast, 3 auto (skinny allowed; = 0)
 void gemm_f32_set_mode(int mode) { g_mode = mode; }
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus) {
   GemmPlan plan;
+  if (g_mode == 0 || g_mode == 3) {
+    plan.skinny = gemm_skinny_kind(a);
+    if (plan.skinny) return plan;
+  }
   if (g_mode != 1 && gemm_f32_fast_ok(a)) {
     gemm_f32_fast_plan(a, num_cus, plan);
     return plan;
@@ -328,6 +332,11 @@ GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus) {
 
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
+  if (plan.skinny) {
+    gemm_skinny_run(plan.skinny, a, s);
+    if (a.opt.kind != 0) gemm_opt_fallback(a, s);
+    return;
+  }
   if (plan.fast) {
     gemm_f32_fast_run(a, plan, ws, s);
     return;

@@ -1,0 +1,208 @@
+// Skinny fp32 GEMMs: one dimension <= 16 (a classifier head with few classes, its gradients).
+//
+// The toy MLP / AlexNet head Linear(4096, 10) produces three GEMMs with a dimension of 10: the
+// forward [B x 10] = X[B x 4096] . W^T (N = 10), the input gradient [B x 4096] = dY[B x 10] . W
+// (K = 10) and the weight gradient [10 x 4096] = dY^T . X (M = 10). On the MFMA tile kernels
+// they cost a split-K launch + a combine, or a 64-wide tile that is 85 % padding (9-15 us each,
+// profiles/mlp_dp1_eager_kernel_stats_v3.md); here each is one small bandwidth-shaped launch:
+//   * skinny_n : one workgroup per output row, K spread over its 256 lanes as f32x4 chunks, the
+//                N <= 16 dot products kept in registers, reduced across waves at the end;
+//   * skinny_k : every lane produces 4 adjacent outputs of a row from the K <= 16 row of A
+//                (wave-uniform scalar loads) and K f32x4 rows of B;
+//   * skinny_m : A staged in LDS, 64 columns x 4 K-quarters per workgroup, M <= 16
+//                accumulators per lane, the quarters combined through LDS; the bias gradient
+//                (row sums of A) comes from workgroup 0.
+// All three apply the usual epilogue (bias, beta * C, ReLU) and need 16-B aligned rows.
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace tdp {
+namespace {
+
+constexpr int kSkinnyMax = 16;
+
+struct SkinnyParams {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  float* rowsum;
+  long lda, ldb, ldc;
+  int M, N, K;
+  float beta, rowsum_beta;
+  int relu;
+};
+
+__device__ __forceinline__ float epi(float v, const SkinnyParams& p, const float* crow, int col) {
+  if (p.bias) v += p.bias[col];
+  if (p.beta != 0.f) v += p.beta * crow[col];
+  if (p.relu) v = fmaxf(v, 0.f);
+  return v;
+}
+
+// C[M, N<=16] = A[M, K] . B[N, K]^T  (A and B K-contiguous, K % 4 == 0). One 256-thread
+// workgroup per row: the K axis is spread over all 256 lanes as f32x4 chunks (4 chunks per lane
+// for K = 4096, unrolled so every load of the row is in flight at once), then the N partial dot
+// products are reduced across the wave (shuffles) and the 4 waves (LDS).
+template <int NMAX>
+__global__ __launch_bounds__(256) void skinny_n_kernel(SkinnyParams p) {
+  __shared__ float red[4][NMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x;
+  const float* a = p.A + (long)row * p.lda;
+  float acc[NMAX];
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) acc[n] = 0.f;
+#pragma unroll 4
+  for (int k = threadIdx.x * 4; k < p.K; k += 1024) {
+    const f32x4 av = *reinterpret_cast<const f32x4*>(a + k);
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+      if (n < p.N) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.B + (long)n * p.ldb + k);
+        acc[n] = fmaf(av[0], bv[0], fmaf(av[1], bv[1], fmaf(av[2], bv[2], fmaf(av[3], bv[3],
+                                                                             acc[n]))));
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) {
+    const float v = wave_sum(acc[n]);
+    if (lane == 0) red[w][n] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < p.N) {
+    const int n = threadIdx.x;
+    const float v = red[0][n] + red[1][n] + red[2][n] + red[3][n];
+    float* crow = p.C + (long)row * p.ldc;
+    crow[n] = epi(v, p, crow, n);
+  }
+}
+
+// C[M, N] = A[M, K<=16] . B[K, N]  (A K-contiguous, B [K][N] row-major, N % 4 == 0)
+__global__ __launch_bounds__(256) void skinny_k_kernel(SkinnyParams p) {
+  const long per_row = p.N / 4;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= per_row * p.M) return;
+  const int row = (int)(t / per_row);
+  const int col = (int)(t % per_row) * 4;
+  const float* a = p.A + (long)row * p.lda;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < p.K; ++k) {
+    const float av = a[k];
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(p.B + (long)k * p.ldb + col);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = fmaf(av, bv[e], acc[e]);
+  }
+  float* crow = p.C + (long)row * p.ldc;
+  f32x4 out;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[e] = epi(acc[e], p, crow, col + e);
+  *reinterpret_cast<f32x4*>(crow + col) = out;
+}
+
+// C[M<=16, N] = A^T . B with A stored [K][M], B stored [K][N]; rowsum[m] = sum_k A[k][m].
+// A (K x M, a few KiB) is staged in LDS once per workgroup; each workgroup owns 64 columns and
+// splits K over its 4 waves (unrolled by 8 so the B loads overlap), partials combined in LDS.
+template <int MMAX>
+__global__ __launch_bounds__(256) void skinny_m_kernel(SkinnyParams p) {
+  extern __shared__ float smem[];  // [K][MMAX] copy of A, then reused for the 4 x MMAX x 64 sums
+  const int cl = threadIdx.x & 63;
+  const int q = threadIdx.x >> 6;  // K quarter
+  const int col = blockIdx.x * 64 + cl;
+  for (int i = threadIdx.x; i < p.K * MMAX; i += 256) {
+    const int k = i / MMAX, m = i % MMAX;
+    smem[i] = m < p.M ? p.A[(long)k * p.lda + m] : 0.f;
+  }
+  __syncthreads();
+  const int kq = (p.K + 3) / 4;
+  const int k0 = q * kq, k1 = min(p.K, k0 + kq);
+  float acc[MMAX];
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) acc[m] = 0.f;
+  const int cc = col < p.N ? col : p.N - 1;
+#pragma unroll 8
+  for (int k = k0; k < k1; ++k) {
+    const float bv = p.B[(long)k * p.ldb + cc];
+    const float* arow = smem + k * MMAX;
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) acc[m] = fmaf(arow[m], bv, acc[m]);
+  }
+  float rs = 0.f;  // bias gradient: block 0 sums A's column m = threadIdx.x over K (from LDS)
+  if (p.rowsum && blockIdx.x == 0 && threadIdx.x < p.M)
+    for (int k = 0; k < p.K; ++k) rs += smem[k * MMAX + threadIdx.x];
+  __syncthreads();  // A no longer needed: reuse LDS for the cross-wave partial sums
+  float* red = smem;  // [4][MMAX][64]
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) red[(q * MMAX + m) * 64 + cl] = acc[m];
+  __syncthreads();
+  for (int o = threadIdx.x; o < MMAX * 64; o += 256) {
+    const int m = o / 64, c = o % 64;
+    const int gc = blockIdx.x * 64 + c;
+    if (m < p.M && gc < p.N) {
+      const float v = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
+                      red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
+      float* crow = p.C + (long)m * p.ldc;
+      crow[gc] = epi(v, p, crow, gc);
+    }
+  }
+  if (p.rowsum && blockIdx.x == 0 && threadIdx.x < p.M) {
+    const int m = threadIdx.x;
+    p.rowsum[m] = (p.rowsum_beta != 0.f ? p.rowsum_beta * p.rowsum[m] : 0.f) + rs;
+  }
+}
+
+bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+SkinnyParams params_of(const GemmF32Args& a) {
+  SkinnyParams p;
+  p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.rowsum = a.rowsum;
+  p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
+  p.M = a.M; p.N = a.N; p.K = a.K;
+  p.beta = a.beta; p.rowsum_beta = a.rowsum_beta; p.relu = a.relu ? 1 : 0;
+  return p;
+}
+
+}  // namespace
+
+int gemm_skinny_kind(const GemmF32Args& a) {
+  if (a.mask || a.opt.kind != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0) return 0;
+  if (a.a_kcontig && a.b_kcontig && a.N <= kSkinnyMax && a.rowsum == nullptr &&
+      a.K % 4 == 0 && al16(a.A) && al16(a.B) && a.lda % 4 == 0 && a.ldb % 4 == 0)
+    return 1;
+  if (a.a_kcontig && !a.b_kcontig && a.K <= kSkinnyMax && a.rowsum == nullptr &&
+      a.N % 4 == 0 && al16(a.B) && al16(a.C) && a.ldb % 4 == 0 && a.ldc % 4 == 0 &&
+      (a.bias == nullptr || al16(a.bias)))
+    return 2;
+  // skinny_m stages A (K x 8 or K x 16 floats) in LDS: keep it within the default 64 KiB
+  if (!a.a_kcontig && !a.b_kcontig && a.M <= kSkinnyMax &&
+      (long)a.K * (a.M <= 8 ? 8 : kSkinnyMax) * 4 <= 65536)
+    return 3;
+  return 0;
+}
+
+void gemm_skinny_run(int kind, const GemmF32Args& a, hipStream_t s) {
+  const SkinnyParams p = params_of(a);
+  if (kind == 1) {
+    if (a.N <= 8)
+      hipLaunchKernelGGL(skinny_n_kernel<8>, dim3(a.M), dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL(skinny_n_kernel<kSkinnyMax>, dim3(a.M), dim3(256), 0, s, p);
+  } else if (kind == 2) {
+    const long threads = (long)a.M * (a.N / 4);
+    hipLaunchKernelGGL(skinny_k_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       p);
+  } else {
+    const int grid = (a.N + 63) / 64;
+    const int mm = a.M <= 8 ? 8 : kSkinnyMax;
+    const size_t lds = sizeof(float) * (size_t)std::max(a.K * mm, 4 * mm * 64);
+    if (mm == 8)
+      hipLaunchKernelGGL(skinny_m_kernel<8>, dim3(grid), dim3(256), lds, s, p);
+    else
+      hipLaunchKernelGGL(skinny_m_kernel<kSkinnyMax>, dim3(grid), dim3(256), lds, s, p);
+  }
+}
+
+}  // namespace tdp

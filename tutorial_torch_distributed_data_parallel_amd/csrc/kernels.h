@@ -71,11 +71,15 @@ struct GemmPlan {
   int splits = 1;
   int k_per_split = 0;
   long ws_floats = 0;   // split-K workspace needed (0 when splits == 1)
+  int skinny = 0;       // > 0: one of the skinny kernels (gemm_skinny.hip) runs instead
 };
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
 bool gemm_f32_fast_ok(const GemmF32Args& a);
+// skinny GEMM kind for a dimension <= 16 (1: N, 2: K, 3: M; 0: not applicable), and its launch
+int gemm_skinny_kind(const GemmF32Args& a);
+void gemm_skinny_run(int kind, const GemmF32Args& a, hipStream_t s);
 // C (contiguous, ldc == N) holds a finished gradient: apply a.opt as a flat update over it
 void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s);
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
@@ -129,6 +133,19 @@ void count_correct(const float* logits, const int64_t* labels, int B, int C, lon
 // Optimizers: fused single-pass updates over a flat arena or a multi-tensor chunk table.
 // ------------------------------------------------------------------------------------------------
 void sgd_flat(float* p, const float* g, float* buf, long n, const SgdHyper& h, hipStream_t s);
+// Up to kMaxRanges disjoint element ranges [begin, begin + len) of equally laid out flat buffers
+// (parameter / gradient / state arenas), updated by ONE launch (the world-size-1 reducer collects
+// every range the weight-gradient epilogues did not already update).
+constexpr int kMaxRanges = 16;
+struct RangeSet {
+  int n = 0;
+  long begin[kMaxRanges];
+  long len[kMaxRanges];
+};
+void sgd_ranges(float* p, const float* g, float* buf, const RangeSet& r, const SgdHyper& h,
+                hipStream_t s);
+void adam_ranges(float* p, const float* g, float* m, float* v, float* vmax, const RangeSet& r,
+                 const AdamHyper& h, hipStream_t s);
 
 void adam_flat(float* p, const float* g, float* m, float* v, float* vmax, long n,
                const AdamHyper& h, hipStream_t s);

@@ -175,6 +175,72 @@ void sgd_flat(float* p, const float* g, float* buf, long n, const SgdHyper& h, h
                        h);
 }
 
+// ------------------------------------------------------------------ multi-range (one launch)
+namespace {
+// element e of the concatenated ranges -> arena index (ranges are few: linear scan)
+__device__ __forceinline__ long range_index(const RangeSet& r, long e) {
+  for (int i = 0; i < r.n; ++i) {
+    if (e < r.len[i]) return r.begin[i] + e;
+    e -= r.len[i];
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void sgd_ranges_kernel(float* __restrict__ p,
+                                                         const float* __restrict__ g,
+                                                         float* __restrict__ buf, RangeSet r,
+                                                         long total, SgdHyper h) {
+  const bool mom = h.momentum != 0.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const long i = range_index(r, e);
+    float pe = p[i], be = (mom && !h.first_step) ? buf[i] : 0.f;
+    sgd_elem(pe, g[i], be, h);
+    p[i] = pe;
+    if (mom) buf[i] = be;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_ranges_kernel(float* __restrict__ p,
+                                                          const float* __restrict__ g,
+                                                          float* __restrict__ m,
+                                                          float* __restrict__ v,
+                                                          float* __restrict__ vmax, RangeSet r,
+                                                          long total, AdamHyper h) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const long i = range_index(r, e);
+    float pe = p[i], me = m[i], ve = v[i];
+    adam_elem(pe, g[i], me, ve, vmax ? vmax + i : nullptr, h);
+    p[i] = pe;
+    m[i] = me;
+    v[i] = ve;
+  }
+}
+}  // namespace
+
+static long range_total(const RangeSet& r) {
+  long t = 0;
+  for (int i = 0; i < r.n; ++i) t += r.len[i];
+  return t;
+}
+
+void sgd_ranges(float* p, const float* g, float* buf, const RangeSet& r, const SgdHyper& h,
+                hipStream_t s) {
+  const long total = range_total(r);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(sgd_ranges_kernel, dim3(grid_for(total)), dim3(256), 0, s, p, g, buf, r,
+                     total, h);
+}
+
+void adam_ranges(float* p, const float* g, float* m, float* v, float* vmax, const RangeSet& r,
+                 const AdamHyper& h, hipStream_t s) {
+  const long total = range_total(r);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(adam_ranges_kernel, dim3(grid_for(total)), dim3(256), 0, s, p, g, m, v,
+                     vmax, r, total, h);
+}
+
 void adam_flat(float* p, const float* g, float* m, float* v, float* vmax, long n,
                const AdamHyper& h, hipStream_t s) {
   if (n <= 0) return;

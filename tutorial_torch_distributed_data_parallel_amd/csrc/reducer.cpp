@@ -61,8 +61,22 @@ static ncclDataType_t nccl_dtype(int elem_size) {
 
 void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
   const bool collective = !(skip_single_rank_ && comm_->world() == 1);
-  if (!collective && fused.kind == 0) {
-    // one rank: the average over ranks is the local gradient -- no collective, no stream hop
+  if (!collective) {
+    // one rank: the average over ranks is the local gradient -- no collective, no stream hop.
+    // With a fused optimizer the remaining (non-epilogue) updates of every bucket are applied
+    // by one launch when backward ends (flush_deferred).
+    if (fused.kind != 0 && end > begin) {
+      if (fused.kind == 1 && !fused.fresh.empty()) {
+        deferred_first_ = deferred_first_ || (bool)fused.fresh[bucket];
+        fused.fresh[bucket] = 0;
+      }
+      if (fused.kind == 2 && bucket == 0 && !bucket0_launched_) {
+        ++fused.adam_step;
+        bucket0_launched_ = true;
+      }
+      deferred_.push_back({begin, end});
+      launched_any_ = true;
+    }
     if (post_bucket) post_bucket(bucket, begin, end, compute);
     return;
   }
@@ -200,7 +214,54 @@ void RcclBackend::apply_fused_range(int64_t off, int64_t cnt, bool first, hipStr
   }
 }
 
+// Apply the deferred world-size-1 bucket updates minus the epilogue-updated ranges, in launches
+// of up to kMaxRanges ranges (one launch for the models here: biases + small weights).
+void RcclBackend::flush_deferred(hipStream_t compute) {
+  if (deferred_.empty()) return;
+  std::sort(deferred_.begin(), deferred_.end());
+  std::vector<std::pair<int64_t, int64_t>> todo;
+  for (const auto& d : deferred_) {
+    int64_t cur = d.first;
+    for (const auto& r : epi_done_) {
+      if (r.second <= cur || r.first >= d.second) continue;
+      if (r.first > cur) todo.push_back({cur, r.first});
+      cur = std::max(cur, r.second);
+    }
+    if (cur < d.second) todo.push_back({cur, d.second});
+  }
+  // merge touching ranges
+  std::vector<std::pair<int64_t, int64_t>> merged;
+  for (const auto& t : todo) {
+    if (!merged.empty() && merged.back().second == t.first) merged.back().second = t.second;
+    else merged.push_back(t);
+  }
+  const bool first = deferred_first_;
+  deferred_.clear();
+  deferred_first_ = false;
+  float* g = reinterpret_cast<float*>(arena_);
+  for (size_t i0 = 0; i0 < merged.size(); i0 += kMaxRanges) {
+    RangeSet rs;
+    for (size_t i = i0; i < merged.size() && rs.n < kMaxRanges; ++i) {
+      rs.begin[rs.n] = merged[i].first;
+      rs.len[rs.n] = merged[i].second - merged[i].first;
+      ++rs.n;
+    }
+    if (fused.kind == 1) {
+      SgdHyper h = fused.sgd;
+      h.first_step = first;
+      sgd_ranges(fused.p, g, fused.s0, rs, h, compute);
+    } else if (fused.kind == 2) {
+      AdamHyper h = fused.adam;
+      const double t = (double)(fused.adam_step > 0 ? fused.adam_step : 1);
+      h.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
+      h.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
+      adam_ranges(fused.p, g, fused.s0, fused.s1, fused.s2, rs, h, compute);
+    }
+  }
+}
+
 void RcclBackend::wait_all(hipStream_t compute) {
+  flush_deferred(compute);
   // iteration boundary: epilogue bookkeeping restarts
   epi_done_.clear();
   if (fused.kind != 0) epi_fresh_ = false;

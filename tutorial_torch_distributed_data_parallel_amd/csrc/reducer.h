@@ -90,7 +90,11 @@ class RcclBackend : public ReducerBackend {
  private:
   void apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs);
   void apply_fused_range(int64_t off, int64_t cnt, bool first, hipStream_t cs);
+  void flush_deferred(hipStream_t compute);
   std::vector<std::pair<int64_t, int64_t>> epi_done_;  // ranges updated by GEMM epilogues
+  // world size 1: bucket updates deferred to the end of backward, applied by one launch
+  std::vector<std::pair<int64_t, int64_t>> deferred_;
+  bool deferred_first_ = false;
   bool epi_fresh_ = false;        // SGD momentum of epilogue-updated ranges not yet initialised
   bool bucket0_launched_ = false;  // this iteration's Adam step counter already advanced
   std::shared_ptr<Communicator> comm_;
