@@ -6,17 +6,21 @@ Model: ToyMLP 9216 -> 4096 -> 4096 -> 10 (Linear+ReLU; = the reference AlexNet's
 per-rank batch 128 (REF/multi-GPU-training-torch.py:88), synthetic on-device data, random init,
 fp32 (the reference's dtype), CrossEntropyLoss, SGD(momentum=0.9) (the north star's fused SGD),
 one full DDP step per iteration: sampler-ordered batch gather -> forward -> loss -> backward with
-bucketed RCCL all-reduce -> optimizer step. Weak scaling: per-GPU work is fixed.
+bucketed RCCL gradient reduction -> optimizer step. Weak scaling: per-GPU work is fixed.
 
   python bench.py                                   # 1 GPU
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
   python bench.py --impl torch                      # stock torch DDP + torch.optim (comparison)
+  python bench.py --api accelerate                  # the same step through Accelerator.prepare()
 
 Execution: eager by default (GPU-bound with the native kernels); ``--graph`` replays a captured
 hipGraph of the whole step instead.
 
 Timing: W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
-both sides; the max over ranks is reported; rank 0 prints one JSON line.
+both sides; the max over ranks is reported; rank 0 prints one JSON line. Native libraries (RCCL
+prints a version banner when a communicator is created) write to file descriptor 1, so the
+process points fd 1 at stderr and writes the JSON line to a private duplicate of the original
+stdout: stdout carries exactly one line.
 """
 from __future__ import annotations
 
@@ -31,6 +35,19 @@ import torch
 
 METRIC = "samples/sec (whole node) toy-MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
 ROOT = Path(__file__).resolve().parent
+# In eager execution the bucket collectives run on the compute stream (csrc/reducer.cpp,
+# profiles/side_stream_eager.md), so they serialise with backward anyway: fewer, larger
+# collectives move the same bytes at a higher RCCL bus bandwidth. Under --graph they overlap
+# backward on the comm stream, so DDP's 25 MiB buckets are kept there.
+EAGER_MULTI_GPU_BUCKET_MB = 256.0
+
+
+def _private_stdout():
+    """Return a writer on the original stdout and point fd 1 at stderr (see module doc)."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
 
 
 def parse():
@@ -40,11 +57,16 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128, help="per-rank batch")
     ap.add_argument("--impl", choices=["tdp", "torch"], default="tdp")
+    ap.add_argument("--api", choices=["ddp", "accelerate"], default="ddp",
+                    help="tdp: drive the step through DDP directly, or through the Accelerate-style "
+                         "Accelerator.prepare() facade (BASELINE.json config 4)")
     ap.add_argument("--optim", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
     ap.add_argument("--model", choices=["toy_mlp", "alexnet", "resnet50"], default="toy_mlp",
                     help="toy_mlp = the headline config; alexnet / resnet50 = the CNN configs")
+    ap.add_argument("--mlp-dims", type=str, default=None,
+                    help="toy MLP in,hidden1,hidden2 (tests only; the headline is 9216,4096,4096)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--dataset", type=int, default=None,
                     help="synthetic samples per rank (default 8192 MLP, 512 CNN)")
@@ -52,7 +74,7 @@ def parse():
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--graph", action="store_true",
                     help="tdp: capture the whole step into a hipGraph and replay it (bucket "
-                         "all-reduces then overlap backward on a side stream). Off by default: "
+                         "collectives then overlap backward on a side stream). Off by default: "
                          "with the native kernels the eager step is GPU-bound and measured as "
                          "fast on one GPU (profiles/bench/mode*.json), and eager keeps RCCL out "
                          "of stream capture on multi-GPU runs")
@@ -83,7 +105,7 @@ def baseline_for(n_gpus: int, impl: str, syncbn: bool, model: str = "toy_mlp"):
 
 
 MODEL_DESC = {
-    "toy_mlp": "toy-MLP 9216-4096-4096-10 (Linear+ReLU{bn})",
+    "toy_mlp": "toy-MLP {dims} (Linear+ReLU{bn})",
     "alexnet": "AlexNet (torchvision topology, 10 classes, 3x{s}x{s}{bn})",
     "resnet50": "ResNet-50 (torchvision v1.5 topology, 10 classes, 3x{s}x{s}{bn})",
 }
@@ -91,14 +113,19 @@ MODEL_DESC = {
 
 def main():
     a = parse()
+    out = _private_stdout()
     if a.dataset is None:
         a.dataset = 8192 if a.model == "toy_mlp" else 512
+    dims = tuple(int(v) for v in a.mlp_dims.split(",")) if a.mlp_dims else (9216, 4096, 4096)
     metric = METRIC if a.model == "toy_mlp" else \
         f"samples/sec (whole node) {a.model} DDP at 1/2/4/8 MI355X"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_gpu = torch.cuda.is_available() and not a.cpu
+    graph = use_gpu and a.graph and not a.eager
+    in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
+    fused = False
 
     if a.impl == "tdp":
         import tutorial_torch_distributed_data_parallel_amd as tdp
@@ -106,64 +133,67 @@ def main():
                                                                         DistributedSampler,
                                                                         SyntheticDataset)
         from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
-        from tutorial_torch_distributed_data_parallel_amd.models.registry import (build_model,
-                                                                                  input_shape)
+        from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
 
         tdp.init_process_group("nccl" if use_gpu else "gloo")
         rank, world, dev = rt.get_rank(), rt.get_world_size(), rt.device()
         torch.manual_seed(1234 + rank)
         if a.model == "toy_mlp":
-            model = ToyMLP(batchnorm=a.syncbn, device=dev)
+            model = ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
         else:
             model = build_model(a.model, device=dev)
         if a.syncbn:
             model = tdp.nn.convert_sync_batchnorm(model)
-        ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
-                      bucket_cap_mb=a.bucket_mb,
-                      grad_compression=None if a.compression == "none" else a.compression)
-        crit = tdp.nn.CrossEntropyLoss()
-        if a.optim == "sgd":
-            opt = tdp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9)
-        else:
-            opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
-        fused = False
+        bucket_mb = a.bucket_mb
+        if bucket_mb is None and world > 1 and not graph:
+            bucket_mb = EAGER_MULTI_GPU_BUCKET_MB
+
+        def make_opt(params):
+            if a.optim == "sgd":
+                return tdp.optim.SGD(params, lr=0.01, momentum=0.9)
+            return tdp.optim.Adam(params, lr=1e-3)
+
         # auto = on: world > 1 shards the update inside the reduction; world 1 applies it in
         # the weight-gradient GEMM epilogues (the local gradient is already the average)
-        want_fused = a.fused_opt in ("on", "auto")
-        if use_gpu and want_fused and not a.no_fused_opt:
-            fused = ddp.register_fused_optimizer(opt)
-        data = SyntheticDataset(a.dataset, input_shape(a.model, a.image_size), 10, seed=rank,
-                                device=dev)
-        sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
-        loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+        want_fused = a.fused_opt in ("on", "auto") and not a.no_fused_opt
         barrier = rt.barrier
         finish = tdp.destroy_process_group
         acc = torch.zeros(3, device=dev)
 
-        def loss_fn(out, y):
-            return tdp.ops.cross_entropy(out, y, acc=acc)
+        def loss_fn(out_, y):
+            return tdp.ops.cross_entropy(out_, y, acc=acc)
 
-        # batches are gathered on the device by the sampler's indices (one H2D copy per epoch)
-        idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
-        cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices()}
+        if a.api == "accelerate":
+            # BASELINE.json config 4: the step through the Accelerate-style facade. One dataset
+            # shared by all ranks, dealt out by whole batches (Accelerate's BatchSamplerShard).
+            from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
 
-        def advance():
-            if cur["pos"] + a.batch > len(cur["idx"]):
-                cur["epoch"] += 1
-                sampler.set_epoch(cur["epoch"])
-                cur["idx"], cur["pos"] = loader.epoch_indices(), 0
-            idx_static.copy_(cur["idx"][cur["pos"]: cur["pos"] + a.batch])
-            cur["pos"] += a.batch
+            accel = Accelerator(ddp_kwargs=dict(bucket_cap_mb=bucket_mb))
+            opt = make_opt(model.parameters())
+            data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
+            loader = DeviceLoader(data, a.batch, drop_last=True)
+            model, opt, loader = accel.prepare(model, opt, loader)
+            if use_gpu and want_fused and world > 1:
+                fused = model.register_fused_optimizer(opt.optimizer)
+            sampler = loader  # set_epoch lives on the prepared loader
 
-        def tdp_step():
-            x = data.x.index_select(0, idx_static)
-            y = data.y.index_select(0, idx_static)
-            opt.zero_grad(set_to_none=True)
-            loss = loss_fn(ddp(x), y)
-            loss.backward()
-            opt.step()
-            return loss
+            def run_step(x, y):
+                opt.zero_grad(set_to_none=True)
+                loss = loss_fn(model(x), y)
+                accel.backward(loss)
+                opt.step()
+                return loss
+        else:
+            ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
+                          bucket_cap_mb=bucket_mb,
+                          grad_compression=None if a.compression == "none" else a.compression)
+            opt = make_opt(ddp.parameters())
+            if use_gpu and want_fused:
+                fused = ddp.register_fused_optimizer(opt)
+            data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
+            sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
+            loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
     else:
         import torch.distributed as dist
         import torch.nn as nn
@@ -189,7 +219,7 @@ def main():
         sys.path.insert(0, str(ROOT / "scripts"))
         from stock_models import stock_model
 
-        model = stock_model(a.model, a.syncbn).to(dev)
+        model = stock_model(a.model, a.syncbn, dims=dims).to(dev)
         ddp = TorchDDP(model, device_ids=[local] if use_gpu else None,
                        bucket_cap_mb=a.bucket_mb if a.bucket_mb else 25)
         crit = nn.CrossEntropyLoss()
@@ -197,8 +227,7 @@ def main():
                else torch.optim.Adam(ddp.parameters(), lr=1e-3))
         g = torch.Generator(device=dev)
         g.manual_seed(rank)
-        shape = (9216,) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
-        X = torch.randn(a.dataset, *shape, generator=g, device=dev)
+        X = torch.randn(a.dataset, *in_shape, generator=g, device=dev)
         Y = torch.randint(0, 10, (a.dataset,), generator=g, device=dev)
 
         class _DS:
@@ -207,10 +236,11 @@ def main():
         sampler = TorchSampler(_DS(), num_replicas=world, rank=rank, shuffle=True)
 
         class _Loader:
+            # same data path as the native bench: the epoch's indices go to the device once
             def __iter__(self):
-                idx = torch.as_tensor(list(sampler), dtype=torch.long)
+                idx = torch.as_tensor(list(sampler), dtype=torch.long).to(dev)
                 for s in range(0, len(idx) - len(idx) % a.batch, a.batch):
-                    b = idx[s:s + a.batch].to(dev, non_blocking=True)
+                    b = idx[s:s + a.batch]
                     yield X.index_select(0, b), Y.index_select(0, b)
         loader = _Loader()
 
@@ -220,9 +250,18 @@ def main():
         def finish():
             dist.destroy_process_group()
 
-        def loss_fn(out, y):
-            return crit(out, y)
+        def run_step(x, y):
+            opt.zero_grad(set_to_none=True)
+            loss = crit(ddp(x), y)
+            loss.backward()
+            opt.step()
+            return loss
 
+    if use_gpu and os.environ.get("TDP_BENCH_STREAM") == "1":
+        # measurement knob: run the loop on a non-default stream
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(s)
     sync = (torch.cuda.synchronize if use_gpu else (lambda: None))
     epoch = [0]
     it = [iter(loader)]
@@ -236,10 +275,37 @@ def main():
             it[0] = iter(loader)
             return next(it[0])
 
-    if a.impl == "tdp":
+    if a.impl == "tdp" and a.api == "ddp":
+        # batches are gathered on the device by the sampler's indices (one H2D copy per epoch);
+        # a captured graph reads them from a static index tensor, eager steps from a slice
+        idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
+        cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices(), "b": None}
+
+        def advance():
+            if cur["pos"] + a.batch > len(cur["idx"]):
+                cur["epoch"] += 1
+                sampler.set_epoch(cur["epoch"])
+                cur["idx"], cur["pos"] = loader.epoch_indices(), 0
+            b = cur["idx"][cur["pos"]: cur["pos"] + a.batch]
+            if graph:
+                idx_static.copy_(b)
+                b = idx_static
+            cur["b"] = b
+            cur["pos"] += a.batch
+
+        def tdp_step():
+            b = idx_static if graph else cur["b"]
+            x = data.x.index_select(0, b)
+            y = data.y.index_select(0, b)
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(ddp(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
         advance()
         run = tdp_step
-        if use_gpu and a.graph and not a.eager:
+        if graph:
             from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
 
             run = try_capture(tdp_step, warmup=3,
@@ -250,13 +316,7 @@ def main():
             return run()
     else:
         def step():
-            x, y = next_batch()
-            opt.zero_grad(set_to_none=True)
-            out = ddp(x)
-            loss = loss_fn(out, y)
-            loss.backward()
-            opt.step()
-            return loss
+            return run_step(*next_batch())
 
     for _ in range(a.warmup):
         step()
@@ -282,6 +342,15 @@ def main():
     value = a.batch * world * a.steps / dt
     base = baseline_for(world, a.impl, a.syncbn, a.model)
     if rank == 0:
+        desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
+                                          bn=", +SyncBatchNorm" if a.syncbn else "")
+        if a.impl == "tdp":
+            impl = "tdp (native gfx950 kernels + RCCL reducer" + \
+                (", hipGraph step)" if graph else ", eager)")
+            if a.api == "accelerate":
+                impl += " via Accelerator.prepare()"
+        else:
+            impl = "stock torch DDP + torch.optim"
         rec = {
             "metric": metric,
             "value": round(value, 2),
@@ -296,21 +365,17 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (on-device random features, random-init weights)",
             "config": {
-                "model": MODEL_DESC[a.model].format(
-                    s=a.image_size, bn=", +SyncBatchNorm" if a.syncbn else ""),
+                "model": desc,
                 "global_batch": a.batch * world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "impl": ("tdp (native gfx950 kernels + RCCL reducer" +
-                         (", hipGraph step)" if (use_gpu and a.graph and not a.eager)
-                          else ", eager)"))
-                        if a.impl == "tdp" else "stock torch DDP + torch.optim",
-                "optimizer": a.optim + (" (fused into the bucket reduction)"
+                "impl": impl,
+                "optimizer": a.optim + (" (fused into the gradient reduction)"
                                         if a.impl == "tdp" and fused else ""),
                 "final_loss": round(float(loss.item()), 5),
             },
         }
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec), file=out, flush=True)
     finish()
 
 

@@ -9,14 +9,15 @@ from __future__ import annotations
 import torch.nn as nn
 
 
-def stock_mlp(syncbn: bool = False):
-    layers = [nn.Linear(9216, 4096)]
+def stock_mlp(syncbn: bool = False, dims=(9216, 4096, 4096)):
+    d_in, h1, h2 = dims
+    layers = [nn.Linear(d_in, h1)]
     if syncbn:
-        layers.append(nn.BatchNorm1d(4096))
-    layers += [nn.ReLU(inplace=True), nn.Linear(4096, 4096)]
+        layers.append(nn.BatchNorm1d(h1))
+    layers += [nn.ReLU(inplace=True), nn.Linear(h1, h2)]
     if syncbn:
-        layers.append(nn.BatchNorm1d(4096))
-    layers += [nn.ReLU(inplace=True), nn.Linear(4096, 10)]
+        layers.append(nn.BatchNorm1d(h2))
+    layers += [nn.ReLU(inplace=True), nn.Linear(h2, 10)]
     m = nn.Sequential(*layers)
     return nn.SyncBatchNorm.convert_sync_batchnorm(m) if syncbn else m
 
@@ -73,8 +74,8 @@ def stock_resnet50(num_classes: int = 10):
     return m
 
 
-def stock_model(name: str, syncbn: bool = False):
+def stock_model(name: str, syncbn: bool = False, dims=(9216, 4096, 4096)):
     if name == "toy_mlp":
-        return stock_mlp(syncbn)
+        return stock_mlp(syncbn, dims)
     m = stock_alexnet() if name == "alexnet" else stock_resnet50()
     return nn.SyncBatchNorm.convert_sync_batchnorm(m) if syncbn else m

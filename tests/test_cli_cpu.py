@@ -61,3 +61,24 @@ def test_launch_writes_condor_file(tmp_path):
     sub = open(os.path.join(s["out_dir"], "submission_file.sub")).read()
     assert "request_gpus = 2" in sub and "TARGET.CUDAGlobalMemoryMb > 60000" in sub
     assert sub.strip().endswith("queue")
+
+
+import json  # noqa: E402
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("api", ["ddp", "accelerate"])
+def test_bench_two_ranks_one_json_line(api):
+    """bench.py under the launcher on 2 gloo ranks: exactly one JSON line on stdout (RCCL/native
+    banners go to stderr), whole-job throughput, dp2."""
+    r = _run(["-m", "tutorial_torch_distributed_data_parallel_amd.parallel.launcher", "--nproc",
+              "2", "bench.py", "--cpu", "--gpus", "2", "--steps", "3", "--warmup", "1",
+              "--dataset", "256", "--batch", "16", "--mlp-dims", "64,32,32", "--api", api])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 32
+    assert rec["value"] > 0 and rec["steps"] == 3 and rec["warmup"] == 1
+    assert ("Accelerator.prepare" in rec["config"]["impl"]) == (api == "accelerate")

@@ -39,6 +39,8 @@ RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_
   stream_mode_ = m == "side" ? kStreamSide
                  : m == "compute" ? kStreamCompute
                  : m == "hostsync" ? kStreamHostSync
+                 : m == "hostjoin" ? kStreamHostJoin
+                 : m == "nojoin" ? kStreamNoJoin
                                    : kStreamAuto;
 }
 
@@ -277,9 +279,14 @@ void RcclBackend::wait_all(hipStream_t compute) {
     check_hip(hipEventRecord(t1_, cs), "hipEventRecord");
     timed_pending_ = true;
   }
-  check_hip(hipEventRecord(done_, cs), "hipEventRecord");
-  check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
   launched_any_ = false;
+  if (stream_mode_ == kStreamNoJoin) return;
+  check_hip(hipEventRecord(done_, cs), "hipEventRecord");
+  if (stream_mode_ == kStreamHostJoin) {
+    check_hip(hipEventSynchronize(done_), "hipEventSynchronize");
+    return;
+  }
+  check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
 }
 
 void RcclBackend::zero(int64_t begin, int64_t end, hipStream_t compute) {

@@ -107,7 +107,13 @@ class RcclBackend : public ReducerBackend {
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false;
   // where bucket collectives run: auto = side stream only while capturing a hipGraph
-  enum { kStreamAuto = 0, kStreamSide = 1, kStreamCompute = 2, kStreamHostSync = 3 };
+  // hostjoin: side stream, but the end-of-backward join is a host wait on the comm stream's
+  // event instead of a device-side hipStreamWaitEvent on the compute stream; nojoin: no join
+  // at all (measurement only: the next forward may race the last buckets)
+  enum {
+    kStreamAuto = 0, kStreamSide = 1, kStreamCompute = 2, kStreamHostSync = 3,
+    kStreamHostJoin = 4, kStreamNoJoin = 5
+  };
   int stream_mode_ = kStreamAuto;
   bool launched_side_ = false;
   uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets

@@ -110,28 +110,24 @@ def flatten_module(module: torch.nn.Module, device=None) -> ParamArena:
 
 
 class BufferArena:
-    """Float buffers of a module packed the same way, so DDP's per-forward buffer broadcast
-     is one collective with no copies."""
+    """A module's buffers packed into one flat tensor per (device, dtype), so DDP's per-forward
+    buffer broadcast is one collective per dtype with no copies (ResNet-50:
+    2 broadcasts -- float running stats, int64 num_batches_tracked -- instead of 160)."""
 
     def __init__(self, module: torch.nn.Module):
-        self.bufs = [b for b in module.buffers() if b.is_floating_point()]
-        self.others = [b for b in module.buffers() if not b.is_floating_point()]
-        if not self.bufs:
-            self.data = None
-            return
-        dev, dt = self.bufs[0].device, self.bufs[0].dtype
-        same = all(b.device == dev and b.dtype == dt for b in self.bufs)
-        if not same:
-            self.data = None
-            self.others = list(module.buffers())
-            return
-        total, offs = 0, []
-        for b in self.bufs:
-            offs.append(total)
-            total = _round_up(total + b.numel(), ALIGN)
-        self.data = torch.zeros(max(total, ALIGN), device=dev, dtype=dt)
-        with torch.no_grad():
-            for b, o in zip(self.bufs, offs):
-                v = self.data[o: o + b.numel()].view(b.shape)
-                v.copy_(b)
-                b.data = v
+        groups = {}
+        for b in module.buffers():
+            groups.setdefault((b.device, b.dtype), []).append(b)
+        self.flats = []
+        for (dev, dt), bufs in groups.items():
+            total, offs = 0, []
+            for b in bufs:
+                offs.append(total)
+                total = _round_up(total + b.numel(), ALIGN)
+            flat = torch.zeros(max(total, ALIGN), device=dev, dtype=dt)
+            with torch.no_grad():
+                for b, o in zip(bufs, offs):
+                    v = flat[o: o + b.numel()].view(b.shape)
+                    v.copy_(b)
+                    b.data = v
+            self.flats.append(flat)

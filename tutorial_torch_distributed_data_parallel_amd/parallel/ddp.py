@@ -174,11 +174,8 @@ class DistributedDataParallel(nn.Module):
     def _sync_buffers(self):
         if self.world_size == 1:
             return
-        ba = self.buffers_arena
-        if ba.data is not None:
-            rt.broadcast(ba.data, 0)
-        for b in ba.others:
-            rt.broadcast(b, 0)
+        for flat in self.buffers_arena.flats:
+            rt.broadcast(flat, 0)
 
     # --------------------------------------------------------------------------- debug
     def replica_checksum(self) -> torch.Tensor:
