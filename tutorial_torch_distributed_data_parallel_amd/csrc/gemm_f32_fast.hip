@@ -27,6 +27,8 @@
 //     its transpose-stride form for the input gradient, shifted pixels for the weight gradient);
 //     taps that fall into the zero padding read a 16-B zero page. With C % 32 == 0 a K tile
 //     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
+#include <cstdlib>
+
 #include "common.h"
 #include "conv.h"
 #include "kernels.h"
@@ -303,8 +305,9 @@ struct SrcOf<R, kImWgrad, false> : ImSrcB<R, false> {};
 template <int R>
 struct SrcOf<R, kImWgradT, true> : ImSrcB<R, true> {};
 
+// One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel.
 template <int FN, int AKIND, int BKIND, int S, int OPTK>
-__global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
+__device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, lds_char* smem) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
   constexpr int FM = 2;
@@ -313,19 +316,10 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   constexpr int STG = A_BYTES + B_BYTES;
   constexpr int GA = A_BYTES / 1024 / 4, GB = B_BYTES / 1024 / 4;  // glds per wave per tile
   constexpr int G = GA + GB;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = smem_raw;
-
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid >> 1, wn = wid & 1;
 
-  // XCD-aware remap (bijective): hardware ids b and b+8 share an XCD; give each XCD a
-  // contiguous range of logical tiles, ordered split-major so an XCD shares one K slice.
-  const int nwg = gridDim.x;
-  const int b = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
   const int tiles_mn = p.tiles_n * p.tiles_m;
   const int z = lid / tiles_mn;
   const int t_mn = lid % tiles_mn;
@@ -487,23 +481,26 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
     constexpr bool PAIR = !BKC && FN == 2;
     constexpr int NG = PAIR ? 1 : FN;       // column groups per accumulator row
     constexpr int NE = PAIR ? 2 : 1;        // elements per group
-    constexpr int FB = PAIR ? 1 : FM;       // row tiles per batch
-    constexpr int NB = FB * 16 * NG;        // groups per batch
+    constexpr int FB = PAIR ? 1 : (SGD ? FM : 1);  // row tiles per batch
+    constexpr int RB = (PAIR && !SGD) ? 8 : 16;    // accumulator rows per batch (Adam: 3 arrays)
+    constexpr int NB = FB * RB * NG;        // groups per batch
 #pragma unroll
     for (int f0 = 0; f0 < FM; f0 += FB) {
+#pragma unroll
+      for (int r0 = 0; r0 < 16; r0 += RB) {
       int idx[NB];
       float pv[NB * NE], s0v[NB * NE], s1v[SGD ? 1 : NB * NE];
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int f = f0 + fb;
+        for (int rr = 0; rr < RB; ++rr) {
+          const int f = f0 + fb, r = r0 + rr;
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
           const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
 #pragma unroll
           for (int g = 0; g < NG; ++g) {
             const int col = PAIR ? n0 + wn * 64 + 2 * l31 : n0 + wn * (32 * FN) + g * 32 + l31;
-            const int j = (fb * 16 + r) * NG + g;
+            const int j = (fb * RB + rr) * NG + g;
             // PAIR: N % 4 == 0 (fast-path precondition), so col + 1 < N whenever col < N;
             // out-of-range lanes are marked by idx = -1 (and read element 0)
             const bool ok = row < p.M && col < p.N;
@@ -531,15 +528,15 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
 #pragma unroll
       for (int fb = 0; fb < FB; ++fb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int rr = 0; rr < RB; ++rr) {
 #pragma unroll
           for (int g = 0; g < NG; ++g) {
-            const int j = (fb * 16 + r) * NG + g;
+            const int j = (fb * RB + rr) * NG + g;
             const int i = idx[j];
             if (i < 0) continue;
 #pragma unroll
             for (int e = 0; e < NE; ++e) {
-              const float gr = acc[f0 + fb][PAIR ? e : g][r];
+              const float gr = acc[f0 + fb][PAIR ? e : g][r0 + rr];
               float pe = pv[j * NE + e];
               float b0 = (!SGD || mom_rd) ? s0v[j * NE + e] : 0.f;
               if (SGD) {
@@ -565,6 +562,7 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
             }
           }
         }
+      }
       }
     }
     return;
@@ -617,6 +615,42 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
         }
       }
     }
+  }
+}
+
+template <int FN, int AKIND, int BKIND, int S, int OPTK>
+__global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = smem_raw;
+  // XCD-aware tile order (bijective): hardware ids b and b+8 share an XCD; each XCD gets a
+  // contiguous range of logical tiles, ordered split-major so an XCD shares one K slice.
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
+  if constexpr (OPTK != 0) {
+    // Persistent form of the optimizer-epilogue kernel (grid = 2 workgroups per CU when the
+    // planner asks for it): each workgroup walks tiles of its XCD's range. A tile alternates an
+    // MFMA phase with an HBM-bound epilogue (read p + state, write them back); with one tile
+    // per workgroup the two workgroups of a CU run both phases in lockstep (fc1 wgrad+SGD
+    // measured = GEMM time + epilogue time). Persistence plus a start offset for the second
+    // workgroup of each CU lets one workgroup's epilogue stream while the other computes.
+    const int T = p.tiles_m * p.tiles_n;
+    const int q8 = nwg / 8, r8 = nwg % 8;
+    const int per = q8 + (xcd < r8 ? 1 : 0);            // workgroups on this XCD
+    const int before = xcd * q8 + (xcd < r8 ? xcd : r8);  // workgroups on lower XCDs
+    const int j = b / 8;
+    // tiles split in proportion to the workgroups of each XCD (an XCD may have none)
+    const int t0 = (int)((long)T * before / nwg), t1 = (int)((long)T * (before + per) / nwg);
+    if (t1 - t0 > per && j >= per / 2) {
+      __builtin_amdgcn_s_sleep(127);
+      __builtin_amdgcn_s_sleep(127);
+    }
+    for (int lid = t0 + j; lid < t1; lid += per) {
+      gemm_tile<FN, AKIND, BKIND, S, OPTK>(p, lid, smem);
+      __builtin_amdgcn_s_barrier();  // every wave is done with this tile's LDS stages
+    }
+  } else {
+    const int q8 = nwg / 8, r8 = nwg % 8;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    gemm_tile<FN, AKIND, BKIND, S, OPTK>(p, lid, smem);
   }
 }
 
@@ -684,6 +718,11 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   }
   if (o_splits > 0 && a.rowsum == nullptr) splits = o_splits;
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
+  plan.grid = 0;
+  if (a.opt.kind != 0) {
+    const char* e = std::getenv("TDP_OPT_PERSIST");
+    if (!(e && e[0] == '0')) plan.grid = 2 * num_cus;  // persistent: 2 workgroups per CU
+  }
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
   plan.bm = 128;
@@ -717,8 +756,9 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   // B = X both MN-contiguous); any other use stores C and applies the flat update afterwards
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
   if (opt) {
-    if (a.opt.kind == 1) launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nblocks, s);
-    else launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nblocks, s);
+    const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
+    if (a.opt.kind == 1) launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nb, s);
+    else launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nb, s);
     return;
   }
   p.opt.kind = 0;

@@ -72,6 +72,7 @@ struct GemmPlan {
   int k_per_split = 0;
   long ws_floats = 0;   // split-K workspace needed (0 when splits == 1)
   int skinny = 0;       // > 0: one of the skinny kernels (gemm_skinny.hip) runs instead
+  int grid = 0;         // fast kernel: > 0 = persistent launch of this many workgroups
 };
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
