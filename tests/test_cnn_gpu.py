@@ -230,3 +230,30 @@ def test_model_matches_cpu_reference(name, hw, n):
         worst.append((err, pn))
     worst.sort(reverse=True)
     assert worst[0][0] <= 2e-3, worst[:5]
+
+
+@pytest.mark.parametrize("orient", [-1, 0, 1])
+@pytest.mark.parametrize("override", [(0, 0, 0), (2, 0, 0), (1, 32, 0), (2, 8, 2), (1, 3, 3)])
+@pytest.mark.parametrize("Co,C,R", [(192, 64, 5), (256, 128, 3)])
+def test_conv_wgrad_plans(orient, override, Co, C, R):
+    """Every weight-gradient plan (dW / dW^T orientation, tile width, split-K, pipeline depth)
+    the planner can pick matches the float64 reference."""
+    from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    N_ = native()
+    torch.manual_seed(Co + C + R)
+    x = torch.randn(4, C, 13, 13, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, R, R, device="cuda") / (C * R * R) ** 0.5).requires_grad_()
+    dy = torch.randn(4, Co, 13, 13, device="cuda")
+    try:
+        N_.conv_set_wgrad_transposed(orient)
+        N_.gemm_f32_set_override(*override)
+        ops.conv2d(x, w, None, 1, R // 2).backward(dy)
+        torch.cuda.synchronize()
+    finally:
+        N_.conv_set_wgrad_transposed(-1)
+        N_.gemm_f32_set_override(0, 0, 0)
+    wr = w.detach().double().cpu().requires_grad_()
+    F.conv2d(x.double().cpu(), wr, None, 1, R // 2).backward(dy.double().cpu())
+    torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=2e-3)

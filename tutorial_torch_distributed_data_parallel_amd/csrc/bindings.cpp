@@ -756,11 +756,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
   m.def("conv_nhwc_dgrad_phase", &conv_nhwc_dgrad_phase_op);
-  m.def("conv_wgrad_transposed", [](int64_t cout) {
+  m.def("conv_wgrad_transposed", [](int64_t cout, int64_t R, int64_t S, int64_t C) {
     ConvGeom g{};
-    g.Cout = (int)cout;
+    g.Cout = (int)cout; g.R = (int)R; g.S = (int)S; g.C = (int)C;
     return conv_wgrad_transposed(g);
-  });
+  }, py::arg("cout"), py::arg("R") = 0, py::arg("S") = 0, py::arg("C") = 0);
+  m.def("conv_set_wgrad_transposed", &conv_set_wgrad_transposed);
+  m.def("conv_set_wgrad_target", &conv_set_wgrad_target);
   m.def("conv2d_dgrad", &conv2d_dgrad_op);
   m.def("conv2d_wgrad", &conv2d_wgrad_op);
   m.def("chan_relu_bias_bwd", &chan_relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),

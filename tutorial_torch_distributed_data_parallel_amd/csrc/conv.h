@@ -30,6 +30,8 @@ void conv_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float
 bool conv_nhwc_ok(int mode, const ConvGeom& g);
 // weight gradient computed as dW^T [R*S*C][Cout] (small Cout: keeps the 128-row tiles full)
 bool conv_wgrad_transposed(const ConvGeom& g);
+void conv_set_wgrad_transposed(int mode);  // -1 auto, 0 / 1 force
+void conv_set_wgrad_target(int per_cu);     // split-K workgroups per CU (<= 0: auto)
 ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
 void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,

@@ -10,26 +10,27 @@
 namespace tdp {
 namespace {
 
-// block: 64 column groups (x4 when VEC) x 4 row groups; grid.y slices the rows
+// block: CGB column groups (x4 when VEC) x 256/CGB row groups; grid.y slices the rows. CGB
+// follows N (16 groups for a 64-channel conv output) so no lane idles on narrow outputs (a fixed
+// 64-group block left 3/4 of the lanes of AlexNet's 64-channel layers idle).
 template <bool VEC>
 __global__ __launch_bounds__(256) void relu_bias_part_kernel(const float* __restrict__ dy,
                                                              const float* __restrict__ y,
                                                              int B, int N, long ld,
                                                              float* __restrict__ g,
                                                              float* __restrict__ part,
-                                                             int rows_per) {
+                                                             int rows_per, int cgb) {
   constexpr int W = VEC ? 4 : 1;
-  __shared__ float red[4][64 * W];
-  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int col = (blockIdx.x * 64 + lane) * W;
+  __shared__ f32x4 red[256];
+  const int rgn = 256 / cgb;
+  const int cl = threadIdx.x % cgb, rg = threadIdx.x / cgb;
+  const int col = (blockIdx.x * cgb + cl) * W;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(B, r0 + rows_per);
-  float s[W];
-#pragma unroll
-  for (int e = 0; e < W; ++e) s[e] = 0.f;
-  if (col < N) {
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < N && rg < rgn) {
 #pragma unroll 4
-    for (int r = r0 + rg; r < r1; r += 4) {
+    for (int r = r0 + rg; r < r1; r += rgn) {
       const long off = (long)r * ld + col;
       if (VEC) {
         f32x4 d = *reinterpret_cast<const f32x4*>(dy + off);
@@ -39,8 +40,7 @@ __global__ __launch_bounds__(256) void relu_bias_part_kernel(const float* __rest
           for (int e = 0; e < 4; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
           *reinterpret_cast<f32x4*>(g + (long)r * N + col) = d;
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s[e] += d[e];
+        s += d;
       } else {
         float d = dy[off];
         if (y) {
@@ -51,25 +51,21 @@ __global__ __launch_bounds__(256) void relu_bias_part_kernel(const float* __rest
       }
     }
   }
-#pragma unroll
-  for (int e = 0; e < W; ++e) red[rg][lane * W + e] = s[e];
+  if (!part) return;
+  red[threadIdx.x] = s;
   __syncthreads();
-  if (rg == 0 && col < N && part) {
+  if (rg == 0 && col < N) {
+    f32x4 t = red[cl];
+    for (int i = 1; i < rgn; ++i) t += red[i * cgb + cl];
 #pragma unroll
-    for (int e = 0; e < W; ++e)
-      part[(long)blockIdx.y * N + col + e] =
-          red[0][lane * W + e] + red[1][lane * W + e] + red[2][lane * W + e] +
-          red[3][lane * W + e];
+    for (int e = 0; e < W; ++e) part[(long)blockIdx.y * N + col + e] = t[e];
   }
 }
 
-__global__ void bias_final_kernel(const float* __restrict__ part, int slices, int N,
-                                  float* __restrict__ db, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float t = 0.f;
-  for (int z = 0; z < slices; ++z) t += part[(long)z * N + c];
-  db[c] = (beta != 0.f ? beta * db[c] : 0.f) + t;
+// column groups per block of relu_bias_part_kernel
+int relu_bias_cgb(int N) {
+  const int cg = (N % 4 == 0) ? N / 4 : N;
+  return cg <= 128 ? (cg < 1 ? 1 : cg) : 64;
 }
 
 }  // namespace
@@ -81,21 +77,23 @@ void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, fl
                    (y == nullptr || ((uintptr_t)y & 15) == 0) && (((uintptr_t)g & 15) == 0);
   const int rows_per = (B + slices - 1) / slices;
   const int cols = vec ? N / 4 : N;
-  dim3 grid((cols + 63) / 64, slices);
+  const int cgb = vec ? relu_bias_cgb(N) : (N <= 128 ? N : 64);
+  dim3 grid((cols + cgb - 1) / cgb, slices);
   if (vec)
     hipLaunchKernelGGL(relu_bias_part_kernel<true>, grid, dim3(256), 0, s, dy, y, B, N, ld, g,
-                       db ? part : nullptr, rows_per);
+                       db ? part : nullptr, rows_per, cgb);
   else
     hipLaunchKernelGGL(relu_bias_part_kernel<false>, grid, dim3(256), 0, s, dy, y, B, N, ld, g,
-                       db ? part : nullptr, rows_per);
-  if (db)
-    hipLaunchKernelGGL(bias_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, slices,
-                       N, db, beta_db);
+                       db ? part : nullptr, rows_per, cgb);
+  // db = beta*db + column sums of the partials: the split-axis-parallel split-K combine
+  if (db) splitk_reduce(part, slices, 1, N, db, false, N, nullptr, beta_db, false, s);
 }
 
 int relu_bias_slices(int B, int N, int num_cus) {
-  const int col_blocks = ((N % 4 == 0) ? N / 4 : N) / 64 + 1;
-  int sl = (2 * num_cus + col_blocks - 1) / col_blocks;
+  const int cg = (N % 4 == 0) ? N / 4 : N;
+  const int cgb = (N % 4 == 0) ? relu_bias_cgb(N) : (N <= 128 ? N : 64);
+  const int col_blocks = (cg + cgb - 1) / cgb;
+  int sl = (8 * num_cus + col_blocks - 1) / col_blocks;  // streaming: ~8 workgroups per CU
   const int cap = (B + 15) / 16;  // >= 16 rows per slice
   if (sl > cap) sl = cap;
   return sl < 1 ? 1 : sl;

@@ -221,33 +221,53 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(Params p) {
     }
 }
 
-// grid: (ceil(N4 / 64), ceil(M / 4)); a 256-thread block covers 4 rows x 64 column groups
+// Split-K combine over the flattened [M][N] plane (N % 4 == 0 for VEC: a float4 group never
+// straddles a row). A 256-thread block covers G = 256 / ZT consecutive groups x ZT split lanes:
+// the split axis is itself spread over threads (tree-reduced in LDS), because a weight gradient
+// has few outputs and many splits (ResNet-50 layer1 1x1 wgrad: 4096 outputs x 512 splits — one
+// thread per output serialised 512 loads per thread on 4 workgroups).
 template <bool VEC>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws,
                                                             int splits, int M, int N, void* Cv,
                                                             int c_bf16, long ldc,
                                                             const float* __restrict__ bias,
-                                                            float beta, int relu) {
-  const long plane = (long)M * N;
-  const int row = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+                                                            float beta, int relu, int zt_log2) {
   constexpr int W = VEC ? 4 : 1;
-  const int col = (blockIdx.x * 64 + (threadIdx.x & 63)) * W;
-  if (col >= N) return;
-  const long base = (long)row * N + col;
-  float v[W];
-  if (VEC) {
-    f32x4 t = *reinterpret_cast<const f32x4*>(ws + base);
-    for (int z = 1; z < splits; ++z) t += *reinterpret_cast<const f32x4*>(ws + z * plane + base);
-    for (int e = 0; e < 4; ++e) v[e] = t[e];
-  } else {
-    float t = 0.f;
-    for (int z = 0; z < splits; ++z) t += ws[z * plane + base];
-    v[0] = t;
+  const int ZT = 1 << zt_log2, G = 256 >> zt_log2;
+  const int g = threadIdx.x % G, zt = threadIdx.x / G;
+  const long plane = (long)M * N;
+  const long ng = plane / W;
+  const long idx = (long)blockIdx.x * G + g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (idx < ng) {
+    if (VEC) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(ws) + idx;
+      const long step = ng;
+#pragma unroll 4
+      for (int z = zt; z < splits; z += ZT) acc += src[z * step];
+    } else {
+      float t = 0.f;
+#pragma unroll 4
+      for (int z = zt; z < splits; z += ZT) t += ws[z * plane + idx];
+      acc[0] = t;
+    }
   }
+  __shared__ f32x4 red[256];
+  if (ZT > 1) {
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = ZT >> 1; h > 0; h >>= 1) {
+      if (zt < h) red[threadIdx.x] += red[threadIdx.x + h * G];
+      __syncthreads();
+    }
+    acc = red[threadIdx.x];
+  }
+  if (zt != 0 || idx >= ng) return;
+  const long e0 = idx * W;
+  const int row = (int)(e0 / N), col = (int)(e0 - (long)row * N);
 #pragma unroll
   for (int e = 0; e < W; ++e) {
-    float x = v[e];
+    float x = acc[e];
     if (bias) x += bias[col + e];
     if (c_bf16) {
       unsigned short* C = reinterpret_cast<unsigned short*>(Cv) + (long)row * ldc + col + e;
@@ -369,14 +389,19 @@ void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf
                    const float* bias, float beta, bool relu, hipStream_t s) {
   const bool vec = (N % 4 == 0) && (ldc % 4 == 0) && aligned16(C) &&
                    (bias == nullptr || aligned16(bias));
-  const int cols = vec ? N / 4 : N;
-  dim3 grid((cols + 63) / 64, (M + 3) / 4);
+  const long groups = vec ? (long)M * N / 4 : (long)M * N;
+  // split lanes per output group: enough threads in flight (~1024 per CU) without starving the
+  // column axis; at most 64 lanes and never more than the splits
+  int zl = 0;
+  while (zl < 6 && (2 << zl) <= splits && groups * (2 << zl) <= 256L * 1024) ++zl;
+  const int G = 256 >> zl;
+  const dim3 grid((unsigned)((groups + G - 1) / G));
   if (vec)
     hipLaunchKernelGGL(splitk_reduce_kernel<true>, grid, dim3(256), 0, s, ws, splits, M, N, C,
-                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl);
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<false>, grid, dim3(256), 0, s, ws, splits, M, N, C,
-                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0);
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl);
 }
 
 }  // namespace tdp

@@ -787,7 +787,35 @@ static int ilog2_exact(int v) {
   return (1 << l) == v ? l : -1;
 }
 
-static bool wgrad_transposed(const ConvGeom& g) { return g.Cout < 128; }
+// Weight-gradient orientation: dWt [Cout][R*S*C] (M = Cout) or dWt^T [R*S*C][Cout] (M = R*S*C).
+// Pick the one whose 128 x (64*fn) tiles waste the fewest padded MACs (Cout = 192 wastes a
+// quarter of its second 128-row tile as M, nothing as N = 3 x 64); ties keep M = Cout.
+static int o_wgrad_t = -1;  // -1 auto, 0 / 1 force (per-layer sweeps)
+void conv_set_wgrad_transposed(int mode) { o_wgrad_t = mode; }
+// Weight-gradient tile width: the 128-wide tile (FN = 2, twice the MACs per LDS byte) whenever it
+// pads N no more than the 64-wide one (measured: AlexNet features.8 / ResNet-50 3x3 wgrads run
+// 1.3-1.7x faster with FN = 2 at equal workgroup counts).
+static int wgrad_fn(int M, int N) {
+  return (M >= 128 && N >= 128 && 2 * ceil_div(N, 128) == ceil_div(N, 64)) ? 2 : 1;
+}
+static long padded_macs(int M, int N) {
+  const int bn = 64 * wgrad_fn(M, N);
+  return (long)ceil_div(M, 128) * 128 * ((long)ceil_div(N, bn) * bn);
+}
+// Workgroups the weight-gradient split-K aims for, in units of CUs. K = N*P*Q is long and the
+// tile count small, so the split count sets the grid. Measured per layer (scripts/sweep_wgrad.py,
+// profiles/wgrad_split_target.md): 1x1 filters are bound by the partial-sum traffic and want
+// the fewest splits that fill the chip (2 per CU); R*S > 1 filters re-read each pixel R*S times
+// from L2 and gain from 8 per CU (AlexNet features.3: 898 us at 2, 710 us at 8).
+static int o_wgrad_target = 0;  // > 0: override (sweeps)
+void conv_set_wgrad_target(int per_cu) { o_wgrad_target = per_cu > 0 ? per_cu : 0; }
+static bool wgrad_transposed(const ConvGeom& g) {
+  if (o_wgrad_t == 0 || o_wgrad_t == 1) return o_wgrad_t == 1;
+  const int rsc = g.R * g.S * g.C;
+  if (rsc <= 0) return g.Cout < 128;
+  const long t = padded_macs(rsc, g.Cout), n = padded_macs(g.Cout, rsc);
+  return t != n ? t < n : g.Cout < 128;
+}
 bool conv_wgrad_transposed(const ConvGeom& g) { return wgrad_transposed(g); }
 
 bool conv_nhwc_ok(int mode, const ConvGeom& g) {
@@ -807,6 +835,23 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
   a.M = pl.M; a.N = pl.N; a.K = pl.K;
   GemmPlan gp;
   gemm_f32_fast_plan(a, num_cus, gp);
+  if (mode == kConvWgrad && o_fn == 0 && o_splits == 0) {
+    const int fn = wgrad_fn(pl.M, pl.N);
+    const long tiles = (long)ceil_div(pl.M, 128) * ceil_div(pl.N, 64 * fn);
+    const int per_cu = o_wgrad_target > 0 ? o_wgrad_target : (g.R * g.S == 1 ? 2 : 8);
+    const long target = (long)per_cu * num_cus;
+    const int kmax = pl.K / (kBK * 8);
+    int splits = (int)((target + tiles - 1) / tiles);
+    splits = splits < kmax ? splits : kmax;
+    if (splits < 1) splits = 1;
+    const int kps = ceil_div(ceil_div(pl.K, splits), kBK) * kBK;
+    gp.tile = fn;
+    gp.k_per_split = kps;
+    gp.splits = ceil_div(pl.K, kps);
+    gp.ws_floats = gp.splits > 1 ? (long)gp.splits * pl.M * pl.N : 0;
+    gp.stages = (fn == 1 && ceil_div(kps, kBK) > 4) ? 3 : 2;
+    if (o_stages == 2 || o_stages == 3) gp.stages = o_stages;
+  }
   pl.fn = gp.tile;
   pl.fm = gp.stages;  // pipeline depth (the NHWC path always uses BM = 128)
   pl.splits = gp.splits;

@@ -123,8 +123,8 @@ class _ConvNHWCFn(torch.autograd.Function):
         dx = dw = None
         if needs(ctx, 1):
             dw = grad_dest(w_param)
-            if C.conv_wgrad_transposed(Cout):
-                # small Cout: dW^T [(r,s,c)][co] keeps the 128-row MFMA tiles full
+            if C.conv_wgrad_transposed(Cout, R, S, Cp):
+                # dW^T [(r,s,c)][co] when it pads the 128-row MFMA tiles less (small Cout, Cout=192)
                 dwT = torch.empty((R, S, Cp, Cout), device=dy.device, dtype=dy.dtype)
                 C.conv_nhwc_wgrad(g, xp, dwT, R, S, sh, sw, ph, pw, 0.0)
                 dw.copy_(dwT[:, :, :Cin, :].permute(3, 2, 0, 1))
