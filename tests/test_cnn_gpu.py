@@ -128,11 +128,12 @@ FMTS = [torch.contiguous_format, torch.channels_last]
 
 @pytest.mark.parametrize("fmt", FMTS)
 @pytest.mark.parametrize("k,s,p,H", [(3, 2, 0, 55), (3, 2, 0, 13), (3, 2, 1, 112), (2, 2, 0, 8)])
-def test_maxpool(k, s, p, H, fmt):
+@pytest.mark.parametrize("C", [5, 64])  # 64: the 4-channel vector kernels (channels_last)
+def test_maxpool(k, s, p, H, fmt, C):
     from tutorial_torch_distributed_data_parallel_amd import ops
 
     torch.manual_seed(H)
-    x = torch.randn(2, 5, H, H + 1, device="cuda").contiguous(memory_format=fmt)
+    x = torch.randn(2, C, H, H + 1, device="cuda").contiguous(memory_format=fmt)
     x.requires_grad_()
     y = ops.max_pool2d(x, k, s, p)
     xr = x.detach().clone().requires_grad_()
