@@ -1,0 +1,16 @@
+#!/bin/bash
+# Conv planner: 2 stages for FN=1, FN=2 fwd/dgrad when N%128==0: tests, benches, AlexNet stats, ResNet-50.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/r18; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_cnn_gpu.py tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
+timeout -k 10 120 python bench.py --steps 300 --warmup 30 > $O/mlp.json 2> $O/mlp.err && \
+timeout -k 10 200 python bench.py --model alexnet --steps 50 --warmup 10 > $O/alex.json 2> $O/alex.err && \
+timeout -k 10 200 python bench.py --model alexnet --steps 50 --warmup 10 --impl torch > $O/alex_torch.json 2> $O/alex_torch.err && \
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_alex -o run -- python3 bench.py --model alexnet --steps 20 --warmup 5 > $O/prof_alex.log 2>&1 && \
+timeout -k 10 300 python bench.py --model resnet50 --steps 30 --warmup 5 > $O/r50.json 2> $O/r50.err && \
+timeout -k 10 300 python scripts/bench_conv.py alexnet 128 > $O/conv_alexnet.jsonl 2> $O/conv_alexnet.err
+rc=$?
+tail -3 $O/pytest.log
+for f in $O/*.json; do echo "$f: $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], d["config"]["final_loss"])' 2>/dev/null)"; done
+exit $rc

@@ -245,16 +245,22 @@ def test_conv_wgrad_plans(orient, override, Co, C, R):
     N_ = native()
     torch.manual_seed(Co + C + R)
     x = torch.randn(4, C, 13, 13, device="cuda").contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
     w = (torch.randn(Co, C, R, R, device="cuda") / (C * R * R) ** 0.5).requires_grad_()
     dy = torch.randn(4, Co, 13, 13, device="cuda")
     try:
         N_.conv_set_wgrad_transposed(orient)
         N_.gemm_f32_set_override(*override)
-        ops.conv2d(x, w, None, 1, R // 2).backward(dy)
+        y = ops.conv2d(x, w, None, 1, R // 2)
+        y.backward(dy)
         torch.cuda.synchronize()
     finally:
         N_.conv_set_wgrad_transposed(-1)
         N_.gemm_f32_set_override(0, 0, 0)
+    xr = x.detach().double().cpu().requires_grad_()
     wr = w.detach().double().cpu().requires_grad_()
-    F.conv2d(x.double().cpu(), wr, None, 1, R // 2).backward(dy.double().cpu())
+    yr = F.conv2d(xr, wr, None, 1, R // 2)
+    yr.backward(dy.double().cpu())
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=2e-3)

@@ -849,9 +849,24 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
     gp.k_per_split = kps;
     gp.splits = ceil_div(pl.K, kps);
     gp.ws_floats = gp.splits > 1 ? (long)gp.splits * pl.M * pl.N : 0;
-    gp.stages = (fn == 1 && ceil_div(kps, kBK) > 4) ? 3 : 2;
+    gp.stages = 2;
     if (o_stages == 2 || o_stages == 3) gp.stages = o_stages;
+  } else if (mode != kConvWgrad && o_fn == 0 && g.R * g.S > 1 && pl.N % 128 == 0 &&
+             pl.N >= 256) {
+    // R*S > 1 forward / input gradient with N (Cout / C) a multiple of 128: the 128-wide tile
+    // (AlexNet features.8 input gradient 377 -> 351 us, ResNet-50 layer3 3x3 346 -> 331 us)
+    const long tiles = (long)ceil_div(pl.M, 128) * (pl.N / 128);
+    if (tiles >= 2L * num_cus) {
+      gp.tile = 2;
+      gp.splits = 1;
+      gp.k_per_split = ceil_div(pl.K, kBK) * kBK;
+      gp.ws_floats = 0;
+    }
   }
+  // Convolutions: the 64-wide tile keeps 2 LDS stages (48 KiB, 3 workgroups per CU instead of
+  // 2 with 3 stages); measured faster on 86 of 112 (layer, plan) pairs of AlexNet / ResNet-50
+  // and on every forward / input-gradient shape (scripts/sweep_conv_fd.py).
+  if (gp.tile == 1 && o_stages == 0) gp.stages = 2;
   pl.fn = gp.tile;
   pl.fm = gp.stages;  // pipeline depth (the NHWC path always uses BM = 128)
   pl.splits = gp.splits;
