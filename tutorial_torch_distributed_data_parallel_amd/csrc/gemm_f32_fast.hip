@@ -72,6 +72,21 @@ struct FastParams {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef char lds_char;  // generic pointer into the dynamic LDS array (reads infer ds_read)
 
+// optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
+constexpr int kOptWide = 4;  // SGD with paired columns: one batch covers both row tiles
+constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
+
+template <bool NT>
+__device__ __forceinline__ f32x2 ld_epi(const float* q) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(q));
+  else return *reinterpret_cast<const f32x2*>(q);
+}
+template <bool NT>
+__device__ __forceinline__ void st_epi(float* q, f32x2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(q));
+  else *reinterpret_cast<f32x2*>(q) = v;
+}
+
 __device__ __forceinline__ void glds16(const float* src, lds_char* dst) {
   __builtin_amdgcn_global_load_lds(
       (const void*)src, (void __attribute__((address_space(3)))*)(
@@ -474,14 +489,19 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     // FN == 2. With interleaved MN-contiguous B (FN == 2) a lane owns two ADJACENT columns, read
     // and written as float2 (two half-sector stores per line would force partial write-backs).
     // Offsets are 32-bit (a parameter has < 2^31 elements; checked on the host).
-    constexpr bool SGD = OPTK == 1;
+    // OPTK = kind (1 SGD, 2 Adam) | kOptWide (PAIR SGD: both row tiles in one batch, one HBM
+    // round trip per tile) | kOptNT (non-temporal p / state traffic: touched once per step, so it
+    // should not evict the L2-resident dY / X operand tiles)
+    constexpr bool SGD = (OPTK & 3) == 1;
+    constexpr bool NT = (OPTK & kOptNT) != 0;
     const OptEpilogue& o = p.opt;
     const bool mom_rd = SGD && o.sgd.momentum != 0.f && !o.sgd.first_step;
     const bool mom_wr = SGD && o.sgd.momentum != 0.f;
     constexpr bool PAIR = !BKC && FN == 2;
     constexpr int NG = PAIR ? 1 : FN;       // column groups per accumulator row
     constexpr int NE = PAIR ? 2 : 1;        // elements per group
-    constexpr int FB = PAIR ? 1 : (SGD ? FM : 1);  // row tiles per batch
+    constexpr bool WIDE = SGD && (OPTK & kOptWide) != 0;
+    constexpr int FB = PAIR ? (WIDE ? FM : 1) : (SGD ? FM : 1);  // row tiles per batch
     constexpr int RB = (PAIR && !SGD) ? 8 : 16;    // accumulator rows per batch (Adam: 3 arrays)
     constexpr int NB = FB * RB * NG;        // groups per batch
 #pragma unroll
@@ -507,14 +527,14 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             idx[j] = ok ? row * (int)p.ldc + col : -1;
             const int i = ok ? idx[j] : 0;
             if (PAIR) {
-              const f32x2 v = *reinterpret_cast<const f32x2*>(o.p + i);
+              const f32x2 v = ld_epi<NT>(o.p + i);
               pv[2 * j] = v[0]; pv[2 * j + 1] = v[1];
               if (!SGD || mom_rd) {
-                const f32x2 w = *reinterpret_cast<const f32x2*>(o.s0 + i);
+                const f32x2 w = ld_epi<NT>(o.s0 + i);
                 s0v[2 * j] = w[0]; s0v[2 * j + 1] = w[1];
               }
               if (!SGD) {
-                const f32x2 u = *reinterpret_cast<const f32x2*>(o.s1 + i);
+                const f32x2 u = ld_epi<NT>(o.s1 + i);
                 s1v[2 * j] = u[0]; s1v[2 * j + 1] = u[1];
               }
             } else {
@@ -550,11 +570,9 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
               s0v[j * NE + e] = b0;
             }
             if (PAIR) {
-              *reinterpret_cast<f32x2*>(o.p + i) = f32x2{pv[2 * j], pv[2 * j + 1]};
-              if (!SGD || mom_wr)
-                *reinterpret_cast<f32x2*>(o.s0 + i) = f32x2{s0v[2 * j], s0v[2 * j + 1]};
-              if (!SGD)
-                *reinterpret_cast<f32x2*>(o.s1 + i) = f32x2{s1v[2 * j], s1v[2 * j + 1]};
+              st_epi<NT>(o.p + i, f32x2{pv[2 * j], pv[2 * j + 1]});
+              if (!SGD || mom_wr) st_epi<NT>(o.s0 + i, f32x2{s0v[2 * j], s0v[2 * j + 1]});
+              if (!SGD) st_epi<NT>(o.s1 + i, f32x2{s1v[2 * j], s1v[2 * j + 1]});
             } else {
               o.p[i] = pv[j];
               if (!SGD || mom_wr) o.s0[i] = s0v[j];
@@ -757,8 +775,24 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
   if (opt) {
     const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
-    if (a.opt.kind == 1) launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nb, s);
-    else launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nb, s);
+    // TDP_OPT_VARIANT: SGD epilogue variant flags (kOptWide | kOptNT). Default kOptNT: toy MLP
+    // 0.502 ms/step vs 0.507 plain, kOptWide 0.56 (register pressure; profiles/opt_epilogue_variants.md)
+    static const int variant = [] {
+      const char* e = std::getenv("TDP_OPT_VARIANT");
+      return e ? (std::atoi(e) & (kOptWide | kOptNT)) : kOptNT;
+    }();
+    if (a.opt.kind == 1) {
+      switch (variant) {
+        case kOptWide: launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide>(p, fn, st, nb, s); break;
+        case kOptNT: launch_kinds<kDenseMN, kDenseMN, 1 | kOptNT>(p, fn, st, nb, s); break;
+        case kOptWide | kOptNT:
+          launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide | kOptNT>(p, fn, st, nb, s);
+          break;
+        default: launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nb, s);
+      }
+    } else {
+      launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nb, s);
+    }
     return;
   }
   p.opt.kind = 0;
