@@ -61,13 +61,14 @@ def main():
         p = ddp.arena.data[off: off + M * N]
         b = mom[off: off + M * N]
         flops = 2.0 * M * N * 128
-        for fn, st in ((0, 0), (1, 2), (1, 3), (2, 2)):
+        for fn, st, wgs in ((0, 0, 2), (1, 2, 2), (1, 2, 3), (1, 3, 2), (2, 2, 2)):
             C.gemm_f32_set_override(fn, 0, st)
+            os.environ["TDP_OPT_WGS"] = str(wgs)  # persistent epilogue grid: workgroups per CU
             t_gemm = timed(lambda: C.gemm_f32(g, a, dw, False, False))
             t_sgd = timed(lambda: C.sgd_flat(p, dw.view(-1), b, 1e-6, 0.9, 0.0, 0.0, False, False,
                                              False, 1.0))
             t_epi = timed(lambda: C.gemm_f32_opt(g, a, dw, False, False, be, off))
-            rec = {"layer": name, "fn": fn, "stages": st, "gemm_us": round(t_gemm, 1),
+            rec = {"layer": name, "fn": fn, "stages": st, "wgs": wgs, "gemm_us": round(t_gemm, 1),
                    "sgd_us": round(t_sgd, 1), "gemm+sgd_us": round(t_gemm + t_sgd, 1),
                    "epilogue_us": round(t_epi, 1),
                    "mfma_floor_us": round(flops / 157e12 * 1e6, 1),
@@ -75,6 +76,7 @@ def main():
             out.append(rec)
             print(json.dumps(rec), flush=True)
     C.gemm_f32_set_override(0, 0, 0)
+    os.environ.pop("TDP_OPT_WGS", None)
     tdp.destroy_process_group()
 
 

@@ -739,7 +739,10 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   plan.grid = 0;
   if (a.opt.kind != 0) {
     const char* e = std::getenv("TDP_OPT_PERSIST");
-    if (!(e && e[0] == '0')) plan.grid = 2 * num_cus;  // persistent: 2 workgroups per CU
+    // persistent: 2 workgroups per CU (TDP_OPT_WGS overrides, for measurements: 3 fit with FN=1)
+    const char* w = std::getenv("TDP_OPT_WGS");
+    const int wgs = w ? std::atoi(w) : 2;
+    if (!(e && e[0] == '0')) plan.grid = (wgs >= 1 && wgs <= 4 ? wgs : 2) * num_cus;
   }
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
