@@ -16,8 +16,11 @@ bias-corrected Adam with a per-parameter step counter.
 """
 from __future__ import annotations
 
+import functools
+
 import torch
 from torch.optim import Optimizer
+from torch.optim.optimizer import _global_optimizer_post_hooks, _global_optimizer_pre_hooks
 
 from .._native import native
 from ..parallel.arena import arena_of
@@ -34,6 +37,30 @@ def _flat_arena(group):
     return a
 
 
+def _hooks_or_profiler(opt) -> bool:
+    return bool(_global_optimizer_pre_hooks or _global_optimizer_post_hooks or
+                opt._optimizer_step_pre_hooks or opt._optimizer_step_post_hooks or
+                torch.autograd.profiler._is_profiler_enabled)
+
+
+def _lean_step_hook(func):
+    """torch wraps ``step`` (TORCH/optim/optimizer.py ``profile_hook_step``) in a record_function
+    range plus the hook dispatch on EVERY call: ~10 us of host time per training step, and the
+    eager toy-MLP step is host-bound right after the loss (profiles/host_overhead.md). Same
+    behaviour, paid only when a hook is registered or the profiler is on."""
+
+    @functools.wraps(func)
+    def wrapper(self, *args, **kwargs):
+        if _hooks_or_profiler(self):
+            return Optimizer.profile_hook_step(func)(self, *args, **kwargs)
+        out = func(self, *args, **kwargs)
+        self._optimizer_step_code()
+        return out
+
+    wrapper.hooked = True  # torch's _patch_step_function leaves a hooked step alone
+    return wrapper
+
+
 class _FusedBase(Optimizer):
     _state_keys: tuple = ()
 
@@ -41,6 +68,20 @@ class _FusedBase(Optimizer):
         super().__init__(params, defaults)
         self._flat_bufs = {}  # id(arena) -> {key: flat tensor}
         self._flat_step = {}  # id(arena) -> int step shared by every arena parameter (Adam)
+
+    def __init_subclass__(cls, **kwargs):
+        super().__init_subclass__(**kwargs)
+        if "step" in cls.__dict__ and not getattr(cls.__dict__["step"], "hooked", False):
+            cls.step = _lean_step_hook(cls.__dict__["step"])
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """torch's zero_grad, without its per-call record_function range / dynamo guard when
+        gradients are simply dropped (the default) and the profiler is off."""
+        if not set_to_none or torch.autograd.profiler._is_profiler_enabled:
+            return super().zero_grad(set_to_none)
+        for g in self.param_groups:
+            for p in g["params"]:
+                p.grad = None
 
     def _flat_state(self, arena, keys):
         """Arena-shaped state buffers; adopts values already in self.state (load_state_dict)."""
