@@ -266,6 +266,7 @@ def test_gemm_fast_wgrad_rowsum(C):
 
 
 @pytest.mark.parametrize("M,N,K,a_k,b_k", [(128, 10, 4096, True, True), (77, 13, 260, True, True),
+                                           (50, 1, 64, True, True), (20, 9, 1000, True, True),
                                            (128, 4096, 10, True, False), (33, 64, 16, True, False),
                                            (10, 4096, 128, False, False), (16, 100, 300, False, False),
                                            (3, 7, 5, False, False)])
