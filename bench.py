@@ -132,6 +132,7 @@ def main():
         from tutorial_torch_distributed_data_parallel_amd.data import (DeviceLoader,
                                                                         DistributedSampler,
                                                                         SyntheticDataset)
+        from tutorial_torch_distributed_data_parallel_amd.data.synthetic import gather_batch
         from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
         from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
@@ -295,8 +296,7 @@ def main():
 
         def tdp_step():
             b = idx_static if graph else cur["b"]
-            x = data.x.index_select(0, b)
-            y = data.y.index_select(0, b)
+            x, y = gather_batch(data.x, data.y, b)
             opt.zero_grad(set_to_none=True)
             loss = loss_fn(ddp(x), y)
             loss.backward()

@@ -293,3 +293,19 @@ def test_gemm_skinny_epilogues(C, M, N, K, a_k, b_k):
         C.gemm_f32(A, B, out, a_k, b_k, rowsum=rs, rowsum_beta=1.0)
         _close(out, ref, rtol=1e-4, atol=tol)
         _close(rs, rs0 + A.double().sum(0).float(), rtol=1e-4, atol=1e-3)
+
+
+def test_gather_batch_matches_index_select(C):
+    """One-launch loader gather (samples + labels) == two index_selects, incl. F % 4 != 0."""
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import gather_batch
+
+    torch.manual_seed(5)
+    for shape in [(300, 9216), (50, 3, 7, 5), (9, 1)]:
+        x = torch.randn(*shape, device="cuda")
+        y = torch.randint(0, 10, (shape[0],), device="cuda")
+        idx = torch.randint(0, shape[0], (37,), device="cuda")
+        xb, yb = C.gather_batch(x, y, idx)
+        assert xb.shape == (37,) + shape[1:]
+        assert torch.equal(xb, x.index_select(0, idx)) and torch.equal(yb, y.index_select(0, idx))
+        xb2, yb2 = gather_batch(x, y, idx[5:20])
+        assert torch.equal(xb2, x[idx[5:20]]) and torch.equal(yb2, y[idx[5:20]])

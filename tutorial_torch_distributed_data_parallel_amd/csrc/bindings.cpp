@@ -673,6 +673,25 @@ Tensor relu_mask_op(const Tensor& dy, const Tensor& y) {
   return g;
 }
 
+// x [n, ...] fp32 contiguous, y [n] int64, idx [B] int64 (all on the GPU) -> (x[idx], y[idx])
+std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tensor& idx) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_GPU(y); CHECK_CONTIG(y); CHECK_GPU(idx);
+  CHECK_CONTIG(idx);
+  TORCH_CHECK(y.scalar_type() == at::kLong && idx.scalar_type() == at::kLong && idx.dim() == 1,
+              "gather_batch: int64 labels and a 1-d int64 index");
+  TORCH_CHECK(x.dim() >= 1 && y.dim() == 1 && y.size(0) == x.size(0) && x.size(0) > 0,
+              "gather_batch: x [n, ...] and y [n]");
+  const long n = x.size(0), F = x.numel() / n;
+  const int B = (int)idx.numel();
+  auto xs = x.sizes().vec();
+  xs[0] = B;
+  auto xb = at::empty(xs, x.options());
+  auto yb = at::empty({B}, y.options());
+  gather_batch(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F, B,
+               xb.data_ptr<float>(), yb.data_ptr<int64_t>(), cur_stream());
+  return {xb, yb};
+}
+
 // ---------------------------------------------------------------------------------------- comm
 ncclDataType_t nccl_dt(const Tensor& t) {
   switch (t.scalar_type()) {
@@ -778,6 +797,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout_op);
   m.def("add_relu", &add_relu_op);
   m.def("relu_mask", &relu_mask_op);
+  m.def("gather_batch", &gather_batch_op);
   m.def("bn_moments", &bn_moments_op);
   m.def("bn_merge", &bn_merge_op);
   m.def("bn_elemt", &bn_elemt_op);

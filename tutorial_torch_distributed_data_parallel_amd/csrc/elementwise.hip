@@ -100,3 +100,44 @@ int relu_bias_slices(int B, int N, int num_cus) {
 }
 
 }  // namespace tdp
+
+// ------------------------------------------------------------------ batch gather
+// One launch gathers a batch of samples AND their labels by the sampler's indices (the loader's
+// two index_selects were two launches per step): workgroup b copies sample idx[b] (F floats,
+// float4 when F % 4 == 0) and lane 0 copies its label. Indices are checked on the host side of
+// the epoch (DistributedSampler output) and clamped here, so a bad index cannot fault.
+namespace tdp {
+namespace {
+__global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ x,
+                                                           const int64_t* __restrict__ y,
+                                                           const int64_t* __restrict__ idx,
+                                                           long n, long F, float* __restrict__ xb,
+                                                           int64_t* __restrict__ yb) {
+  // grid.y splits a row into slices: B = 128 rows alone would leave half of the 256 CUs idle
+  const int b = blockIdx.x;
+  long i = idx[b];
+  i = i < 0 ? 0 : (i >= n ? n - 1 : i);
+  const float* src = x + i * F;
+  float* dst = xb + (long)b * F;
+  const long step = 256L * gridDim.y, k0 = threadIdx.x + 256L * blockIdx.y;
+  if ((F & 3) == 0) {
+    const long F4 = F >> 2;
+    for (long k = k0; k < F4; k += step)
+      reinterpret_cast<f32x4*>(dst)[k] = reinterpret_cast<const f32x4*>(src)[k];
+  } else {
+    for (long k = k0; k < F; k += step) dst[k] = src[k];
+  }
+  if (threadIdx.x == 0 && blockIdx.y == 0) yb[b] = y[i];
+}
+}  // namespace
+
+void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, long F, int B,
+                  float* xb, int64_t* yb, hipStream_t s) {
+  if (B <= 0) return;
+  const long units = (F & 3) == 0 ? F / 4 : F;  // float4 (or float) moves per row
+  const long want = (units + 255) / 256;
+  const int slices = (int)(want < 8 ? (want < 1 ? 1 : want) : 8);
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(B, slices), dim3(256), 0, s, x, y, idx, n, F, xb,
+                     yb);
+}
+}  // namespace tdp

@@ -172,6 +172,9 @@ int relu_bias_slices(int B, int N, int num_cus);
 void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, float* g,
                       float* db, float beta_db, float* part, int slices, hipStream_t s);
 void fill_f32(float* x, long n, float v, hipStream_t s);
+// xb[b] = x[idx[b]] (rows of F floats), yb[b] = y[idx[b]]: a loader batch in one launch
+void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, long F, int B,
+                  float* xb, int64_t* yb, hipStream_t s);
 void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
 void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);
 // sum of squares of x into out[0] (+= when accumulate), for grad-norm clipping

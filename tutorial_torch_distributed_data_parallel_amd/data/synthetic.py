@@ -41,6 +41,19 @@ class SyntheticDataset(torch.utils.data.Dataset):
         return self.x[i], self.y[i]
 
 
+def gather_batch(x: torch.Tensor, y: torch.Tensor, idx: torch.Tensor):
+    """``(x[idx], y[idx])``: on the GPU one native launch for samples and labels
+    (csrc/elementwise.hip ``gather_batch``), else two ``index_select``."""
+    if (x.is_cuda and idx.is_cuda and x.dtype == torch.float32 and y.dtype == torch.long and
+            idx.dtype == torch.long and x.is_contiguous() and y.is_contiguous() and
+            idx.is_contiguous() and y.device == x.device and len(idx) > 0):
+        from .._native import native
+
+        xb, yb = native().gather_batch(x, y, idx)
+        return xb, yb
+    return x.index_select(0, idx), y.index_select(0, idx)
+
+
 class DeviceLoader:
     """Iterates (inputs, labels) batches of a tensor dataset by sampler order, on device.
 
@@ -88,8 +101,7 @@ class DeviceLoader:
     def __iter__(self):
         x, y = self.dataset.x, self.dataset.y
         for b in self._index_batches():
-            xb = x.index_select(0, b)
-            yb = y.index_select(0, b)
+            xb, yb = gather_batch(x, y, b)
             if xb.device != self.device:
                 xb = xb.to(self.device, non_blocking=True)
                 yb = yb.to(self.device, non_blocking=True)
