@@ -75,6 +75,8 @@ typedef char lds_char;  // generic pointer into the dynamic LDS array (reads inf
 // optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
 constexpr int kOptWide = 4;  // SGD with paired columns: one batch covers both row tiles
 constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
+constexpr int kOptLds = 16;  // SGD, 128-wide paired tiles: gradient tile staged through LDS,
+                             // float4 p / momentum traffic
 
 template <bool NT>
 __device__ __forceinline__ f32x2 ld_epi(const float* q) {
@@ -500,6 +502,68 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     constexpr bool PAIR = !BKC && FN == 2;
     constexpr int NG = PAIR ? 1 : FN;       // column groups per accumulator row
     constexpr int NE = PAIR ? 2 : 1;        // elements per group
+    if constexpr (SGD && PAIR && !AK && (OPTK & kOptLds) != 0) {
+      // kOptLds: stage the 128 x 128 gradient tile through LDS (the pipeline stages are free
+      // once every wave has left the K loop) so each p / momentum access is a 16-B-per-lane,
+      // 512-B-per-row coalesced float4 (the MFMA layout alone gives lanes column PAIRS).
+      static_assert(BM * BN * 4 <= S * STG, "gradient tile must fit in the LDS stages");
+      float* T = reinterpret_cast<float*>(smem);
+      __syncthreads();  // every wave is done reading the last K stage
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int lr = wm * 64 + 2 * rl + f;
+          *reinterpret_cast<f32x2*>(T + lr * BN + wn * 64 + 2 * l31) =
+              f32x2{acc[f][0][r], acc[f][FN - 1][r]};
+        }
+      __syncthreads();
+      constexpr int C4 = BN / 4;                  // float4 per tile row
+      constexpr int IT = BM * C4 / kT;            // float4 per thread (16)
+      constexpr int HB = 8;                       // float4 per batch (one HBM round trip)
+#pragma unroll
+      for (int i0 = 0; i0 < IT; i0 += HB) {
+        int gi[HB];
+        f32x4 pv4[HB], mv4[HB];
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          const int e = (i0 + i) * kT + threadIdx.x;
+          const int row = m0 + e / C4, col = n0 + (e % C4) * 4;
+          gi[i] = (row < p.M && col < p.N) ? row * (int)p.ldc + col : -1;
+          const int q = gi[i] < 0 ? 0 : gi[i];
+          if constexpr (NT) {
+            pv4[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.p + q));
+            if (mom_rd) mv4[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s0 + q));
+          } else {
+            pv4[i] = *reinterpret_cast<const f32x4*>(o.p + q);
+            if (mom_rd) mv4[i] = *reinterpret_cast<const f32x4*>(o.s0 + q);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          if (gi[i] < 0) continue;
+          const int e = (i0 + i) * kT + threadIdx.x;
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(T + (e / C4) * BN + (e % C4) * 4);
+          f32x4 pe = pv4[i], be = mom_rd ? mv4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float pc = pe[c], bc = be[c];
+            sgd_elem(pc, g4[c], bc, o.sgd);
+            pe[c] = pc;
+            be[c] = bc;
+          }
+          if constexpr (NT) {
+            __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
+            if (mom_wr) __builtin_nontemporal_store(be, reinterpret_cast<f32x4*>(o.s0 + gi[i]));
+          } else {
+            *reinterpret_cast<f32x4*>(o.p + gi[i]) = pe;
+            if (mom_wr) *reinterpret_cast<f32x4*>(o.s0 + gi[i]) = be;
+          }
+        }
+      }
+      return;  // the persistent loop's barrier protects T before the next tile's DMA
+    }
     constexpr bool WIDE = SGD && (OPTK & kOptWide) != 0;
     constexpr int FB = PAIR ? (WIDE ? FM : 1) : (SGD ? FM : 1);  // row tiles per batch
     constexpr int RB = (PAIR && !SGD) ? 8 : 16;    // accumulator rows per batch (Adam: 3 arrays)
@@ -778,14 +842,20 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
   if (opt) {
     const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
-    // TDP_OPT_VARIANT: SGD epilogue variant flags (kOptWide | kOptNT). Default kOptNT: toy MLP
-    // 0.502 ms/step vs 0.507 plain, kOptWide 0.56 (register pressure; profiles/opt_epilogue_variants.md)
+    // TDP_OPT_VARIANT: SGD epilogue variant flags (kOptWide | kOptNT | kOptLds). Default
+    // kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four 0.498), kOptLds alone 0.468,
+    // kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure; profiles/opt_epilogue_variants.md).
+    // Non-128-wide tiles ignore kOptLds.
     static const int variant = [] {
       const char* e = std::getenv("TDP_OPT_VARIANT");
-      return e ? (std::atoi(e) & (kOptWide | kOptNT)) : kOptNT;
+      return e ? (std::atoi(e) & (kOptWide | kOptNT | kOptLds)) : (kOptLds | kOptNT);
     }();
     if (a.opt.kind == 1) {
       switch (variant) {
+        case kOptLds: launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds>(p, fn, st, nb, s); break;
+        case kOptLds | kOptNT:
+          launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT>(p, fn, st, nb, s);
+          break;
         case kOptWide: launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide>(p, fn, st, nb, s); break;
         case kOptNT: launch_kinds<kDenseMN, kDenseMN, 1 | kOptNT>(p, fn, st, nb, s); break;
         case kOptWide | kOptNT:
