@@ -75,8 +75,8 @@ typedef char lds_char;  // generic pointer into the dynamic LDS array (reads inf
 // optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
 constexpr int kOptWide = 4;  // SGD with paired columns: one batch covers both row tiles
 constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
-constexpr int kOptLds = 16;  // SGD, 128-wide paired tiles: gradient tile staged through LDS,
-                             // float4 p / momentum traffic
+constexpr int kOptLds = 16;  // 128-wide paired tiles: gradient tile staged through LDS,
+                             // float4 p / optimizer-state traffic (SGD and Adam)
 
 template <bool NT>
 __device__ __forceinline__ f32x2 ld_epi(const float* q) {
@@ -564,6 +564,71 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
       }
       return;  // the persistent loop's barrier protects T before the next tile's DMA
     }
+    if constexpr (!SGD && PAIR && !AK && (OPTK & kOptLds) != 0) {
+      // the same LDS staging for Adam: p, exp_avg, exp_avg_sq as float4 rows (4 per batch)
+      static_assert(BM * BN * 4 <= S * STG, "gradient tile must fit in the LDS stages");
+      float* T = reinterpret_cast<float*>(smem);
+      __syncthreads();
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int lr = wm * 64 + 2 * rl + f;
+          *reinterpret_cast<f32x2*>(T + lr * BN + wn * 64 + 2 * l31) =
+              f32x2{acc[f][0][r], acc[f][FN - 1][r]};
+        }
+      __syncthreads();
+      constexpr int C4 = BN / 4;
+      constexpr int IT = BM * C4 / kT;
+      constexpr int HB = 4;
+#pragma unroll
+      for (int i0 = 0; i0 < IT; i0 += HB) {
+        int gi[HB];
+        f32x4 pv4[HB], mv4[HB], vv4[HB];
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          const int e = (i0 + i) * kT + threadIdx.x;
+          const int row = m0 + e / C4, col = n0 + (e % C4) * 4;
+          gi[i] = (row < p.M && col < p.N) ? row * (int)p.ldc + col : -1;
+          const int q = gi[i] < 0 ? 0 : gi[i];
+          if constexpr (NT) {
+            pv4[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.p + q));
+            mv4[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s0 + q));
+            vv4[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s1 + q));
+          } else {
+            pv4[i] = *reinterpret_cast<const f32x4*>(o.p + q);
+            mv4[i] = *reinterpret_cast<const f32x4*>(o.s0 + q);
+            vv4[i] = *reinterpret_cast<const f32x4*>(o.s1 + q);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          if (gi[i] < 0) continue;
+          const int e = (i0 + i) * kT + threadIdx.x;
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(T + (e / C4) * BN + (e % C4) * 4);
+          f32x4 pe = pv4[i], me = mv4[i], ve = vv4[i];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float pc = pe[c], mc = me[c], vc = ve[c];
+            adam_elem(pc, g4[c], mc, vc, o.s2 ? o.s2 + gi[i] + c : nullptr, o.adam);
+            pe[c] = pc;
+            me[c] = mc;
+            ve[c] = vc;
+          }
+          if constexpr (NT) {
+            __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
+            __builtin_nontemporal_store(me, reinterpret_cast<f32x4*>(o.s0 + gi[i]));
+            __builtin_nontemporal_store(ve, reinterpret_cast<f32x4*>(o.s1 + gi[i]));
+          } else {
+            *reinterpret_cast<f32x4*>(o.p + gi[i]) = pe;
+            *reinterpret_cast<f32x4*>(o.s0 + gi[i]) = me;
+            *reinterpret_cast<f32x4*>(o.s1 + gi[i]) = ve;
+          }
+        }
+      }
+      return;
+    }
     constexpr bool WIDE = SGD && (OPTK & kOptWide) != 0;
     constexpr int FB = PAIR ? (WIDE ? FM : 1) : (SGD ? FM : 1);  // row tiles per batch
     constexpr int RB = (PAIR && !SGD) ? 8 : 16;    // accumulator rows per batch (Adam: 3 arrays)
@@ -850,6 +915,12 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
       const char* e = std::getenv("TDP_OPT_VARIANT");
       return e ? (std::atoi(e) & (kOptWide | kOptNT | kOptLds)) : (kOptLds | kOptNT);
     }();
+    // TDP_OPT_ADAM_VARIANT: Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam
+    // 0.555 ms/step vs 0.566 LDS only, 0.594 register epilogue (profiles/opt_epilogue_variants.md)
+    static const int adam_variant = [] {
+      const char* e = std::getenv("TDP_OPT_ADAM_VARIANT");
+      return e ? (std::atoi(e) & (kOptNT | kOptLds)) : (kOptLds | kOptNT);
+    }();
     if (a.opt.kind == 1) {
       switch (variant) {
         case kOptLds: launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds>(p, fn, st, nb, s); break;
@@ -863,6 +934,10 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
           break;
         default: launch_kinds<kDenseMN, kDenseMN, 1>(p, fn, st, nb, s);
       }
+    } else if (adam_variant == (kOptLds | kOptNT)) {
+      launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT>(p, fn, st, nb, s);
+    } else if (adam_variant == kOptLds) {
+      launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds>(p, fn, st, nb, s);
     } else {
       launch_kinds<kDenseMN, kDenseMN, 2>(p, fn, st, nb, s);
     }
