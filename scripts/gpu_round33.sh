@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-end check of the committed default build: GPU suite, smoke, default bench, SGD + Adam benches.
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/r33; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 120 python bench.py > $O/mlp_default.json 2> $O/mlp_default.err && \
+timeout -k 10 120 python bench.py --steps 500 --warmup 30 > $O/mlp.json 2> $O/mlp.err && \
+timeout -k 10 120 python bench.py --steps 300 --warmup 30 --optim adam > $O/adam.json 2> $O/adam.err && \
+TDP_FORCE_COLLECTIVE=1 timeout -k 10 120 python bench.py --steps 300 --warmup 30 > $O/mlp_coll.json 2> $O/mlp_coll.err
+rc=$?
+tail -n 1 $O/pytest.log; tail -n 1 $O/smoke.log
+for f in $O/*.json; do echo "$f: $(grep -o '"ms_per_step": [0-9.]*' $f) $(grep -o '"value": [0-9.]*' $f)"; done
+exit $rc
