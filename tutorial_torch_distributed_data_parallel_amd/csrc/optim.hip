@@ -25,7 +25,34 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p,
   const long n4 = VEC ? n / 4 : 0;
   const long stride = (long)gridDim.x * blockDim.x;
   const bool mom = h.momentum != 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const bool mrd = mom && !h.first_step;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // main body: U float4 per stream in flight per lane (one HBM round trip per U elements), and
+  // non-temporal traffic -- every element is touched once per step
+  constexpr int U = 4;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    f32x4 pv[U], gv[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i + u * stride);
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i + u * stride);
+      bv[u] = mrd ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf) + i + u * stride)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = pv[u][e], be = bv[u][e];
+        sgd_elem(pe, gv[u][e], be, h);
+        pv[u][e] = pe;
+        bv[u][e] = be;
+      }
+      __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4*>(p) + i + u * stride);
+      if (mom) __builtin_nontemporal_store(bv[u], reinterpret_cast<f32x4*>(buf) + i + u * stride);
+    }
+  }
+  for (; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
