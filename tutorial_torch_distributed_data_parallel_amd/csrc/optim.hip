@@ -84,7 +84,36 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p,
                                                         AdamHyper h) {
   const long n4 = VEC ? n / 4 : 0;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // main body (no amsgrad): U float4 per stream in flight per lane, non-temporal traffic
+  constexpr int U = 2;
+  if (!h.amsgrad) {
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+      f32x4 pv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long j = i + u * stride;
+        pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + j);
+        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + j);
+        mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + j);
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + j);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pe = pv[u][e], me = mv[u][e], ve = vv[u][e];
+          adam_elem(pe, gv[u][e], me, ve, nullptr, h);
+          pv[u][e] = pe; mv[u][e] = me; vv[u][e] = ve;
+        }
+        const long j = i + u * stride;
+        __builtin_nontemporal_store(pv[u], reinterpret_cast<f32x4*>(p) + j);
+        __builtin_nontemporal_store(mv[u], reinterpret_cast<f32x4*>(m) + j);
+        __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v) + j);
+      }
+    }
+  }
+  for (; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
     f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
