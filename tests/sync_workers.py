@@ -1,0 +1,230 @@
+"""Multi-rank workers for the gradient-sync algorithm (csrc/reducer.cpp SyncBackend) on CPU/gloo.
+
+The C++ SyncBackend drives parallel/ddp.py ``_CpuSyncOps`` here exactly as it drives RcclOps on
+MI355X, so these runs exercise the production bucket order, the sharded reduce-scatter -> 1/W
+update -> all-gather path with tails that do not divide by W, in-reduction clipping, device-style
+hyper blocks (LR changes, Adam step count) and state consolidation for checkpoints, at world
+sizes 2 and 3. The oracle is stock ``torch.nn.parallel.DistributedDataParallel`` +
+``torch.optim`` on the same data (SURVEY.md §4.3 oracles 1-2).
+"""
+import copy
+import os
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+import tutorial_torch_distributed_data_parallel_amd as tdp
+from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+
+# odd layer sizes: no parameter, bucket or arena size divides evenly by 2 or 3
+DIMS = dict(in_features=37, hidden=(29, 23), num_classes=5)
+# ~1.9k parameters: 2 KiB buckets, params above 1.5 KiB split -> ~6 buckets with shard tails
+BUCKETS = dict(bucket_cap_mb=2048 / 2 ** 20, first_bucket_cap_mb=600 / 2 ** 20,
+               split_bucket_mb=1536 / 2 ** 20)
+
+
+def _gather(obj):
+    out = [None] * rt.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def _make_opts(kind, ours_params, ref_params, lr):
+    if kind == "sgd":
+        hp = dict(lr=lr, momentum=0.9, weight_decay=1e-3, nesterov=True)
+        return tdp.optim.SGD(ours_params, **hp), torch.optim.SGD(ref_params, **hp)
+    if kind == "adamw":
+        hp = dict(lr=lr, weight_decay=5e-2)
+        return tdp.optim.AdamW(ours_params, **hp), torch.optim.AdamW(ref_params, **hp)
+    hp = dict(lr=lr, weight_decay=1e-3, amsgrad=kind == "amsgrad")
+    return tdp.optim.Adam(ours_params, **hp), torch.optim.Adam(ref_params, **hp)
+
+
+def _batch(r, step):
+    g = torch.Generator().manual_seed(1000 * step + r)
+    return torch.randn(6, 37, generator=g) * (1 + r), torch.randint(0, 5, (6,), generator=g)
+
+
+def _check_close(model, ref, tag, atol=2e-5):
+    for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), atol=atol, rtol=1e-4,
+                                   msg=lambda m: f"{tag} {n}: {m}")
+
+
+def _check_replicas(model):
+    allp = _gather([p.detach().clone() for p in model.parameters()])
+    for other in allp[1:]:
+        for a, b in zip(other, allp[0]):
+            assert torch.equal(a, b), "replicas diverged"
+
+
+def _teardown():
+    # stock torch DDP objects (dropped by the caller) must die before their process group does:
+    # their reducer / gloo work threads otherwise abort the process at exit
+    import gc
+
+    gc.collect()
+    dist.barrier()
+    tdp.destroy_process_group()
+
+
+def fused_parity(rank, out_dir, kind="sgd", shard=True, clip=None, steps=5):
+    """Fused (in-reduction) optimizer vs torch DDP + torch.optim, with an LR change mid-run,
+    then consolidate -> save -> load into fresh objects -> continue."""
+    tdp.init_process_group("gloo")
+    r = rt.get_rank()
+    torch.manual_seed(0)
+    model = ToyMLP(**DIMS)
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, **BUCKETS)
+    assert ddp._backend.collective
+    opt, ropt = _make_opts(kind, ddp.parameters(), ref.parameters(), 0.05 if kind == "sgd"
+                           else 1e-2)
+    assert ddp.register_fused_optimizer(opt, shard=shard, clip_grad_norm=clip)
+    nb = len(ddp._bounds) - 1
+    assert nb >= 4, ddp._bounds
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+
+    def both_steps(n0, n1):
+        for step in range(n0, n1):
+            if step == 3:  # LR schedule: the fused update must see the new value
+                for o in (opt, ropt):
+                    o.param_groups[0]["lr"] *= 0.5
+            x, y = _batch(r, step)
+            opt.zero_grad()
+            tdp.ops.cross_entropy(ddp(x), y).backward()
+            opt.step()  # no-op: the update ran inside the reduction
+            ropt.zero_grad()
+            F.cross_entropy(rddp(x), y).backward()
+            if clip:
+                torch.nn.utils.clip_grad_norm_(rddp.parameters(), clip)
+            ropt.step()
+        _check_close(model, ref, f"{kind} shard={shard} clip={clip} after {n1} steps")
+        _check_replicas(model)
+
+    both_steps(0, steps)
+    if clip:
+        norm = float(ddp.last_grad_norm())
+        assert norm > 0
+    # checkpoint: consolidate the sharded state, every rank holds the complete optimizer state
+    ddp.consolidate_optimizer_state()
+    sd = opt.state_dict()
+    rsd = ropt.state_dict()
+    for pid, st in rsd["state"].items():
+        for k, v in st.items():
+            if k == "step":
+                assert int(sd["state"][pid]["step"]) == int(v), (k, sd["state"][pid]["step"], v)
+            else:
+                torch.testing.assert_close(sd["state"][pid][k], v, atol=2e-5, rtol=1e-4,
+                                           msg=lambda m: f"state {pid}.{k}: {m}")
+    path = os.path.join(out_dir, f"state_{r}.pt")
+    torch.save({"model": {k: v.clone() for k, v in model.state_dict().items()}, "opt": sd}, path)
+    dist.barrier()
+    # fresh objects: load, register, continue; must track the reference exactly as before
+    ck = torch.load(path, weights_only=True)
+    torch.manual_seed(123)
+    model2 = ToyMLP(**DIMS)
+    model2.load_state_dict(ck["model"])
+    ddp2 = tdp.DDP(model2, **BUCKETS)
+    opt2, _ = _make_opts(kind, ddp2.parameters(), [torch.nn.Parameter(torch.zeros(1))], 1.0)
+    opt2.load_state_dict(ck["opt"])
+    ddp2.register_fused_optimizer(opt2, shard=shard, clip_grad_norm=clip)
+    model, ddp, opt = model2, ddp2, opt2
+    both_steps(steps, steps + 2)
+    rddp = None  # noqa: F841
+    _teardown()
+
+
+def local_clip_parity(rank, out_dir, max_norm=0.05, fused=True):
+    """README pitfall (REF/README.md:92-95): every rank clips its OWN gradient before the
+    average. Oracle: per-rank torch clip_grad_norm_ on a plain model, manual average, step."""
+    tdp.init_process_group("gloo")
+    r, W = rt.get_rank(), rt.get_world_size()
+    torch.manual_seed(0)
+    model = ToyMLP(**DIMS)
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, **BUCKETS)
+    ddp.clip_grad_norm_before_aggregation(max_norm)
+    opt = tdp.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    if fused:
+        ddp.register_fused_optimizer(opt)
+    for step in range(4):
+        x, y = _batch(r, step)
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        ropt.zero_grad()
+        F.cross_entropy(ref(x), y).backward()
+        n = torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm)
+        assert float(n) > max_norm  # the clip is active
+        for p in ref.parameters():
+            dist.all_reduce(p.grad)
+            p.grad.div_(W)
+        ropt.step()
+        torch.testing.assert_close(ddp.last_grad_norm(), n, atol=1e-5, rtol=1e-4)
+    _check_close(model, ref, f"local clip fused={fused}")
+    _check_replicas(model)
+    tdp.destroy_process_group()
+
+
+def comm_hook_keeps_fused_state(rank, out_dir):
+    """register_comm_hook after register_fused_optimizer must keep the Adam step count,
+    the shard flag and the state buffers."""
+    tdp.init_process_group("gloo")
+    r = rt.get_rank()
+    torch.manual_seed(0)
+    model = ToyMLP(**DIMS)
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, **BUCKETS)
+    opt, ropt = _make_opts("adam", ddp.parameters(), ref.parameters(), 1e-2)
+    ddp.register_fused_optimizer(opt)
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    for step in range(4):
+        if step == 2:
+            ddp.register_comm_hook(None, "fp32")  # rebuilds the reducer backend
+            assert ddp._backend.shard and ddp._backend.fused_kind == 2
+        x, y = _batch(r, step)
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        ropt.zero_grad()
+        F.cross_entropy(rddp(x), y).backward()
+        ropt.step()
+    assert opt.device_step(0) == 4
+    _check_close(model, ref, "comm hook rebuild")
+    rddp = None  # noqa: F841
+    _teardown()
+
+
+def shared_parameter(rank, out_dir):
+    """one Linear applied twice in a forward. The gradient is the SUM of both
+    uses' contributions, averaged over ranks."""
+    tdp.init_process_group("gloo")
+    r = rt.get_rank()
+
+    class Twice(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.inp = tdp.nn.Linear(10, 16, relu=True)
+            self.mid = tdp.nn.Linear(16, 16, relu=True)  # applied twice
+            self.out = tdp.nn.Linear(16, 4)
+
+        def forward(self, x):
+            return self.out(self.mid(self.mid(self.inp(x))))
+
+    torch.manual_seed(0)
+    model = Twice()
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model)
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    g = torch.Generator().manual_seed(r)
+    x, y = torch.randn(8, 10, generator=g), torch.randint(0, 4, (8,), generator=g)
+    tdp.ops.cross_entropy(ddp(x), y).backward()
+    F.cross_entropy(rddp(x), y).backward()
+    for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-6, rtol=1e-5,
+                                   msg=lambda m: f"{n}: {m}")
+    rddp = None  # noqa: F841
+    _teardown()

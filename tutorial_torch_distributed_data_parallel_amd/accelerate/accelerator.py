@@ -206,7 +206,10 @@ class Accelerator:
         (loss / self.gradient_accumulation_steps).backward(**kwargs)
 
     def clip_grad_norm_(self, parameters, max_norm: float, norm_type: float = 2.0):
-        return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type)
+        """Clip the (already averaged) gradients: native on MI355X (tdp.nn.utils)."""
+        from ..nn.utils import clip_grad_norm_
+
+        return clip_grad_norm_(parameters, max_norm, norm_type)
 
     def wait_for_everyone(self):
         rt.barrier()

@@ -98,7 +98,7 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
 // RcclBackend::epilogue_opt). C must be that contiguous arena slice (its contents are left as
 // they were: the gradient is never materialised).
 bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
-                     RcclBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
+                     SyncBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
                      double rowsum_beta) {
   CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
   CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
@@ -109,6 +109,8 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
   TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm: B cols != C cols");
   TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm: inner dims differ");
   TORCH_CHECK(backend.epilogue_allowed(), "optimizer epilogue: no fused optimizer at world 1");
+  auto ops = std::dynamic_pointer_cast<RcclOps>(backend.ops());
+  TORCH_CHECK(ops != nullptr, "optimizer epilogue needs the device (RCCL) backend");
   GemmF32Args a;
   a.A = A.data_ptr<float>(); a.B = B.data_ptr<float>(); a.C = C.data_ptr<float>();
   a.lda = A.stride(0); a.ldb = B.stride(0); a.ldc = N;
@@ -127,7 +129,17 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
   probe.opt.kind = 1;
   const GemmPlan pp = gemm_f32_plan(probe, num_cus(C.get_device()));
   const bool epi = pp.fast && !pp.skinny && pp.splits == 1 && !a_kcontig && !b_kcontig;
-  if (epi) a.opt = backend.epilogue_opt(offset, (int64_t)M * N);
+  if (epi) {
+    const FusedOptimizer& f = ops->fused;
+    backend.note_epilogue(offset, (int64_t)M * N);
+    a.opt.kind = f.kind;
+    a.opt.p = f.p + offset;
+    a.opt.s0 = f.s0 ? f.s0 + offset : nullptr;
+    a.opt.s1 = f.s1 ? f.s1 + offset : nullptr;
+    a.opt.s2 = f.s2 ? f.s2 + offset : nullptr;
+    a.opt.sgd = f.sgd;    // scalars: from the device hyper block (f.sgd.dev)
+    a.opt.adam = f.adam;
+  }
   const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
@@ -190,31 +202,70 @@ void count_correct_op(const Tensor& logits, const Tensor& labels, Tensor& acc) {
 }
 
 // ---------------------------------------------------------------------------------- optimizers
+const float* hyper_ptr(const c10::optional<Tensor>& blk) {
+  if (!blk.has_value() || !blk->defined()) return nullptr;
+  CHECK_GPU(*blk); CHECK_F32(*blk); CHECK_CONTIG(*blk);
+  TORCH_CHECK(blk->numel() >= kHSlots, "hyper block needs ", kHSlots, " floats");
+  return blk->data_ptr<float>();
+}
+
+// `hyper` (optional device hyper block, kernels.h HyperSlot): the kernel reads lr / momentum /
+// betas / bias corrections / first-step flag / clip coefficient from it (graph-replay safe);
+// the by-value arguments then only carry the structural flags.
 void sgd_flat_op(Tensor& p, const Tensor& g, const c10::optional<Tensor>& buf, double lr,
                  double momentum, double dampening, double wd, bool nesterov, bool maximize,
-                 bool first_step, double grad_scale) {
+                 bool first_step, double grad_scale, const c10::optional<Tensor>& hyper) {
   CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p); CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "sgd: p/g size mismatch");
   if (momentum != 0.0)
     TORCH_CHECK(buf.has_value() && buf->numel() == p.numel(), "sgd: momentum buffer required");
   SgdHyper h{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
-             first_step, (float)grad_scale};
+             first_step, (float)grad_scale, hyper_ptr(hyper)};
   sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), fptr(buf), p.numel(), h, cur_stream());
 }
 
 void adam_flat_op(Tensor& p, const Tensor& g, Tensor& m, Tensor& v,
                   const c10::optional<Tensor>& vmax, double lr, double b1, double b2, double eps,
                   double wd, bool amsgrad, bool maximize, bool decoupled, int64_t step,
-                  double grad_scale) {
+                  double grad_scale, const c10::optional<Tensor>& hyper) {
   CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(),
               "adam: size mismatch");
   if (amsgrad) TORCH_CHECK(vmax.has_value() && vmax->numel() == p.numel(), "adam: need vmax");
   AdamHyper h{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, amsgrad, maximize,
               decoupled, (float)(1.0 - std::pow(b1, (double)step)),
-              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale};
+              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale,
+              hyper_ptr(hyper)};
   adam_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
             fptr(vmax), p.numel(), h, cur_stream());
+}
+
+void opt_step_begin_op(Tensor& hyper, int64_t kind) {
+  opt_step_begin(const_cast<float*>(hyper_ptr(hyper)), (int)kind, cur_stream());
+}
+
+// torch.nn.utils.clip_grad_norm_ over a list of gradients, entirely on the device: one
+// deterministic sum-of-squares pass per <= 16 tensors into the block, the coefficient, one
+// scaling pass. Returns nothing; the total norm is left at hyper[kHNorm].
+void clip_grad_norm_op(const std::vector<Tensor>& grads, Tensor& hyper, double max_norm) {
+  float* blk = const_cast<float*>(hyper_ptr(hyper));
+  hipStream_t s = cur_stream();
+  // reset the accumulator and set the threshold without a host round trip
+  fill_f32(blk + kHSumsq, 1, 0.f, s);
+  fill_f32(blk + kHMaxNorm, 1, (float)max_norm, s);
+  RangeSet one;
+  one.n = 1;
+  one.begin[0] = 0;
+  for (const auto& g : grads) {
+    CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
+    one.len[0] = (long)g.numel();
+    sumsq_ranges(g.data_ptr<float>(), one, blk, s);
+  }
+  clip_coef_from_sumsq(blk, s);
+  for (const auto& g : grads) {
+    one.len[0] = (long)g.numel();
+    scale_ranges_by(g.data_ptr<float>(), one, blk, s);
+  }
 }
 
 // Build the chunk table (<= 64K elements per workgroup) on the host, ship it with the launch.
@@ -246,14 +297,15 @@ Tensor chunk_table(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
 
 void sgd_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
                   const std::vector<Tensor>& bufs, double lr, double momentum, double dampening,
-                  double wd, bool nesterov, bool maximize, bool first_step, double grad_scale) {
+                  double wd, bool nesterov, bool maximize, bool first_step, double grad_scale,
+                  const c10::optional<Tensor>& hyper) {
   if (ps.empty()) return;
   for (auto& t : ps) { CHECK_GPU(t); CHECK_F32(t); CHECK_CONTIG(t); }
   for (auto& t : gs) { CHECK_F32(t); CHECK_CONTIG(t); }
   int count = 0;
   auto tab = chunk_table(ps, gs, bufs, {}, {}, &count);
   SgdHyper h{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
-             first_step, (float)grad_scale};
+             first_step, (float)grad_scale, hyper_ptr(hyper)};
   sgd_multi(reinterpret_cast<const TensorChunk*>(tab.data_ptr()), count, h, cur_stream());
 }
 
@@ -261,14 +313,15 @@ void adam_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
                    const std::vector<Tensor>& ms, const std::vector<Tensor>& vs,
                    const std::vector<Tensor>& vmaxs, double lr, double b1, double b2, double eps,
                    double wd, bool amsgrad, bool maximize, bool decoupled, int64_t step,
-                   double grad_scale) {
+                   double grad_scale, const c10::optional<Tensor>& hyper) {
   if (ps.empty()) return;
   for (auto& t : ps) { CHECK_GPU(t); CHECK_F32(t); CHECK_CONTIG(t); }
   int count = 0;
   auto tab = chunk_table(ps, gs, ms, vs, amsgrad ? vmaxs : std::vector<Tensor>{}, &count);
   AdamHyper h{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, amsgrad, maximize,
               decoupled, (float)(1.0 - std::pow(b1, (double)step)),
-              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale};
+              (float)std::sqrt(1.0 - std::pow(b2, (double)step)), (float)grad_scale,
+              hyper_ptr(hyper)};
   adam_multi(reinterpret_cast<const TensorChunk*>(tab.data_ptr()), count, h, cur_stream());
 }
 
@@ -299,19 +352,6 @@ Tensor relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
 void scale_op(Tensor& x, double a) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
   scale_inplace(x.data_ptr<float>(), x.numel(), (float)a, cur_stream());
-}
-
-Tensor sumsq_op(const Tensor& x, const c10::optional<Tensor>& into) {
-  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
-  Tensor out = (into.has_value() && into->defined()) ? *into : at::zeros({1}, x.options());
-  sumsq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), true, cur_stream());
-  return out;
-}
-
-void clip_op(Tensor& x, const Tensor& total, double max_norm) {
-  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
-  clip_scale(x.data_ptr<float>(), x.numel(), total.data_ptr<float>(), (float)max_norm,
-             cur_stream());
 }
 
 void cast_f32_bf16_op(const Tensor& x, Tensor& y) {
@@ -730,17 +770,48 @@ std::shared_ptr<Communicator> make_comm(py::bytes uid, int rank, int world, int 
   return std::make_shared<Communicator>(v, rank, world, device);
 }
 
-// Python-callable reducer backend (torch.distributed / gloo for CPU runs and tests).
-struct PyBackend : ReducerBackend {
-  py::function launch_fn, wait_fn, zero_fn;
-  PyBackend(py::function l, py::function w, py::function z)
-      : launch_fn(std::move(l)), wait_fn(std::move(w)), zero_fn(std::move(z)) {}
-  void launch(int bucket, int64_t begin, int64_t end, hipStream_t) override {
-    launch_fn(bucket, begin, end);
+// SyncOps over Python callables: torch.distributed (gloo) collectives and torch math on CPU arenas
+// (parallel/ddp.py _cpu_sync_ops). The C++ SyncBackend algorithm -- bucket order, sharding, tails,
+// clipping, deferred updates -- runs unchanged on top, so the multi-rank logic is exercised by
+// the gloo tests at any world size.
+struct PyOps : SyncOps {
+  int rank_, world_;
+  py::object fns;  // object with one method per operation
+  PyOps(int rank, int world, py::object f) : rank_(rank), world_(world), fns(std::move(f)) {}
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  bool on_device() const override { return false; }
+  static py::list pylist(const Ranges& r) {
+    py::list l;
+    for (const auto& x : r) l.append(py::make_tuple(x.first, x.second));
+    return l;
   }
-  void wait_all(hipStream_t) override { wait_fn(); }
-  void zero(int64_t begin, int64_t end, hipStream_t) override { zero_fn(begin, end); }
+  void all_reduce_avg(int64_t off, int64_t n, hipStream_t) override {
+    fns.attr("all_reduce_avg")(off, n);
+  }
+  void reduce_scatter_avg(int64_t off, int64_t cnt, hipStream_t) override {
+    fns.attr("reduce_scatter_avg")(off, cnt);
+  }
+  void all_gather_params(int64_t off, int64_t cnt, hipStream_t) override {
+    fns.attr("all_gather_params")(off, cnt);
+  }
+  void zero_grads(int64_t off, int64_t n, hipStream_t) override { fns.attr("zero_grads")(off, n); }
+  void opt_begin(hipStream_t) override { fns.attr("opt_begin")(); }
+  void opt_update(const Ranges& r, hipStream_t) override { fns.attr("opt_update")(pylist(r)); }
+  void clip_begin(int b, hipStream_t) override { fns.attr("clip_begin")(b); }
+  void grad_sumsq(int b, const Ranges& r, hipStream_t) override {
+    fns.attr("grad_sumsq")(b, pylist(r));
+  }
+  void sumsq_all_reduce(int b, hipStream_t) override { fns.attr("sumsq_all_reduce")(b); }
+  void clip_coef(int b, hipStream_t) override { fns.attr("clip_coef")(b); }
+  void scale_grads(int b, const Ranges& r, hipStream_t) override {
+    fns.attr("scale_grads")(b, pylist(r));
+  }
 };
+
+float* block_ptr(const c10::optional<Tensor>& blk) {
+  return const_cast<float*>(hyper_ptr(blk));
+}
 
 }  // namespace
 
@@ -762,13 +833,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd_op);
   m.def("ce_bwd", &ce_bwd_op);
   m.def("count_correct", &count_correct_op);
-  m.def("sgd_flat", &sgd_flat_op);
-  m.def("adam_flat", &adam_flat_op);
-  m.def("sgd_multi", &sgd_multi_op);
-  m.def("adam_multi", &adam_multi_op);
+  m.def("sgd_flat", &sgd_flat_op, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"),
+        py::arg("maximize"), py::arg("first_step"), py::arg("grad_scale") = 1.0,
+        py::arg("hyper") = py::none());
+  m.def("opt_step_begin", &opt_step_begin_op, py::arg("hyper"), py::arg("kind"));
+  m.def("clip_grad_norm", &clip_grad_norm_op, py::arg("grads"), py::arg("hyper"),
+        py::arg("max_norm"));
+  m.def("hyper_slots", []() {
+    return py::dict(py::arg("lr") = (int)kHLr, py::arg("mom") = (int)kHMom,
+                    py::arg("damp") = (int)kHDamp, py::arg("wd") = (int)kHWd,
+                    py::arg("eps") = (int)kHEps, py::arg("bc1") = (int)kHBc1,
+                    py::arg("bc2") = (int)kHBc2, py::arg("first") = (int)kHFirst,
+                    py::arg("first_next") = (int)kHFirstNext, py::arg("scale") = (int)kHScale,
+                    py::arg("sumsq") = (int)kHSumsq, py::arg("max_norm") = (int)kHMaxNorm,
+                    py::arg("step") = (int)kHStep, py::arg("norm") = (int)kHNorm,
+                    py::arg("size") = (int)kHSlots);
+  });
+  m.def("gemm_f32_set_opt_variant", &gemm_f32_set_opt_variant, py::arg("sgd") = -1,
+        py::arg("adam") = -1, py::arg("persist") = -1, py::arg("wgs") = -1);
+  m.def("adam_flat", &adam_flat_op, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"),
+        py::arg("vmax"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("weight_decay"), py::arg("amsgrad"), py::arg("maximize"), py::arg("decoupled"),
+        py::arg("step"), py::arg("grad_scale") = 1.0, py::arg("hyper") = py::none());
+  m.def("sgd_multi", &sgd_multi_op, py::arg("ps"), py::arg("gs"), py::arg("bufs"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"),
+        py::arg("maximize"), py::arg("first_step"), py::arg("grad_scale") = 1.0,
+        py::arg("hyper") = py::none());
+  m.def("adam_multi", &adam_multi_op, py::arg("ps"), py::arg("gs"), py::arg("ms"), py::arg("vs"),
+        py::arg("vmaxs"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("weight_decay"), py::arg("amsgrad"), py::arg("maximize"), py::arg("decoupled"),
+        py::arg("step"), py::arg("grad_scale") = 1.0, py::arg("hyper") = py::none());
   m.def("scale_", &scale_op);
-  m.def("sumsq", &sumsq_op, py::arg("x"), py::arg("into") = py::none());
-  m.def("clip_", &clip_op);
   m.def("cast_f32_bf16", &cast_f32_bf16_op);
   m.def("conv2d_fwd", &conv2d_fwd_op);
   m.def("conv_nhwc_fwd", &conv_nhwc_fwd_op);
@@ -855,62 +951,83 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<ReducerBackend, std::shared_ptr<ReducerBackend>>(m, "ReducerBackend")
       .def("last_comm_ms", &ReducerBackend::last_comm_ms);
-  py::class_<RcclBackend, ReducerBackend, std::shared_ptr<RcclBackend>>(m, "RcclBackend")
-      .def(py::init([](std::shared_ptr<Communicator> comm, Tensor arena, int num_buckets,
-                       int compression, bool timing, bool skip_single_rank) {
-             CHECK_GPU(arena); CHECK_CONTIG(arena);
-             return std::make_shared<RcclBackend>(
-                 comm, arena.data_ptr(), arena.numel(), (int)arena.element_size(), num_buckets,
-                 static_cast<Compression>(compression), timing, skip_single_rank);
+  py::class_<SyncOps, std::shared_ptr<SyncOps>>(m, "SyncOps")
+      .def_property_readonly("rank", &SyncOps::rank)
+      .def_property_readonly("world", &SyncOps::world);
+  py::class_<RcclOps, SyncOps, std::shared_ptr<RcclOps>>(m, "RcclOps")
+      .def(py::init([](std::shared_ptr<Communicator> comm, Tensor grad, Tensor param,
+                       int compression) {
+             CHECK_GPU(grad); CHECK_CONTIG(grad); CHECK_F32(grad);
+             CHECK_GPU(param); CHECK_CONTIG(param); CHECK_F32(param);
+             TORCH_CHECK(grad.numel() == param.numel(), "grad/param arenas differ in size");
+             return std::make_shared<RcclOps>(comm, grad.data_ptr<float>(), param.data_ptr<float>(),
+                                              grad.numel(), static_cast<Compression>(compression));
            }),
-           py::arg("comm"), py::arg("arena"), py::arg("num_buckets"),
-           py::arg("compression") = 0, py::arg("timing") = false,
-           py::arg("skip_single_rank") = true)
-      // fused optimizer: kind 1 = SGD(p, momentum_buf), 2 = Adam(p, exp_avg, exp_avg_sq[, max])
+           py::arg("comm"), py::arg("grad"), py::arg("param"), py::arg("compression") = 0)
+      // fused optimizer over the arenas; scalars come from the device hyper block
       .def("set_fused_sgd",
-           [](RcclBackend& b, Tensor p, c10::optional<Tensor> buf, double lr, double momentum,
-              double dampening, double wd, bool nesterov, bool maximize, bool fresh) {
+           [](RcclOps& o, Tensor p, c10::optional<Tensor> buf, bool momentum, bool nesterov,
+              bool maximize, Tensor hyper) {
              CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
-             b.fused.kind = 1;
-             b.fused.p = p.data_ptr<float>();
-             b.fused.s0 = fptr(buf);
-             b.fused.sgd = SgdHyper{(float)lr, (float)momentum, (float)dampening, (float)wd,
-                                    nesterov, maximize, false, 1.f};
-             if (fresh) {
-               b.fused.fresh.assign(1 << 16, 1);
-               b.set_epilogue_fresh(true);
-             }
+             TORCH_CHECK(!momentum || (buf.has_value() && buf->numel() == p.numel()),
+                         "fused SGD: momentum buffer required");
+             o.fused.kind = 1;
+             o.fused.p = p.data_ptr<float>();
+             o.fused.s0 = momentum ? fptr(buf) : nullptr;
+             o.fused.s1 = o.fused.s2 = nullptr;
+             o.fused.hyper = block_ptr(hyper);
+             o.fused.sgd = SgdHyper{0.f, momentum ? 1.f : 0.f, 0.f, 0.f, nesterov, maximize, false,
+                                    1.f, o.fused.hyper};
            })
       .def("set_fused_adam",
-           [](RcclBackend& b, Tensor p, Tensor m, Tensor v, c10::optional<Tensor> vmax,
-              double lr, double b1, double b2, double eps, double wd, bool amsgrad,
-              bool maximize, bool decoupled, int64_t step) {
+           [](RcclOps& o, Tensor p, Tensor m, Tensor v, c10::optional<Tensor> vmax, bool amsgrad,
+              bool maximize, bool decoupled, Tensor hyper) {
              CHECK_GPU(p); CHECK_F32(p); CHECK_CONTIG(p);
-             b.fused.kind = 2;
-             b.fused.p = p.data_ptr<float>();
-             b.fused.s0 = m.data_ptr<float>();
-             b.fused.s1 = v.data_ptr<float>();
-             b.fused.s2 = fptr(vmax);
-             b.fused.adam = AdamHyper{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                                      amsgrad, maximize, decoupled, 1.f, 1.f, 1.f};
-             b.fused.adam_beta1 = (float)b1;
-             b.fused.adam_beta2 = (float)b2;
-             b.fused.adam_step = step;
+             TORCH_CHECK(m.numel() == p.numel() && v.numel() == p.numel(), "fused Adam: state size");
+             TORCH_CHECK(!amsgrad || (vmax.has_value() && vmax->numel() == p.numel()),
+                         "fused Adam: amsgrad needs max_exp_avg_sq");
+             o.fused.kind = 2;
+             o.fused.p = p.data_ptr<float>();
+             o.fused.s0 = m.data_ptr<float>();
+             o.fused.s1 = v.data_ptr<float>();
+             o.fused.s2 = amsgrad ? fptr(vmax) : nullptr;
+             o.fused.hyper = block_ptr(hyper);
+             o.fused.adam = AdamHyper{0.f, 0.f, 0.f, 0.f, 0.f, amsgrad, maximize, decoupled,
+                                      1.f, 1.f, 1.f, o.fused.hyper};
            })
-      .def("clear_fused", [](RcclBackend& b) { b.fused = FusedOptimizer{}; })
-      .def_property_readonly("epilogue_allowed", &RcclBackend::epilogue_allowed)
-      .def_property("fused_shard", [](RcclBackend& b) { return b.fused.shard; },
-                    [](RcclBackend& b, bool v) { b.fused.shard = v; })
-      .def_property_readonly("fused_adam_step",
-                             [](RcclBackend& b) { return b.fused.adam_step; });
-  py::class_<PyBackend, ReducerBackend, std::shared_ptr<PyBackend>>(m, "PyBackend")
-      .def(py::init<py::function, py::function, py::function>());
+      .def("clear_fused", [](RcclOps& o) { o.fused = FusedOptimizer{}; })
+      .def("set_clip_block", [](RcclOps& o, c10::optional<Tensor> blk) {
+        o.clip_block = block_ptr(blk);
+      });
+  py::class_<PyOps, SyncOps, std::shared_ptr<PyOps>>(m, "PyOps")
+      .def(py::init<int, int, py::object>(), py::arg("rank"), py::arg("world"), py::arg("fns"));
+  py::class_<SyncBackend, ReducerBackend, std::shared_ptr<SyncBackend>>(m, "SyncBackend")
+      .def(py::init<std::shared_ptr<SyncOps>, int64_t, int, bool, bool>(), py::arg("ops"),
+           py::arg("numel"), py::arg("num_buckets"), py::arg("timing") = false,
+           py::arg("skip_single_rank") = true)
+      .def_readwrite("fused_kind", &SyncBackend::fused_kind)
+      .def_readwrite("shard", &SyncBackend::shard)
+      .def_readwrite("compressed", &SyncBackend::compressed)
+      .def_property("clip", [](SyncBackend& b) { return (int)b.clip; },
+                    [](SyncBackend& b, int v) {
+                      TORCH_CHECK(v >= 0 && v <= 2, "clip mode 0 none | 1 global | 2 local");
+                      b.clip = static_cast<ClipMode>(v);
+                    })
+      .def_property_readonly("epilogue_allowed", &SyncBackend::epilogue_allowed)
+      .def_property_readonly("collective", &SyncBackend::collective)
+      .def("owned_shard", &SyncBackend::owned_shard)
+      .def("begin_iteration", [](SyncBackend& b, bool gpu) {
+        b.begin_iteration(gpu ? cur_stream() : nullptr);
+      });
 
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
                     std::shared_ptr<ReducerBackend>>())
       .def_static("compute_bucket_bounds", &Reducer::compute_bucket_bounds)
-      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("prepare_for_backward",
+           [](Reducer& r, bool gpu) { r.prepare_for_backward(gpu ? cur_stream() : nullptr); },
+           py::arg("gpu") = false)
+      .def_property_readonly("head_of_line_waits", &Reducer::head_of_line_waits)
       .def("mark_ready",
            [](Reducer& r, int p, bool gpu) { r.mark_ready(p, gpu ? cur_stream() : nullptr); })
       .def("finalize", [](Reducer& r, bool gpu,

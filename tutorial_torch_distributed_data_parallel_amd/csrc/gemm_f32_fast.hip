@@ -28,6 +28,7 @@
 //     taps that fall into the zero padding read a 16-B zero page. With C % 32 == 0 a K tile
 //     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 #include "conv.h"
@@ -496,7 +497,10 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     // should not evict the L2-resident dY / X operand tiles)
     constexpr bool SGD = (OPTK & 3) == 1;
     constexpr bool NT = (OPTK & kOptNT) != 0;
-    const OptEpilogue& o = p.opt;
+    // per-step scalars from the device hyper block (graph-replay safe, kernels.h HyperSlot)
+    OptEpilogue o = p.opt;
+    if constexpr (SGD) load_hyper(o.sgd);
+    else load_hyper(o.adam);
     const bool mom_rd = SGD && o.sgd.momentum != 0.f && !o.sgd.first_step;
     const bool mom_wr = SGD && o.sgd.momentum != 0.f;
     constexpr bool PAIR = !BKC && FN == 2;
@@ -846,6 +850,38 @@ bool gemm_f32_fast_ok(const GemmF32Args& a) {
 // LDS per workgroup must stay <= 80 KiB for two per CU: FN=1 (24 KiB/stage) allows 3 stages,
 // FN=2 (32 KiB/stage) 2 stages.
 static int o_fn = 0, o_splits = 0, o_stages = 0;
+
+// Optimizer-epilogue variant knobs: TDP_OPT_VARIANT / TDP_OPT_ADAM_VARIANT / TDP_OPT_PERSIST /
+// TDP_OPT_WGS at first use, overridable at run time (gemm_f32_set_opt_variant) so one test
+// process can cover every variant.
+struct OptVariant {
+  int sgd, adam, wgs;
+  bool persist;
+};
+static OptVariant& opt_variant() {
+  static OptVariant v = [] {
+    OptVariant o;
+    const char* e = std::getenv("TDP_OPT_VARIANT");
+    o.sgd = e ? (std::atoi(e) & (kOptWide | kOptNT | kOptLds)) : (kOptLds | kOptNT);
+    e = std::getenv("TDP_OPT_ADAM_VARIANT");
+    o.adam = e ? (std::atoi(e) & (kOptNT | kOptLds)) : (kOptLds | kOptNT);
+    e = std::getenv("TDP_OPT_PERSIST");
+    o.persist = !(e && e[0] == '0');
+    e = std::getenv("TDP_OPT_WGS");
+    o.wgs = e ? std::atoi(e) : 2;
+    return o;
+  }();
+  return v;
+}
+
+std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs) {
+  OptVariant& v = opt_variant();
+  if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds);
+  if (adam >= 0) v.adam = adam & (kOptNT | kOptLds);
+  if (persist >= 0) v.persist = persist != 0;
+  if (wgs > 0) v.wgs = wgs;
+  return {v.sgd, v.adam, v.persist ? 1 : 0, v.wgs};
+}
 void gemm_f32_set_override(int fn, int splits, int stages) {
   o_fn = fn; o_splits = splits; o_stages = stages;
 }
@@ -867,11 +903,9 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   plan.grid = 0;
   if (a.opt.kind != 0) {
-    const char* e = std::getenv("TDP_OPT_PERSIST");
     // persistent: 2 workgroups per CU (TDP_OPT_WGS overrides, for measurements: 3 fit with FN=1)
-    const char* w = std::getenv("TDP_OPT_WGS");
-    const int wgs = w ? std::atoi(w) : 2;
-    if (!(e && e[0] == '0')) plan.grid = (wgs >= 1 && wgs <= 4 ? wgs : 2) * num_cus;
+    const OptVariant& v = opt_variant();
+    if (v.persist) plan.grid = (v.wgs >= 1 && v.wgs <= 4 ? v.wgs : 2) * num_cus;
   }
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
@@ -911,16 +945,10 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
     // kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four 0.498), kOptLds alone 0.468,
     // kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure; profiles/opt_epilogue_variants.md).
     // Non-128-wide tiles ignore kOptLds.
-    static const int variant = [] {
-      const char* e = std::getenv("TDP_OPT_VARIANT");
-      return e ? (std::atoi(e) & (kOptWide | kOptNT | kOptLds)) : (kOptLds | kOptNT);
-    }();
+    const int variant = opt_variant().sgd;
     // TDP_OPT_ADAM_VARIANT: Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam
     // 0.555 ms/step vs 0.566 LDS only, 0.594 register epilogue (profiles/opt_epilogue_variants.md)
-    static const int adam_variant = [] {
-      const char* e = std::getenv("TDP_OPT_ADAM_VARIANT");
-      return e ? (std::atoi(e) & (kOptNT | kOptLds)) : (kOptLds | kOptNT);
-    }();
+    const int adam_variant = opt_variant().adam;
     if (a.opt.kind == 1) {
       switch (variant) {
         case kOptLds: launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds>(p, fn, st, nb, s); break;

@@ -7,15 +7,47 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tdp {
 
 // ------------------------------------------------------------------------------------------------
 // Optimizer hyper-parameters (fused single-pass updates, csrc/optim.hip + optim_elem.h)
 // ------------------------------------------------------------------------------------------------
+//
+// Device-resident hyper-parameter block ("hyper block": kHSlots floats in device memory, one per
+// optimizer parameter group). A kernel whose SgdHyper / AdamHyper has `dev != nullptr` takes the
+// per-step scalars from the block instead of its by-value fields, so a step captured into a
+// hipGraph replays with the CURRENT learning rate, Adam step count and bias corrections: the host
+// rewrites the block with a stream-ordered copy when a hyper-parameter changes, opt_step_begin()
+// advances the step counter / bias corrections / SGD first-step flag on the device, and the
+// gradient-clipping kernels leave their coefficient in kHScale. The structural flags (nesterov,
+// maximize, amsgrad, decoupled, momentum == 0) stay by-value: changing them needs a re-capture.
+enum HyperSlot : int {
+  kHLr = 0,
+  kHMom = 1,        // SGD momentum | Adam beta1
+  kHDamp = 2,       // SGD dampening | Adam beta2
+  kHWd = 3,         // weight decay
+  kHEps = 4,        // Adam eps
+  kHBc1 = 5,        // Adam 1 - beta1^t          (written by opt_step_begin)
+  kHBc2 = 6,        // Adam sqrt(1 - beta2^t)    (written by opt_step_begin)
+  kHFirst = 7,      // SGD: momentum buffers are initialised by this step (1/0)
+  kHFirstNext = 8,  // host request: the next step initialises the momentum buffers
+  kHScale = 9,      // gradient multiplier of this step (clip coefficient; 1 = none)
+  kHSumsq = 10,     // squared-gradient-norm accumulator of this step
+  kHMaxNorm = 11,   // clip threshold (<= 0: no clipping)
+  kHStep = 12,      // int32: optimizer step count t (advanced by opt_step_begin)
+  kHNorm = 13,      // total gradient norm of the last clipped step (for the caller)
+  kHPartials = 16,  // workspace: per-workgroup partial sums of the deterministic norm reduction
+  kHPartialsMax = 1024,
+  kHSlots = kHPartials + kHPartialsMax
+};
+
 struct SgdHyper {
   float lr, momentum, dampening, weight_decay;
   bool nesterov, maximize, first_step;
   float grad_scale;  // grads are multiplied by this first (1/world for sum-reduced grads)
+  const float* dev = nullptr;  // hyper block (kHLr.. kHScale override the fields above)
 };
 
 struct AdamHyper {
@@ -23,7 +55,20 @@ struct AdamHyper {
   bool amsgrad, maximize, decoupled;  // decoupled = AdamW
   float bc1, bc2_sqrt;                // 1-beta1^t, sqrt(1-beta2^t)
   float grad_scale;
+  const float* dev = nullptr;  // hyper block (see HyperSlot)
 };
+
+// Advance a hyper block by one optimizer step (one thread): step += 1, Adam bias corrections for
+// the new step (kind 2), first-step flag from the host request, clip accumulators reset.
+void opt_step_begin(float* dev, int kind, hipStream_t s);
+// Global-norm clipping on the device: kHNorm = sqrt(kHSumsq) and
+// kHScale = min(1, kHMaxNorm / (kHNorm + 1e-6)) (torch.nn.utils.clip_grad_norm_ semantics).
+void clip_coef_from_sumsq(float* dev, hipStream_t s);
+// kHSumsq += sum of squares of x[begin[i] : begin[i] + len[i]) for every range (one launch)
+struct RangeSet;
+void sumsq_ranges(const float* x, const RangeSet& r, float* dev, hipStream_t s);
+// x[ranges] *= dev[kHScale] (per-rank clip before aggregation)
+void scale_ranges_by(float* x, const RangeSet& r, const float* dev, hipStream_t s);
 
 // Optimizer update applied by a GEMM epilogue in place of storing the result: when C is a weight
 // gradient, the epilogue reads p / state at C's element index (same layout and leading dimension
@@ -89,6 +134,9 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
 void gemm_f32_set_mode(int mode);
 // benchmarking knob: force the fast kernel's tile width / split-K / stages (0 = planner's choice)
 void gemm_f32_set_override(int fn, int splits, int stages);
+// optimizer-epilogue variant (SGD flags, Adam flags, persistent grid on/off, workgroups per CU);
+// negative = keep. Returns the active {sgd, adam, persist, wgs}.
+std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs);
 
 // bf16-operand GEMM (AMP path): same contract, A/B bf16 (uint16 storage), C fp32 or bf16.
 struct GemmBF16Args {
@@ -177,10 +225,6 @@ void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, 
                   float* xb, int64_t* yb, hipStream_t s);
 void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
 void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);
-// sum of squares of x into out[0] (+= when accumulate), for grad-norm clipping
-void sumsq(const float* x, long n, float* out, bool accumulate, hipStream_t s);
-// x *= min(1, max_norm / (sqrt(total[0]) + eps))
-void clip_scale(float* x, long n, const float* total_sumsq, float max_norm, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------------
 // Batch norm (BatchNorm1d/2d and SyncBatchNorm). x is viewed as [N][C][HW] (HW = 1 for 1d).

@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p,
                                                        const float* __restrict__ g,
                                                        float* __restrict__ buf, long n,
                                                        SgdHyper h) {
+  load_hyper(h);
   const long n4 = VEC ? n / 4 : 0;
   const long stride = (long)gridDim.x * blockDim.x;
   const bool mom = h.momentum != 0.f;
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p,
                                                         float* __restrict__ v,
                                                         float* __restrict__ vmax, long n,
                                                         AdamHyper h) {
+  load_hyper(h);
   const long n4 = VEC ? n / 4 : 0;
   const long stride = (long)gridDim.x * blockDim.x;
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -143,6 +145,7 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ p,
 // One workgroup per chunk-table entry (chunks are <= 64K elements, built on the host).
 __global__ __launch_bounds__(256) void sgd_multi_kernel(const TensorChunk* __restrict__ table,
                                                         SgdHyper h) {
+  load_hyper(h);
   const TensorChunk c = table[blockIdx.x];
   const bool mom = h.momentum != 0.f;
   for (long i = threadIdx.x; i < c.n; i += blockDim.x) {
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(const TensorChunk* __res
 
 __global__ __launch_bounds__(256) void adam_multi_kernel(const TensorChunk* __restrict__ table,
                                                          AdamHyper h) {
+  load_hyper(h);
   const TensorChunk c = table[blockIdx.x];
   for (long i = threadIdx.x; i < c.n; i += blockDim.x) {
     float pe = c.p[i], me = c.s0[i], ve = c.s1[i];
@@ -189,24 +193,74 @@ __global__ void bf2f_kernel(const unsigned short* __restrict__ x, float* __restr
     y[i] = bf16_to_f32(x[i]);
 }
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n,
-                                                    float* out) {
-  __shared__ float red[4];
-  float s = 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x)
-    s = fmaf(x[i], x[i], s);
-  s = block_sum<256>(s, red);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+// ---------------------------------------------------------------- device hyper block (kernels.h)
+__global__ void opt_step_begin_kernel(float* d, int kind) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int* di = reinterpret_cast<int*>(d);
+  const int t = di[kHStep] + 1;
+  di[kHStep] = t;
+  d[kHFirst] = d[kHFirstNext];
+  d[kHFirstNext] = 0.f;
+  d[kHScale] = 1.f;
+  d[kHSumsq] = 0.f;
+  if (kind == 2) {
+    // double precision like torch's host-side bias corrections (TORCH/optim/adam.py)
+    d[kHBc1] = (float)(1.0 - pow((double)d[kHMom], (double)t));
+    d[kHBc2] = (float)sqrt(1.0 - pow((double)d[kHDamp], (double)t));
+  }
 }
 
-__global__ void clip_kernel(float* x, long n, const float* total, float max_norm) {
-  const float norm = sqrtf(total[0]);
-  const float coef = max_norm / (norm + 1e-6f);
-  if (coef >= 1.f) return;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x)
-    x[i] *= coef;
+__global__ void clip_coef_kernel(float* d) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const float norm = sqrtf(d[kHSumsq]);
+  d[kHNorm] = norm;
+  const float mx = d[kHMaxNorm];
+  // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6), clamped to 1
+  d[kHScale] = mx > 0.f ? fminf(1.f, mx / (norm + 1e-6f)) : 1.f;
+}
+
+// Deterministic two-pass sum of squares over a RangeSet: every workgroup of a FIXED grid writes
+// its partial to d[kHPartials + blockIdx.x]; the finish kernel adds them in index order. The
+// result is therefore bit-identical on every rank that holds the same values (the clip
+// coefficient must agree across replicas).
+__device__ __forceinline__ long range_index_d(const RangeSet& r, long e);
+
+__global__ __launch_bounds__(256) void sumsq_ranges_kernel(const float* __restrict__ x,
+                                                           RangeSet r, long total, float* d) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const float v = x[range_index_d(r, e)];
+    s = fmaf(v, v, s);
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) d[kHPartials + blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sumsq_finish_kernel(float* d, int parts) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < parts; i += 256) s += d[kHPartials + i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) d[kHSumsq] += s;
+}
+
+__global__ __launch_bounds__(256) void scale_ranges_kernel(float* __restrict__ x, RangeSet r,
+                                                           long total, const float* d) {
+  const float a = d[kHScale];
+  if (a == 1.f) return;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x)
+    x[range_index_d(r, e)] *= a;
+}
+
+__device__ __forceinline__ long range_index_d(const RangeSet& r, long e) {
+  for (int i = 0; i < r.n; ++i) {
+    if (e < r.len[i]) return r.begin[i] + e;
+    e -= r.len[i];
+  }
+  return -1;
 }
 
 inline int grid_for(long work, int cap = 2048) {
@@ -246,6 +300,7 @@ __global__ __launch_bounds__(256) void sgd_ranges_kernel(float* __restrict__ p,
                                                          const float* __restrict__ g,
                                                          float* __restrict__ buf, RangeSet r,
                                                          long total, SgdHyper h) {
+  load_hyper(h);
   const bool mom = h.momentum != 0.f;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
        e += (long)gridDim.x * blockDim.x) {
@@ -263,6 +318,7 @@ __global__ __launch_bounds__(256) void adam_ranges_kernel(float* __restrict__ p,
                                                           float* __restrict__ v,
                                                           float* __restrict__ vmax, RangeSet r,
                                                           long total, AdamHyper h) {
+  load_hyper(h);
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
        e += (long)gridDim.x * blockDim.x) {
     const long i = range_index(r, e);
@@ -337,15 +393,29 @@ void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s) {
                        y, n);
 }
 
-void sumsq(const float* x, long n, float* out, bool accumulate, hipStream_t s) {
-  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float), s);
-  if (n > 0) hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 1024)), dim3(256), 0, s, x, n, out);
+void opt_step_begin(float* dev, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(opt_step_begin_kernel, dim3(1), dim3(64), 0, s, dev, kind);
 }
 
-void clip_scale(float* x, long n, const float* total_sumsq, float max_norm, hipStream_t s) {
-  if (n > 0)
-    hipLaunchKernelGGL(clip_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, total_sumsq,
-                       max_norm);
+void clip_coef_from_sumsq(float* dev, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, dev);
+}
+
+void sumsq_ranges(const float* x, const RangeSet& r, float* dev, hipStream_t s) {
+  long total = 0;
+  for (int i = 0; i < r.n; ++i) total += r.len[i];
+  if (total <= 0) return;
+  const int parts = grid_for(total, kHPartialsMax);
+  hipLaunchKernelGGL(sumsq_ranges_kernel, dim3(parts), dim3(256), 0, s, x, r, total, dev);
+  hipLaunchKernelGGL(sumsq_finish_kernel, dim3(1), dim3(256), 0, s, dev, parts);
+}
+
+void scale_ranges_by(float* x, const RangeSet& r, const float* dev, hipStream_t s) {
+  long total = 0;
+  for (int i = 0; i < r.n; ++i) total += r.len[i];
+  if (total > 0)
+    hipLaunchKernelGGL(scale_ranges_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, r, total,
+                       dev);
 }
 
 }  // namespace tdp

@@ -10,6 +10,32 @@
 
 namespace tdp {
 
+// Take the per-step scalars from the device hyper block when there is one (kernels.h HyperSlot).
+// Uniform loads at kernel start; the structural flags stay as launched.
+__device__ __forceinline__ void load_hyper(SgdHyper& h) {
+  const float* d = h.dev;
+  if (d == nullptr) return;
+  h.lr = d[kHLr];
+  if (h.momentum != 0.f) h.momentum = d[kHMom];  // zero momentum is structural (no buffer)
+  h.dampening = d[kHDamp];
+  h.weight_decay = d[kHWd];
+  h.first_step = d[kHFirst] != 0.f;
+  h.grad_scale *= d[kHScale];
+}
+
+__device__ __forceinline__ void load_hyper(AdamHyper& h) {
+  const float* d = h.dev;
+  if (d == nullptr) return;
+  h.lr = d[kHLr];
+  h.beta1 = d[kHMom];
+  h.beta2 = d[kHDamp];
+  h.weight_decay = d[kHWd];
+  h.eps = d[kHEps];
+  h.bc1 = d[kHBc1];
+  h.bc2_sqrt = d[kHBc2];
+  h.grad_scale *= d[kHScale];
+}
+
 __device__ __forceinline__ void sgd_elem(float& p, float g, float& b, const SgdHyper& h) {
   g *= h.grad_scale;
   if (h.maximize) g = -g;

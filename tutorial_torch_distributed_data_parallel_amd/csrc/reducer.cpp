@@ -1,39 +1,146 @@
 #include "reducer.h"
 
 #include <algorithm>
-#include <cstdlib>
-#include <string>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "kernels.h"
 
 namespace tdp {
 
 // ------------------------------------------------------------------------------------------------
-// RcclBackend
+// RcclOps: the MI355X side effects
 // ------------------------------------------------------------------------------------------------
-RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_t numel,
-                         int elem_size, int num_buckets, Compression compression, bool timing,
-                         bool skip_single_rank)
-    : comm_(std::move(comm)),
-      arena_(static_cast<char*>(arena)),
-      numel_(numel),
-      elem_size_(elem_size),
-      compression_(compression),
-      timing_(timing),
-      skip_single_rank_(skip_single_rank) {
-  if (compression_ == Compression::BF16 && elem_size_ != 4)
-    throw std::runtime_error("bf16 gradient compression needs an fp32 arena");
-  ready_.resize(num_buckets);
-  for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
-  check_hip(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
-  if (timing_) {
-    check_hip(hipEventCreate(&t0_), "event");
-    check_hip(hipEventCreate(&t1_), "event");
-  }
+RcclOps::RcclOps(std::shared_ptr<Communicator> comm, float* grad, float* param, int64_t numel,
+                 Compression compression)
+    : comm_(std::move(comm)), grad_(grad), param_(param), numel_(numel),
+      compression_(compression) {
   if (compression_ == Compression::BF16)
     check_hip(hipMalloc(&wire_, sizeof(uint16_t) * (size_t)numel_), "hipMalloc(wire)");
+}
+
+RcclOps::~RcclOps() {
+  if (wire_) (void)hipFree(wire_);
+}
+
+void RcclOps::all_reduce_avg(int64_t off, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  float* g = grad_ + off;
+  if (compression_ == Compression::BF16) {
+    uint16_t* w = wire_ + off;
+    f32_to_bf16_copy(g, w, n, s);
+    comm_->all_reduce(w, w, (size_t)n, ncclBfloat16, ncclAvg, s);
+    bf16_to_f32_copy(w, g, n, s);
+  } else {
+    comm_->all_reduce(g, g, (size_t)n, ncclFloat32, ncclAvg, s);
+  }
+}
+
+void RcclOps::reduce_scatter_avg(int64_t off, int64_t cnt, hipStream_t s) {
+  if (cnt <= 0) return;
+  float* g = grad_ + off;
+  // in place: RCCL's recvbuff == sendbuff + rank * recvcount
+  comm_->reduce_scatter(g, g + (int64_t)comm_->rank() * cnt, (size_t)cnt, ncclFloat32, ncclAvg, s);
+}
+
+void RcclOps::all_gather_params(int64_t off, int64_t cnt, hipStream_t s) {
+  if (cnt <= 0) return;
+  float* p = param_ + off;
+  comm_->all_gather(p + (int64_t)comm_->rank() * cnt, p, (size_t)cnt, ncclFloat32, s);
+}
+
+void RcclOps::zero_grads(int64_t off, int64_t n, hipStream_t s) {
+  if (n > 0)
+    check_hip(hipMemsetAsync(grad_ + off, 0, (size_t)n * sizeof(float), s), "hipMemsetAsync");
+}
+
+void RcclOps::opt_begin(hipStream_t s) {
+  if (fused.kind != 0 && fused.hyper) opt_step_begin(fused.hyper, fused.kind, s);
+}
+
+// Ranges of at least kFlat elements get the vectorised flat kernel (several float4 per stream in
+// flight); the small rest (biases, shard tails) goes out in multi-range launches.
+static constexpr int64_t kFlat = 1 << 16;
+
+template <class F>
+static void for_range_sets(const Ranges& r, F&& f) {
+  RangeSet rs;
+  for (const auto& x : r) {
+    if (x.second <= x.first) continue;
+    rs.begin[rs.n] = x.first;
+    rs.len[rs.n] = x.second - x.first;
+    if (++rs.n == kMaxRanges) {
+      f(rs);
+      rs.n = 0;
+    }
+  }
+  if (rs.n > 0) f(rs);
+}
+
+void RcclOps::opt_update(const Ranges& r, hipStream_t s) {
+  if (fused.kind == 0) return;
+  Ranges small;
+  for (const auto& x : r) {
+    const int64_t n = x.second - x.first, o = x.first;
+    if (n <= 0) continue;
+    if (n < kFlat) {
+      small.push_back(x);
+      continue;
+    }
+    if (fused.kind == 1)
+      sgd_flat(fused.p + o, grad_ + o, fused.s0 ? fused.s0 + o : nullptr, n, fused.sgd, s);
+    else
+      adam_flat(fused.p + o, grad_ + o, fused.s0 + o, fused.s1 + o,
+                fused.s2 ? fused.s2 + o : nullptr, n, fused.adam, s);
+  }
+  for_range_sets(small, [&](const RangeSet& rs) {
+    if (fused.kind == 1) sgd_ranges(fused.p, grad_, fused.s0, rs, fused.sgd, s);
+    else adam_ranges(fused.p, grad_, fused.s0, fused.s1, fused.s2, rs, fused.adam, s);
+  });
+}
+
+void RcclOps::clip_begin(int b, hipStream_t s) {
+  if (b == 1 && clip_block) opt_step_begin(clip_block, 0, s);
+}
+
+void RcclOps::grad_sumsq(int b, const Ranges& r, hipStream_t s) {
+  float* blk = block(b);
+  if (!blk) throw std::runtime_error("gradient clipping without a hyper block");
+  for_range_sets(r, [&](const RangeSet& rs) { sumsq_ranges(grad_, rs, blk, s); });
+}
+
+void RcclOps::sumsq_all_reduce(int b, hipStream_t s) {
+  float* blk = block(b);
+  if (comm_->world() > 1)
+    comm_->all_reduce(blk + kHSumsq, blk + kHSumsq, 1, ncclFloat32, ncclSum, s);
+}
+
+void RcclOps::clip_coef(int b, hipStream_t s) { clip_coef_from_sumsq(block(b), s); }
+
+void RcclOps::scale_grads(int b, const Ranges& r, hipStream_t s) {
+  const float* blk = block(b);
+  for_range_sets(r, [&](const RangeSet& rs) { scale_ranges_by(grad_, rs, blk, s); });
+}
+
+// ------------------------------------------------------------------------------------------------
+// SyncBackend: the bucket algorithm
+// ------------------------------------------------------------------------------------------------
+SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_buckets,
+                         bool timing, bool skip_single_rank)
+    : ops_(std::move(ops)), numel_(numel), timing_(timing), skip_single_rank_(skip_single_rank) {
+  if (ops_->on_device()) {
+    ready_.resize(num_buckets);
+    for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    check_hip(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
+    if (timing_) {
+      check_hip(hipEventCreate(&t0_), "event");
+      check_hip(hipEventCreate(&t1_), "event");
+    }
+  } else {
+    timing_ = false;
+  }
   const char* mode = std::getenv("TDP_COMM_STREAM");
   const std::string m = mode ? mode : "auto";
   stream_mode_ = m == "side" ? kStreamSide
@@ -44,50 +151,51 @@ RcclBackend::RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_
                                    : kStreamAuto;
 }
 
-RcclBackend::~RcclBackend() {
+SyncBackend::~SyncBackend() {
   for (auto& e : ready_) (void)hipEventDestroy(e);
   if (done_) (void)hipEventDestroy(done_);
   if (t0_) (void)hipEventDestroy(t0_);
   if (t1_) (void)hipEventDestroy(t1_);
-  if (wire_) (void)hipFree(wire_);
 }
 
-static ncclDataType_t nccl_dtype(int elem_size) {
-  switch (elem_size) {
-    case 4: return ncclFloat32;
-    case 2: return ncclBfloat16;
-    case 8: return ncclFloat64;
-    default: throw std::runtime_error("unsupported arena element size");
-  }
+bool SyncBackend::epilogue_allowed() const {
+  return fused_kind != 0 && ops_->world() == 1 && skip_single_rank_ && !compressed &&
+         clip == ClipMode::NONE && ops_->on_device();
 }
 
-void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
-  const bool collective = !(skip_single_rank_ && comm_->world() == 1);
-  if (!collective) {
-    // one rank: the average over ranks is the local gradient -- no collective, no stream hop.
-    // With a fused optimizer the remaining (non-epilogue) updates of every bucket are applied
-    // by one launch when backward ends (flush_deferred).
-    if (fused.kind != 0 && end > begin) {
-      if (fused.kind == 1 && !fused.fresh.empty()) {
-        deferred_first_ = deferred_first_ || (bool)fused.fresh[bucket];
-        fused.fresh[bucket] = 0;
-      }
-      if (fused.kind == 2 && bucket == 0 && !bucket0_launched_) {
-        ++fused.adam_step;
-        bucket0_launched_ = true;
-      }
-      deferred_.push_back({begin, end});
-      launched_any_ = true;
-    }
-    if (post_bucket) post_bucket(bucket, begin, end, compute);
-    return;
-  }
-  // Stream choice (measured on MI355X, profiles/bench/mode*.json): in EAGER execution a side
-  // stream costs 1.5-3x step time -- a hipStreamWaitEvent barrier left pending on one hardware
-  // queue while the host runs ahead slows every kernel dispatched on the other queue (ResNet-50:
-  // 95 ms vs 65 ms). Inside a hipGraph the same dependency is free and the all-reduce overlaps
-  // backward. So: side stream while capturing, the compute stream itself otherwise
-  // (TDP_COMM_STREAM=side|compute|hostsync overrides for measurements).
+void SyncBackend::note_epilogue(int64_t off, int64_t n) {
+  if (!epilogue_allowed()) throw std::runtime_error("optimizer epilogue needs world size 1");
+  if (off < 0 || n <= 0 || off + n > numel_) throw std::runtime_error("epilogue range");
+  const Range r{off, off + n};
+  for (const auto& e : epi_done_)
+    if (e.first < r.second && r.first < e.second)
+      throw std::runtime_error("optimizer epilogue: a parameter range was updated twice");
+  epi_done_.insert(std::lower_bound(epi_done_.begin(), epi_done_.end(), r), r);
+}
+
+Range SyncBackend::owned_shard(int64_t begin, int64_t end) const {
+  const int W = ops_->world(), r = ops_->rank();
+  // shards are multiples of 64 elements so every rank's slice stays 256-B aligned for the
+  // vectorised update kernels; the remainder (< 64 W elements) is all-reduced and replicated
+  const int64_t cnt = (end - begin) / W / 64 * 64;
+  return {begin + (int64_t)r * cnt, begin + (int64_t)(r + 1) * cnt};
+}
+
+void SyncBackend::begin_iteration(hipStream_t compute) {
+  epi_done_.clear();
+  pending_.clear();
+  deferred_.clear();
+  if (fused_kind != 0) ops_->opt_begin(compute);
+  if (clip == ClipMode::LOCAL) ops_->clip_begin(1, compute);
+}
+
+hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute) {
+  if (!ops_->on_device()) return nullptr;
+  // Stream choice (measured on MI355X, profiles/side_stream_eager.md): in EAGER execution a
+  // side stream costs 1.5-3x step time -- a hipStreamWaitEvent left pending on one hardware
+  // queue while the host runs ahead slows every launch on the other queue. Inside a hipGraph the
+  // same dependency is a graph edge and the collectives overlap backward. So: side stream while
+  // capturing, the compute stream itself otherwise (TDP_COMM_STREAM overrides for measurements).
   bool side = true;
   if (stream_mode_ == kStreamAuto) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -97,7 +205,7 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
     side = stream_mode_ != kStreamCompute;
   }
   if (!side && launched_side_) side = true;  // never switch streams within one iteration
-  hipStream_t cs = side ? comm_->comm_stream() : compute;
+  hipStream_t cs = side ? ops_->comm_stream() : compute;
   if (side) {
     launched_side_ = true;
     check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
@@ -108,195 +216,180 @@ void RcclBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   }
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
+  return cs;
+}
+
+static bool is_sharded(const SyncBackend& b, int W) {
+  return b.fused_kind != 0 && b.shard && W > 1 && !b.compressed;
+}
+
+void SyncBackend::reduce_bucket(int64_t begin, int64_t end, hipStream_t cs) {
   const int64_t n = end - begin;
-  const int W = comm_->world();
-  bool first = false;
-  if (n > 0 && fused.kind == 1 && !fused.fresh.empty()) {
-    first = (bool)fused.fresh[bucket];
-    fused.fresh[bucket] = 0;
-  }
-  if (n > 0 && fused.kind == 2 && bucket == 0 && !bucket0_launched_) {
-    ++fused.adam_step;
-    bucket0_launched_ = true;
-  }
-  float* g = reinterpret_cast<float*>(arena_) + begin;
-  if (n > 0 && collective && fused.kind != 0 && fused.shard && W > 1 &&
-      compression_ == Compression::NONE && elem_size_ == 4) {
+  if (n <= 0) return;
+  if (is_sharded(*this, ops_->world())) {
     // Sharded update (ZeRO-1 inside DDP): reduce-scatter the averaged gradient so this rank owns
     // 1/W of the bucket, update only that shard, all-gather the updated parameters. Same bytes
     // on the wire as the all-reduce, 1/W of the optimizer's HBM traffic; the parameters end up
-    // identical on every rank, exactly as after all-reduce + replicated update. The < W-element
-    // tail that does not divide evenly is all-reduced and updated everywhere.
-    const int r = comm_->rank();
-    const int64_t cnt = n / W, body = cnt * W, tail = n - body;
-    if (cnt > 0) {
-      comm_->reduce_scatter(g, g + (int64_t)r * cnt, (size_t)cnt, ncclFloat32, ncclAvg, cs);
-      apply_fused(begin + (int64_t)r * cnt, cnt, first, cs);
-      comm_->all_gather(fused.p + begin + (int64_t)r * cnt, fused.p + begin, (size_t)cnt,
-                        ncclFloat32, cs);
-    }
-    if (tail > 0) {
-      comm_->all_reduce(g + body, g + body, (size_t)tail, ncclFloat32, ncclAvg, cs);
-      apply_fused(begin + body, tail, first, cs);
-    }
+    // identical on every rank, exactly as after all-reduce + replicated update.
+    const Range own = owned_shard(begin, end);
+    const int64_t cnt = own.second - own.first;
+    const int64_t body = cnt * ops_->world();
+    if (cnt > 0) ops_->reduce_scatter_avg(begin, cnt, cs);
+    if (n > body) ops_->all_reduce_avg(begin + body, n - body, cs);
   } else {
-    if (n > 0 && collective) {
-      char* ptr = arena_ + begin * elem_size_;
-      if (compression_ == Compression::BF16) {
-        uint16_t* w = wire_ + begin;
-        f32_to_bf16_copy(reinterpret_cast<float*>(ptr), w, n, cs);
-        comm_->all_reduce(w, w, (size_t)n, ncclBfloat16, ncclAvg, cs);
-        bf16_to_f32_copy(w, reinterpret_cast<float*>(ptr), n, cs);
-      } else {
-        comm_->all_reduce(ptr, ptr, (size_t)n, nccl_dtype(elem_size_), ncclAvg, cs);
-      }
-    }
-    if (n > 0) apply_fused(begin, n, first, cs);
-  }
-  if (post_bucket) post_bucket(bucket, begin, end, cs);
-}
-
-// optimizer update of arena elements [off, off + cnt) minus the ranges a GEMM epilogue already
-// updated this iteration (no-op without a fused optimizer)
-void RcclBackend::apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs) {
-  if (cnt <= 0 || fused.kind == 0) return;
-  int64_t cur = off;
-  const int64_t end = off + cnt;
-  for (const auto& r : epi_done_) {  // sorted, disjoint
-    if (r.second <= cur || r.first >= end) continue;
-    if (r.first > cur) apply_fused_range(cur, r.first - cur, first, cs);
-    cur = std::max(cur, r.second);
-  }
-  if (cur < end) apply_fused_range(cur, end - cur, first, cs);
-}
-
-bool RcclBackend::epilogue_allowed() const {
-  return fused.kind != 0 && comm_->world() == 1 && skip_single_rank_ &&
-         compression_ == Compression::NONE && elem_size_ == 4;
-}
-
-OptEpilogue RcclBackend::epilogue_opt(int64_t off, int64_t n) {
-  if (!epilogue_allowed()) throw std::runtime_error("optimizer epilogue needs world size 1");
-  if (off < 0 || n <= 0 || off + n > numel_) throw std::runtime_error("epilogue range");
-  OptEpilogue o;
-  o.kind = fused.kind;
-  o.p = fused.p + off;
-  o.s0 = fused.s0 ? fused.s0 + off : nullptr;
-  o.s1 = fused.s1 ? fused.s1 + off : nullptr;
-  o.s2 = fused.s2 ? fused.s2 + off : nullptr;
-  if (fused.kind == 1) {
-    o.sgd = fused.sgd;
-    o.sgd.first_step = epi_fresh_;
-  } else {
-    // the step counter advances with this iteration's first bucket; an epilogue can run before it
-    const double t = (double)(fused.adam_step + (bucket0_launched_ ? 0 : 1));
-    o.adam = fused.adam;
-    o.adam.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
-    o.adam.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
-  }
-  auto it = std::lower_bound(epi_done_.begin(), epi_done_.end(), std::make_pair(off, off + n));
-  epi_done_.insert(it, {off, off + n});
-  return o;
-}
-
-void RcclBackend::apply_fused_range(int64_t off, int64_t cnt, bool first, hipStream_t cs) {
-  if (cnt <= 0) return;
-  float* g = reinterpret_cast<float*>(arena_) + off;
-  if (fused.kind == 1) {
-    SgdHyper h = fused.sgd;
-    h.first_step = first;
-    sgd_flat(fused.p + off, g, fused.s0 ? fused.s0 + off : nullptr, cnt, h, cs);
-  } else if (fused.kind == 2) {
-    AdamHyper h = fused.adam;
-    const double t = (double)(fused.adam_step > 0 ? fused.adam_step : 1);
-    h.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
-    h.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
-    adam_flat(fused.p + off, g, fused.s0 + off, fused.s1 + off,
-              fused.s2 ? fused.s2 + off : nullptr, cnt, h, cs);
+    ops_->all_reduce_avg(begin, n, cs);
   }
 }
 
-// Apply the deferred world-size-1 bucket updates minus the epilogue-updated ranges, in launches
-// of up to kMaxRanges ranges (one launch for the models here: biases + small weights).
-void RcclBackend::flush_deferred(hipStream_t compute) {
-  if (deferred_.empty()) return;
-  std::sort(deferred_.begin(), deferred_.end());
-  std::vector<std::pair<int64_t, int64_t>> todo;
-  for (const auto& d : deferred_) {
+Ranges SyncBackend::minus_epilogue(const Ranges& in) const {
+  Ranges out;
+  for (const auto& d : in) {
     int64_t cur = d.first;
-    for (const auto& r : epi_done_) {
+    for (const auto& r : epi_done_) {  // sorted, disjoint
       if (r.second <= cur || r.first >= d.second) continue;
-      if (r.first > cur) todo.push_back({cur, r.first});
+      if (r.first > cur) out.push_back({cur, r.first});
       cur = std::max(cur, r.second);
     }
-    if (cur < d.second) todo.push_back({cur, d.second});
+    if (cur < d.second) out.push_back({cur, d.second});
   }
-  // merge touching ranges
-  std::vector<std::pair<int64_t, int64_t>> merged;
-  for (const auto& t : todo) {
-    if (!merged.empty() && merged.back().second == t.first) merged.back().second = t.second;
-    else merged.push_back(t);
+  return out;
+}
+
+Ranges SyncBackend::update_ranges(int64_t begin, int64_t end) const {
+  if (!is_sharded(*this, ops_->world())) return minus_epilogue({{begin, end}});
+  const Range own = owned_shard(begin, end);
+  const int64_t body = (own.second - own.first) * ops_->world();
+  Ranges r;
+  if (own.second > own.first) r.push_back(own);
+  if (begin + body < end) r.push_back({begin + body, end});
+  return minus_epilogue(r);
+}
+
+void SyncBackend::finish_bucket(int64_t begin, int64_t end, hipStream_t cs) {
+  if (fused_kind == 0 || end <= begin) return;
+  ops_->opt_update(update_ranges(begin, end), cs);
+  if (is_sharded(*this, ops_->world())) {
+    const Range own = owned_shard(begin, end);
+    const int64_t cnt = own.second - own.first;
+    if (cnt > 0) ops_->all_gather_params(begin, cnt, cs);
   }
-  const bool first = deferred_first_;
-  deferred_.clear();
-  deferred_first_ = false;
-  float* g = reinterpret_cast<float*>(arena_);
-  for (size_t i0 = 0; i0 < merged.size(); i0 += kMaxRanges) {
-    RangeSet rs;
-    for (size_t i = i0; i < merged.size() && rs.n < kMaxRanges; ++i) {
-      rs.begin[rs.n] = merged[i].first;
-      rs.len[rs.n] = merged[i].second - merged[i].first;
-      ++rs.n;
+}
+
+void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
+  if (end <= begin) return;
+  if (clip == ClipMode::LOCAL) {
+    // the local norm needs the whole local gradient: nothing goes on the wire before backward ends
+    pending_.push_back({begin, end});
+    launched_any_ = true;
+    return;
+  }
+  if (!collective()) {
+    // one rank: the average over ranks is the local gradient -- no collective, no stream hop;
+    // the bucket updates the GEMM epilogues did not do are applied by one launch at the end
+    if (fused_kind != 0) {
+      deferred_.push_back({begin, end});
+      launched_any_ = true;
     }
-    if (fused.kind == 1) {
-      SgdHyper h = fused.sgd;
-      h.first_step = first;
-      sgd_ranges(fused.p, g, fused.s0, rs, h, compute);
-    } else if (fused.kind == 2) {
-      AdamHyper h = fused.adam;
-      const double t = (double)(fused.adam_step > 0 ? fused.adam_step : 1);
-      h.bc1 = (float)(1.0 - std::pow((double)fused.adam_beta1, t));
-      h.bc2_sqrt = (float)std::sqrt(1.0 - std::pow((double)fused.adam_beta2, t));
-      adam_ranges(fused.p, g, fused.s0, fused.s1, fused.s2, rs, h, compute);
+    return;
+  }
+  hipStream_t cs = pick_stream(bucket, compute);
+  reduce_bucket(begin, end, cs);
+  if (fused_kind == 0) return;
+  if (clip == ClipMode::GLOBAL) {
+    pending_.push_back({begin, end});  // the update needs the norm of every bucket
+    return;
+  }
+  finish_bucket(begin, end, cs);
+}
+
+void SyncBackend::run_clip_local(hipStream_t s) {
+  Ranges all;
+  for (const auto& p : pending_) all.push_back({p.begin, p.end});
+  ops_->grad_sumsq(1, all, s);  // this rank's own gradient: no collective
+  ops_->clip_coef(1, s);
+  ops_->scale_grads(1, all, s);
+  const auto buckets = pending_;
+  pending_.clear();
+  for (const auto& p : buckets) {
+    if (collective()) {
+      reduce_bucket(p.begin, p.end, s);
+      finish_bucket(p.begin, p.end, s);
+    } else if (fused_kind != 0) {
+      deferred_.push_back({p.begin, p.end});
     }
   }
 }
 
-void RcclBackend::wait_all(hipStream_t compute) {
-  flush_deferred(compute);
-  // iteration boundary: epilogue bookkeeping restarts
-  epi_done_.clear();
-  if (fused.kind != 0) epi_fresh_ = false;
-  bucket0_launched_ = false;
-  if (!launched_any_) return;
-  if (!launched_side_) {  // everything ran on the compute stream: already ordered
-    launched_any_ = false;
-    return;
+void SyncBackend::run_clip_global(hipStream_t s) {
+  // norm of the averaged gradient: with sharding each rank holds its shards (+ the replicated
+  // tails, counted once by rank 0) and one 1-element all-reduce sums the parts; otherwise every
+  // rank holds the whole averaged gradient and computes the same norm locally (deterministic
+  // reduction: bit-identical on every rank)
+  const bool sh = is_sharded(*this, ops_->world());
+  Ranges norm_r;
+  for (const auto& p : pending_) {
+    if (!sh) {
+      norm_r.push_back({p.begin, p.end});
+      continue;
+    }
+    const Range own = owned_shard(p.begin, p.end);
+    const int64_t body = (own.second - own.first) * ops_->world();
+    if (own.second > own.first) norm_r.push_back(own);
+    if (ops_->rank() == 0 && p.begin + body < p.end) norm_r.push_back({p.begin + body, p.end});
   }
-  launched_side_ = false;
-  hipStream_t cs = comm_->comm_stream();
-  if (timing_) {
-    check_hip(hipEventRecord(t1_, cs), "hipEventRecord");
-    timed_pending_ = true;
+  ops_->grad_sumsq(0, norm_r, s);
+  if (sh) ops_->sumsq_all_reduce(0, s);
+  ops_->clip_coef(0, s);  // the update kernels multiply their gradient by it
+  const auto buckets = pending_;
+  pending_.clear();
+  for (const auto& p : buckets) finish_bucket(p.begin, p.end, s);
+}
+
+void SyncBackend::wait_all(hipStream_t compute) {
+  // 1. join the comm stream: the compute stream waits for every bucket launched on it
+  if (launched_side_) {
+    launched_side_ = false;
+    hipStream_t cs = ops_->comm_stream();
+    if (timing_) {
+      check_hip(hipEventRecord(t1_, cs), "hipEventRecord");
+      timed_pending_ = true;
+    }
+    if (stream_mode_ == kStreamHostJoin) {
+      check_hip(hipEventRecord(done_, cs), "hipEventRecord");
+      check_hip(hipEventSynchronize(done_), "hipEventSynchronize");
+    } else if (stream_mode_ != kStreamNoJoin) {
+      check_hip(hipEventRecord(done_, cs), "hipEventRecord");
+      check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
+    }
   }
   launched_any_ = false;
-  if (stream_mode_ == kStreamNoJoin) return;
-  check_hip(hipEventRecord(done_, cs), "hipEventRecord");
-  if (stream_mode_ == kStreamHostJoin) {
-    check_hip(hipEventSynchronize(done_), "hipEventSynchronize");
-    return;
+  // 2. work that needed the whole backward, on the compute stream
+  if (clip == ClipMode::LOCAL && !pending_.empty()) run_clip_local(compute);
+  if (clip == ClipMode::GLOBAL && fused_kind != 0) {
+    if (!deferred_.empty()) {  // world size 1: the deferred buckets ARE the gradient
+      for (const auto& d : deferred_) pending_.push_back({d.first, d.second});
+      deferred_.clear();
+    }
+    if (!pending_.empty()) run_clip_global(compute);
   }
-  check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
+  // 3. world size 1: the bucket updates not done by GEMM epilogues, merged, in few launches
+  if (!deferred_.empty()) {
+    std::sort(deferred_.begin(), deferred_.end());
+    Ranges merged;
+    for (const auto& t : minus_epilogue(deferred_)) {
+      if (!merged.empty() && merged.back().second == t.first) merged.back().second = t.second;
+      else merged.push_back(t);
+    }
+    deferred_.clear();
+    ops_->opt_update(merged, compute);
+  }
 }
 
-void RcclBackend::zero(int64_t begin, int64_t end, hipStream_t compute) {
-  if (end > begin)
-    check_hip(hipMemsetAsync(arena_ + begin * elem_size_, 0, (size_t)(end - begin) * elem_size_,
-                             compute),
-              "hipMemsetAsync");
+void SyncBackend::zero(int64_t begin, int64_t end, hipStream_t compute) {
+  ops_->zero_grads(begin, end - begin, compute);
 }
 
-double RcclBackend::last_comm_ms() {
+double SyncBackend::last_comm_ms() {
   if (!timing_ || !timed_pending_) return -1.0;
   if (hipEventQuery(t1_) != hipSuccess) return -1.0;  // not finished yet: never block here
   float ms = 0.f;
@@ -368,10 +461,12 @@ Reducer::Reducer(std::vector<int64_t> offsets, std::vector<int64_t> numels,
   bucket_ready_.assign(nb, 0);
 }
 
-void Reducer::prepare_for_backward() {
+void Reducer::prepare_for_backward(hipStream_t compute) {
+  backend_->begin_iteration(compute);
   pending_ = bucket_nparams_;
   std::fill(param_ready_.begin(), param_ready_.end(), 0);
   for (int b = 0; b < num_buckets(); ++b) bucket_ready_[b] = (bucket_nparams_[b] == 0);
+  hol_seen_.assign(num_buckets(), 0);
   next_bucket_ = 0;
   expecting_ = true;
 }
@@ -393,6 +488,13 @@ void Reducer::mark_ready(int p, hipStream_t compute) {
 
 void Reducer::launch_ready(hipStream_t compute) {
   const int nb = num_buckets();
+  // head-of-line accounting: a complete bucket stuck behind an incomplete lower-index one
+  if (next_bucket_ < nb && !bucket_ready_[next_bucket_])
+    for (int b = next_bucket_ + 1; b < nb; ++b)
+      if (bucket_ready_[b] && !hol_seen_[b]) {
+        hol_seen_[b] = 1;
+        ++hol_waits_;
+      }
   while (next_bucket_ < nb && bucket_ready_[next_bucket_]) {
     backend_->launch(next_bucket_, bounds_[next_bucket_], bounds_[next_bucket_ + 1], compute);
     ++next_bucket_;

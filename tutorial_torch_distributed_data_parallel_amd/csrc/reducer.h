@@ -4,19 +4,24 @@
 // gradient into a bucket, divides by world size, all-reduces, and copies back (K24: 2 x 217 MiB of
 // copies per AlexNet step), starts from one all-parameter bucket and rebuilds buckets after
 // iteration 0. Here:
-//   * every parameter's .grad IS a view of one flat arena laid out in backward order, so a bucket
-//     is just a contiguous [begin, end) element range: no copy-in, no copy-out;
-//   * a bucket boundary may fall inside a large parameter (fc1's 144 MiB weight can be split);
-//   * averaging is ncclAvg inside the all-reduce (no div_ pass);
+//   * every parameter's .grad IS a view of one flat arena, so a bucket is a contiguous
+//     [begin, end) element range: no copy-in, no copy-out; the arena is laid out in backward
+//     order (re-laid out once from the observed ready order, parallel/ddp.py _rebuild_buckets);
+//   * a bucket boundary may fall inside a large parameter (fc1's 144 MiB weight is split);
+//   * averaging is ncclAvg inside the collective (no div_ pass);
 //   * buckets launch strictly in index order as soon as every parameter overlapping them is
 //     ready (identical collective order on every rank). While a hipGraph is being captured they
 //     go to the communicator's high-priority stream after an event recorded on the compute
 //     stream (overlapping backward) and finalize() makes the compute stream wait on the last
 //     bucket; in eager execution they are issued on the compute stream itself, because a
 //     cross-queue wait left pending while the host runs ahead was measured to slow every kernel
-//     on MI355X (see RcclBackend::launch). Either way no host sync is needed.
-// The backend is abstract so that the same bucketing/readiness logic runs over RCCL on MI355X
-// and over torch.distributed (gloo) in the CPU tests.
+//     on MI355X (profiles/side_stream_eager.md). Either way no host sync is needed.
+//
+// The bucket / shard / clip ALGORITHM (SyncBackend) is separated from its side effects (SyncOps):
+// RcclOps runs it on MI355X (RCCL collectives over xGMI + gfx950 optimizer kernels); PyOps
+// (bindings.cpp) runs the very same C++ logic over torch.distributed/gloo with torch math on CPU
+// arenas, which is how the multi-rank paths (sharded update, tails, clipping) are tested without
+// a multi-GPU node.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,6 +29,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "comm.h"
@@ -31,8 +37,13 @@
 
 namespace tdp {
 
+using Range = std::pair<int64_t, int64_t>;  // [first, second) arena elements
+using Ranges = std::vector<Range>;
+
 struct ReducerBackend {
   virtual ~ReducerBackend() = default;
+  // start of an iteration's backward (forward of a step that will sync gradients)
+  virtual void begin_iteration(hipStream_t compute) { (void)compute; }
   // average arena elements [begin, end) across ranks, ordered after work already on `compute`
   virtual void launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) = 0;
   // make `compute` wait for every bucket launched so far in this iteration
@@ -47,76 +58,144 @@ struct ReducerBackend {
 // bf16 on the comm stream, all-reduces that and casts back (torch's bf16_compress_hook).
 enum class Compression : int { NONE = 0, BF16 = 1 };
 
-// Optimizer update fused into the reduction (torch's DDP._register_fused_optim idea): as soon as a
-// bucket's averaged gradient exists, its slice of the parameter arena is updated on the comm
-// stream, overlapping the update of early buckets with the backward compute / all-reduce of
-// later ones. Parameters, gradients and optimizer state share the arena layout, so a bucket's
-// update is the flat kernel on [begin, end) of every buffer.
+// Gradient clipping done inside the reduction.
+//   GLOBAL: torch.nn.utils.clip_grad_norm_ of the AVERAGED gradient, before the fused optimizer
+//           update (the norm of the whole model needs every bucket: updates wait for the last one).
+//   LOCAL:  the README pitfall "clip gradients before they are aggregated"
+//           (REF/README.md:92-95): every rank clips its OWN gradient to max_norm before any byte
+//           goes on the wire, so one rank's exploding gradient cannot dominate the average.
+enum class ClipMode : int { NONE = 0, GLOBAL = 1, LOCAL = 2 };
+
+// Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
+struct SyncOps {
+  virtual ~SyncOps() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  virtual bool on_device() const = 0;
+  virtual hipStream_t comm_stream() { return nullptr; }
+  // gradient arena collectives, in place, averaged over ranks
+  virtual void all_reduce_avg(int64_t off, int64_t n, hipStream_t s) = 0;
+  // [off, off + W*cnt): rank r ends up with the average of its slice [off + r*cnt, +cnt)
+  virtual void reduce_scatter_avg(int64_t off, int64_t cnt, hipStream_t s) = 0;
+  // parameter arena: every rank's slice [off + r*cnt, +cnt) -> everyone, in place
+  virtual void all_gather_params(int64_t off, int64_t cnt, hipStream_t s) = 0;
+  virtual void zero_grads(int64_t off, int64_t n, hipStream_t s) = 0;
+  // fused optimizer (ranges of p / grad / state, one launch per call)
+  virtual void opt_begin(hipStream_t s) = 0;
+  virtual void opt_update(const Ranges& r, hipStream_t s) = 0;
+  // clipping: `block` 0 = the optimizer's hyper block (GLOBAL), 1 = the DDP clip block (LOCAL)
+  virtual void clip_begin(int block, hipStream_t s) = 0;
+  virtual void grad_sumsq(int block, const Ranges& r, hipStream_t s) = 0;  // += ||g[r]||^2
+  virtual void sumsq_all_reduce(int block, hipStream_t s) = 0;             // sum over ranks
+  virtual void clip_coef(int block, hipStream_t s) = 0;                    // from sumsq
+  virtual void scale_grads(int block, const Ranges& r, hipStream_t s) = 0; // g[r] *= coef
+};
+
+// Device implementation: RCCL communicator + gfx950 kernels over the device arenas.
 struct FusedOptimizer {
   int kind = 0;  // 0 none, 1 SGD, 2 Adam
   float* p = nullptr;
   float* s0 = nullptr;  // momentum buffer / exp_avg
   float* s1 = nullptr;  // exp_avg_sq
   float* s2 = nullptr;  // max_exp_avg_sq
-  SgdHyper sgd{};
+  SgdHyper sgd{};       // structural flags; per-step scalars come from `hyper`
   AdamHyper adam{};
-  float adam_beta1 = 0.9f, adam_beta2 = 0.999f;
-  int64_t adam_step = 0;       // incremented when the first bucket of an iteration updates
-  std::vector<char> fresh;     // per bucket: SGD momentum not yet initialised
-  bool shard = false;          // reduce-scatter / update 1/W / all-gather (world > 1)
+  float* hyper = nullptr;  // device hyper block of the optimizer (kernels.h HyperSlot)
 };
 
-class RcclBackend : public ReducerBackend {
+class RcclOps : public SyncOps {
  public:
-  RcclBackend(std::shared_ptr<Communicator> comm, void* arena, int64_t numel, int elem_size,
-              int num_buckets, Compression compression, bool timing, bool skip_single_rank);
-  ~RcclBackend() override;
+  RcclOps(std::shared_ptr<Communicator> comm, float* grad, float* param, int64_t numel,
+          Compression compression);
+  ~RcclOps() override;
+  int rank() const override { return comm_->rank(); }
+  int world() const override { return comm_->world(); }
+  bool on_device() const override { return true; }
+  hipStream_t comm_stream() override { return comm_->comm_stream(); }
+  void all_reduce_avg(int64_t off, int64_t n, hipStream_t s) override;
+  void reduce_scatter_avg(int64_t off, int64_t cnt, hipStream_t s) override;
+  void all_gather_params(int64_t off, int64_t cnt, hipStream_t s) override;
+  void zero_grads(int64_t off, int64_t n, hipStream_t s) override;
+  void opt_begin(hipStream_t s) override;
+  void opt_update(const Ranges& r, hipStream_t s) override;
+  void clip_begin(int block, hipStream_t s) override;
+  void grad_sumsq(int block, const Ranges& r, hipStream_t s) override;
+  void sumsq_all_reduce(int block, hipStream_t s) override;
+  void clip_coef(int block, hipStream_t s) override;
+  void scale_grads(int block, const Ranges& r, hipStream_t s) override;
+
+  FusedOptimizer fused;
+  float* clip_block = nullptr;  // DDP-owned hyper block for LOCAL clipping
+  Compression compression() const { return compression_; }
+  std::shared_ptr<Communicator> comm() const { return comm_; }
+
+ private:
+  float* block(int b) const { return b == 0 ? fused.hyper : clip_block; }
+  std::shared_ptr<Communicator> comm_;
+  float* grad_;
+  float* param_;
+  int64_t numel_;
+  Compression compression_;
+  uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
+};
+
+// The bucket algorithm (one instance per DDP model).
+class SyncBackend : public ReducerBackend {
+ public:
+  SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_buckets, bool timing,
+              bool skip_single_rank);
+  ~SyncBackend() override;
+  void begin_iteration(hipStream_t compute) override;
   void launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) override;
   void wait_all(hipStream_t compute) override;
   void zero(int64_t begin, int64_t end, hipStream_t compute) override;
   double last_comm_ms() override;
-  // called after a bucket's all-reduce is enqueued, with the comm stream (fused optimizer hook)
-  std::function<void(int, int64_t, int64_t, hipStream_t)> post_bucket;
-  FusedOptimizer fused;
+
+  // configuration (set by parallel/ddp.py)
+  int fused_kind = 0;     // 0 none, 1 SGD, 2 Adam (ops apply it)
+  bool shard = false;     // world > 1: reduce-scatter / update own 1/W / all-gather
+  ClipMode clip = ClipMode::NONE;
+  bool compressed = false;  // wire compression active (sharding needs the plain fp32 path)
 
   // Optimizer-in-GEMM-epilogue (world size 1 only: the local gradient IS the averaged one): the
   // weight-gradient GEMM of arena elements [off, off + n) applies the fused optimizer instead of
-  // storing the gradient. Returns the epilogue arguments (pointers offset to `off`, this
-  // iteration's hyper-parameters) and records the range so the bucket update skips it.
-  OptEpilogue epilogue_opt(int64_t off, int64_t n);
+  // storing the gradient; the range is recorded so the bucket update skips it.
   bool epilogue_allowed() const;
-  void set_epilogue_fresh(bool v) { epi_fresh_ = v; }
+  void note_epilogue(int64_t off, int64_t n);
+
+  // the shard of bucket [begin, end) this rank owns under the sharded update (tail excluded)
+  Range owned_shard(int64_t begin, int64_t end) const;
+  std::shared_ptr<SyncOps> ops() const { return ops_; }
+  bool collective() const { return !(skip_single_rank_ && ops_->world() == 1); }
 
  private:
-  void apply_fused(int64_t off, int64_t cnt, bool first, hipStream_t cs);
-  void apply_fused_range(int64_t off, int64_t cnt, bool first, hipStream_t cs);
-  void flush_deferred(hipStream_t compute);
-  std::vector<std::pair<int64_t, int64_t>> epi_done_;  // ranges updated by GEMM epilogues
-  // world size 1: bucket updates deferred to the end of backward, applied by one launch
-  std::vector<std::pair<int64_t, int64_t>> deferred_;
-  bool deferred_first_ = false;
-  bool epi_fresh_ = false;        // SGD momentum of epilogue-updated ranges not yet initialised
-  bool bucket0_launched_ = false;  // this iteration's Adam step counter already advanced
-  std::shared_ptr<Communicator> comm_;
-  char* arena_;
+  struct Pending {
+    int64_t begin, end;
+  };
+  void reduce_bucket(int64_t begin, int64_t end, hipStream_t cs);   // collectives only
+  void finish_bucket(int64_t begin, int64_t end, hipStream_t cs);   // update + all-gather
+  Ranges update_ranges(int64_t begin, int64_t end) const;           // own ranges minus epilogue
+  Ranges minus_epilogue(const Ranges& in) const;
+  hipStream_t pick_stream(int bucket, hipStream_t compute);
+  void run_clip_local(hipStream_t cs);
+  void run_clip_global(hipStream_t cs);
+
+  std::shared_ptr<SyncOps> ops_;
   int64_t numel_;
-  int elem_size_;
-  Compression compression_;
   bool timing_, skip_single_rank_;
+  Ranges epi_done_;              // ranges updated by GEMM epilogues this iteration (sorted)
+  std::vector<Pending> pending_; // buckets reduced but not yet updated (clipping) / not reduced
+  Ranges deferred_;              // world size 1: bucket updates deferred to the end of backward
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
-  bool launched_any_ = false, timed_pending_ = false;
-  // where bucket collectives run: auto = side stream only while capturing a hipGraph
-  // hostjoin: side stream, but the end-of-backward join is a host wait on the comm stream's
-  // event instead of a device-side hipStreamWaitEvent on the compute stream; nojoin: no join
-  // at all (measurement only: the next forward may race the last buckets)
+  bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;
+  // where bucket collectives run: auto = side stream only while capturing a hipGraph;
+  // hostjoin: side stream, end-of-backward join by a host wait; nojoin: no join (measurement)
   enum {
     kStreamAuto = 0, kStreamSide = 1, kStreamCompute = 2, kStreamHostSync = 3,
     kStreamHostJoin = 4, kStreamNoJoin = 5
   };
   int stream_mode_ = kStreamAuto;
-  bool launched_side_ = false;
-  uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
 };
 
 class Reducer {
@@ -133,7 +212,7 @@ class Reducer {
                                                     int64_t first_cap_bytes, int64_t cap_bytes,
                                                     int64_t split_bytes);
 
-  void prepare_for_backward();
+  void prepare_for_backward(hipStream_t compute);
   void mark_ready(int param, hipStream_t compute);
   // launch whatever is left, zero never-ready params when allowed, make `compute` wait
   void finalize(hipStream_t compute, bool allow_unused);
@@ -142,6 +221,9 @@ class Reducer {
   int64_t iteration() const { return iteration_; }
   std::vector<int64_t> bucket_bounds() const { return bounds_; }
   std::vector<int> ready_order() const { return first_ready_order_; }
+  // buckets (summed over iterations) that were complete while a lower-indexed bucket was not:
+  // each one waited only because buckets launch in index order
+  int64_t head_of_line_waits() const { return hol_waits_; }
   std::vector<int> unready_params() const;
   int num_buckets() const { return (int)bounds_.size() - 1; }
   double last_comm_ms() { return backend_->last_comm_ms(); }
@@ -158,6 +240,8 @@ class Reducer {
   int next_bucket_ = 0;
   bool expecting_ = false;
   int64_t iteration_ = 0;
+  int64_t hol_waits_ = 0;
+  std::vector<char> hol_seen_;
 };
 
 }  // namespace tdp

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
-from ._grad import epilogue_target, grad_dest, needs
+from ._grad import epilogue_target, grad_dest, needs, note_use
 
 
 class _LinearFn(torch.autograd.Function):
@@ -76,5 +76,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     x2 = x.reshape(-1, x.shape[-1])
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
+    if torch.is_grad_enabled():
+        note_use(weight)
     y = _LinearFn.apply(x2, weight, bias, relu)
     return y.reshape(*lead, weight.shape[0])

@@ -17,6 +17,7 @@ bias-corrected Adam with a per-parameter step counter.
 from __future__ import annotations
 
 import functools
+import weakref
 
 import torch
 from torch.optim import Optimizer
@@ -61,19 +62,98 @@ def _lean_step_hook(func):
     return wrapper
 
 
+_LIVE = weakref.WeakSet()  # optimizers that own device hyper blocks (CapturedStep re-syncs them)
+
+
+def hyper_slots() -> dict:
+    """Slot indices of the device hyper block (csrc/kernels.h HyperSlot)."""
+    global _SLOTS
+    if _SLOTS is None:
+        _SLOTS = dict(native().hyper_slots())
+    return _SLOTS
+
+
+_SLOTS = None
+
+
+def sync_all_hyper() -> None:
+    """Push host-side hyper-parameter changes (LR schedulers, ...) of every live optimizer into
+    its device hyper block; called before each hipGraph replay (train/graph.py)."""
+    for opt in list(_LIVE):
+        opt.sync_hyper()
+
+
 class _FusedBase(Optimizer):
     _state_keys: tuple = ()
+    _kind = 0  # hyper-block kind: 1 SGD, 2 Adam
 
     def __init__(self, params, defaults):
         super().__init__(params, defaults)
         self._flat_bufs = {}  # id(arena) -> {key: flat tensor}
         self._flat_step = {}  # id(arena) -> int step shared by every arena parameter (Adam)
+        self._blocks = {}     # group index -> [device hyper block, host copy of its scalars]
 
     def __init_subclass__(cls, **kwargs):
         super().__init_subclass__(**kwargs)
         if "step" in cls.__dict__ and not getattr(cls.__dict__["step"], "hooked", False):
             cls.step = _lean_step_hook(cls.__dict__["step"])
 
+    # ------------------------------------------------------------------ device hyper block
+    def _scalars(self, g) -> tuple:
+        raise NotImplementedError
+
+    def hyper_block(self, gi: int = 0, device=None, step: int = 0,
+                    first: bool = False) -> torch.Tensor:
+        """The device-resident hyper-parameter block of parameter group ``gi`` (created on first
+        use with step count ``step``; ``first`` = the next step initialises the SGD momentum
+        buffers). Kernels read lr / momentum / betas / bias corrections from it, so a captured
+        hipGraph replays with the current values (csrc/kernels.h HyperSlot)."""
+        ent = self._blocks.get(gi)
+        if ent is not None:
+            return ent[0]
+        S = hyper_slots()
+        g = self.param_groups[gi]
+        dev = device if device is not None else g["params"][0].device
+        vals = self._scalars(g)
+        host = torch.zeros(S["size"], dtype=torch.float32)
+        host[:len(vals)] = torch.tensor(vals, dtype=torch.float64).float()
+        host[S["scale"]] = 1.0
+        host[S["first_next"]] = 1.0 if first else 0.0
+        host.view(torch.int32)[S["step"]] = int(step)
+        blk = host.to(dev)
+        self._blocks[gi] = [blk, vals]
+        _LIVE.add(self)
+        return blk
+
+    def sync_hyper(self) -> None:
+        """Stream-ordered write of changed scalars (lr, momentum / betas, weight decay, eps) into
+        the device blocks. Nothing is issued when nothing changed."""
+        for gi, ent in self._blocks.items():
+            vals = self._scalars(self.param_groups[gi])
+            if vals == ent[1]:
+                continue
+            blk = ent[0]
+            if blk.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("hyper-parameters changed while a hipGraph was being captured")
+            src = torch.tensor(vals, dtype=torch.float64).float()
+            if blk.is_cuda:
+                blk[:len(vals)].copy_(src.pin_memory(), non_blocking=True)
+            else:
+                blk[:len(vals)].copy_(src)
+            ent[1] = vals
+
+    def device_step(self, gi: int = 0):
+        """Step count held by the device block of group ``gi`` (None without a block). Reading
+        it synchronises with the device."""
+        ent = self._blocks.get(gi)
+        if ent is None:
+            return None
+        return int(ent[0].view(torch.int32)[hyper_slots()["step"]].item())
+
+    def _request_first(self, blk) -> None:
+        blk[hyper_slots()["first_next"]] = 1.0
+
+    # ------------------------------------------------------------------ torch API
     def zero_grad(self, set_to_none: bool = True) -> None:
         """torch's zero_grad, without its per-call record_function range / dynamo guard when
         gradients are simply dropped (the default) and the profiler is off."""
@@ -110,6 +190,7 @@ class _FusedBase(Optimizer):
         super().load_state_dict(state_dict)
         self._flat_bufs = {}  # re-adopted into flat buffers on the next step
         self._flat_step = {}
+        self._blocks = {}     # re-created with the loaded step count
         ddp = getattr(self, "_fused_ddp", None)
         if ddp is not None:
             ddp.push_fused_hyper(self, initial=True)
@@ -128,10 +209,14 @@ class _FusedBase(Optimizer):
         return max(steps) if steps else 0
 
     def state_dict(self):
-        # materialise the shared flat step counter into torch's per-parameter "step" entries
-        ddp = getattr(self, "_fused_ddp", None)
-        if ddp is not None and self.__class__.__name__ != "SGD":
-            self._flat_step[id(ddp.arena)] = int(ddp._backend.fused_adam_step)
+        # materialise the flat step counter (held by the device block: graph replays advance it
+        # without the host) into torch's per-parameter "step" entries
+        if self._kind == 2:
+            for gi, g in enumerate(self.param_groups):
+                a = arena_of(g["params"])
+                dstep = self.device_step(gi)
+                if a is not None and dstep is not None:
+                    self._flat_step[id(a)] = dstep
         for g in self.param_groups:
             a = arena_of(g["params"])
             if a is not None and id(a) in self._flat_step:
@@ -153,6 +238,12 @@ class SGD(_FusedBase):
                                       weight_decay=weight_decay, nesterov=nesterov,
                                       maximize=maximize, grad_scale=grad_scale))
 
+    _kind = 1
+
+    def _scalars(self, g) -> tuple:
+        return (float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
+                float(g["weight_decay"]), 0.0)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -161,7 +252,7 @@ class SGD(_FusedBase):
                 loss = closure()
         if self._fused_step():
             return loss
-        for g in self.param_groups:
+        for gi, g in enumerate(self.param_groups):
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -174,14 +265,22 @@ class SGD(_FusedBase):
             mom = g["momentum"] != 0
             arena = _flat_arena(g) if len(ps) == len(g["params"]) else None
             if arena is not None:
+                buf, fresh = None, False
                 if mom:
                     # fresh == the buffers were just created (torch: buf = clone(grad))
                     bufs, fresh = self._flat_state(arena, ("momentum_buffer",))
-                    C.sgd_flat(arena.data, arena.grad, bufs["momentum_buffer"], *hyper[:5],
-                               hyper[5], fresh, g["grad_scale"])
+                    buf = bufs["momentum_buffer"]
+                # scalars and the first-step flag come from the device block (graph-safe)
+                if gi in self._blocks:
+                    blk = self._blocks[gi][0]
+                    self.sync_hyper()
+                    if fresh:
+                        self._request_first(blk)
                 else:
-                    C.sgd_flat(arena.data, arena.grad, None, *hyper[:5], hyper[5], False,
-                               g["grad_scale"])
+                    blk = self.hyper_block(gi, first=fresh)
+                C.opt_step_begin(blk, 1)
+                C.sgd_flat(arena.data, arena.grad, buf, *hyper[:5], hyper[5], False,
+                           g["grad_scale"], hyper=blk)
                 continue
             new, old = [], []
             for p in ps:
@@ -229,6 +328,12 @@ class Adam(_FusedBase):
                                       weight_decay=weight_decay, amsgrad=amsgrad,
                                       maximize=maximize, grad_scale=grad_scale))
 
+    _kind = 2
+
+    def _scalars(self, g) -> tuple:
+        b1, b2 = g["betas"]
+        return (float(g["lr"]), float(b1), float(b2), float(g["weight_decay"]), float(g["eps"]))
+
     def _keys(self, g):
         return ("exp_avg", "exp_avg_sq") + (("max_exp_avg_sq",) if g["amsgrad"] else ())
 
@@ -251,7 +356,7 @@ class Adam(_FusedBase):
                 loss = closure()
         if self._fused_step():
             return loss
-        for g in self.param_groups:
+        for gi, g in enumerate(self.param_groups):
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -274,15 +379,27 @@ class Adam(_FusedBase):
                         self._flat_step[key] = prev.pop()
                 if key in self._flat_step:
                     bufs, _ = self._flat_state(arena, keys)
+                    # the step count and bias corrections advance ON THE DEVICE (opt_step_begin),
+                    # so a captured step replays correctly; the host count mirrors it eagerly
+                    if gi in self._blocks:
+                        blk = self._blocks[gi][0]
+                        self.sync_hyper()
+                    else:
+                        blk = self.hyper_block(gi, step=self._flat_step[key])
                     self._flat_step[key] += 1
+                    C.opt_step_begin(blk, 2)
                     C.adam_flat(arena.data, arena.grad, bufs["exp_avg"], bufs["exp_avg_sq"],
                                 bufs.get("max_exp_avg_sq"), *args, self._flat_step[key],
-                                g["grad_scale"])
+                                g["grad_scale"], hyper=blk)
                     continue
             for k2 in list(self._flat_step):  # leaving the flat path: write the counter back
                 a2 = arena_of(g["params"])
                 if a2 is not None and id(a2) == k2:
-                    t = torch.tensor(float(self._flat_step.pop(k2)))
+                    dstep = self.device_step(gi)
+                    self._blocks.pop(gi, None)
+                    t = torch.tensor(float(dstep if dstep is not None else
+                                           self._flat_step[k2]))
+                    self._flat_step.pop(k2)
                     for p in a2.params:
                         self.state[p]["step"] = t.clone()
             by_step = {}

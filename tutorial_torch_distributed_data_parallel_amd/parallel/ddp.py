@@ -102,27 +102,26 @@ class DistributedDataParallel(nn.Module):
         cap = (bucket_cap_mb if bucket_cap_mb is not None else 25.0) * _MB
         first = (first_bucket_cap_mb if first_bucket_cap_mb is not None else 1.0) * _MB
         split = (split_bucket_mb or 0.0) * _MB
-        C = native() if self._gpu else None
-        esize = self.arena.data.element_size()
-        if C is not None:
-            bounds = C.Reducer.compute_bucket_bounds(self.arena.offsets, self.arena.numels,
-                                                     self.arena.numel, esize, int(first),
-                                                     int(cap), int(split))
-        else:
-            bounds = _bucket_bounds_py(self.arena.offsets, self.arena.numels, self.arena.numel,
-                                       esize, int(first), int(cap), int(split))
-        self._bounds = bounds
+        self._caps = (int(first), int(cap), int(split))
+        self._bounds = self._plan_buckets()
         self._compression = grad_compression
         self._timing = timing
+        self._fused_opt = None
+        self._fused_shard = False
+        self._clip_global = None   # max_norm of the in-reduction global-norm clip (fused optimizer)
+        self._clip_local = None    # max_norm of the per-rank clip before aggregation
+        self._clip_block = None
+        self._force_collective = False
+        self._epi_on = False
+        self._epi_index = {}
+        self._uses = {}            # id(param) -> forward uses in the current iteration
+        self._fwd_ms, self._bwd_ms = [], []
         self._build_reducer()
         self._hooks = []
         for i, p in enumerate(self.arena.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self._callback_queued = False
         self._iter = 0
-        self._fused_opt = None
-        self._epi_on = False
-        self._epi_index = {}
         # SURVEY.md §5.2 debug mode: every N forwards, verify that all replicas hold bit-identical
         # parameters (a checksum all-gather); TDP_CHECK_REPLICAS=N sets it from the environment
         env_every = int(os.environ.get("TDP_CHECK_REPLICAS", "0") or 0)
@@ -131,24 +130,39 @@ class DistributedDataParallel(nn.Module):
 
     # --------------------------------------------------------------------------- reducer
     def _build_reducer(self):
+        """SyncBackend (csrc/reducer.h: the bucket / shard / clip algorithm) over RcclOps on GPUs
+        or over _CpuSyncOps (gloo + torch math) on CPU, plus the Reducer that tracks readiness.
+        Re-applies the fused-optimizer / clipping configuration, so rebuilding (comm hook change,
+        bucket rebuild) never loses optimizer state or flags."""
         nb = len(self._bounds) - 1
+        C = native()
+        comp = {None: 0, "none": 0, "fp32": 0, "bf16": 1}[self._compression]
         if self._gpu:
-            C = native()
-            comp = {None: 0, "none": 0, "fp32": 0, "bf16": 1}[self._compression]
             comm = rt.comm()
             if comm is None:
                 raise RuntimeError("GPU DDP needs the RCCL backend (init_process_group('nccl'))")
-            # TDP_FORCE_COLLECTIVE=1 keeps the all-reduce (and its stream hop) at world size 1:
-            # the single-GPU rehearsal of the multi-GPU schedule
-            skip = os.environ.get("TDP_FORCE_COLLECTIVE", "0") != "1"
-            self._backend = C.RcclBackend(comm, self.arena.grad, nb, compression=comp,
-                                          timing=self._timing, skip_single_rank=skip)
-            self.reducer = C.Reducer(self.arena.offsets, self.arena.numels, self._bounds,
-                                     self._backend)
+            self._ops = C.RcclOps(comm, self.arena.grad, self.arena.data, compression=comp)
         else:
-            self._works = []
-            self._backend = None
-            self.reducer = _make_py_reducer(self)
+            self._cpu_ops = _CpuSyncOps(self, compression=comp)
+            self._ops = C.PyOps(self.rank, self.world_size, self._cpu_ops)
+        # TDP_FORCE_COLLECTIVE=1 keeps the collectives (and their stream hop) at world size 1:
+        # the single-GPU rehearsal of the multi-GPU schedule
+        skip = os.environ.get("TDP_FORCE_COLLECTIVE", "0") != "1" and not self._force_collective
+        self._backend = C.SyncBackend(self._ops, self.arena.numel, nb, timing=self._timing,
+                                      skip_single_rank=skip)
+        self._backend.compressed = comp != 0
+        self.reducer = C.Reducer(self.arena.offsets, self.arena.numels, self._bounds,
+                                 self._backend)
+        if self._fused_opt is not None:
+            self._configure_fused()
+        if self._clip_local is not None:
+            self._configure_local_clip()
+
+    def _plan_buckets(self):
+        first, cap, split = self._caps
+        return native().Reducer.compute_bucket_bounds(
+            self.arena.offsets, self.arena.numels, self.arena.numel,
+            self.arena.data.element_size(), first, cap, split)
 
     def _make_hook(self, idx):
         arena = self.arena
@@ -204,11 +218,13 @@ class DistributedDataParallel(nn.Module):
                 self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled():
             self.check_replicas()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
-            self.reducer.prepare_for_backward()
             if self._fused_opt is not None:
                 # hyper-parameters as they are NOW (after any LR-scheduler step) drive this
-                # iteration's in-reduction update
-                self.push_fused_hyper(self._fused_opt)
+                # iteration's in-reduction update: a stream-ordered write into the device block
+                # when something changed, before the block is advanced by prepare_for_backward
+                self._fused_opt.sync_hyper()
+            self._uses.clear()
+            self.reducer.prepare_for_backward(self._gpu)
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._sync_buffers()
@@ -224,24 +240,30 @@ class DistributedDataParallel(nn.Module):
             self.require_backward_grad_sync = old
 
     # --------------------------------------------------------------------------- fused optimizer
-    def register_fused_optimizer(self, optimizer, shard: bool | None = None) -> bool:
+    def register_fused_optimizer(self, optimizer, shard: bool | None = None,
+                                 clip_grad_norm: float | None = None) -> bool:
         """Apply ``optimizer`` bucket by bucket inside the reduction (torch's
         ``DDP._register_fused_optim``): each bucket's parameters are updated right after its
-        gradient is averaged. ``optimizer.step()`` becomes a no-op; the DDP forward hands the
-        current hyper-parameters to the update. Requires a tdp SGD/Adam over exactly this DDP's
-        parameters (one param group). Returns False (optimizer left unfused) on CPU.
+        gradient is averaged. ``optimizer.step()`` becomes a no-op. The optimizer's per-step
+        scalars live in its device hyper block (csrc/kernels.h HyperSlot): the DDP forward pushes
+        host-side changes (LR schedulers) and the reducer advances the Adam step count on the
+        device, so a captured hipGraph step stays correct. Requires a tdp SGD/Adam over exactly
+        this DDP's parameters (one param group).
 
         ``shard`` (default: world_size > 1) turns each bucket's all-reduce into reduce-scatter ->
         update of this rank's 1/W slice -> all-gather of the updated parameters (ZeRO stage 1
         inside DDP, cf. torch's ZeroRedundancyOptimizer): the same bytes over xGMI, 1/W of the
-        optimizer's HBM traffic, identical parameters on every rank. Gradients are not averaged
-        outside the owned slice afterwards, and optimizer state is only current in the owned
-        slices until :meth:`consolidate_optimizer_state` (called by the checkpoint helpers).
-        """
+        optimizer's HBM traffic, identical parameters on every rank. Afterwards ``p.grad`` holds
+        the averaged gradient only inside this rank's slices, and optimizer state is current only
+        there until :meth:`consolidate_optimizer_state` (the checkpoint helpers call it).
+
+        ``clip_grad_norm`` = max_norm: ``torch.nn.utils.clip_grad_norm_`` of the averaged
+        gradient applied before the update, inside the reduction (the norm of the whole model is
+        reduced on the device -- one 1-element all-reduce when sharded -- and the update kernels
+        scale their gradient by the coefficient; updates then wait for the last bucket).
+        Returns True."""
         from ..optim.fused import SGD, Adam
 
-        if not self._gpu:
-            return False
         if self.find_unused_parameters:
             raise ValueError("a fused optimizer needs every parameter to get a gradient")
         if len(optimizer.param_groups) != 1:
@@ -251,28 +273,132 @@ class DistributedDataParallel(nn.Module):
             raise ValueError("fused optimizer must own exactly the DDP model's parameters")
         if not isinstance(optimizer, (SGD, Adam)):
             raise TypeError("fused optimizer must be tdp.optim.SGD / Adam / AdamW")
+        if optimizer.param_groups[0].get("grad_scale", 1.0) != 1.0:
+            raise ValueError("fused optimizer: grad_scale must be 1 (ncclAvg already averages)")
         self._fused_opt = optimizer
         optimizer._fused_ddp = self
-        self.push_fused_hyper(optimizer, initial=True)
         self._fused_shard = bool(self.world_size > 1 if shard is None else shard) and \
             self.world_size > 1
-        self._backend.fused_shard = self._fused_shard
+        self._clip_global = float(clip_grad_norm) if clip_grad_norm else None
+        self.push_fused_hyper(optimizer, initial=True)
+        return True
+
+    def _configure_fused(self):
+        """(Re-)apply the fused-optimizer configuration to the current backend."""
+        opt = self._fused_opt
+        b = self._backend
+        b.shard = self._fused_shard
+        b.clip = 1 if self._clip_global else (2 if self._clip_local else 0)
+        self._bind_fused_buffers(opt)
+        b.fused_kind = opt._kind
         # world size 1: the local gradient is already the average, so weight-gradient GEMMs may
         # apply the update in their epilogue (TDP_OPT_EPILOGUE=0 keeps the per-bucket update)
         self._epi_index = {id(p): i for i, p in enumerate(self.arena.params)}
-        self._epi_on = (os.environ.get("TDP_OPT_EPILOGUE", "1") != "0" and
-                        bool(self._backend.epilogue_allowed))
-        if self._epi_on:
-            me = weakref.ref(self)
-            for p in self.arena.params:
-                p._tdp_epi = me
-        return True
+        self._epi_on = (self._gpu and os.environ.get("TDP_OPT_EPILOGUE", "1") != "0" and
+                        bool(b.epilogue_allowed))
+        me = weakref.ref(self) if self._epi_on else None
+        owner = weakref.ref(self)
+        for p in self.arena.params:
+            p._tdp_epi = me
+            p._tdp_fused_owner = owner  # tdp.nn.utils.clip_grad_norm_ refuses these grads
+
+    def _bind_fused_buffers(self, opt):
+        from ..optim.fused import SGD, hyper_slots
+
+        g = opt.param_groups[0]
+        a = self.arena
+        S = hyper_slots()
+        if isinstance(opt, SGD):
+            buf, fresh = None, False
+            if g["momentum"] != 0:
+                # fresh == the momentum buffers were just created: the first update initialises
+                # them with the gradient (torch: buf = clone(grad)), via the block's first flag
+                bufs, fresh = opt._flat_state(a, ("momentum_buffer",))
+                buf = bufs["momentum_buffer"]
+            blk = opt.hyper_block(0, device=self.device, first=fresh)
+            if fresh:
+                opt._request_first(blk)
+            if self._gpu:
+                self._ops.set_fused_sgd(a.data, buf, g["momentum"] != 0, g["nesterov"],
+                                        g["maximize"], blk)
+            else:
+                self._cpu_ops.set_fused(opt, blk, {"momentum_buffer": buf})
+        else:
+            keys = opt._keys(g)
+            bufs, _ = opt._flat_state(a, keys)
+            blk = opt.hyper_block(0, device=self.device, step=opt._current_flat_step(a))
+            if self._gpu:
+                self._ops.set_fused_adam(a.data, bufs["exp_avg"], bufs["exp_avg_sq"],
+                                         bufs.get("max_exp_avg_sq"), g["amsgrad"], g["maximize"],
+                                         opt._decoupled, blk)
+            else:
+                self._cpu_ops.set_fused(opt, blk, bufs)
+        if self._clip_global:
+            blk[S["max_norm"]] = float(self._clip_global)
+        opt.sync_hyper()
+
+    def push_fused_hyper(self, opt, initial: bool = False):
+        """Bind the optimizer's buffers and device block to the reducer (``initial``: after
+        registration or load_state_dict); later calls only push changed scalars."""
+        if initial:
+            self._configure_fused()
+        else:
+            opt.sync_hyper()
+
+    def clip_grad_norm_before_aggregation(self, max_norm: float | None) -> None:
+        """The README pitfall "clip gradients before they are aggregated" (REF/README.md:92-95):
+        every rank scales its OWN gradient to norm <= max_norm before any byte goes on the wire,
+        so one rank's exploding gradient cannot dominate the average. The local norm needs the
+        whole local gradient, so all bucket collectives move to the end of backward. None turns
+        it off."""
+        if max_norm is not None and self._clip_global:
+            raise ValueError("choose either the global in-reduction clip or the local one")
+        self._clip_local = float(max_norm) if max_norm else None
+        self._configure_local_clip()
+        if self._fused_opt is not None:
+            self._configure_fused()
+
+    def _configure_local_clip(self):
+        from ..optim.fused import hyper_slots
+
+        b = self._backend
+        if self._clip_local is None:
+            b.clip = 1 if self._clip_global else 0
+            return
+        S = hyper_slots()
+        if self._clip_block is None:
+            self._clip_block = torch.zeros(S["size"], device=self.device)
+            self._clip_block[S["scale"]] = 1.0
+        self._clip_block[S["max_norm"]] = self._clip_local
+        if self._gpu:
+            self._ops.set_clip_block(self._clip_block)
+        else:
+            self._cpu_ops.clip_block = self._clip_block
+        b.clip = 2
+
+    def last_grad_norm(self) -> torch.Tensor | None:
+        """Total gradient norm computed by the in-reduction clip of the last step (device
+        scalar; the local clip reports this rank's norm), or None without clipping."""
+        from ..optim.fused import hyper_slots
+
+        n = hyper_slots()["norm"]
+        if self._clip_local is not None:
+            return self._clip_block[n]
+        if self._clip_global and self._fused_opt is not None:
+            return self._fused_opt.hyper_block(0)[n]
+        return None
+
+    def _note_use(self, p):
+        self._uses[id(p)] = self._uses.get(id(p), 0) + 1
 
     def epilogue_slot(self, p):
         """(backend, arena offset) for an optimizer-epilogue weight-gradient GEMM of ``p`` in the
-        current backward, or None when the update must stay in the bucket path."""
+        current backward, or None when the update must stay in the bucket path (also when ``p``
+        was used more than once in this forward: its gradient is the sum of several GEMMs)."""
         if not (self._epi_on and self.require_backward_grad_sync and self.reducer.expecting and
                 self._backend.epilogue_allowed):
+            return None
+        if self._uses.get(id(p), 0) != 1:
             return None
         i = self._epi_index.get(id(p))
         if i is None or not self.arena.numels[i]:
@@ -282,46 +408,20 @@ class DistributedDataParallel(nn.Module):
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
         each bucket's state slices in place (the tails are already replicated)."""
-        if not getattr(self, "_fused_shard", False) or self._fused_opt is None:
+        if not self._fused_shard or self._fused_opt is None:
             return
         opt = self._fused_opt
         bufs = opt._flat_bufs.get(id(self.arena), {})
-        comm = rt.comm()
         W, r = self.world_size, self.rank
         for name, buf in bufs.items():
             if not torch.is_tensor(buf) or buf.numel() != self.arena.numel:
                 continue
             for i in range(len(self._bounds) - 1):
                 begin, end = self._bounds[i], self._bounds[i + 1]
-                cnt = (end - begin) // W
+                lo, hi = self._backend.owned_shard(begin, end)
+                cnt = (hi - lo)
                 if cnt > 0:
-                    comm.all_gather(buf[begin: begin + cnt * W],
-                                    buf[begin + r * cnt: begin + (r + 1) * cnt])
-
-    def push_fused_hyper(self, opt, initial: bool = False):
-        from ..optim.fused import SGD
-
-        g = opt.param_groups[0]
-        a = self.arena
-        if isinstance(opt, SGD):
-            buf, fresh = None, False
-            if g["momentum"] != 0:
-                # fresh == the momentum buffers were just created: each bucket's first update
-                # initialises them with the gradient (torch: buf = clone(grad))
-                bufs, fresh = opt._flat_state(a, ("momentum_buffer",))
-                buf = bufs["momentum_buffer"]
-            self._backend.set_fused_sgd(a.data, buf, g["lr"], g["momentum"], g["dampening"],
-                                        g["weight_decay"], g["nesterov"], g["maximize"],
-                                        bool(fresh) and initial)
-        else:
-            keys = opt._keys(g)
-            bufs, _ = opt._flat_state(a, keys)
-            step = opt._current_flat_step(a) if initial else self._backend.fused_adam_step
-            b1, b2 = g["betas"]
-            self._backend.set_fused_adam(a.data, bufs["exp_avg"], bufs["exp_avg_sq"],
-                                         bufs.get("max_exp_avg_sq"), g["lr"], b1, b2, g["eps"],
-                                         g["weight_decay"], g["amsgrad"], g["maximize"],
-                                         opt._decoupled, int(step))
+                    _all_gather_inplace(buf[begin: begin + cnt * W], r, cnt)
 
     def register_comm_hook(self, state, hook):
         """Gradient compression hooks: torch's bf16_compress_hook (or the string "bf16")."""
@@ -332,10 +432,8 @@ class DistributedDataParallel(nn.Module):
             self._compression = None
         else:
             raise NotImplementedError(f"comm hook {name!r} is not supported (bf16 | fp32)")
-        if self._gpu:
-            self._build_reducer()
-            if self._fused_opt is not None:
-                self.push_fused_hyper(self._fused_opt, initial=False)
+        # rebuilding keeps the fused optimizer's buffers, device block (step count) and flags
+        self._build_reducer()
 
     # --------------------------------------------------------------------------- logging
     def _get_ddp_logging_data(self) -> dict:
@@ -357,135 +455,183 @@ class DistributedDataParallel(nn.Module):
         }
 
 
-def _bucket_bounds_py(offsets, numels, arena_numel, esize, first_cap, cap, split):
-    """Python twin of Reducer::compute_bucket_bounds (used when no native module: CPU)."""
-    b = [0]
-    cur = 0
-    split_el = max(split // esize, 1) if split > 0 else 0
-    for i, (o, n) in enumerate(zip(offsets, numels)):
-        c = first_cap if len(b) == 1 else cap
-        nbytes = n * esize
-        if cur > 0 and cur + nbytes > c:
-            b.append(o)
-            cur = 0
-        if split_el and n > split_el:
-            if b[-1] != o:
-                b.append(o)
-            b.extend(o + s for s in range(split_el, n, split_el))
-            if i + 1 < len(offsets):
-                b.append(o + n)
-            cur = 0
-            continue
-        cur += nbytes
-    if b[-1] != arena_numel:
-        b.append(arena_numel)
-    out = [b[0]]
-    for x in b[1:]:
-        if x > out[-1]:
-            out.append(x)
-    if len(out) == 1:
-        out.append(arena_numel)
-    return out
+def _all_gather_inplace(flat: torch.Tensor, rank: int, cnt: int) -> None:
+    """Slice [rank*cnt, (rank+1)*cnt) of ``flat`` from every rank -> everyone, in place."""
+    if flat.is_cuda:
+        rt.comm().all_gather(flat, flat[rank * cnt: (rank + 1) * cnt])
+    else:
+        dist.all_gather_into_tensor(flat, flat[rank * cnt: (rank + 1) * cnt].clone())
 
 
-def _make_py_reducer(ddp: DistributedDataParallel):
-    """Reducer over torch.distributed (gloo) for CPU runs. Uses the native C++ Reducer logic
-    when the extension is importable (it is, on every supported machine), else a Python twin."""
-    arena = ddp.arena
-    world = ddp.world_size
+class _CpuSyncOps:
+    """SyncOps (csrc/reducer.h) for CPU arenas: torch.distributed/gloo collectives and torch math.
 
-    def launch(bucket, begin, end):
-        t = arena.grad[begin:end]
-        if world > 1:
-            t.div_(world)  # DDP semantics: divide, then SUM (gloo has no AVG)
-            ddp._works.append(dist.all_reduce(t, async_op=True))
+    The C++ SyncBackend drives it exactly as it drives RcclOps on MI355X, so the gloo tests run
+    the production bucket / shard / tail / clip algorithm at any world size. The optimizer math
+    mirrors csrc/optim_elem.h (torch's SGD / Adam semantics) and reads its scalars from the same
+    hyper-block layout, advanced by opt_begin like opt_step_begin_kernel advances the device one.
+    With TDP_POISON_UNOWNED=1 the gradient slices a rank does not own after a reduce-scatter are
+    overwritten with NaN, so a test fails if anything reads them."""
 
-    def wait():
-        for w in ddp._works:
-            w.wait()
-        ddp._works.clear()
+    def __init__(self, ddp, compression: int = 0):
+        self._ddp = weakref.ref(ddp)
+        self.arena = ddp.arena
+        self.W, self.r = ddp.world_size, ddp.rank
+        self.compression = compression
+        self.kind = 0
+        self.blk = None
+        self.clip_block = None
+        self.bufs = {}
+        self.poison = os.environ.get("TDP_POISON_UNOWNED", "0") == "1"
+        if self.poison:
+            # alignment gaps between parameters hold no gradient: they must stay zero (no
+            # backward ever rewrites them, so NaN left there would leak into later reductions)
+            keep = torch.ones(self.arena.numel, dtype=torch.bool)
+            for o, n in zip(self.arena.offsets, self.arena.numels):
+                keep[o: o + n] = False
+            self._gaps = keep.nonzero().flatten()
 
-    def zero(begin, end):
-        arena.grad[begin:end].zero_()
+    def set_fused(self, opt, blk, bufs):
+        from ..optim.fused import SGD
 
-    try:
-        C = native()
-        backend = C.PyBackend(launch, wait, zero)
-        return C.Reducer(arena.offsets, arena.numels, ddp._bounds, backend)
-    except Exception:  # pragma: no cover - extension missing on a CPU-only box
-        return _PyReducer(arena.offsets, arena.numels, ddp._bounds, launch, wait, zero)
+        g = opt.param_groups[0]
+        self.kind = 1 if isinstance(opt, SGD) else 2
+        self.blk, self.bufs = blk, dict(bufs)
+        self.flags = dict(nesterov=g.get("nesterov", False), maximize=g["maximize"],
+                          amsgrad=g.get("amsgrad", False),
+                          decoupled=getattr(opt, "_decoupled", False),
+                          momentum=g.get("momentum", 0.0) != 0)
 
+    # collectives (DDP semantics: divide by W, then SUM -- gloo has no AVG)
+    def _wire(self, t):
+        if self.compression:
+            t.copy_(t.bfloat16().float())
 
-class _PyReducer:
-    def __init__(self, offsets, numels, bounds, launch, wait, zero):
-        self.offsets, self.numels, self.bounds = offsets, numels, bounds
-        self._launch, self._wait, self._zero = launch, wait, zero
-        nb = len(bounds) - 1
-        self.param_buckets = []
-        self.nparams = [0] * nb
-        for o, n in zip(offsets, numels):
-            bs = [b for b in range(nb) if n and bounds[b] < o + n and bounds[b + 1] > o]
-            self.param_buckets.append(bs)
-            for b in bs:
-                self.nparams[b] += 1
-        self.expecting = False
-        self.iteration = 0
-        self.num_buckets = nb
-        self._order = []
+    def all_reduce_avg(self, off, n):
+        t = self.arena.grad[off: off + n]
+        self._wire(t)
+        if self.W > 1:
+            t.div_(self.W)
+            dist.all_reduce(t)
 
-    def prepare_for_backward(self):
-        self.pending = list(self.nparams)
-        self.ready = [n == 0 for n in self.nparams]
-        self.pready = [False] * len(self.offsets)
-        self.next = 0
-        self.expecting = True
+    def reduce_scatter_avg(self, off, cnt):
+        W, r = self.W, self.r
+        full = self.arena.grad[off: off + W * cnt]
+        src = full.div(W)
+        out = torch.empty(cnt, dtype=full.dtype)
+        dist.reduce_scatter_tensor(out, src)
+        full[r * cnt: (r + 1) * cnt].copy_(out)
+        if self.poison:
+            full[: r * cnt].fill_(float("nan"))
+            full[(r + 1) * cnt:].fill_(float("nan"))
+            self.arena.grad[self._gaps] = 0.0
 
-    def mark_ready(self, p, gpu=False):
-        if not self.expecting:
-            return
-        if self.pready[p]:
-            raise RuntimeError("Expected to mark a variable ready only once")
-        self.pready[p] = True
-        if self.iteration == 0:
-            self._order.append(p)
-        for b in self.param_buckets[p]:
-            self.pending[b] -= 1
-            if self.pending[b] == 0:
-                self.ready[b] = True
-        self._launch_ready()
+    def all_gather_params(self, off, cnt):
+        _all_gather_inplace(self.arena.data[off: off + self.W * cnt], self.r, cnt)
 
-    def _launch_ready(self):
-        while self.next < self.num_buckets and self.ready[self.next]:
-            self._launch(self.next, self.bounds[self.next], self.bounds[self.next + 1])
-            self.next += 1
+    def zero_grads(self, off, n):
+        self.arena.grad[off: off + n].zero_()
 
-    def finalize(self, gpu=False, allow_unused=False):
-        if not self.expecting:
-            return
-        unready = [i for i, r in enumerate(self.pready) if not r and self.numels[i]]
-        if unready and not allow_unused:
-            raise RuntimeError(f"parameters {unready} received no gradient; pass "
-                               "find_unused_parameters=True")
-        for p in unready:
-            self._zero(self.offsets[p], self.offsets[p] + self.numels[p])
-            self.pready[p] = True
-            for b in self.param_buckets[p]:
-                self.pending[b] -= 1
-                if self.pending[b] == 0:
-                    self.ready[b] = True
-        self._launch_ready()
-        self._wait()
-        self.expecting = False
-        self.iteration += 1
+    # optimizer (csrc/optim_elem.h semantics, scalars from the hyper block)
+    def opt_begin(self):
+        from ..optim.fused import hyper_slots
 
-    def bucket_bounds(self):
-        return list(self.bounds)
+        S, b = hyper_slots(), self.blk
+        step = int(b.view(torch.int32)[S["step"]]) + 1
+        b.view(torch.int32)[S["step"]] = step
+        b[S["first"]] = b[S["first_next"]]
+        b[S["first_next"]] = 0.0
+        b[S["scale"]] = 1.0
+        b[S["sumsq"]] = 0.0
+        if self.kind == 2:
+            b1, b2 = float(b[S["mom"]]), float(b[S["damp"]])
+            b[S["bc1"]] = 1.0 - b1 ** step
+            b[S["bc2"]] = (1.0 - b2 ** step) ** 0.5
 
-    def ready_order(self):
-        return list(self._order)
+    def opt_update(self, ranges):
+        from ..optim.fused import hyper_slots
 
-    def last_comm_ms(self):
-        return -1.0
+        S, b, f = hyper_slots(), self.blk, self.flags
+        lr, wd, scale = float(b[S["lr"]]), float(b[S["wd"]]), float(b[S["scale"]])
+        P, G = self.arena.data, self.arena.grad
+        with torch.no_grad():
+            for lo, hi in ranges:
+                p, g = P[lo:hi], G[lo:hi] * scale
+                if f["maximize"]:
+                    g = -g
+                if self.kind == 1:
+                    if wd:
+                        g = g.add(p, alpha=wd)
+                    if f["momentum"]:
+                        mom, damp = float(b[S["mom"]]), float(b[S["damp"]])
+                        buf = self.bufs["momentum_buffer"][lo:hi]
+                        if float(b[S["first"]]):
+                            buf.copy_(g)
+                        else:
+                            buf.mul_(mom).add_(g, alpha=1 - damp)
+                        g = g.add(buf, alpha=mom) if f["nesterov"] else buf
+                    p.add_(g, alpha=-lr)
+                else:
+                    b1, b2, eps = float(b[S["mom"]]), float(b[S["damp"]]), float(b[S["eps"]])
+                    bc1, bc2 = float(b[S["bc1"]]), float(b[S["bc2"]])
+                    if wd:
+                        if f["decoupled"]:
+                            p.mul_(1 - lr * wd)
+                        else:
+                            g = g.add(p, alpha=wd)
+                    m, v = self.bufs["exp_avg"][lo:hi], self.bufs["exp_avg_sq"][lo:hi]
+                    m.lerp_(g, 1 - b1)
+                    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                    vv = v
+                    if f["amsgrad"]:
+                        vm = self.bufs["max_exp_avg_sq"][lo:hi]
+                        torch.maximum(vm, v, out=vm)
+                        vv = vm
+                    p.addcdiv_(m, vv.sqrt() / bc2 + eps, value=-lr / bc1)
+
+    # clipping
+    def _block(self, which):
+        return self.blk if which == 0 else self.clip_block
+
+    def clip_begin(self, which):
+        from ..optim.fused import hyper_slots
+
+        S, b = hyper_slots(), self._block(which)
+        b[S["sumsq"]] = 0.0
+        b[S["scale"]] = 1.0
+
+    def grad_sumsq(self, which, ranges):
+        from ..optim.fused import hyper_slots
+
+        S, b = hyper_slots(), self._block(which)
+        G = self.arena.grad
+        for lo, hi in ranges:
+            b[S["sumsq"]] += G[lo:hi].pow(2).sum()
+
+    def sumsq_all_reduce(self, which):
+        from ..optim.fused import hyper_slots
+
+        S, b = hyper_slots(), self._block(which)
+        if self.W > 1:
+            t = b[S["sumsq"]: S["sumsq"] + 1].clone()
+            dist.all_reduce(t)
+            b[S["sumsq"]] = t[0]
+
+    def clip_coef(self, which):
+        from ..optim.fused import hyper_slots
+
+        S, b = hyper_slots(), self._block(which)
+        norm = float(b[S["sumsq"]]) ** 0.5
+        b[S["norm"]] = norm
+        mx = float(b[S["max_norm"]])
+        b[S["scale"]] = min(1.0, mx / (norm + 1e-6)) if mx > 0 else 1.0
+
+    def scale_grads(self, which, ranges):
+        from ..optim.fused import hyper_slots
+
+        a = float(self._block(which)[hyper_slots()["scale"]])
+        for lo, hi in ranges:
+            self.arena.grad[lo:hi].mul_(a)
 
 
 DDP = DistributedDataParallel

@@ -15,10 +15,15 @@ slows every kernel (the reducer therefore runs eager collectives on the compute 
 
 Contract (as for torch.cuda.graphs): the captured function reads its varying inputs from static
 tensors the caller refreshes before ``replay`` (here: a device index tensor for the batch);
-hyper-parameters are baked in at capture (re-capture after an LR change); optimizer state and
-gradients live in fixed buffers (the flat arenas), so replay updates them in place. The
-``warmup`` steps really execute; the capturing call only records (it does not advance the
-model), so after construction the model has taken exactly ``warmup`` steps.
+optimizer state and gradients live in fixed buffers (the flat arenas), so replay updates them in
+place. Per-step optimizer scalars are NOT baked in: every tdp optimizer keeps lr, momentum /
+betas, weight decay, the Adam step count and bias corrections in a device hyper block
+(csrc/kernels.h HyperSlot) that the kernels read; ``replay`` first pushes host-side changes
+(an LR scheduler's step) into those blocks with stream-ordered copies, and the captured
+``opt_step_begin`` kernel advances the step count on the device. Structural changes (momentum
+switched on/off, amsgrad, a new parameter group) still need a re-capture. The ``warmup`` steps
+really execute; the capturing call only records (it does not advance the model), so after
+construction the model has taken exactly ``warmup`` steps.
 """
 from __future__ import annotations
 
@@ -43,6 +48,9 @@ class CapturedStep:
         torch.cuda.synchronize()
 
     def replay(self):
+        from ..optim.fused import sync_all_hyper
+
+        sync_all_hyper()  # LR schedules etc. reach the captured kernels through the hyper blocks
         self.graph.replay()
         return self.output
 
