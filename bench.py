@@ -13,8 +13,19 @@ bucketed RCCL gradient reduction -> optimizer step. Weak scaling: per-GPU work i
   python bench.py --impl torch                      # stock torch DDP + torch.optim (comparison)
   python bench.py --api accelerate                  # the same step through Accelerator.prepare()
 
-Execution: eager by default (GPU-bound with the native kernels); ``--graph`` replays a captured
-hipGraph of the whole step instead.
+Execution: at world size > 1 the whole step is captured into a hipGraph and replayed, so the
+bucket collectives run on the communicator's side stream and overlap backward (inside a graph the
+cross-stream dependency is free; eagerly it slows every launch, profiles/side_stream_eager.md).
+Optimizer scalars live in device hyper blocks, so the captured step stays exact (LR changes,
+Adam's step count). World size 1 runs eagerly (nothing to overlap: no collective at all, the
+optimizer runs in the weight-gradient GEMM epilogues). ``--graph`` / ``--eager`` force a mode.
+
+Diagnostics (after the timed region, in the JSON line's "diagnostics"): at world size > 1 the
+collectives of one step alone (``comm_ms``), the same captured step with its collectives turned
+into no-ops (``compute_ms``), the share of the collective time hidden behind compute
+(``overlap_pct``) and a short RCCL bus-bandwidth sweep; at world size 1 the single-GPU rehearsal
+of the multi-GPU schedule (``rehearsal_ms``: RCCL collectives kept, per-bucket fused update,
+captured step).
 
 Timing: W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
 both sides; the max over ranks is reported; rank 0 prints one JSON line. Native libraries (RCCL
@@ -35,11 +46,12 @@ import torch
 
 METRIC = "samples/sec (whole node) toy-MLP DDP at 1/2/4/8 MI355X; scaling efficiency"
 ROOT = Path(__file__).resolve().parent
-# In eager execution the bucket collectives run on the compute stream (csrc/reducer.cpp,
-# profiles/side_stream_eager.md), so they serialise with backward anyway: fewer, larger
-# collectives move the same bytes at a higher RCCL bus bandwidth. Under --graph they overlap
-# backward on the comm stream, so DDP's 25 MiB buckets are kept there.
-EAGER_MULTI_GPU_BUCKET_MB = 256.0
+# Bucket plan (csrc/reducer.cpp compute_bucket_bounds): DDP's 25 MiB cap and 1 MiB first bucket;
+# a parameter larger than the cap is one bucket, and the small leftovers in front of it ride along
+# (toy MLP: {fc3, fc2} 64.2 MiB ready after fc2's weight gradient, overlapping fc1's backward;
+# {fc1} 144 MiB at the end) -- torch DDP's own post-rebuild plan, without its 1-MiB collectives.
+# Splitting fc1 (--split-mb) buys no overlap: its whole gradient comes from one GEMM.
+DIAG_SWEEP_MB = (1, 8, 32, 128)
 
 
 def _private_stdout():
@@ -62,6 +74,10 @@ def parse():
                          "Accelerator.prepare() facade (BASELINE.json config 4)")
     ap.add_argument("--optim", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--split-mb", type=float, default=None,
+                    help="cut parameters larger than this into buckets of this size")
+    ap.add_argument("--no-diag", action="store_true",
+                    help="skip the post-measurement diagnostics (comm / compute / rehearsal)")
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
     ap.add_argument("--model", choices=["toy_mlp", "alexnet", "resnet50"], default="toy_mlp",
                     help="toy_mlp = the headline config; alexnet / resnet50 = the CNN configs")
@@ -73,12 +89,12 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--graph", action="store_true",
-                    help="tdp: capture the whole step into a hipGraph and replay it (bucket "
-                         "collectives then overlap backward on a side stream). Off by default: "
-                         "with the native kernels the eager step is GPU-bound and measured as "
-                         "fast on one GPU (profiles/bench/mode*.json), and eager keeps RCCL out "
-                         "of stream capture on multi-GPU runs")
-    ap.add_argument("--eager", action="store_true", help="tdp: run eagerly (the default)")
+                    help="tdp: capture the whole step into a hipGraph and replay it (the default "
+                         "at world size > 1: bucket collectives then overlap backward on the comm "
+                         "stream)")
+    ap.add_argument("--eager", action="store_true",
+                    help="tdp: run eagerly (the default at world size 1; collectives then run on "
+                         "the compute stream without overlap)")
     ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
                     help="tdp: apply the optimizer inside the gradient reduction (DDP "
                          "register_fused_optimizer): with world_size > 1 per bucket and sharded "
@@ -92,7 +108,7 @@ def parse():
 def baseline_for(n_gpus: int, impl: str, syncbn: bool, model: str = "toy_mlp"):
     """Stock torch DDP number on MI355X for the same config (bench_baseline.json), if measured."""
     f = ROOT / "bench_baseline.json"
-    if impl != "tdp" or not f.exists():
+    if impl != "tdp" or not f.exists() or not torch.cuda.is_available():
         return None
     try:
         tab = json.loads(f.read_text())
@@ -111,6 +127,58 @@ MODEL_DESC = {
 }
 
 
+def _time_steps(step, n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1000.0 / n
+
+
+def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
+    """Post-measurement evidence for the scaling curve (module doc). Every rank runs the same
+    collectives in the same order; rank 0 reports."""
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commbench
+    from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
+
+    n = max(10, min(a.steps, 50))
+    out = {"mode": "graph" if graph else "eager"}
+    if world > 1 or os.environ.get("TDP_DIAG_MULTI") == "1":  # (the latter: test at world 1)
+        comm_ms = commbench.ddp_comm_ms(ddp, iters=10)
+        # the same step with its collectives turned into no-ops (re-captured when graphed)
+        ddp._ops.skip_collectives = True
+        try:
+            st = step
+            if graph:
+                st = try_capture(getattr(step, "raw", step), warmup=2, log=lambda m: None)
+            barrier()
+            compute_ms = _time_steps(st, n)
+        finally:
+            ddp._ops.skip_collectives = False
+        t = torch.tensor([comm_ms, compute_ms], dtype=torch.float64, device=rt.device())
+        rt.all_reduce(t, "max")
+        comm_ms, compute_ms = (float(v) for v in t.tolist())
+        # share of the collective time that ran concurrently with compute
+        hidden = max(0.0, comm_ms + compute_ms - step_ms)
+        out.update(comm_ms=round(comm_ms, 4), compute_ms=round(compute_ms, 4),
+                   overlap_pct=round(100.0 * min(hidden, comm_ms) / comm_ms, 1)
+                   if comm_ms > 0 else None)
+        sweep = commbench.collective_busbw([m * 2 ** 20 for m in DIAG_SWEEP_MB], iters=5,
+                                           warmup=2)
+        out["busbw_GBps"] = {f"{r['op']}@{r['bytes'] >> 20}MiB": r["busbw_GBps"] for r in sweep}
+    elif build_rehearsal is not None:
+        from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+        d2, st = build_rehearsal()
+        g = CapturedStep(st, warmup=3)
+        out["rehearsal_ms"] = round(_time_steps(g.replay, n), 4)
+        out["rehearsal_buckets"] = len(d2._bounds) - 1
+        del g, d2
+    return out
+
+
 def main():
     a = parse()
     out = _private_stdout()
@@ -123,7 +191,8 @@ def main():
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_gpu = torch.cuda.is_available() and not a.cpu
-    graph = use_gpu and a.graph and not a.eager
+    graph = use_gpu and not a.eager and (a.graph or world > 1) and a.impl == "tdp" and \
+        a.api == "ddp"
     in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
     fused = False
 
@@ -147,8 +216,6 @@ def main():
         if a.syncbn:
             model = tdp.nn.convert_sync_batchnorm(model)
         bucket_mb = a.bucket_mb
-        if bucket_mb is None and world > 1 and not graph:
-            bucket_mb = EAGER_MULTI_GPU_BUCKET_MB
 
         def make_opt(params):
             if a.optim == "sgd":
@@ -187,7 +254,7 @@ def main():
                 return loss
         else:
             ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
-                          bucket_cap_mb=bucket_mb,
+                          bucket_cap_mb=bucket_mb, split_bucket_mb=a.split_mb,
                           grad_compression=None if a.compression == "none" else a.compression)
             opt = make_opt(ddp.parameters())
             if use_gpu and want_fused:
@@ -276,7 +343,29 @@ def main():
             it[0] = iter(loader)
             return next(it[0])
 
+    build_rehearsal = None
     if a.impl == "tdp" and a.api == "ddp":
+        def build_rehearsal():
+            """World size 1: the multi-GPU schedule on one GPU (RCCL collectives kept at world
+            size 1, per-bucket fused update instead of the GEMM epilogue, captured step)."""
+            torch.manual_seed(99)
+            m2 = (ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
+                  if a.model == "toy_mlp" else build_model(a.model, device=dev))
+            if a.syncbn:
+                m2 = tdp.nn.convert_sync_batchnorm(m2)
+            d2 = tdp.DDP(m2, device_ids=[dev.index], bucket_cap_mb=bucket_mb,
+                         split_bucket_mb=a.split_mb, force_collective=True)
+            o2 = make_opt(d2.parameters())
+            if want_fused:
+                d2.register_fused_optimizer(o2)
+
+            def st():
+                x, y = gather_batch(data.x, data.y, idx_static)
+                o2.zero_grad(set_to_none=True)
+                loss_fn(d2(x), y).backward()
+                o2.step()
+            return d2, st
+
         # batches are gathered on the device by the sampler's indices (one H2D copy per epoch);
         # a captured graph reads them from a static index tensor, eager steps from a slice
         idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
@@ -314,6 +403,7 @@ def main():
         def step():
             advance()
             return run()
+        step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
     else:
         def step():
             return run_step(*next_batch())
@@ -341,6 +431,13 @@ def main():
     ms = dt * 1000.0 / a.steps
     value = a.batch * world * a.steps / dt
     base = baseline_for(world, a.impl, a.syncbn, a.model)
+    final_loss = round(float(loss.item()), 5)
+    diag = None
+    if a.impl == "tdp" and a.api == "ddp" and use_gpu and not a.no_diag:
+        try:
+            diag = diagnostics(a, ddp, step, ms, world, graph, barrier, build_rehearsal)
+        except Exception as e:  # diagnostics never cost the measurement
+            diag = {"error": repr(e)[:300]}
     if rank == 0:
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
                                           bn=", +SyncBatchNorm" if a.syncbn else "")
@@ -372,9 +469,14 @@ def main():
                 "impl": impl,
                 "optimizer": a.optim + (" (fused into the gradient reduction)"
                                         if a.impl == "tdp" and fused else ""),
-                "final_loss": round(float(loss.item()), 5),
+                "final_loss": final_loss,
+                "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)
+                              for i in range(len(ddp._bounds) - 1)]
+                if a.impl == "tdp" and a.api == "ddp" else None,
             },
         }
+        if diag is not None:
+            rec["diagnostics"] = diag
         print(json.dumps(rec), file=out, flush=True)
     finish()
 

@@ -263,3 +263,16 @@ def test_in_reduction_clip_gpu(pg, mode, monkeypatch):
         torch.testing.assert_close(ddp.last_grad_norm(), n, atol=1e-5, rtol=1e-4)
     for p, r in zip(model.parameters(), params):
         torch.testing.assert_close(p.detach(), r.detach(), atol=2e-5, rtol=1e-4)
+
+
+def test_commbench_at_world1(pg):
+    """parallel/commbench.py (bench.py diagnostics, scripts/rccl_sweep.py) runs end to end."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commbench
+
+    rows = commbench.collective_busbw([4096, 1 << 20], iters=2, warmup=1)
+    assert len(rows) == 6 and all(r["ms"] > 0 for r in rows)
+    m = ToyMLP(in_features=256, hidden=(128,), num_classes=10, device="cuda")
+    d = tdp.DDP(m, device_ids=[0])
+    assert commbench.ddp_comm_ms(d, iters=2, warmup=1) > 0

@@ -995,6 +995,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              o.fused.adam = AdamHyper{0.f, 0.f, 0.f, 0.f, 0.f, amsgrad, maximize, decoupled,
                                       1.f, 1.f, 1.f, o.fused.hyper};
            })
+      .def_readwrite("skip_collectives", &RcclOps::skip_collectives)
       .def("clear_fused", [](RcclOps& o) { o.fused = FusedOptimizer{}; })
       .def("set_clip_block", [](RcclOps& o, c10::optional<Tensor> blk) {
         o.clip_block = block_ptr(blk);

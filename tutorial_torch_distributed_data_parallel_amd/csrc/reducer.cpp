@@ -26,7 +26,7 @@ RcclOps::~RcclOps() {
 }
 
 void RcclOps::all_reduce_avg(int64_t off, int64_t n, hipStream_t s) {
-  if (n <= 0) return;
+  if (n <= 0 || skip_collectives) return;
   float* g = grad_ + off;
   if (compression_ == Compression::BF16) {
     uint16_t* w = wire_ + off;
@@ -39,14 +39,14 @@ void RcclOps::all_reduce_avg(int64_t off, int64_t n, hipStream_t s) {
 }
 
 void RcclOps::reduce_scatter_avg(int64_t off, int64_t cnt, hipStream_t s) {
-  if (cnt <= 0) return;
+  if (cnt <= 0 || skip_collectives) return;
   float* g = grad_ + off;
   // in place: RCCL's recvbuff == sendbuff + rank * recvcount
   comm_->reduce_scatter(g, g + (int64_t)comm_->rank() * cnt, (size_t)cnt, ncclFloat32, ncclAvg, s);
 }
 
 void RcclOps::all_gather_params(int64_t off, int64_t cnt, hipStream_t s) {
-  if (cnt <= 0) return;
+  if (cnt <= 0 || skip_collectives) return;
   float* p = param_ + off;
   comm_->all_gather(p + (int64_t)comm_->rank() * cnt, p, (size_t)cnt, ncclFloat32, s);
 }
@@ -113,7 +113,7 @@ void RcclOps::grad_sumsq(int b, const Ranges& r, hipStream_t s) {
 
 void RcclOps::sumsq_all_reduce(int b, hipStream_t s) {
   float* blk = block(b);
-  if (comm_->world() > 1)
+  if (comm_->world() > 1 && !skip_collectives)
     comm_->all_reduce(blk + kHSumsq, blk + kHSumsq, 1, ncclFloat32, ncclSum, s);
 }
 
@@ -411,13 +411,18 @@ std::vector<int64_t> Reducer::compute_bucket_bounds(const std::vector<int64_t>& 
   for (size_t i = 0; i < offsets.size(); ++i) {
     const int64_t cap = (b.size() == 1 ? first_cap_bytes : cap_bytes);
     const int64_t bytes = numels[i] * elem_size;
-    if (cur_bytes > 0 && cur_bytes + bytes > cap) {
+    // A partial bucket smaller than the first-bucket cap in front of a parameter that alone
+    // overflows the cap rides along with it instead of going out as its own collective: such a
+    // tiny collective costs a full RCCL latency (tens of us on xGMI) for no overlap gained --
+    // the big parameter's gradient lands right after it (toy MLP: fc3 + fc2.bias join fc2.weight).
+    const bool merge_small = bytes > cap && cur_bytes > 0 && cur_bytes < first_cap_bytes;
+    if (cur_bytes > 0 && cur_bytes + bytes > cap && !merge_small) {
       b.push_back(offsets[i]);
       cur_bytes = 0;
     }
     if (split > 0 && numels[i] > split) {
       // a large parameter gets its own buckets, cut every `split` elements
-      if (b.back() != offsets[i]) b.push_back(offsets[i]);
+      if (!merge_small && b.back() != offsets[i]) b.push_back(offsets[i]);
       for (int64_t s = split; s < numels[i]; s += split) b.push_back(offsets[i] + s);
       const int64_t tail = offsets[i] + numels[i];
       if (i + 1 < offsets.size()) b.push_back(tail);

@@ -127,6 +127,8 @@ class RcclOps : public SyncOps {
   FusedOptimizer fused;
   float* clip_block = nullptr;  // DDP-owned hyper block for LOCAL clipping
   Compression compression() const { return compression_; }
+  // measurement only (bench.py compute-only rehearsal): collectives become no-ops
+  bool skip_collectives = false;
   std::shared_ptr<Communicator> comm() const { return comm_; }
 
  private:
@@ -205,7 +207,9 @@ class Reducer {
 
   // Boundaries (element offsets, first 0, last = arena numel) for parameters laid out at
   // `offsets` (ascending). Small parameters are grouped up to cap_bytes (first_cap_bytes for the
-  // first bucket); a parameter larger than split_bytes (> 0) is cut into split_bytes pieces.
+  // first bucket); a parameter larger than split_bytes (> 0) is cut into split_bytes pieces; a
+  // partial bucket under first_cap_bytes is merged into a following parameter that alone
+  // overflows the cap.
   static std::vector<int64_t> compute_bucket_bounds(const std::vector<int64_t>& offsets,
                                                     const std::vector<int64_t>& numels,
                                                     int64_t arena_numel, int elem_size,

@@ -1,0 +1,96 @@
+"""RCCL bus-bandwidth measurements over the native communicator (SURVEY.md §5.8, §4.2 "comm" tier).
+
+``collective_busbw`` times all-reduce / reduce-scatter / all-gather back to back on the current
+stream and reports nccl-tests' bus bandwidth (algbw x 2(n-1)/n for all-reduce, x (n-1)/n for the
+other two), which is what the 7 point-to-point xGMI links of a rank bound. ``ddp_comm_ms`` times
+exactly the collectives one DDP step issues (the bucket plan of a model, sharded or not) with no
+compute around them: the denominator of the overlap figure bench.py reports.
+Used by ``scripts/rccl_sweep.py`` and, at world size > 1, by ``bench.py`` itself (the driver's
+multi-GPU run is where the measurements come from).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import runtime as rt
+
+
+def _time(fn, iters: int, warmup: int) -> float:
+    for _ in range(warmup):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def collective_busbw(sizes_bytes, ops=("all_reduce", "reduce_scatter", "all_gather"),
+                     iters: int = 10, warmup: int = 3, dtype=torch.float32) -> list[dict]:
+    comm = rt.comm()
+    if comm is None:
+        raise RuntimeError("collective_busbw needs the RCCL communicator")
+    n, dev = comm.world, rt.device()
+    esz = torch.tensor([], dtype=dtype).element_size()
+    out = []
+    for size in sizes_bytes:
+        count = max(size // esz // n * n, n)
+        buf = torch.ones(count, dtype=dtype, device=dev)
+        part = buf[: count // n]
+        for op in ops:
+            if op == "all_reduce":
+                ms = _time(lambda: comm.all_reduce(buf, "sum"), iters, warmup)
+                factor = 2.0 * (n - 1) / n
+            elif op == "reduce_scatter":
+                ms = _time(lambda: comm.reduce_scatter(part, buf, "sum"), iters, warmup)
+                factor = (n - 1) / n
+            else:
+                ms = _time(lambda: comm.all_gather(buf, part), iters, warmup)
+                factor = (n - 1) / n
+            nbytes = count * esz
+            algbw = nbytes / (ms * 1e-3) / 1e9
+            out.append({"op": op, "bytes": int(nbytes), "ms": round(ms, 4),
+                        "algbw_GBps": round(algbw, 2), "busbw_GBps": round(algbw * factor, 2),
+                        "n": n})
+        del buf
+    return out
+
+
+def ddp_comm_ms(ddp, iters: int = 10, warmup: int = 3) -> float:
+    """Milliseconds per step of the bucket collectives of ``ddp`` alone (its bucket bounds, its
+    sharded or all-reduce schedule), on scratch buffers of the arena's size."""
+    comm = rt.comm()
+    if comm is None or not ddp._gpu:
+        return 0.0
+    W, r = ddp.world_size, ddp.rank
+    g = torch.zeros_like(ddp.arena.grad)
+    p = torch.zeros_like(ddp.arena.data)
+    sharded = bool(ddp._fused_opt is not None and ddp._fused_shard)
+    plan = []
+    b = ddp._bounds
+    for i in range(len(b) - 1):
+        lo, hi = b[i], b[i + 1]
+        if sharded:
+            s0, s1 = ddp._backend.owned_shard(lo, hi)
+            cnt = s1 - s0
+            plan.append((lo, hi, cnt))
+        else:
+            plan.append((lo, hi, 0))
+
+    def step():
+        for lo, hi, cnt in plan:
+            if cnt > 0:
+                comm.reduce_scatter(g[lo + r * cnt: lo + (r + 1) * cnt], g[lo: lo + W * cnt],
+                                    "avg")
+                if lo + W * cnt < hi:
+                    comm.all_reduce(g[lo + W * cnt: hi], "avg")
+                comm.all_gather(p[lo: lo + W * cnt], p[lo + r * cnt: lo + (r + 1) * cnt])
+            else:
+                comm.all_reduce(g[lo:hi], "avg")
+
+    ms = _time(step, iters, warmup)
+    del g, p
+    return ms

@@ -59,7 +59,8 @@ class DistributedDataParallel(nn.Module):
                  check_reduction: bool = False, gradient_as_bucket_view: bool = True,
                  static_graph: bool = False, first_bucket_cap_mb: float | None = None,
                  split_bucket_mb: float | None = None, grad_compression: str | None = None,
-                 timing: bool = False, check_replicas_every: int | None = None):
+                 timing: bool = False, check_replicas_every: int | None = None,
+                 force_collective: bool = False):
         super().__init__()
         if process_group is not None:
             raise NotImplementedError("sub-groups are not supported: DDP uses the world group")
@@ -111,7 +112,9 @@ class DistributedDataParallel(nn.Module):
         self._clip_global = None   # max_norm of the in-reduction global-norm clip (fused optimizer)
         self._clip_local = None    # max_norm of the per-rank clip before aggregation
         self._clip_block = None
-        self._force_collective = False
+        # issue the collectives even at world size 1 (the single-GPU rehearsal of the multi-GPU
+        # schedule; TDP_FORCE_COLLECTIVE=1 does the same from the environment)
+        self._force_collective = bool(force_collective)
         self._epi_on = False
         self._epi_index = {}
         self._uses = {}            # id(param) -> forward uses in the current iteration
