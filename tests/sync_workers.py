@@ -228,3 +228,67 @@ def shared_parameter(rank, out_dir):
                                    msg=lambda m: f"{n}: {m}")
     rddp = None  # noqa: F841
     _teardown()
+
+
+def logger_stats(rank, out_dir):
+    """DDP Logger: sampled forward / backward / comm times and bucket info."""
+    tdp.init_process_group("gloo")
+    torch.manual_seed(0)
+    ddp = tdp.DDP(ToyMLP(**DIMS), timing=True, **BUCKETS)
+    for step in range(3):
+        x, y = _batch(rt.get_rank(), step)
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+    info = ddp._get_ddp_logging_data()
+    assert info["sampled_iterations"] == 3, info
+    assert info["avg_forward_compute_time_ms"] > 0 and info["avg_backward_compute_time_ms"] > 0
+    assert info["avg_backward_exposed_comm_time_ms"] >= 0
+    assert info["num_buckets"] == len(info["bucket_sizes"]) >= 4
+    assert info["head_of_line_waits"] == 0  # a sequential model: buckets become ready in order
+    tdp.destroy_process_group()
+
+
+def bucket_rebuild(rank, out_dir, fused=True):
+    """Bucket rebuild (torch DDP ``_rebuild_buckets``): layers registered in a different order
+    than they run, one bucket per parameter -> head-of-line waits in iteration 0 -> the arena is
+    re-laid out in ready order, and training (sharded fused Adam at W=2) still matches torch."""
+    tdp.init_process_group("gloo")
+    r = rt.get_rank()
+
+    class Shuffled(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = tdp.nn.Linear(12, 40, relu=True)
+            self.c = tdp.nn.Linear(40, 5)          # registered second, runs last
+            self.b = tdp.nn.Linear(40, 40, relu=True)
+
+        def forward(self, x):
+            return self.c(self.b(self.a(x)))
+
+    torch.manual_seed(0)
+    model = Shuffled()
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, bucket_cap_mb=100 / 2 ** 20, first_bucket_cap_mb=100 / 2 ** 20)
+    opt = tdp.optim.Adam(ddp.parameters(), lr=1e-2)
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    if fused:
+        ddp.register_fused_optimizer(opt)
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    for step in range(5):
+        g = torch.Generator().manual_seed(100 * step + r)
+        x, y = torch.randn(8, 12, generator=g), torch.randint(0, 5, (8,), generator=g)
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        ropt.zero_grad()
+        F.cross_entropy(rddp(x), y).backward()
+        ropt.step()
+        if step == 0:
+            assert ddp.reducer.head_of_line_waits > 0
+            assert ddp._rebuild_order is not None
+        if step == 1:
+            assert ddp._rebuilt and ddp.reducer.head_of_line_waits == 0
+    assert ddp._get_ddp_logging_data()["has_rebuilt_buckets"] == 1
+    _check_close(model, ref, f"after rebuild fused={fused}")
+    _check_replicas(model)
+    rddp = None  # noqa: F841
+    _teardown()

@@ -51,3 +51,12 @@ def test_comm_hook_keeps_fused_state(tmp_path):
 
 def test_shared_parameter_gradient(tmp_path):
     run(SW.shared_parameter, tmp_path, n=2)
+
+
+def test_ddp_logger_runtime_stats(tmp_path):
+    run(SW.logger_stats, tmp_path, n=2)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_bucket_rebuild_from_ready_order(tmp_path, fused):
+    run(SW.bucket_rebuild, tmp_path, n=2, fused=fused)

@@ -173,6 +173,9 @@ class _FusedBase(Optimizer):
             bufs = {k: arena.new_state() for k in keys}
             self._flat_bufs[id(arena)] = bufs
             fresh = True
+            if not hasattr(arena, "_optimizers"):
+                arena._optimizers = weakref.WeakSet()
+            arena._optimizers.add(self)  # a DDP bucket rebuild re-lays the state out too
         for i, p in enumerate(arena.params):
             st = self.state[p]
             for k in keys:
@@ -185,6 +188,19 @@ class _FusedBase(Optimizer):
                     st[k] = view
                     fresh = False
         return bufs, fresh
+
+    def _relayout(self, arena, remap) -> None:
+        """The arena was re-laid out (DDP bucket rebuild): move the flat state buffers the same
+        way and re-point the per-parameter state views."""
+        bufs = self._flat_bufs.get(id(arena))
+        if not bufs:
+            return
+        for k in list(bufs):
+            bufs[k] = remap(bufs[k])
+        for i, p in enumerate(arena.params):
+            st = self.state[p]
+            for k, buf in bufs.items():
+                st[k] = arena.state_view(buf, i)
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)

@@ -79,6 +79,45 @@ class ParamArena:
         """A zeroed buffer with the arena's layout (optimizer state: momentum, exp_avg, ...)."""
         return torch.zeros_like(self.data)
 
+    def relayout(self, order):
+        """Re-lay the arena out with the parameters in ``order`` (indices into ``self.params``):
+        DDP's bucket rebuild from the observed gradient-ready order (torch
+        ``Reducer::rebuild_buckets``, TORCH/nn/parallel/distributed.py:1199-1229). Parameter data
+        and arena gradients move to fresh buffers; ``p.data`` / ``p.grad`` / grad slots follow.
+        Returns ``remap(buf) -> new_buf`` that moves any other arena-shaped buffer (optimizer
+        state) the same way. The arena object keeps its identity."""
+        order = list(order)
+        if sorted(order) != list(range(len(self.params))):
+            raise ValueError("relayout order must be a permutation of the parameter indices")
+        old_off = list(self.offsets)
+        params = [self.params[i] for i in order]
+        offsets, off = [], 0
+        for p in params:
+            offsets.append(off)
+            off = _round_up(off + p.numel(), ALIGN)
+        numel = max(off, ALIGN)
+        moves = [(old_off[i], offsets[k], self.numels[i]) for k, i in enumerate(order)]
+
+        def remap(buf: torch.Tensor) -> torch.Tensor:
+            new = torch.zeros(numel, device=buf.device, dtype=buf.dtype)
+            for src, dst, n in moves:
+                new[dst: dst + n].copy_(buf[src: src + n])
+            return new
+
+        had_grad = [self.is_arena_grad(i) for i in range(len(self.params))]
+        data, grad = remap(self.data), remap(self.grad)
+        with torch.no_grad():
+            for k, i in enumerate(order):
+                p, o, n = self.params[i], offsets[k], self.numels[i]
+                p.data = data[o: o + n].view(p.shape)
+                p._tdp_gslot = (grad, o)
+                if had_grad[i]:
+                    p.grad = grad[o: o + n].view(p.shape)
+        self.params, self.offsets = params, offsets
+        self.numels = [p.numel() for p in params]
+        self.numel, self.data, self.grad = numel, data, grad
+        return remap
+
     def state_view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
         o, n = self.offsets[i], self.numels[i]
         return buf[o: o + n].view(self.params[i].shape)

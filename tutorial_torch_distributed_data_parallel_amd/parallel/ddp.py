@@ -20,6 +20,7 @@ import os
 
 import contextlib
 import hashlib
+import time
 import weakref
 
 import torch
@@ -60,7 +61,7 @@ class DistributedDataParallel(nn.Module):
                  static_graph: bool = False, first_bucket_cap_mb: float | None = None,
                  split_bucket_mb: float | None = None, grad_compression: str | None = None,
                  timing: bool = False, check_replicas_every: int | None = None,
-                 force_collective: bool = False):
+                 force_collective: bool = False, rebuild_buckets: bool = True):
         super().__init__()
         if process_group is not None:
             raise NotImplementedError("sub-groups are not supported: DDP uses the world group")
@@ -118,11 +119,20 @@ class DistributedDataParallel(nn.Module):
         self._epi_on = False
         self._epi_index = {}
         self._uses = {}            # id(param) -> forward uses in the current iteration
-        self._fwd_ms, self._bwd_ms = [], []
+        # DDP Logger: every `_sample_every`-th iteration is timed with device
+        # events -- forward compute, backward compute (first gradient ready -> end of backward),
+        # bucket communication -- and averaged in _get_ddp_logging_data (TDP_DDP_TIMING=N or
+        # timing=True for every iteration; 0 = off)
+        self._sample_every = 1 if timing else int(os.environ.get("TDP_DDP_TIMING", "0") or 0)
+        self._samples = []   # finished (fwd_ms, bwd_ms, comm_ms) tuples
+        self._cur_ev = None  # events of the iteration being sampled
+        self._pending_samples = []
         self._build_reducer()
         self._hooks = []
-        for i, p in enumerate(self.arena.params):
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self._register_hooks()
+        self._rebuild_enabled = rebuild_buckets
+        self._rebuild_order = None
+        self._rebuilt = False
         self._callback_queued = False
         self._iter = 0
         # SURVEY.md §5.2 debug mode: every N forwards, verify that all replicas hold bit-identical
@@ -167,6 +177,37 @@ class DistributedDataParallel(nn.Module):
             self.arena.offsets, self.arena.numels, self.arena.numel,
             self.arena.data.element_size(), first, cap, split)
 
+    def _register_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                       for i, p in enumerate(self.arena.params)]
+
+    def _plan_rebuild(self):
+        """After iteration 0 (torch: ``_rebuild_buckets``): if some bucket was complete while a
+        lower-indexed one was not -- gradients arrive in a different order than the arena layout
+        -- re-lay the arena out in the observed ready order at the next forward. Rank 0's
+        decision is broadcast, so every rank rebuilds identically."""
+        P = len(self.arena.params)
+        order = [int(i) for i in self.reducer.ready_order()]
+        seen = set(order)
+        order += [i for i in range(P) if i not in seen]  # never-ready (unused) params last
+        want = int(self.reducer.head_of_line_waits) > 0 and order != list(range(P))
+        msg = torch.tensor([1 if want else 0] + order, dtype=torch.int64, device=self.device)
+        rt.broadcast(msg, 0)
+        if int(msg[0]):
+            self._rebuild_order = [int(v) for v in msg[1:].tolist()]
+
+    def _rebuild_buckets(self):
+        order, self._rebuild_order = self._rebuild_order, None
+        remap = self.arena.relayout(order)
+        for opt in list(getattr(self.arena, "_optimizers", ())):
+            opt._relayout(self.arena, remap)
+        self._bounds = self._plan_buckets()
+        self._build_reducer()
+        self._register_hooks()
+        self._rebuilt = True
+
     def _make_hook(self, idx):
         arena = self.arena
 
@@ -180,13 +221,50 @@ class DistributedDataParallel(nn.Module):
                 if not self._callback_queued:
                     torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
                     self._callback_queued = True
+                    if self._cur_ev is not None:
+                        self._cur_ev["bwd0"] = self._event()
                 self.reducer.mark_ready(idx, self._gpu)
         return hook
 
     def _finalize(self):
         self._callback_queued = False
+        ev = self._cur_ev
+        if ev is not None:
+            ev["bwd1"] = self._event()
         self.reducer.finalize(self._gpu, self.find_unused_parameters)
+        if self._iter == 0 and self._rebuild_enabled and self.reducer.iteration == 1:
+            self._plan_rebuild()
+        if ev is not None:
+            ev["comm1"] = self._event()
+            self._pending_samples.append(ev)
+            self._cur_ev = None
         self._iter += 1
+
+    # --------------------------------------------------------------------------- DDP Logger
+    def _event(self):
+        if self._gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def _elapsed(self, a, b) -> float:
+        return a.elapsed_time(b) if self._gpu else (b - a) * 1000.0
+
+    def _collect_samples(self):
+        """Turn finished sampled iterations into (forward, backward compute, backward comm) ms.
+        Backward comm = end of backward compute -> every bucket done (the exposed part) plus the
+        communicator's own time when the backend measured it."""
+        keep = []
+        for ev in self._pending_samples:
+            if self._gpu and not ev["comm1"].query():
+                keep.append(ev)
+                continue
+            fwd = self._elapsed(ev["fwd0"], ev["fwd1"])
+            bwd = self._elapsed(ev["bwd0"], ev["bwd1"]) if "bwd0" in ev else float("nan")
+            tail = self._elapsed(ev["bwd1"], ev["comm1"])
+            self._samples.append((fwd, bwd, tail))
+        self._pending_samples = keep
 
     def _sync_buffers(self):
         if self.world_size == 1:
@@ -220,6 +298,13 @@ class DistributedDataParallel(nn.Module):
         if self.check_replicas_every and self._iter and \
                 self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled():
             self.check_replicas()
+        sample = (self._sample_every and torch.is_grad_enabled() and
+                  self._iter % self._sample_every == 0 and
+                  not (self._gpu and torch.cuda.is_current_stream_capturing()))
+        if sample:
+            self._cur_ev = {"fwd0": self._event()}
+        if self._rebuild_order is not None:
+            self._rebuild_buckets()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             if self._fused_opt is not None:
                 # hyper-parameters as they are NOW (after any LR-scheduler step) drive this
@@ -231,7 +316,10 @@ class DistributedDataParallel(nn.Module):
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._sync_buffers()
-        return self.module(*inputs, **kwargs)
+        out = self.module(*inputs, **kwargs)
+        if sample:
+            self._cur_ev["fwd1"] = self._event()
+        return out
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -440,20 +528,34 @@ class DistributedDataParallel(nn.Module):
 
     # --------------------------------------------------------------------------- logging
     def _get_ddp_logging_data(self) -> dict:
+        """torch's ``DistributedDataParallel._get_ddp_logging_data`` fields (sampled runtime
+        stats in ms instead of ns) plus the reducer's own: head-of-line waits, comm time."""
         b = self._bounds
         esize = self.arena.data.element_size()
+        self._collect_samples()
+        s = self._samples
+
+        def avg(i):
+            v = [x[i] for x in s if x[i] == x[i]]
+            return sum(v) / len(v) if v else None
+        comm = self.reducer.last_comm_ms()
         return {
+            "avg_forward_compute_time_ms": avg(0),
+            "avg_backward_compute_time_ms": avg(1),
+            "avg_backward_exposed_comm_time_ms": avg(2),
+            "sampled_iterations": len(s),
+            "head_of_line_waits": int(self.reducer.head_of_line_waits),
+            "has_rebuilt_buckets": int(getattr(self, "_rebuilt", False)),
             "world_size": self.world_size,
             "backend_name": rt.get_backend(),
             "bucket_cap_bytes": None,
             "bucket_sizes": [(b[i + 1] - b[i]) * esize for i in range(len(b) - 1)],
             "num_buckets": len(b) - 1,
-            "has_rebuilt_buckets": 0,
             "iterations": self._iter,
             "gradient_as_bucket_view": True,
             "find_unused_parameters": self.find_unused_parameters,
             "first_iteration_ready_order": list(self.reducer.ready_order()),
-            "avg_backward_comm_time_ms": self.reducer.last_comm_ms(),
+            "avg_backward_comm_time_ms": comm if comm >= 0 else None,
             "grad_compression": self._compression or "none",
         }
 

@@ -185,17 +185,22 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
 
 
 def all_reduce_coalesced(tensors, op: str = "sum"):
-    """ONE collective for many small tensors (the reference issues 5)."""
+    """One collective per dtype for many small tensors (the reference issues
+    5 for its epoch metrics). Tensors are packed in their OWN dtype, so integer counters stay
+    exact at any size (no float32 round trip above 2^24)."""
     if _S.world == 1 or not tensors:
         return tensors
-    flat = torch.cat([t.reshape(-1).to(torch.float64 if t.dtype == torch.float64 else
-                                       torch.float32) for t in tensors])
-    all_reduce(flat, op)
-    off = 0
+    groups = {}
     for t in tensors:
-        n = t.numel()
-        t.copy_(flat[off: off + n].view_as(t))
-        off += n
+        groups.setdefault((t.dtype, t.device), []).append(t)
+    for (dt, dev), ts in groups.items():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        all_reduce(flat, op)
+        off = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_(flat[off: off + n].view_as(t))
+            off += n
     return tensors
 
 
