@@ -82,3 +82,16 @@ def test_bench_two_ranks_one_json_line(api):
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 32
     assert rec["value"] > 0 and rec["steps"] == 3 and rec["warmup"] == 1
     assert ("Accelerator.prepare" in rec["config"]["impl"]) == (api == "accelerate")
+
+
+def test_train_ddp_host_pipeline_two_ranks(tmp_path):
+    """train.data: cifar_uint8 -- CIFAR-layout uint8 host images through the native prefetcher
+    and the Resize / Flip / Normalize transform into AlexNet, 2 gloo ranks."""
+    p, s = _settings(tmp_path)
+    s["train"].update(model="alexnet", data="cifar_uint8", image_size=64, n_train=32,
+                      n_test=16, train_batch_size=4, test_batch_size=4, num_epochs=1,
+                      max_steps_per_epoch=2)
+    p.write_text(yaml.safe_dump(s))
+    r = _run([os.path.join(ROOT, "scripts", "train_ddp.py"), "--settings_file", str(p)])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "Epoch 1/1, Train Loss:" in r.stdout

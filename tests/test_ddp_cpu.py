@@ -49,3 +49,20 @@ def test_accelerate_facade_two_ranks(tmp_path):
 
 def test_replica_consistency_check(tmp_path):
     run(W.replica_check, tmp_path)
+
+
+def test_stalled_peer_times_out(tmp_path, monkeypatch):
+    """a rank that hangs (alive, never reaching the next collective) is detected
+    by the surviving rank's collective timeout (TDP_TIMEOUT_S; on MI355X the RCCL watchdog of
+    csrc/comm.h aborts the communicator and exits 86), which fails the job instead of hanging."""
+    import time
+
+    monkeypatch.setenv("TDP_FAULT", "1:3:stall")
+    monkeypatch.setenv("TDP_TIMEOUT_S", "4")
+    t0 = time.perf_counter()
+    with pytest.raises(ProcessRaisedException) as ei:
+        run(W.fault_worker, tmp_path)
+    elapsed = time.perf_counter() - t0
+    assert elapsed < 60, elapsed
+    msg = str(ei.value)
+    assert "Process 0" in msg and "Timed out" in msg, msg

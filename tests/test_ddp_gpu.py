@@ -152,7 +152,7 @@ def test_fused_optimizer_matches_unfused(pg, opt_name):
     def build(fused):
         torch.manual_seed(4)
         m = ToyMLP(in_features=256, hidden=(192, 128), num_classes=10, device="cuda")
-        d = tdp.DDP(m, device_ids=[0], bucket_cap_mb=0.05, first_bucket_cap_mb=0.02)
+        d = tdp.DDP(m, device_ids=[0], bucket_cap_mb=0.05, first_bucket_cap_mb=0.004)
         o = (tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9) if opt_name == "sgd"
              else tdp.optim.Adam(d.parameters(), lr=1e-3))
         if fused:

@@ -276,3 +276,47 @@ def test_commbench_at_world1(pg):
     m = ToyMLP(in_features=256, hidden=(128,), num_classes=10, device="cuda")
     d = tdp.DDP(m, device_ids=[0])
     assert commbench.ddp_comm_ms(d, iters=2, warmup=1) > 0
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_bucket_rebuild_gpu(pg, fused):
+    """Arena relayout from the observed ready order on the device path (RcclOps, optimizer
+    epilogue offsets and state re-bound) keeps training identical to torch."""
+    tdp = pg
+
+    class Shuffled(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = tdp.nn.Linear(256, 512, relu=True, device="cuda")
+            self.c = tdp.nn.Linear(512, 10, device="cuda")
+            self.b = tdp.nn.Linear(512, 512, relu=True, device="cuda")
+
+        def forward(self, x):
+            return self.c(self.b(self.a(x)))
+
+    torch.manual_seed(5)
+    model = Shuffled()
+    names = [n for n, _ in model.named_parameters()]
+    params = {n: p.detach().clone().requires_grad_(True) for n, p in model.named_parameters()}
+    ddp = tdp.DDP(model, device_ids=[0], bucket_cap_mb=0.001, first_bucket_cap_mb=0.001)
+    opt = tdp.optim.Adam(ddp.parameters(), lr=1e-3)
+    ropt = torch.optim.Adam(params.values(), lr=1e-3)
+    if fused:
+        ddp.register_fused_optimizer(opt)
+    for step in range(4):
+        x = torch.randn(128, 256, device="cuda")
+        y = torch.randint(0, 10, (128,), device="cuda")
+        opt.zero_grad(set_to_none=True)
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        ropt.zero_grad(set_to_none=True)
+        P = params
+        h = torch.relu(F.linear(x, P["a.weight"], P["a.bias"]))
+        h = torch.relu(F.linear(h, P["b.weight"], P["b.bias"]))
+        F.cross_entropy(F.linear(h, P["c.weight"], P["c.bias"]), y).backward()
+        ropt.step()
+        if step == 1:
+            assert ddp._rebuilt
+    for n, p in model.named_parameters():
+        torch.testing.assert_close(p.detach(), params[n].detach(), atol=5e-5, rtol=1e-4,
+                                   msg=lambda m: f"{n}: {m}")

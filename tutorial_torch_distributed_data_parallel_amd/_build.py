@@ -83,7 +83,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         o = BUILD / (s.stem + ".cpp.o")
         if force or _needs(o, s, headers):
             extra = torch_flags if s.name == "bindings.cpp" else []
-            jobs_list.append([cxx, *common, *extra, "-Wno-deprecated-declarations",
+            jobs_list.append([cxx, *common, *extra, "-pthread", "-Wno-deprecated-declarations",
                               "-c", str(s), "-o", str(o)])
     jobs = jobs or min(len(jobs_list), max(1, min(8, os.cpu_count() or 1))) or 1
     if jobs_list:
@@ -99,7 +99,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         tmp = out.with_suffix(".tmp.so")
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp),
               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-              "-ltorch_python", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}"])
+              "-ltorch_python", "-lamdhip64", "-lrccl", "-pthread", f"-Wl,-rpath,{tlib}"])
         os.replace(tmp, out)
     return out
 

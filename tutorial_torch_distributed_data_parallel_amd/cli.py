@@ -12,7 +12,8 @@
 * ``launch`` -- replaces REF/submit_job.py (§3.5, R19/R20): spawns ``num_gpus`` ranks of
   ``script_path`` on this node; ``--write-condor`` still emits the HTCondor submission file with the
   reference's keys for users who schedule through a cluster.
-Data is synthetic (no network): CIFAR-10-shaped tensors resident on the device.
+Data is synthetic (no network): CIFAR-10-shaped tensors resident on the device, or (train.data:
+cifar_uint8) CIFAR-layout uint8 host images through the native input pipeline (data/host.py).
 """
 from __future__ import annotations
 
@@ -37,12 +38,31 @@ def _settings(argv, desc):
 
 
 def _datasets(t, device):
-    from .data import SyntheticDataset
+    """``train.data``: "synthetic" (default: model-shaped float tensors resident on the device)
+    or "cifar_uint8" (CIFAR-10-layout uint8 32x32x3 host images through the native prefetcher
+    and the on-device Resize / Flip / Normalize, the reference's input pipeline)."""
+    from .data import SyntheticDataset, cifar_like_uint8
     from .models.registry import input_shape
 
+    if t.get("data", "synthetic") == "cifar_uint8":
+        if t["model"].lower().startswith(("toy_mlp", "mlp")):
+            raise ValueError("data: cifar_uint8 feeds image models (alexnet, resnet50)")
+        return (cifar_like_uint8(t["n_train"], seed=0), cifar_like_uint8(t["n_test"], seed=1))
     shape = input_shape(t["model"], t["image_size"])
     return (SyntheticDataset(t["n_train"], shape, 10, seed=0, device=device),
             SyntheticDataset(t["n_test"], shape, 10, seed=1, device=device))
+
+
+def _loader(t, ds, batch, sampler, device, train: bool):
+    """DeviceLoader over device-resident data, or the host pipeline (PrefetchLoader: native
+    prefetch threads, uint8 H2D, on-device transform) for host datasets."""
+    from .data import DeviceLoader, HostImageDataset, ImageTransform, PrefetchLoader
+
+    if isinstance(ds, HostImageDataset):
+        tf = ImageTransform(size=t["image_size"], flip_p=0.5 if train else 0.0)
+        return PrefetchLoader(ds, batch, sampler=sampler, transform=tf, device=device,
+                              seed=t.get("base_seed") or 0)
+    return DeviceLoader(ds, batch, sampler=sampler)
 
 
 def _optimizer(t, params):
@@ -75,8 +95,10 @@ def basic_ddp_training_loop(rank: int, world_size: int, save_dir: str, optional_
     train_ds, test_ds = _datasets(train_cfg, device)
     train_sampler = DistributedSampler(train_ds, num_replicas=world_size, rank=rank, shuffle=True)
     test_sampler = DistributedSampler(test_ds, num_replicas=world_size, rank=rank, shuffle=True)
-    train_loader = DeviceLoader(train_ds, train_cfg["train_batch_size"], sampler=train_sampler)
-    test_loader = DeviceLoader(test_ds, train_cfg["test_batch_size"], sampler=test_sampler)
+    train_loader = _loader(train_cfg, train_ds, train_cfg["train_batch_size"], train_sampler,
+                           device, train=True)
+    test_loader = _loader(train_cfg, test_ds, train_cfg["test_batch_size"], test_sampler, device,
+                          train=False)
     model = build_model(train_cfg["model"], device=device)
     ddp_model = DDP(model, device_ids=[device.index] if device.type == "cuda" else None,
                     bucket_cap_mb=train_cfg.get("bucket_cap_mb"))
@@ -122,8 +144,9 @@ def train_accelerate(argv=None):
     accelerator = Accelerator()
     device = accelerator.device
     train_ds, test_ds = _datasets(t, device)
-    train_loader = DeviceLoader(train_ds, t["train_batch_size"])  # no sampler, no shuffle (R11)
-    test_loader = DeviceLoader(test_ds, t["test_batch_size"])
+    # no sampler, no shuffle (R11)
+    train_loader = _loader(t, train_ds, t["train_batch_size"], None, device, train=True)
+    test_loader = _loader(t, test_ds, t["test_batch_size"], None, device, train=False)
     model = build_model(t["model"], device=device)
     criterion = tnn.CrossEntropyLoss()
     optimizer = _optimizer(t, model.parameters())

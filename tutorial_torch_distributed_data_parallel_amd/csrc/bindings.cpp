@@ -15,6 +15,7 @@
 #include "comm.h"
 #include "conv.h"
 #include "kernels.h"
+#include "loader.h"
 #include "pool.h"
 #include "reducer.h"
 
@@ -809,6 +810,98 @@ struct PyOps : SyncOps {
   }
 };
 
+// ------------------------------------------------------------------------------ input pipeline
+// uint8 NHWC batch (device) -> normalised float [B, C, Ho, Wo], channels_last or NCHW memory
+Tensor image_transform_op(const Tensor& x, const c10::optional<Tensor>& flip, int64_t Ho,
+                          int64_t Wo, std::vector<double> mean, std::vector<double> stdv,
+                          bool round_u8, bool channels_last) {
+  CHECK_GPU(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4, "image_transform: uint8 [B,H,W,C]");
+  const int B = (int)x.size(0), Hs = (int)x.size(1), Ws = (int)x.size(2), C = (int)x.size(3);
+  TORCH_CHECK(C == 1 || C == 3 || C == 4, "image_transform: 1, 3 or 4 channels");
+  TORCH_CHECK((int)mean.size() == C && (int)stdv.size() == C, "image_transform: mean/std size");
+  const uint8_t* fl = nullptr;
+  if (flip.has_value() && flip->defined()) {
+    CHECK_GPU(*flip); CHECK_CONTIG(*flip);
+    TORCH_CHECK(flip->scalar_type() == at::kByte && flip->numel() == B, "flip: uint8 [B]");
+    fl = flip->data_ptr<uint8_t>();
+  }
+  ImageNorm nrm{};
+  for (int c = 0; c < C; ++c) {
+    nrm.mean[c] = (float)mean[c];
+    nrm.inv_std[c] = (float)(1.0 / stdv[c]);
+  }
+  auto opts = x.options().dtype(at::kFloat);
+  Tensor out = channels_last
+                   ? at::empty({B, C, Ho, Wo}, opts.memory_format(at::MemoryFormat::ChannelsLast))
+                   : at::empty({B, C, Ho, Wo}, opts);
+  image_transform(x.data_ptr<uint8_t>(), fl, out.data_ptr<float>(), B, Hs, Ws, C, (int)Ho,
+                  (int)Wo, nrm, round_u8, channels_last, cur_stream());
+  return out;
+}
+
+// the native prefetcher plus the tensors whose memory it reads
+struct PyHostLoader {
+  Tensor data, labels;
+  std::vector<int64_t> sample_shape;
+  int64_t row_bytes = 0;
+  bool pinned = true;
+  std::unique_ptr<HostBatchLoader> L;
+};
+
+std::shared_ptr<PyHostLoader> make_host_loader(Tensor data, Tensor labels, int batch, int depth,
+                                               int threads, bool pinned) {
+  TORCH_CHECK(!data.is_cuda() && !labels.is_cuda(), "host loader: CPU tensors");
+  TORCH_CHECK(data.scalar_type() == at::kByte, "host loader: uint8 samples");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.dim() == 1, "host loader: int64 labels");
+  TORCH_CHECK(data.dim() >= 2 && data.size(0) == labels.size(0), "host loader: [n, ...] samples");
+  auto h = std::make_shared<PyHostLoader>();
+  h->data = data.contiguous();
+  h->labels = labels.contiguous();
+  h->sample_shape.assign(data.sizes().begin() + 1, data.sizes().end());
+  h->row_bytes = h->data.numel() / h->data.size(0);
+  h->pinned = pinned;
+  h->L = std::make_unique<HostBatchLoader>(h->data.data_ptr<uint8_t>(),
+                                           h->labels.data_ptr<int64_t>(), h->data.size(0),
+                                           h->row_bytes, batch, depth, threads, pinned);
+  return h;
+}
+
+// next batch: (x uint8 [rows, ...], y int64 [rows], flip uint8 [rows]) on `device` (async
+// copies on the current stream from pinned staging), or None at the end of the epoch
+py::object host_loader_next(PyHostLoader& h, const std::string& device) {
+  const uint8_t *x = nullptr, *fl = nullptr;
+  const int64_t* y = nullptr;
+  int rows = 0, slot = -1;
+  {
+    py::gil_scoped_release nogil;  // workers may still be gathering this batch
+    slot = h.L->next(&x, &y, &fl, &rows);
+  }
+  if (slot < 0) return py::none();
+  std::vector<int64_t> xs{rows};
+  xs.insert(xs.end(), h.sample_shape.begin(), h.sample_shape.end());
+  const at::Device dev(device);
+  auto u8 = at::TensorOptions().dtype(at::kByte).device(dev);
+  Tensor dx = at::empty(xs, u8), dfl = at::empty({rows}, u8);
+  Tensor dy = at::empty({rows}, at::TensorOptions().dtype(at::kLong).device(dev));
+  if (dev.is_cuda()) {
+    hipStream_t s = cur_stream();
+    check_hip(hipMemcpyAsync(dx.data_ptr(), x, (size_t)rows * h.row_bytes,
+                             hipMemcpyHostToDevice, s), "loader H2D x");
+    check_hip(hipMemcpyAsync(dy.data_ptr(), y, (size_t)rows * sizeof(int64_t),
+                             hipMemcpyHostToDevice, s), "loader H2D y");
+    check_hip(hipMemcpyAsync(dfl.data_ptr(), fl, (size_t)rows, hipMemcpyHostToDevice, s),
+              "loader H2D flip");
+    h.L->release(slot, s);
+  } else {
+    std::memcpy(dx.data_ptr(), x, (size_t)rows * h.row_bytes);
+    std::memcpy(dy.data_ptr(), y, (size_t)rows * sizeof(int64_t));
+    std::memcpy(dfl.data_ptr(), fl, (size_t)rows);
+    h.L->release(slot, nullptr);
+  }
+  return py::make_tuple(dx, dy, dfl);
+}
+
 float* block_ptr(const c10::optional<Tensor>& blk) {
   return const_cast<float*>(hyper_ptr(blk));
 }
@@ -894,6 +987,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_relu", &add_relu_op);
   m.def("relu_mask", &relu_mask_op);
   m.def("gather_batch", &gather_batch_op);
+  m.def("image_transform", &image_transform_op, py::arg("x"), py::arg("flip"), py::arg("Ho"),
+        py::arg("Wo"), py::arg("mean"), py::arg("std"), py::arg("round_u8") = true,
+        py::arg("channels_last") = true);
+  py::class_<PyHostLoader, std::shared_ptr<PyHostLoader>>(m, "HostBatchLoader")
+      .def(py::init(&make_host_loader), py::arg("data"), py::arg("labels"), py::arg("batch"),
+           py::arg("depth") = 4, py::arg("threads") = 2, py::arg("pinned") = true)
+      .def("start_epoch",
+           [](PyHostLoader& h, std::vector<int64_t> idx, bool drop_last, uint64_t seed,
+              double p) { h.L->start_epoch(idx, drop_last, seed, (float)p); },
+           py::arg("indices"), py::arg("drop_last") = false, py::arg("flip_seed") = 0,
+           py::arg("flip_p") = 0.0)
+      .def("num_batches", [](PyHostLoader& h) { return h.L->num_batches(); })
+      .def("next", &host_loader_next, py::arg("device"));
   m.def("bn_moments", &bn_moments_op);
   m.def("bn_merge", &bn_merge_op);
   m.def("bn_elemt", &bn_elemt_op);
@@ -943,6 +1049,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("group_start", &Communicator::group_start)
       .def("group_end", &Communicator::group_end)
       .def("abort", &Communicator::abort)
+      // collective watchdog (comm.h): the work on the current stream must finish in time
+      .def("watch_current",
+           [](Communicator& c, const std::string& what) { c.watch(cur_stream(), what.c_str()); })
+      .def_property("timeout", &Communicator::timeout, &Communicator::set_timeout)
+      .def("pending_watches", &Communicator::pending_watches)
       // block the host until everything enqueued on the current stream (incl. comms) finished
       .def("synchronize_current", [](Communicator&) {
         py::gil_scoped_release nogil;

@@ -3,6 +3,8 @@
 #include <cstdlib>
 #include <string>
 
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -46,11 +48,72 @@ Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world,
                                         (normal || blocking) ? lo : hi),
             "hipStreamCreateWithPriority");
   check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  // TDP_TIMEOUT_S (seconds) or TDP_TIMEOUT_MIN (minutes); torch's NCCL default is 10 minutes
+  if (const char* t = std::getenv("TDP_TIMEOUT_S")) timeout_s_ = std::atof(t);
+  else if (const char* m = std::getenv("TDP_TIMEOUT_MIN")) timeout_s_ = 60.0 * std::atof(m);
 }
 
 Communicator::~Communicator() {
+  if (thread_.joinable()) {
+    stop_ = true;
+    cv_.notify_all();
+    thread_.join();
+  }
+  for (auto& w : watches_) (void)hipEventDestroy(w.ev);
+  for (auto e : free_events_) (void)hipEventDestroy(e);
   if (comm_) ncclCommDestroy(comm_);
   if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void Communicator::watch(hipStream_t s, const char* what) {
+  if (timeout_s_ <= 0.0 || world_ <= 1) return;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!thread_.joinable()) thread_ = std::thread([this] { watchdog_loop(); });
+  hipEvent_t ev;
+  if (!free_events_.empty()) {
+    ev = free_events_.back();
+    free_events_.pop_back();
+  } else {
+    check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(watch)");
+  }
+  check_hip(hipEventRecord(ev, s), "hipEventRecord(watch)");
+  watches_.push_back({ev, now_s() + timeout_s_, what});
+  cv_.notify_all();
+}
+
+int Communicator::pending_watches() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int)watches_.size();
+}
+
+void Communicator::watchdog_loop() {
+  check_hip(hipSetDevice(device_), "hipSetDevice(watchdog)");
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!stop_) {
+    // retire finished work in order; the oldest unfinished watch decides
+    while (!watches_.empty() && hipEventQuery(watches_.front().ev) == hipSuccess) {
+      free_events_.push_back(watches_.front().ev);
+      watches_.pop_front();
+    }
+    if (!watches_.empty() && now_s() > watches_.front().deadline) {
+      const Watch w = watches_.front();
+      std::fprintf(stderr,
+                   "[tdp] RCCL watchdog: rank %d: '%s' did not finish within %.1f s (a peer "
+                   "rank is gone or stalled); aborting the communicator and exiting\n",
+                   rank_, w.what.c_str(), timeout_s_);
+      std::fflush(stderr);
+      if (comm_) ncclCommAbort(comm_);
+      std::_Exit(86);
+    }
+    cv_.wait_for(lk, std::chrono::milliseconds(100));
+  }
 }
 
 void Communicator::abort() {

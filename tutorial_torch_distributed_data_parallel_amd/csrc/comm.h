@@ -9,8 +9,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace tdp {
@@ -46,10 +51,35 @@ class Communicator {
   void group_end();
   void abort();
 
+  // Collective watchdog (torch's ProcessGroupNCCL watchdog, TORCH/distributed/constants.py:21
+  // default 10 min): watch(s, what) records an event on `s` behind the work
+  // enqueued so far; a host thread polls the oldest unfinished events and, once one is older
+  // than the timeout, reports it, aborts the communicator (which releases RCCL kernels blocked
+  // on a dead peer) and ends the process with exit code 86, so a launcher sees the failure
+  // instead of a hang. A no-op while `s` is being captured into a hipGraph (the replay is
+  // watched by the caller) or when the timeout is 0.
+  void watch(hipStream_t s, const char* what);
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  double timeout() const { return timeout_s_; }
+  int pending_watches();
+
  private:
+  struct Watch {
+    hipEvent_t ev;
+    double deadline;
+    std::string what;
+  };
+  void watchdog_loop();
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   int rank_ = 0, world_ = 1, device_ = 0;
+  double timeout_s_ = 600.0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Watch> watches_;
+  std::vector<hipEvent_t> free_events_;
+  std::thread thread_;
+  std::atomic<bool> stop_{false};
 };
 
 }  // namespace tdp

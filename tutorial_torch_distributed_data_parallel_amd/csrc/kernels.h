@@ -224,6 +224,16 @@ void fill_f32(float* x, long n, float v, hipStream_t s);
 void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, long F, int B,
                   float* xb, int64_t* yb, hipStream_t s);
 void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
+// uint8 [B][Hs][Ws][C] -> bilinear resize to Ho x Wo (align_corners=False), optional per-sample
+// horizontal flip (flip[b] != 0), optional PIL-style rounding, /255, (v - mean) / std; output
+// channels_last [B][Ho][Wo][C] or NCHW. C in {1, 3, 4}.
+struct ImageNorm {
+  float mean[4];
+  float inv_std[4];
+};
+void image_transform(const uint8_t* x, const uint8_t* flip, float* out, int B, int Hs, int Ws,
+                     int C, int Ho, int Wo, const ImageNorm& nrm, bool round_u8,
+                     bool channels_last, hipStream_t s);
 void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------------

@@ -383,6 +383,7 @@ void SyncBackend::wait_all(hipStream_t compute) {
     deferred_.clear();
     ops_->opt_update(merged, compute);
   }
+  if (collective()) ops_->watch(compute, "DDP gradient synchronisation");
 }
 
 void SyncBackend::zero(int64_t begin, int64_t end, hipStream_t compute) {

@@ -89,6 +89,8 @@ struct SyncOps {
   virtual void sumsq_all_reduce(int block, hipStream_t s) = 0;             // sum over ranks
   virtual void clip_coef(int block, hipStream_t s) = 0;                    // from sumsq
   virtual void scale_grads(int block, const Ranges& r, hipStream_t s) = 0; // g[r] *= coef
+  // collective watchdog: the work enqueued on `s` so far must finish within the timeout
+  virtual void watch(hipStream_t s, const char* what) { (void)s; (void)what; }
 };
 
 // Device implementation: RCCL communicator + gfx950 kernels over the device arenas.
@@ -123,6 +125,7 @@ class RcclOps : public SyncOps {
   void sumsq_all_reduce(int block, hipStream_t s) override;
   void clip_coef(int block, hipStream_t s) override;
   void scale_grads(int block, const Ranges& r, hipStream_t s) override;
+  void watch(hipStream_t s, const char* what) override { comm_->watch(s, what); }
 
   FusedOptimizer fused;
   float* clip_block = nullptr;  // DDP-owned hyper block for LOCAL clipping

@@ -118,7 +118,13 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    timeout = timeout or _dt.timedelta(minutes=int(os.environ.get("TDP_TIMEOUT_MIN", "30")))
+    # collective timeout: gloo's PG timeout and the RCCL watchdog (csrc/comm.h) -- TDP_TIMEOUT_S
+    # (seconds) or TDP_TIMEOUT_MIN (minutes); defaults: torch's 30 min (gloo) / 10 min (NCCL)
+    if timeout is None:
+        if os.environ.get("TDP_TIMEOUT_S"):
+            timeout = _dt.timedelta(seconds=float(os.environ["TDP_TIMEOUT_S"]))
+        else:
+            timeout = _dt.timedelta(minutes=float(os.environ.get("TDP_TIMEOUT_MIN", "30")))
     owns = False
     # a single-rank job needs no rendezvous at all (and must not grab MASTER_PORT)
     if world > 1 and not dist.is_initialized():
@@ -251,6 +257,7 @@ def barrier() -> None:
     if _S.comm is not None:
         x = torch.ones(1, device=_S.device)
         _S.comm.all_reduce(x, "sum")
+        _S.comm.watch_current("barrier")
         _S.comm.synchronize_current()
     else:
         dist.barrier()

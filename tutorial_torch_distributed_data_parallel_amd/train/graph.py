@@ -52,6 +52,11 @@ class CapturedStep:
 
         sync_all_hyper()  # LR schedules etc. reach the captured kernels through the hyper blocks
         self.graph.replay()
+        from ..parallel import runtime as rt
+
+        comm = rt.comm()
+        if comm is not None and comm.world > 1:
+            comm.watch_current("captured training step")  # RCCL watchdog covers the replay
         return self.output
 
     __call__ = replay

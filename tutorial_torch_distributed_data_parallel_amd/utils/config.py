@@ -26,6 +26,7 @@ TRAIN_DEFAULTS = {
     "n_train": 50000,            # CIFAR-10 sizes
     "n_test": 10000,
     "image_size": 224,           # Resize(224), REF/data_and_toy_model.py:13
+    "data": "synthetic",         # synthetic (device-resident) | cifar_uint8 (host pipeline)
     "base_seed": None,
     "max_steps_per_epoch": None,
 }
