@@ -264,3 +264,35 @@ def test_conv_wgrad_plans(orient, override, Co, C, R):
     torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("downsample", [False, True])
+def test_bottleneck_fused_join_matches_unfused(downsample):
+    """relu(bn3(conv3) + identity) fused into bn3's normalisation (and its backward writing the
+    identity gradient) == separate bn3 + add_relu; running stats and num_batches_tracked are
+    updated on the device."""
+    import copy
+
+    from tutorial_torch_distributed_data_parallel_amd.models.resnet import Bottleneck
+    from tutorial_torch_distributed_data_parallel_amd.nn import BatchNorm2d, Conv2d
+
+    torch.manual_seed(0)
+    inp, planes, stride = (64, 32, 2) if downsample else (128, 32, 1)
+    ds = torch.nn.Sequential(Conv2d(inp, planes * 4, 1, stride=stride, bias=False),
+                             BatchNorm2d(planes * 4)) if downsample else None
+    a = Bottleneck(inp, planes, stride, ds).cuda()
+    b = copy.deepcopy(a)
+    b._fused_join = False
+    x = torch.randn(8, inp, 28, 28, device="cuda").contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = a(xa), b(xb)
+    torch.testing.assert_close(ya, yb, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad, xb.grad, atol=1e-4, rtol=1e-4)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-4, rtol=1e-4, msg=lambda m: f"{n}: {m}")
+    for (n, p), (_, q) in zip(a.named_buffers(), b.named_buffers()):
+        torch.testing.assert_close(p, q, atol=1e-6, rtol=1e-5, msg=lambda m: f"{n}: {m}")
+    assert int(a.bn3.num_batches_tracked) == 1

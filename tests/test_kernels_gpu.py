@@ -188,7 +188,7 @@ def test_batchnorm_kernels(C, shape):
     gx, gw, gb = torch.autograd.grad(yref, (xr, wr, br), dy)
     dw, db = torch.empty_like(w), torch.empty_like(b)
     sums = C.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0)
-    dx = C.bn_bwd_elemt(dy, x, stats, w, sums, y)
+    dx = C.bn_bwd_elemt(dy, x, stats, w, sums, y)[0]
     _close(dw, gw, atol=1e-3, rtol=1e-4)
     _close(db, gb, atol=1e-3, rtol=1e-4)
     _close(dx, gx, atol=1e-4, rtol=1e-4)

@@ -379,34 +379,46 @@ std::vector<Tensor> bn_moments_op(const Tensor& x) {
   auto out = at::empty({2 * C + 1}, x.options());  // [mean | var | count]
   Tensor ws = at::empty({bn_ws_floats(C, splits)}, x.options());
   bn_moments(x.data_ptr<float>(), N, C, HW, splits, ws.data_ptr<float>(), out.data_ptr<float>(),
-             out.data_ptr<float>() + C, cur_stream());
-  out.narrow(0, 2 * C, 1).fill_((double)N * HW);
+             out.data_ptr<float>() + C, out.data_ptr<float>() + 2 * C, cur_stream());
   return {out};
 }
 
 // gathered: R rows of [mean | var | count] -> stats [mean | invstd | total count]
 Tensor bn_merge_op(const Tensor& gathered, int64_t C, double eps, double momentum,
-                   const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar) {
+                   const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
+                   const c10::optional<Tensor>& num_batches) {
   CHECK_GPU(gathered); CHECK_F32(gathered); CHECK_CONTIG(gathered);
   const int R = (int)(gathered.numel() / (2 * C + 1));
   TORCH_CHECK((int64_t)R * (2 * C + 1) == gathered.numel(), "bn_merge: bad gathered size");
   auto stats = at::empty({2 * C + 1}, gathered.options());
   float* sp = stats.data_ptr<float>();
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    CHECK_GPU(*num_batches);
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+                "bn_merge: num_batches_tracked must be one int64");
+    nb = num_batches->data_ptr<int64_t>();
+  }
   bn_merge(gathered.data_ptr<float>(), R, (int)C, (float)eps, (float)momentum, sp, sp + C,
-           fptr(rmean), fptr(rvar), cur_stream());
+           fptr(rmean), fptr(rvar), nb, cur_stream());
   return stats;
 }
 
 Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Tensor>& w,
-                   const c10::optional<Tensor>& b, bool relu) {
+                   const c10::optional<Tensor>& b, bool relu,
+                   const c10::optional<Tensor>& residual) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
   TORCH_CHECK(stats.numel() == 2 * C + 1, "bn_elemt: stats must be [2C+1]");
+  if (residual.has_value() && residual->defined()) {
+    CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->sizes() == x.sizes(), "bn_elemt: residual must have x's shape");
+  }
   auto y = at::empty_like(x);
   const float* sp = stats.data_ptr<float>();
   bn_elemt(x.data_ptr<float>(), sp, sp + C, fptr(w), fptr(b), N, C, HW, relu,
-           y.data_ptr<float>(), cur_stream());
+           y.data_ptr<float>(), cur_stream(), fptr(residual));
   return y;
 }
 
@@ -439,18 +451,22 @@ Tensor bn_bwd_reduce_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
   return sums;
 }
 
-Tensor bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
-                       const c10::optional<Tensor>& w, const Tensor& sums,
-                       const c10::optional<Tensor>& y_relu) {
+// returns dx, or [dx, dresidual] when residual_grad (the fused residual input's gradient)
+std::vector<Tensor> bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
+                                    const c10::optional<Tensor>& w, const Tensor& sums,
+                                    const c10::optional<Tensor>& y_relu, bool residual_grad) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
   auto dx = at::empty_like(x);
+  Tensor dres;
+  if (residual_grad) dres = at::empty_like(x);
   const float* sp = stats.data_ptr<float>();
   bn_bwd_elemt(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(w),
                sums.data_ptr<float>(), fptr(y_relu), sp + 2 * C, N, C, HW, dx.data_ptr<float>(),
-               cur_stream());
-  return dx;
+               cur_stream(), residual_grad ? dres.data_ptr<float>() : nullptr);
+  if (residual_grad) return {dx, dres};
+  return {dx};
 }
 
 // ---------------------------------------------------------------------------------- conv / pool
@@ -1001,11 +1017,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("num_batches", [](PyHostLoader& h) { return h.L->num_batches(); })
       .def("next", &host_loader_next, py::arg("device"));
   m.def("bn_moments", &bn_moments_op);
-  m.def("bn_merge", &bn_merge_op);
-  m.def("bn_elemt", &bn_elemt_op);
+  m.def("bn_merge", &bn_merge_op, py::arg("gathered"), py::arg("C"), py::arg("eps"),
+        py::arg("momentum"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("num_batches") = py::none());
+  m.def("bn_elemt", &bn_elemt_op, py::arg("x"), py::arg("stats"), py::arg("w"), py::arg("b"),
+        py::arg("relu"), py::arg("residual") = py::none());
   m.def("bn_eval", &bn_eval_op);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_op);
-  m.def("bn_bwd_elemt", &bn_bwd_elemt_op);
+  m.def("bn_bwd_elemt", &bn_bwd_elemt_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
+        py::arg("w"), py::arg("sums"), py::arg("y_relu"), py::arg("residual_grad") = false);
 
   m.def("rccl_unique_id", &unique_id_op);
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")

@@ -244,16 +244,21 @@ void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s);
 int bn_splits(int N, int C, int HW, int num_cus);
 long bn_ws_floats(int C, int splits);  // >= max(3C, 2C) * splits
 // per-channel mean and biased variance (Welford per lane, Chan merges across lanes/blocks)
+// (count_out, optional: the element count N*HW is written there -- the stats' third field)
 void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, float* mean,
-                float* var, hipStream_t s);
+                float* var, float* count_out, hipStream_t s);
 // merge R ranks' rows [mean(C) | var(C) | count(1)] (row stride 2C+1) -> mean, invstd, with the
 // total count written at invstd[C] (callers pass invstd = mean + C of one [2C+1] stats buffer);
 // running stats (optional) updated with momentum and the unbiased variance.
+// num_batches (optional): BatchNorm's num_batches_tracked, incremented by the kernel
 void bn_merge(const float* gathered, int R, int C, float eps, float momentum, float* mean,
-              float* invstd, float* running_mean, float* running_var, hipStream_t s);
+              float* invstd, float* running_mean, float* running_var, int64_t* num_batches,
+              hipStream_t s);
 // y = (x - mean) * invstd * w + b (optional ReLU). w/b may be null (affine=False).
+// residual (optional, [rows, C] form only): y = relu?(bn(x) + residual), the ResNet join
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
-              const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s);
+              const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
+              const float* residual = nullptr);
 // eval: y = (x - rmean) * rsqrt(rvar + eps) * w + b (optional ReLU)
 void bn_eval(const float* x, const float* rmean, const float* rvar, const float* w,
              const float* b, int N, int C, int HW, float eps, bool relu, float* y, hipStream_t s);
@@ -263,8 +268,10 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
                    const float* y_relu, int N, int C, int HW, int splits, float* ws, float* sums,
                    float* dw, float* db, float grad_beta, hipStream_t s);
 // dx = w*invstd*(dy - sum_dy/cnt - (x-mean)*invstd^2*sum_dy_xmu/cnt), sums possibly all-reduced.
+// dres (optional, [rows, C] form only): also write the masked dy -- the gradient of a fused
+// residual input
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
-                  int N, int C, int HW, float* dx, hipStream_t s);
+                  int N, int C, int HW, float* dx, hipStream_t s, float* dres = nullptr);
 
 }  // namespace tdp

@@ -14,6 +14,7 @@
 // workgroup owns one channel (coalesced along HW). Either way the N*HW axis can additionally be
 // split over blockIdx.y so that a small-C layer still puts >= 1 workgroup on every CU.
 #include <initializer_list>
+#include <stdexcept>
 
 #include "common.h"
 #include "kernels.h"
@@ -66,7 +67,9 @@ __device__ __forceinline__ void range_of(long total, int splits, int z, long& b,
 __global__ __launch_bounds__(256) void moments_1d(const float* __restrict__ x, int N, int C,
                                                   int splits, float* __restrict__ ws,
                                                   float* __restrict__ mean,
-                                                  float* __restrict__ var) {
+                                                  float* __restrict__ var,
+    float* __restrict__ cnt_out, float cnt) {
+  if (cnt_out && splits == 1 && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
   __shared__ Wf sh[4][64];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -92,7 +95,9 @@ __global__ __launch_bounds__(256) void moments_1d(const float* __restrict__ x, i
 __global__ __launch_bounds__(256) void moments_2d(const float* __restrict__ x, int N, int C,
                                                   int HW, int splits, float* __restrict__ ws,
                                                   float* __restrict__ mean,
-                                                  float* __restrict__ var) {
+                                                  float* __restrict__ var,
+    float* __restrict__ cnt_out, float cnt) {
+  if (cnt_out && splits == 1 && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
   __shared__ Wf sh[4];
   const int c = blockIdx.x;
   long b, e;
@@ -117,37 +122,48 @@ __global__ __launch_bounds__(256) void moments_2d(const float* __restrict__ x, i
   }
 }
 
-// Split partials -> final: a workgroup owns 64 channels (one per lane, coalesced) and its 4 waves
-// take every 4th split; the four partial results merge through LDS.
+// Split partials -> final: a workgroup owns 16 channels; its 16 lane groups of 16 take every
+// 16th split (each partial row is read 16 channels = 64 B at a time) and merge through LDS. (The
+// first form -- 64 channels, 4 split groups -- was latency-bound on its 64-step dependent merge
+// chains: 37 us per BN layer in the ResNet-50 profile, 2 ms per step.) Also writes the element
+// count into the stats (`cnt_out`), so no separate fill is launched.
 __global__ __launch_bounds__(256) void moments_final(const float* __restrict__ ws, int C,
                                                      int splits, float* __restrict__ mean,
-                                                     float* __restrict__ var) {
-  __shared__ Wf sh[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+                                                     float* __restrict__ var,
+                                                     float* __restrict__ cnt_out, float cnt) {
+  __shared__ Wf sh[16][16];
+  const int lane = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lane;
   Wf w{0.f, 0.f, 0.f};
   if (c < C) {
 #pragma unroll 4
-    for (int z = g; z < splits; z += 4) {
+    for (int z = g; z < splits; z += 16) {
       const float* o = ws + (long)z * 3 * C;
       w = wf_merge(w, Wf{o[c], o[C + c], o[2 * C + c]});
     }
   }
   sh[g][lane] = w;
   __syncthreads();
-  if (g == 0 && c < C) {
-    w = wf_merge(wf_merge(sh[0][lane], sh[1][lane]), wf_merge(sh[2][lane], sh[3][lane]));
+  if (threadIdx.x < 16 && c < C) {
+    Wf a = wf_merge(wf_merge(sh[0][lane], sh[1][lane]), wf_merge(sh[2][lane], sh[3][lane]));
+    Wf b = wf_merge(wf_merge(sh[4][lane], sh[5][lane]), wf_merge(sh[6][lane], sh[7][lane]));
+    Wf d = wf_merge(wf_merge(sh[8][lane], sh[9][lane]), wf_merge(sh[10][lane], sh[11][lane]));
+    Wf e = wf_merge(wf_merge(sh[12][lane], sh[13][lane]), wf_merge(sh[14][lane], sh[15][lane]));
+    w = wf_merge(wf_merge(a, b), wf_merge(d, e));
     mean[c] = w.mean;
     var[c] = w.n > 0.f ? w.m2 / w.n : 0.f;
   }
+  if (cnt_out && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
 }
 
 // Rows of `g`: [mean(C) | var(C) | count], stride 2C+1. Zero-count ranks drop out, as in
 // batch_norm_gather_stats_with_counts (TORCH/nn/modules/_functions.py:96-115).
 __global__ void merge_kernel(const float* __restrict__ g, int R, int C, float eps, float momentum,
                              float* __restrict__ mean, float* __restrict__ invstd,
-                             float* __restrict__ rmean, float* __restrict__ rvar) {
+                             float* __restrict__ rmean, float* __restrict__ rvar,
+                             int64_t* __restrict__ nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt && c == 0) *nbt += 1;  // BatchNorm's num_batches_tracked (one thread, no ATen add_)
   if (c >= C) return;
   const long stride = 2L * C + 1;
   Wf w{0.f, 0.f, 0.f};
@@ -261,13 +277,14 @@ __global__ __launch_bounds__(256) void bwd_reduce_final(const float* __restrict_
                                                         float* __restrict__ sums,
                                                         float* __restrict__ dw,
                                                         float* __restrict__ db, float beta) {
-  __shared__ float s0[4][64], s1[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  // 16 channels per workgroup x 16 split groups (as moments_final)
+  __shared__ float s0[16][16], s1[16][16];
+  const int lane = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lane;
   float a = 0.f, m = 0.f;
   if (c < C) {
 #pragma unroll 4
-    for (int z = g; z < splits; z += 4) {
+    for (int z = g; z < splits; z += 16) {
       a += part[(long)z * 2 * C + c];
       m += part[(long)z * 2 * C + C + c];
     }
@@ -275,9 +292,14 @@ __global__ __launch_bounds__(256) void bwd_reduce_final(const float* __restrict_
   s0[g][lane] = a;
   s1[g][lane] = m;
   __syncthreads();
-  if (g != 0 || c >= C) return;
-  a = (s0[0][lane] + s0[1][lane]) + (s0[2][lane] + s0[3][lane]);
-  m = (s1[0][lane] + s1[1][lane]) + (s1[2][lane] + s1[3][lane]);
+  if (threadIdx.x >= 16 || c >= C) return;
+  a = 0.f;
+  m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    a += s0[k][lane];
+    m += s1[k][lane];
+  }
   sums[c] = a;
   sums[C + c] = m;
   if (dw) dw[c] = (beta != 0.f ? beta * dw[c] : 0.f) + m * invstd[c];
@@ -316,7 +338,9 @@ __device__ __forceinline__ void rows4_layout(int C, int& CB, int& LPR, int& RPW)
 __global__ __launch_bounds__(256) void moments_rows4(const float* __restrict__ x, int N, int C,
                                                      int splits, float* __restrict__ ws,
                                                      float* __restrict__ mean,
-                                                     float* __restrict__ var) {
+                                                     float* __restrict__ var,
+    float* __restrict__ cnt_out, float cnt) {
+  if (cnt_out && splits == 1 && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
   __shared__ float sh[3][1024];
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
@@ -429,6 +453,7 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
                                                    const float* __restrict__ w,
                                                    const float* __restrict__ bb, int N, int C,
                                                    int splits, int relu, int eval, float eps,
+                                                   const float* __restrict__ res,
                                                    float* __restrict__ y) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
@@ -447,10 +472,13 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
 #pragma unroll 4
   for (long r = b + rg; r < e; r += RPW) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + c);
+    // residual join (ResNet: relu(bn3(conv3) + identity)) fused into the normalisation
+    const f32x4 rv = res ? *reinterpret_cast<const f32x4*>(res + r * C + c)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float q = fmaf(v[j], sc[j], sf[j]);
+      const float q = fmaf(v[j], sc[j], sf[j]) + rv[j];
       o[j] = relu ? fmaxf(q, 0.f) : q;
     }
     *reinterpret_cast<f32x4*>(y + r * C + c) = o;
@@ -462,7 +490,7 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ w,
     const float* __restrict__ sums, const float* __restrict__ yr, const float* __restrict__ cnt,
-    int N, int C, int splits, float* __restrict__ dx) {
+    int N, int C, int splits, float* __restrict__ dx, float* __restrict__ dres) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
@@ -497,6 +525,8 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = fmaf(d[j], k1[j], fmaf(xv[j], k2[j], k3[j]));
     *reinterpret_cast<f32x4*>(dx + off) = o;
+    // gradient of the fused residual input: the ReLU-masked dy itself
+    if (dres) *reinterpret_cast<f32x4*>(dres + off) = d;
   }
 }
 
@@ -552,35 +582,39 @@ int bn_splits(int N, int C, int HW, int num_cus) {
 long bn_ws_floats(int C, int splits) { return 3L * C * (splits > 0 ? splits : 1); }
 
 void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, float* mean,
-                float* var, hipStream_t s) {
+                float* var, float* count_out, hipStream_t s) {
+  const float cnt = (float)((double)N * HW);
   if (rows4_ok(C, HW, {x}))
     hipLaunchKernelGGL(moments_rows4, dim3(rows4_nblk(C), splits), dim3(256), 0, s, x, N, C,
-                       splits, ws, mean, var);
+                       splits, ws, mean, var, count_out, cnt);
   else if (HW == 1)
     hipLaunchKernelGGL(moments_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, x, N, C, splits,
-                       ws, mean, var);
+                       ws, mean, var, count_out, cnt);
   else
     hipLaunchKernelGGL(moments_2d, dim3(C, splits), dim3(256), 0, s, x, N, C, HW, splits, ws,
-                       mean, var);
+                       mean, var, count_out, cnt);
   if (splits > 1)
-    hipLaunchKernelGGL(moments_final, dim3((C + 63) / 64), dim3(256), 0, s, ws, C, splits, mean,
-                       var);
+    hipLaunchKernelGGL(moments_final, dim3((C + 15) / 16), dim3(256), 0, s, ws, C, splits, mean,
+                       var, count_out, cnt);
 }
 
 void bn_merge(const float* gathered, int R, int C, float eps, float momentum, float* mean,
-              float* invstd, float* running_mean, float* running_var, hipStream_t s) {
+              float* invstd, float* running_mean, float* running_var, int64_t* num_batches,
+              hipStream_t s) {
   hipLaunchKernelGGL(merge_kernel, dim3((C + 255) / 256), dim3(256), 0, s, gathered, R, C, eps,
-                     momentum, mean, invstd, running_mean, running_var);
+                     momentum, mean, invstd, running_mean, running_var, num_batches);
 }
 
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
-              const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s) {
-  if (rows4_ok(C, HW, {x, y, mean, invstd, w, b})) {
+              const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
+              const float* residual) {
+  if (rows4_ok(C, HW, {x, y, mean, invstd, w, b, residual})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, mean, invstd, w,
-                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, y);
+                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, residual, y);
     return;
   }
+  if (residual) throw std::runtime_error("bn_elemt: a fused residual needs the [rows, C%4] form");
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, mean, invstd, w, b,
                      total, C, HW, relu ? 1 : 0, 0, 0.f, y);
@@ -591,7 +625,7 @@ void bn_eval(const float* x, const float* rmean, const float* rvar, const float*
   if (rows4_ok(C, HW, {x, y})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, rmean, rvar, w,
-                       b, N, C, sp, relu ? 1 : 0, 1, eps, y);
+                       b, N, C, sp, relu ? 1 : 0, 1, eps, (const float*)nullptr, y);
     return;
   }
   const long total = (long)N * C * HW;
@@ -612,19 +646,20 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
   else
     hipLaunchKernelGGL(bwd_reduce_2d, dim3(C, splits), dim3(256), 0, s, dy, x, mean, y_relu, N, C,
                        HW, splits, ws);
-  hipLaunchKernelGGL(bwd_reduce_final, dim3((C + 63) / 64), dim3(256), 0, s, ws, C, splits,
+  hipLaunchKernelGGL(bwd_reduce_final, dim3((C + 15) / 16), dim3(256), 0, s, ws, C, splits,
                      invstd, sums, dw, db, grad_beta);
 }
 
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
-                  int N, int C, int HW, float* dx, hipStream_t s) {
-  if (rows4_ok(C, HW, {dy, x, y_relu, dx})) {
+                  int N, int C, int HW, float* dx, hipStream_t s, float* dres) {
+  if (rows4_ok(C, HW, {dy, x, y_relu, dx, dres})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(bwd_elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, dy, x, mean,
-                       invstd, w, sums, y_relu, count, N, C, sp, dx);
+                       invstd, w, sums, y_relu, count, N, C, sp, dx, dres);
     return;
   }
+  if (dres) throw std::runtime_error("bn_bwd_elemt: a fused residual needs the [rows, C%4] form");
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(bwd_elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, dy, x, mean, invstd,
                      w, sums, y_relu, count, total, C, HW, dx);

@@ -3,8 +3,8 @@
 ``state_dict`` keys match ``torchvision.models.resnet50`` (conv1/bn1/layer1-4/fc, Bottleneck
 conv1-3/bn1-3/downsample.{0,1}); stride sits on the 3x3 conv (v1.5). 25.6 M parameters in 161
 tensors -- many small gradients, which is what stresses the bucketed all-reduce overlap (SURVEY.md
-§2.6). ReLU is fused into the batch-norm kernels (``relu=True``) and the residual join is one
-add+ReLU kernel. ``convert_sync_batchnorm`` turns the BatchNorm2d layers into SyncBatchNorm.
+§2.6). ReLU is fused into the batch-norm kernels (``relu=True``) and the residual join
+``relu(bn3(conv3) + identity)`` is fused into bn3's normalisation pass (and its backward). ``convert_sync_batchnorm`` turns the BatchNorm2d layers into SyncBatchNorm.
 Weights use torchvision's initialisation (Kaiming-normal fan_out convs, BN gamma=1 beta=0).
 """
 from __future__ import annotations
@@ -29,12 +29,17 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNorm2d(planes * 4, device=device)
         self.downsample = downsample
         self.stride = stride
+        self._fused_join = True
 
     def forward(self, x):
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
-        out = self.bn3(self.conv3(out))
         identity = self.downsample(x) if self.downsample is not None else x
+        if self._fused_join and hasattr(self.bn3, "relu_join"):
+            # relu(bn3(conv3(.)) + identity) in the normalisation pass; its backward writes the
+            # identity gradient in the same pass as bn3's (no separate add/ReLU-mask kernels)
+            return self.bn3.relu_join(self.conv3(out), identity)
+        out = self.bn3(self.conv3(out))
         return ops.add_relu(out, identity)
 
 

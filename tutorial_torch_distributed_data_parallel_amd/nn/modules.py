@@ -79,19 +79,31 @@ class _NativeBN(nn.modules.batchnorm._BatchNorm):
     def _group(self):
         return None
 
-    def forward(self, x):
+    def relu_join(self, x, residual):
+        """``relu(bn(x) + residual)`` as one normalisation pass (ResNet's residual join)."""
+        return self.forward(x, residual, relu=True)
+
+    def forward(self, x, residual=None, relu=None):
+        """``relu?(bn(x) [+ residual])``; ``residual`` fuses a residual join into the
+        normalisation (ResNet's ``relu(bn3(conv3(.)) + identity)``, one pass instead of two)."""
         self._check_input_dim(x)
         use_batch = self.training or not self.track_running_stats
         factor = 0.0
+        nbt = None
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
-            self.num_batches_tracked.add_(1)
+            if x.is_cuda:
+                nbt = self.num_batches_tracked  # incremented by the merge kernel (no ATen add_)
+            else:
+                self.num_batches_tracked.add_(1)
             self._nbt += 1
             factor = (1.0 / self._nbt) if self.momentum is None else self.momentum
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return ops.batch_norm(x, rm, rv, self.weight, self.bias, training=use_batch,
-                              momentum=factor, eps=self.eps, relu=self.relu,
-                              group=self._group() if use_batch else None)
+                              momentum=factor, eps=self.eps,
+                              relu=self.relu if relu is None else relu,
+                              group=self._group() if use_batch else None, residual=residual,
+                              num_batches_tracked=nbt)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")

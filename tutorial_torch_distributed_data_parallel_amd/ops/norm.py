@@ -34,7 +34,7 @@ class _TorchKernels:
         cnt = torch.tensor([float(v.shape[0] * v.shape[2])], dtype=x.dtype)
         return [torch.cat([mean, var, cnt])[: 2 * C + 1]]
 
-    def bn_merge(self, gathered, C, eps, momentum, rmean, rvar):
+    def bn_merge(self, gathered, C, eps, momentum, rmean, rvar, num_batches=None):
         g = gathered.reshape(-1, 2 * C + 1)
         g = g[g[:, 2 * C] > 0]
         n = g[:, 2 * C: 2 * C + 1]
@@ -42,13 +42,15 @@ class _TorchKernels:
         mean = (g[:, :C] * n).sum(0) / total
         m2 = (g[:, C: 2 * C] * n + n * (g[:, :C] - mean) ** 2).sum(0)
         var = m2 / total
+        if num_batches is not None:
+            num_batches.add_(1)
         if rmean is not None:
             unbiased = m2 / (total - 1) if total > 1 else var
             rmean.mul_(1 - momentum).add_(mean, alpha=momentum)
             rvar.mul_(1 - momentum).add_(unbiased, alpha=momentum)
         return torch.cat([mean, torch.rsqrt(var + eps), total.reshape(1)])
 
-    def bn_elemt(self, x, stats, w, b, relu):
+    def bn_elemt(self, x, stats, w, b, relu, residual=None):
         C = x.shape[1]
         shape = (1, C) + (1,) * (x.dim() - 2)
         y = (x - stats[:C].view(shape)) * stats[C: 2 * C].view(shape)
@@ -56,6 +58,8 @@ class _TorchKernels:
             y = y * w.view(shape)
         if b is not None:
             y = y + b.view(shape)
+        if residual is not None:
+            y = y + residual
         return F.relu(y) if relu else y
 
     def bn_bwd_reduce(self, dy, x, stats, y, dw, db, beta):
@@ -71,7 +75,7 @@ class _TorchKernels:
             db.copy_(s_dy)
         return torch.cat([s_dy, s_dyx])
 
-    def bn_bwd_elemt(self, dy, x, stats, w, sums, y):
+    def bn_bwd_elemt(self, dy, x, stats, w, sums, y, residual_grad=False):
         C = x.shape[1]
         shape = (1, C) + (1,) * (x.dim() - 2)
         if y is not None:
@@ -83,7 +87,7 @@ class _TorchKernels:
         dx = (dy - mdy - (x - stats[:C].view(shape)) * inv * inv * mdyx) * inv
         if w is not None:
             dx = dx * w.view(shape)
-        return dx
+        return [dx, dy] if residual_grad else [dx]
 
 
 _TORCH_K = _TorchKernels()
@@ -109,7 +113,8 @@ def _kernels(x):
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group,
+                residual, num_batches):
         K = _kernels(x)
         C = x.shape[1]
         # channels_last (NHWC) activations are a [pixels, C] matrix: the BatchNorm1d kernels
@@ -117,13 +122,17 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.nhwc = x.is_cuda and _is_nhwc(x)
         ctx.shape4 = tuple(x.shape)
         x = _rows(x) if ctx.nhwc else x.contiguous()
+        if residual is not None:
+            residual = _rows(residual.contiguous(memory_format=torch.channels_last)) \
+                if ctx.nhwc else residual.contiguous()
         st = K.bn_moments(x)[0]
         gathered = group.all_gather_flat(st) if group is not None else st
-        stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var)
-        y = K.bn_elemt(x, stats, weight, bias, relu)
+        stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var, num_batches)
+        y = K.bn_elemt(x, stats, weight, bias, relu, residual)
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.group = group
+        ctx.has_res = residual is not None
         ctx.save_for_backward(x, weight, stats, y if relu else None)
         return _unrows(y, ctx.shape4) if ctx.nhwc else y
 
@@ -137,24 +146,42 @@ class _BatchNormFn(torch.autograd.Function):
         dw = grad_dest(w_param) if (w_param is not None and needs(ctx, 1)) else None
         db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
         sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0)
-        dx = None
-        if needs(ctx, 0):
+        dx = dres = None
+        want_res = ctx.has_res and needs(ctx, 9)
+        if needs(ctx, 0) or want_res:
             if ctx.group is not None:
                 ctx.group.all_reduce_sum_(sums)
-            dx = K.bn_bwd_elemt(dy, x, stats, weight, sums, y)
+            # one pass: dx, and the residual input's gradient (the ReLU-masked dy) when fused
+            out = K.bn_bwd_elemt(dy, x, stats, weight, sums, y, want_res)
+            dx = out[0] if needs(ctx, 0) else None
+            dres = out[1] if want_res else None
             if ctx.nhwc:
-                dx = _unrows(dx, ctx.shape4)
-        return dx, dw, db, None, None, None, None, None, None
+                dx = _unrows(dx, ctx.shape4) if dx is not None else None
+                dres = _unrows(dres, ctx.shape4) if dres is not None else None
+        return dx, dw, db, None, None, None, None, None, None, dres, None
 
 
 def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
                running_var: torch.Tensor | None, weight: torch.Tensor | None = None,
                bias: torch.Tensor | None = None, training: bool = True, momentum: float = 0.1,
-               eps: float = 1e-5, relu: bool = False, group=None) -> torch.Tensor:
-    """Batch norm over dim 1 of x ([N, C] or [N, C, *]); ``group`` makes it synchronous."""
+               eps: float = 1e-5, relu: bool = False, group=None, residual=None,
+               num_batches_tracked=None) -> torch.Tensor:
+    """``relu?(batch_norm(x) [+ residual])`` over dim 1 of x ([N, C] or [N, C, *]); ``group``
+    makes it synchronous; ``num_batches_tracked`` (training) is incremented on the device."""
     if training:
+        if residual is not None and x.is_cuda and not (x.shape[1] % 4 == 0 and (
+                x.dim() == 2 or _is_nhwc(x))):
+            # the fused residual exists in the [rows, C % 4 == 0] kernels only
+            y = _BatchNormFn.apply(x, weight, bias, running_mean, running_var, float(momentum),
+                                   float(eps), False, group, None, num_batches_tracked)
+            y = y + residual
+            return F.relu(y) if relu else y
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, float(momentum),
-                                  float(eps), bool(relu), group)
+                                  float(eps), bool(relu), group, residual, num_batches_tracked)
+    if residual is not None:
+        y = batch_norm(x, running_mean, running_var, weight, bias, False, momentum, eps, False)
+        y = y + residual
+        return F.relu(y) if relu else y
     if x.is_cuda and not (torch.is_grad_enabled() and (x.requires_grad or (
             weight is not None and weight.requires_grad))):
         if _is_nhwc(x):
