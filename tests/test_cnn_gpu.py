@@ -296,3 +296,32 @@ def test_bottleneck_fused_join_matches_unfused(downsample):
     for (n, p), (_, q) in zip(a.named_buffers(), b.named_buffers()):
         torch.testing.assert_close(p, q, atol=1e-6, rtol=1e-5, msg=lambda m: f"{n}: {m}")
     assert int(a.bn3.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("case", ["pad_nchw", "rows_phase", "zero", "transpose"])
+def test_copy4d(case):
+    """csrc/elementwise.hip copy4d: strided copy over dst's shape, zeros outside src."""
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    if case == "pad_nchw":
+        src = torch.randn(4, 3, 9, 7, device="cuda", generator=g)
+        dst = torch.empty(4, 4, 9, 7, device="cuda").contiguous(memory_format=torch.channels_last)
+        ref = torch.cat([src, torch.zeros(4, 1, 9, 7, device="cuda")], 1)
+    elif case == "rows_phase":
+        src = torch.randn(2, 8, 5, 6, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last)
+        big = torch.zeros(2, 8, 10, 12, device="cuda").contiguous(memory_format=torch.channels_last)
+        dst = big[:, :, 1::2, 0::2]
+        ref = src
+    elif case == "zero":
+        dst = torch.ones(2, 8, 5, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+        src = torch.empty(0, 0, 0, 0, device="cuda")
+        ref = torch.zeros(2, 8, 5, 6, device="cuda")
+    else:
+        src = torch.randn(3, 3, 16, 64, device="cuda", generator=g).permute(3, 2, 0, 1)
+        dst = torch.empty(64, 16, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+        ref = src
+    C.copy4d(dst, src)
+    torch.testing.assert_close(dst, ref)

@@ -532,7 +532,8 @@ ConvGeom nhwc_geom(const std::vector<int64_t>& xs, int64_t cout, int64_t R, int6
 }
 
 Tensor conv_nhwc_exec(int mode, const ConvGeom& g, const Tensor& A, const Tensor& B, Tensor C,
-                      const c10::optional<Tensor>& bias, bool relu, double beta) {
+                      const c10::optional<Tensor>& bias, bool relu, double beta,
+                      const WeightTaps* wtap = nullptr) {
   TORCH_CHECK(conv_nhwc_ok(mode, g), "conv (NHWC): channels must be multiples of 4 and "
               "input-gradient strides powers of two");
   const ConvPlan pl = conv_nhwc_plan(mode, g, num_cus(C.get_device()));
@@ -540,8 +541,64 @@ Tensor conv_nhwc_exec(int mode, const ConvGeom& g, const Tensor& A, const Tensor
   if (pl.ws_floats > 0) ws = at::empty({pl.ws_floats}, C.options());
   conv_nhwc_run(pl, g, A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
                 fptr(bias), relu, (float)beta, pl.ws_floats > 0 ? ws.data_ptr<float>() : nullptr,
-                cur_stream());
+                cur_stream(), wtap);
   return C;
+}
+
+// the weight parameter [Cout, C, R, S] in channels_last memory = a contiguous [Cout][R][S][C]
+void check_weight_cl(const Tensor& w) {
+  CHECK_GPU(w); CHECK_F32(w);
+  TORCH_CHECK(w.dim() == 4 && w.permute({0, 2, 3, 1}).is_contiguous(),
+              "conv weight must be channels_last ([Cout][R][S][C] memory)");
+}
+
+// Input gradient straight from the channels_last weight parameter (stride 1)
+Tensor conv_nhwc_dgrad_w_op(const Tensor& dy, const Tensor& w, std::vector<int64_t> x_shape,
+                            int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy);
+  check_weight_cl(w);
+  const int64_t R = w.size(2), S = w.size(3);
+  TORCH_CHECK(sh == 1 && sw == 1, "dgrad_w: stride 1 (strided gradients go by phases)");
+  const ConvGeom g = nhwc_geom(x_shape, dy.size(1), R, S, sh, sw, ph, pw);
+  TORCH_CHECK(w.size(0) == g.Cout && w.size(1) == g.C, "dgrad_w: weight shape");
+  TORCH_CHECK(dy.size(2) == g.P && dy.size(3) == g.Q && dy.size(0) == g.N, "dgrad_w: dy shape");
+  auto dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const WeightTaps t{(int)R, (int)S, 0, 0, 1, 1};
+  return conv_nhwc_exec(kConvDgrad, g, dy, w, dx, c10::nullopt, false, 0.0, &t);
+}
+
+// One stride phase of a strided input gradient with the phase's taps read from the weight
+Tensor conv_nhwc_dgrad_phase_w_op(const Tensor& dy, const Tensor& w, int64_t Hp, int64_t Wp,
+                                  int64_t Rp, int64_t Sp, int64_t da, int64_t db, int64_t r0,
+                                  int64_t s0, int64_t sh, int64_t sw) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy);
+  check_weight_cl(w);
+  ConvGeom g;
+  g.N = (int)dy.size(0); g.Cout = (int)dy.size(1); g.P = (int)dy.size(2); g.Q = (int)dy.size(3);
+  g.C = (int)w.size(1); g.H = (int)Hp; g.W = (int)Wp; g.R = (int)Rp; g.S = (int)Sp;
+  g.sh = 1; g.sw = 1; g.ph = (int)da; g.pw = (int)db;
+  TORCH_CHECK(w.size(0) == g.Cout, "dgrad phase: weight / dy channels differ");
+  TORCH_CHECK(Rp > 0 && Sp > 0 && Hp > 0 && Wp > 0, "dgrad phase: empty phase");
+  TORCH_CHECK(r0 + (Rp - 1) * sh < w.size(2) && s0 + (Sp - 1) * sw < w.size(3),
+              "dgrad phase: taps outside the filter");
+  TORCH_CHECK((long)g.N * g.C * Hp * Wp < (1L << 31), "dgrad phase: < 2^31 elements");
+  auto out = at::empty({g.N, (int64_t)g.C, Hp, Wp},
+                       dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const WeightTaps t{(int)w.size(2), (int)w.size(3), (int)r0, (int)s0, (int)sh, (int)sw};
+  return conv_nhwc_exec(kConvDgrad, g, dy, w, out, c10::nullopt, false, 0.0, &t);
+}
+
+// dst = src over dst's logical shape (any strides); where an index is outside src's shape the
+// element is 0 (channel padding / un-padding, layout changes, strided phase scatters)
+void copy4d_op(Tensor& dst, const Tensor& src) {
+  CHECK_GPU(dst); CHECK_GPU(src); CHECK_F32(dst); CHECK_F32(src);
+  TORCH_CHECK(dst.dim() == 4 && src.dim() == 4, "copy4d: 4-D tensors");
+  Copy4D c{};
+  for (int i = 0; i < 4; ++i) {
+    c.dsz[i] = dst.size(i); c.dst_stride[i] = dst.stride(i);
+    c.ssz[i] = src.size(i); c.src_stride[i] = src.stride(i);
+  }
+  copy4d(src.data_ptr<float>(), dst.data_ptr<float>(), c, cur_stream());
 }
 
 // x channels_last [N,C,H,W]; wt [Cout, R*S*C] (k = (r, s, c)) -> y channels_last
@@ -980,6 +1037,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
   m.def("conv_nhwc_dgrad_phase", &conv_nhwc_dgrad_phase_op);
+  m.def("conv_nhwc_dgrad_w", &conv_nhwc_dgrad_w_op);
+  m.def("conv_nhwc_dgrad_phase_w", &conv_nhwc_dgrad_phase_w_op);
+  m.def("copy4d", &copy4d_op, py::arg("dst"), py::arg("src"));
   m.def("conv_wgrad_transposed", [](int64_t cout, int64_t R, int64_t S, int64_t C) {
     ConvGeom g{};
     g.Cout = (int)cout; g.R = (int)R; g.S = (int)S; g.C = (int)C;

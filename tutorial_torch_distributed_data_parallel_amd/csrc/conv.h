@@ -33,9 +33,14 @@ bool conv_wgrad_transposed(const ConvGeom& g);
 void conv_set_wgrad_transposed(int mode);  // -1 auto, 0 / 1 force
 void conv_set_wgrad_target(int per_cu);     // split-K workgroups per CU (<= 0: auto)
 ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
+// Input gradient with B read from the weight's own [Cout][R][S][C] storage (no transposed copy):
+// the (phase) taps of the full R x S filter, (r, s) = (r0 + rp*sh, s0 + sp*sw); see WTap.
+struct WeightTaps {
+  int R, S, r0, s0, sh, sw;
+};
 void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,
-                   hipStream_t s);
+                   hipStream_t s, const WeightTaps* wtap = nullptr);
 
 // NCHW ReLU backward + per-channel bias gradient: g = dy*(y>0) (if y), db = sum over n,hw.
 int chan_splits(int N, int C, int HW, int num_cus);

@@ -1,3 +1,4 @@
+#include <algorithm>
 // ReLU backward fused with the bias gradient.
 //
 // For a Linear(+ReLU) layer the backward needs g = dy * (y > 0) twice (weight and input
@@ -140,4 +141,132 @@ void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, 
   hipLaunchKernelGGL(gather_batch_kernel, dim3(B, slices), dim3(256), 0, s, x, y, idx, n, F, xb,
                      yb);
 }
+namespace {
+// general form with 32-bit magic-number index math (total < 2^31)
+struct Copy4D32 {
+  FastDiv d3, d2, d1;
+  int sz3, sz2, sz1, ssz[4];
+  long ds[4], ss[4];
+};
+
+__global__ __launch_bounds__(256) void copy4d32_kernel(const float* __restrict__ src,
+                                                       float* __restrict__ dst, Copy4D32 c,
+                                                       uint32_t total) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t q3 = fdiv(i, c.d3);
+    const int i3 = (int)(i - q3 * (uint32_t)c.sz3);
+    const uint32_t q2 = fdiv(q3, c.d2);
+    const int i2 = (int)(q3 - q2 * (uint32_t)c.sz2);
+    const uint32_t i0 = fdiv(q2, c.d1);
+    const int i1 = (int)(q2 - i0 * (uint32_t)c.sz1);
+    const bool in = (int)i0 < c.ssz[0] && i1 < c.ssz[1] && i2 < c.ssz[2] && i3 < c.ssz[3];
+    const float v = in ? src[i0 * c.ss[0] + i1 * c.ss[1] + i2 * c.ss[2] + i3 * c.ss[3]] : 0.f;
+    dst[i0 * c.ds[0] + i1 * c.ds[1] + i2 * c.ds[2] + i3 * c.ds[3]] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void copy4d_kernel(const float* __restrict__ src,
+                                                     float* __restrict__ dst, Copy4D c,
+                                                     long total) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    long r = i, idx[4];
+#pragma unroll
+    for (int d = 3; d >= 0; --d) {
+      idx[d] = r % c.dsz[d];
+      r /= c.dsz[d];
+    }
+    long so = 0, doff = 0;
+    bool in = true;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      in = in && idx[d] < c.ssz[d];
+      so += idx[d] * c.src_stride[d];
+      doff += idx[d] * c.dst_stride[d];
+    }
+    dst[doff] = in ? src[so] : 0.f;
+  }
+}
+}  // namespace
+
+namespace {
+// channels-last fast path of copy4d: dim 1 (channels) has unit stride on both sides, so every
+// (n, h, w) row is C contiguous floats -- float4 per lane, 32-bit magic-number index math
+struct RowsCopy {
+  int C4d, C4s, H, W;
+  FastDiv dC4, dW, dH;
+  long ds0, ds2, ds3, ss0, ss2, ss3;
+};
+
+__global__ __launch_bounds__(256) void copy4d_rows_kernel(const float* __restrict__ src,
+                                                          float* __restrict__ dst, RowsCopy c,
+                                                          uint32_t total) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t q = fdiv(i, c.dC4);
+    const int c4 = (int)(i - q * (uint32_t)c.C4d);
+    const uint32_t q2 = fdiv(q, c.dW);
+    const int w = (int)(q - q2 * (uint32_t)c.W);
+    const uint32_t n = fdiv(q2, c.dH);
+    const int h = (int)(q2 - n * (uint32_t)c.H);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c4 < c.C4s)
+      v = *reinterpret_cast<const f32x4*>(src + n * c.ss0 + h * c.ss2 + w * c.ss3 + 4 * c4);
+    *reinterpret_cast<f32x4*>(dst + n * c.ds0 + h * c.ds2 + w * c.ds3 + 4 * c4) = v;
+  }
+}
+}  // namespace
+
+void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s) {
+  const long total = c.dsz[0] * c.dsz[1] * c.dsz[2] * c.dsz[3];
+  if (total <= 0) return;
+  // rows fast path: unit channel stride, 16-B aligned rows, same spatial extent
+  const bool empty_src = c.ssz[0] * c.ssz[1] * c.ssz[2] * c.ssz[3] == 0;
+  const bool rows = c.dst_stride[1] == 1 && (empty_src || c.src_stride[1] == 1) &&
+                    c.dsz[1] % 4 == 0 && (empty_src || c.ssz[1] % 4 == 0) &&
+                    (empty_src || (c.ssz[0] >= c.dsz[0] && c.ssz[2] >= c.dsz[2] &&
+                                   c.ssz[3] >= c.dsz[3])) &&
+                    ((uintptr_t)dst & 15) == 0 && (empty_src || ((uintptr_t)src & 15) == 0) &&
+                    c.dst_stride[0] % 4 == 0 && c.dst_stride[2] % 4 == 0 &&
+                    c.dst_stride[3] % 4 == 0 &&
+                    (empty_src || (c.src_stride[0] % 4 == 0 && c.src_stride[2] % 4 == 0 &&
+                                   c.src_stride[3] % 4 == 0)) &&
+                    total / 4 < (1L << 31);
+  if (rows) {
+    RowsCopy r{};
+    r.C4d = (int)(c.dsz[1] / 4);
+    r.C4s = empty_src ? 0 : (int)(std::min(c.ssz[1], c.dsz[1]) / 4);
+    r.H = (int)c.dsz[2];
+    r.W = (int)c.dsz[3];
+    r.dC4 = make_fastdiv(r.C4d);
+    r.dW = make_fastdiv(r.W);
+    r.dH = make_fastdiv(r.H);
+    r.ds0 = c.dst_stride[0]; r.ds2 = c.dst_stride[2]; r.ds3 = c.dst_stride[3];
+    r.ss0 = c.src_stride[0]; r.ss2 = c.src_stride[2]; r.ss3 = c.src_stride[3];
+    const uint32_t n4 = (uint32_t)(total / 4);
+    long g = ((long)n4 + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(copy4d_rows_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, r, n4);
+    return;
+  }
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (total < (1L << 31) && c.dsz[1] < (1L << 31) && c.dsz[2] < (1L << 31) &&
+      c.dsz[3] < (1L << 31)) {
+    Copy4D32 k{};
+    k.sz3 = (int)c.dsz[3]; k.sz2 = (int)c.dsz[2]; k.sz1 = (int)c.dsz[1];
+    k.d3 = make_fastdiv(k.sz3); k.d2 = make_fastdiv(k.sz2); k.d1 = make_fastdiv(k.sz1);
+    for (int d = 0; d < 4; ++d) {
+      k.ssz[d] = (int)std::min<long>(c.ssz[d], 1L << 30);
+      k.ds[d] = c.dst_stride[d];
+      k.ss[d] = c.src_stride[d];
+    }
+    hipLaunchKernelGGL(copy4d32_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, k,
+                       (uint32_t)total);
+    return;
+  }
+  hipLaunchKernelGGL(copy4d_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, c, total);
+}
+
 }  // namespace tdp

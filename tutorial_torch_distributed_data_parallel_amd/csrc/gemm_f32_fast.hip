@@ -28,6 +28,7 @@
 //     taps that fall into the zero padding read a 16-B zero page. With C % 32 == 0 a K tile
 //     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
 #include <cstdlib>
+#include <stdexcept>
 #include <vector>
 
 #include "common.h"
@@ -53,8 +54,20 @@ struct ConvInfo {
   FastDiv dC, dS, dPQ, dQ;
 };
 
+// Input-gradient B read straight from the conv weight's [Cout][Rf][Sf][C] storage (the
+// parameter's channels_last memory) -- no per-step transposed weight copy. GEMM row k =
+// (tap t, co) with co fastest (the dy gather's k order); t = (rp, sp) walks the stride phase's
+// Rp x Sp sub-grid of filter taps (r, s) = (r0 + rp*sh, s0 + sp*sw) (stride 1: the whole filter).
+struct WTap {
+  int Cout, Sp, r0, s0, sh, sw, Sf, C;
+  long rs;      // weight row stride Rf*Sf*C
+  int uniform;  // Cout % 32 == 0: a 32-deep K tile is one tap (decomposed once, wave-uniform)
+  FastDiv dCout, dSp;
+};
+
 struct FastParams {
   ConvInfo cv;
+  WTap wt;
   const float* A;
   const float* B;
   float* C;
@@ -165,7 +178,7 @@ struct TileSrc {
 // (kImWgradT: the same shifted-pixel operand as kImWgrad, used as A of the transposed weight
 // gradient dW^T[(r,s,c)][co] = x_shifted^T . dy when Cout is too small for a 128-row tile)
 constexpr int kDenseK = 0, kDenseMN = 1, kImFwd = 2, kImDgrad = 3, kImWgrad = 4,
-              kImWgradT = 5;
+              kImWgradT = 5, kWTap = 6;
 
 // Implicit K-contiguous A (rows = pixels of the row grid, k = (r, s, c) with c fastest):
 //   FWD   : source x,  pixel (n, p, q), tap reads x[n][p*sh-ph+r][q*sw-pw+s][c]
@@ -290,6 +303,55 @@ struct ImSrcB {
   }
 };
 
+// MN-contiguous B of the input gradient gathered from the weight storage (see WTap)
+template <int R>
+struct WTapSrc {
+  static constexpr int CH = (32 * R * 4) / 1024, NPW = CH / 4;
+  static constexpr int LPR = R / 4, RPC = 1024 / (R * 4);
+  const float* base;
+  int koff[NPW];
+
+  __device__ __forceinline__ void init(const FastParams& p, int r0, int rlim, int wid,
+                                       int lane) {
+    int gc = r0 + (lane % LPR) * 4;
+    gc = gc < rlim ? gc : rlim - 4;
+    base = p.B + gc;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) koff[i] = (wid * NPW + i) * RPC + lane / LPR;
+  }
+
+  __device__ __forceinline__ void issue(const FastParams& p, int k0, int klim, char* dst,
+                                        int wid) const {
+    const WTap& w = p.wt;
+    if (w.uniform) {
+      // one tap for the whole tile (k0 is a multiple of 32, Cout of 32, K of 32): the tap and
+      // the tile's first output channel are scalar; a lane only adds its row offset
+      const uint32_t q = fdiv(k0, w.dCout);
+      const int co0 = k0 - (int)q * w.Cout;
+      const uint32_t rp = fdiv(q, w.dSp);
+      const int sp = (int)q - (int)rp * w.Sp;
+      const int tap = (w.r0 + (int)rp * w.sh) * w.Sf + w.s0 + sp * w.sw;
+      const float* tb = base + (long)co0 * w.rs + (long)tap * w.C;
+#pragma unroll
+      for (int i = 0; i < NPW; ++i)
+        glds16(tb + (long)koff[i] * w.rs, dst + (wid * NPW + i) * 1024);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int j = wid * NPW + i;
+      int gk = k0 + koff[i];
+      gk = gk < klim ? gk : klim - 1;
+      const uint32_t q = fdiv(gk, w.dCout);
+      const int co = gk - (int)q * w.Cout;
+      const uint32_t rp = fdiv(q, w.dSp);
+      const int sp = (int)q - (int)rp * w.Sp;
+      const int tap = (w.r0 + (int)rp * w.sh) * w.Sf + w.s0 + sp * w.sw;
+      glds16(base + (long)co * w.rs + (long)tap * w.C, dst + j * 1024);
+    }
+  }
+};
+
 template <int R, int KIND, bool IS_A>
 struct SrcOf;
 template <int R, bool IS_A>
@@ -322,6 +384,8 @@ template <int R>
 struct SrcOf<R, kImWgrad, false> : ImSrcB<R, false> {};
 template <int R>
 struct SrcOf<R, kImWgradT, true> : ImSrcB<R, true> {};
+template <int R>
+struct SrcOf<R, kWTap, false> : WTapSrc<R> {};
 
 // One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel.
 template <int FN, int AKIND, int BKIND, int S, int OPTK>
@@ -1091,8 +1155,18 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
 //        when conv_wgrad_transposed(g): C = dWt^T [R*S*C][Cout] (A/B arguments unchanged)
 void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,
-                   hipStream_t s) {
+                   hipStream_t s, const WeightTaps* wtap) {
   FastParams p{};
+  if (wtap) {
+    if (pl.mode != kConvDgrad) throw std::runtime_error("weight taps are for the input gradient");
+    p.wt.Cout = g.Cout; p.wt.Sp = g.S;
+    p.wt.r0 = wtap->r0; p.wt.s0 = wtap->s0; p.wt.sh = wtap->sh; p.wt.sw = wtap->sw;
+    p.wt.Sf = wtap->S; p.wt.C = g.C;
+    p.wt.rs = (long)wtap->R * wtap->S * g.C;
+    p.wt.uniform = g.Cout % 32 == 0 ? 1 : 0;
+    p.wt.dCout = make_fastdiv(g.Cout);
+    p.wt.dSp = make_fastdiv(g.S);
+  }
   ConvInfo& cv = p.cv;
   cv.zero = zero_page();
   cv.S = g.S; cv.sh = g.sh; cv.sw = g.sw; cv.ph = g.ph; cv.pw = g.pw;
@@ -1130,6 +1204,7 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
   const int fn = pl.fn, st = pl.fm;
   if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s);
+  else if (pl.mode == kConvDgrad && wtap) launch_kinds<kImDgrad, kWTap>(p, fn, st, nblocks, s);
   else if (pl.mode == kConvDgrad) launch_kinds<kImDgrad, kDenseMN>(p, fn, st, nblocks, s);
   else if (!wt) launch_kinds<kDenseMN, kImWgrad>(p, fn, st, nblocks, s);
   else launch_kinds<kImWgradT, kDenseMN>(p, fn, st, nblocks, s);

@@ -220,6 +220,11 @@ int relu_bias_slices(int B, int N, int num_cus);
 void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, float* g,
                       float* db, float beta_db, float* part, int slices, hipStream_t s);
 void fill_f32(float* x, long n, float v, hipStream_t s);
+// 4-D strided copy over dst's logical shape; elements outside src's shape are written as 0
+struct Copy4D {
+  long dsz[4], dst_stride[4], ssz[4], src_stride[4];
+};
+void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s);
 // xb[b] = x[idx[b]] (rows of F floats), yb[b] = y[idx[b]]: a loader batch in one launch
 void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, long F, int B,
                   float* xb, int64_t* yb, hipStream_t s);

@@ -36,6 +36,11 @@ class Conv2d(nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
                          bias=bias, device=device, dtype=dtype)
         self.relu = relu
+        # The weight lives in channels_last memory ([Cout][R][S][C]): exactly the operand layout
+        # of the implicit-GEMM kernels (forward B, input-gradient taps, weight-gradient output),
+        # so no step permutes or copies it. Shape and state_dict keys stay torch's [Cout, C, R, S].
+        if in_channels % 4 == 0:
+            self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
 
     def forward(self, x):
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, relu=self.relu)

@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import torch
 
+from ..parallel.arena import slot_view
+
 
 _task_id = getattr(torch._C, "_current_graph_task_id", lambda: -1)
 
@@ -33,7 +35,7 @@ def grad_dest(p: torch.Tensor | None) -> torch.Tensor | None:
         if task < 0 or getattr(p, "_tdp_slot_task", None) != task:
             p._tdp_slot_task = task
             buf, off = slot
-            return buf[off: off + p.numel()].view(p.shape)
+            return slot_view(buf, p, off)  # the parameter's own layout (channels_last convs)
     return torch.empty_like(p)
 
 

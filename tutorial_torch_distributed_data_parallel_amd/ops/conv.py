@@ -12,9 +12,10 @@ Main path -- channels_last (NHWC) activations on the LDS-DMA MFMA GEMM pipeline
   * weight gradient -- ``dy^T`` (a plain [pixels][Cout] matrix) times shifted-pixel rows of ``x``,
     split-K over the N*P*Q reduction.
   Outputs are channels_last, so a 1x1 convolution IS a GEMM ([N*H*W, C] x [C, Cout]); batch norm
-  and the ReLU/bias backward treat NHWC tensors as [pixels, C] matrices. Weights keep torch's
-  [Cout][C][R][S] layout (checkpoint compatible); R x S > 1 convs use a transposed copy per step.
-  Input channels that are not a multiple of 4 (the RGB stem) are zero-padded to 4.
+  and the ReLU/bias backward treat NHWC tensors as [pixels, C] matrices. Weights are
+  channels_last parameters (logical [Cout, C, R, S]: state_dict / checkpoints unchanged) whose
+  [Cout][R][S][C] memory every kernel reads or writes directly (see _ConvNHWCFn).
+  Input channels that are not a multiple of 4 (the RGB stem) are zero-padded to 4, natively.
 Fallback -- NCHW register-staged implicit GEMM (``csrc/conv.hip``) for shapes the NHWC path does
 not take (channel counts not a multiple of 4 beyond the stem, non power-of-two strides in dgrad).
 CPU tensors run ``torch.nn.functional.conv2d`` (the oracle of the CPU tests).
@@ -78,7 +79,25 @@ def _rows(t):
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
 
 
+def _as_cl(C, t, channels: int | None = None):
+    """``t`` as a channels_last tensor with ``channels`` channels (zero-padded): ``t`` itself
+    when it already is one, else ONE native strided copy (csrc/elementwise.hip copy4d)."""
+    n, c, h, w = t.shape
+    channels = c if channels is None else channels
+    if channels == c and t.is_contiguous(memory_format=_CL):
+        return t
+    out = torch.empty((n, channels, h, w), device=t.device, dtype=t.dtype, memory_format=_CL)
+    C.copy4d(out, t)
+    return out
+
+
 class _ConvNHWCFn(torch.autograd.Function):
+    """Weights are channels_last parameters ([Cout][R][S][C] memory, nn/modules.py Conv2d): the
+    forward reads them as the GEMM's K-contiguous B, the input gradient gathers its taps straight
+    from them (csrc/gemm_f32_fast.hip WTap), and the weight gradient is written straight into
+    the parameter's gradient slot in that layout -- no per-step permute / pad / copy-back. Only
+    the RGB stem (3 channels, padded to 4 for the 16-B DMA chunks) repacks, natively."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, relu: bool):
         C = native()
@@ -87,31 +106,23 @@ class _ConvNHWCFn(torch.autograd.Function):
         Cp = (Cin + 3) // 4 * 4
         sh, sw = stride
         ph, pw = padding
-        if Cp != Cin:  # zero-pad the channels (RGB stem) so every DMA chunk is 4 channels
-            xp = torch.empty((N, Cp, H, W), device=x.device, dtype=x.dtype, memory_format=_CL)
-            xp[:, Cin:].zero_()
-            xp[:, :Cin].copy_(x)
-        else:
-            xp = x.contiguous(memory_format=_CL)
-        wt = weight.permute(0, 2, 3, 1)  # [Cout, R, S, C]: k = (r, s, c)
-        if Cp != Cin:
-            wt = F.pad(wt, (0, Cp - Cin))
-        wt = wt.contiguous()
-        y = C.conv_nhwc_fwd(xp, wt, bias, R, S, sh, sw, ph, pw, relu)
+        xp = _as_cl(C, x, Cp)
+        wt = _as_cl(C, weight, Cp)  # the parameter itself for every conv but the stem
+        y = C.conv_nhwc_fwd(xp, wt.permute(0, 2, 3, 1), bias, R, S, sh, sw, ph, pw, relu)
         ctx.geom = (R, S, sh, sw, ph, pw, Cin, Cp)
         ctx.relu = relu
         ctx.params = (weight, bias)
-        ctx.save_for_backward(xp, weight, y if relu else None)
+        ctx.save_for_backward(xp, wt, y if relu else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        xp, weight, y = ctx.saved_tensors
+        xp, wt, y = ctx.saved_tensors
         w_param, b_param = ctx.params
         R, S, sh, sw, ph, pw, Cin, Cp = ctx.geom
-        Cout = weight.shape[0]
-        dy = dy.contiguous(memory_format=_CL)
+        Cout = wt.shape[0]
+        dy = _as_cl(C, dy)
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
         # ReLU mask + bias gradient: one pass over dy viewed as [pixels, Cout]
@@ -127,35 +138,35 @@ class _ConvNHWCFn(torch.autograd.Function):
                 # dW^T [(r,s,c)][co] when it pads the 128-row MFMA tiles less (small Cout, Cout=192)
                 dwT = torch.empty((R, S, Cp, Cout), device=dy.device, dtype=dy.dtype)
                 C.conv_nhwc_wgrad(g, xp, dwT, R, S, sh, sw, ph, pw, 0.0)
-                dw.copy_(dwT[:, :, :Cin, :].permute(3, 2, 0, 1))
-            elif R == 1 and S == 1 and Cp == Cin:
-                C.conv_nhwc_wgrad(g, xp, dw, R, S, sh, sw, ph, pw, 0.0)  # [Cout][C] already
+                C.copy4d(dw, dwT.permute(3, 2, 0, 1))
+            elif Cp == Cin and dw.permute(0, 2, 3, 1).is_contiguous():
+                # straight into the gradient slot ([Cout][R][S][C] = the parameter's layout)
+                C.conv_nhwc_wgrad(g, xp, dw.permute(0, 2, 3, 1), R, S, sh, sw, ph, pw, 0.0)
             else:
                 dwt = torch.empty((Cout, R, S, Cp), device=dy.device, dtype=dy.dtype)
                 C.conv_nhwc_wgrad(g, xp, dwt, R, S, sh, sw, ph, pw, 0.0)
-                dw.copy_(dwt[..., :Cin].permute(0, 3, 1, 2))
+                C.copy4d(dw, dwt.permute(0, 3, 1, 2))
         if needs(ctx, 0):
-            w2 = weight.permute(2, 3, 0, 1)  # [R, S, Cout, C]: k = (r, s, co), n = c
-            if Cp != Cin:
-                w2 = F.pad(w2, (0, Cp - Cin))
             if sh == 1 and sw == 1:
-                dx = C.conv_nhwc_dgrad(g, w2.contiguous(), list(xp.shape), R, S, sh, sw, ph, pw)
+                dx = C.conv_nhwc_dgrad_w(g, wt, list(xp.shape), sh, sw, ph, pw)
             else:
-                dx = _dgrad_phases(C, g, w2, xp.shape, R, S, sh, sw, ph, pw)
+                dx = _dgrad_phases(C, g, wt, xp.shape, R, S, sh, sw, ph, pw)
             if Cp != Cin:
                 dx = dx[:, :Cin]
         return dx, dw, db, None, None, None
 
 
-def _dgrad_phases(C, g, w2, x_shape, R, S, sh, sw, ph, pw):
+def _dgrad_phases(C, g, wt, x_shape, R, S, sh, sw, ph, pw):
     """Strided input gradient as sh*sw stride-1 GEMMs, one per output phase.
 
     dx pixels h = a + sh*i only receive taps r = r0 + sh*t with r0 = (a + ph) mod sh, from dy row
     p = i + da - t (da = (a + ph - r0) / sh): a stride-1 convolution over the phase sub-grid with
-    the phase's taps. This skips the (sh*sw - 1)/(sh*sw) of multiply-adds a direct gather spends
-    on the zeros between strided taps (measured 4x on ResNet's stride-2 layers)."""
+    the phase's taps, which the kernel gathers from the weight itself. This skips the
+    (sh*sw - 1)/(sh*sw) of multiply-adds a direct gather spends on the zeros between strided
+    taps (measured 4x on ResNet's stride-2 layers)."""
     N, Cp, H, W = x_shape
     dx = torch.empty(x_shape, device=g.device, dtype=g.dtype, memory_format=_CL)
+    none = torch.empty((0, 0, 0, 0), device=g.device, dtype=g.dtype)
     for a in range(sh):
         r0 = (a + ph) % sh
         Rp, Hp, da = len(range(r0, R, sh)), len(range(a, H, sh)), (a + ph - r0) // sh
@@ -166,10 +177,10 @@ def _dgrad_phases(C, g, w2, x_shape, R, S, sh, sw, ph, pw):
                 continue
             view = dx[:, :, a::sh, b::sw]
             if Rp == 0 or Sp == 0:
-                view.zero_()
+                C.copy4d(view, none)  # no tap reaches this phase: zeros
                 continue
-            w2p = w2[r0::sh, s0::sw].contiguous()
-            view.copy_(C.conv_nhwc_dgrad_phase(g, w2p, Cp, Hp, Wp, Rp, Sp, da, db))
+            C.copy4d(view, C.conv_nhwc_dgrad_phase_w(g, wt, Hp, Wp, Rp, Sp, da, db, r0, s0, sh,
+                                                     sw))
     return dx
 
 

@@ -23,6 +23,21 @@ def _round_up(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
 
+def _cl(p) -> bool:
+    """A 4-D parameter in channels_last memory (conv weights: [Cout][R][S][C])."""
+    return p.dim() == 4 and not p.is_contiguous() and \
+        p.is_contiguous(memory_format=torch.channels_last)
+
+
+def slot_view(buf: torch.Tensor, p, off: int) -> torch.Tensor:
+    """``p``-shaped view of ``buf[off: off + p.numel()]`` with ``p``'s memory layout (contiguous,
+    or channels_last for conv weights) -- arena parameter / gradient / optimizer-state slots."""
+    if _cl(p):
+        C, H, W = p.shape[1], p.shape[2], p.shape[3]
+        return buf.as_strided(p.shape, (H * W * C, 1, W * C, C), off)
+    return buf[off: off + p.numel()].view(p.shape)
+
+
 class ParamArena:
     def __init__(self, params, device=None, dtype=torch.float32):
         params = list(params)
@@ -50,11 +65,11 @@ class ParamArena:
         self.grad = torch.zeros(self.numel, device=device, dtype=dtype)
         with torch.no_grad():
             for p, o, n in zip(uniq, self.offsets, self.numels):
-                view = self.data[o: o + n].view(p.shape)
+                view = slot_view(self.data, p, o)
                 view.copy_(p.data)
                 p.data = view
                 if p.grad is not None:
-                    g = self.grad[o: o + n].view(p.shape)
+                    g = slot_view(self.grad, p, o)
                     g.copy_(p.grad)
                     p.grad = g
                 p._tdp_gslot = (self.grad, o)
@@ -67,8 +82,7 @@ class ParamArena:
         raise KeyError("parameter not in arena")
 
     def grad_view(self, i: int) -> torch.Tensor:
-        o, n = self.offsets[i], self.numels[i]
-        return self.grad[o: o + n].view(self.params[i].shape)
+        return slot_view(self.grad, self.params[i], self.offsets[i])
 
     def is_arena_grad(self, i: int) -> bool:
         g = self.params[i].grad
@@ -108,19 +122,18 @@ class ParamArena:
         data, grad = remap(self.data), remap(self.grad)
         with torch.no_grad():
             for k, i in enumerate(order):
-                p, o, n = self.params[i], offsets[k], self.numels[i]
-                p.data = data[o: o + n].view(p.shape)
+                p, o = self.params[i], offsets[k]
+                p.data = slot_view(data, p, o)
                 p._tdp_gslot = (grad, o)
                 if had_grad[i]:
-                    p.grad = grad[o: o + n].view(p.shape)
+                    p.grad = slot_view(grad, p, o)
         self.params, self.offsets = params, offsets
         self.numels = [p.numel() for p in params]
         self.numel, self.data, self.grad = numel, data, grad
         return remap
 
     def state_view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
-        o, n = self.offsets[i], self.numels[i]
-        return buf[o: o + n].view(self.params[i].shape)
+        return slot_view(buf, self.params[i], self.offsets[i])
 
 
 def arena_of(params):
