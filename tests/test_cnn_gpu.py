@@ -266,18 +266,20 @@ def test_conv_wgrad_plans(orient, override, Co, C, R):
     torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-4, atol=2e-3)
 
 
-@pytest.mark.parametrize("downsample", [False, True])
+@pytest.mark.parametrize("downsample", [False, True, "stride1"])
 def test_bottleneck_fused_join_matches_unfused(downsample):
     """relu(bn3(conv3) + identity) fused into bn3's normalisation (and its backward writing the
-    identity gradient) == separate bn3 + add_relu; running stats and num_batches_tracked are
-    updated on the device."""
+    identity gradient) == separate bn3 + add_relu; the block input's two gradients meet in one
+    shared buffer (conv1's input-gradient GEMM with beta = 1, the strided downsample phase with
+    copy4d accumulate); running stats and num_batches_tracked are updated on the device."""
     import copy
 
     from tutorial_torch_distributed_data_parallel_amd.models.resnet import Bottleneck
     from tutorial_torch_distributed_data_parallel_amd.nn import BatchNorm2d, Conv2d
 
     torch.manual_seed(0)
-    inp, planes, stride = (64, 32, 2) if downsample else (128, 32, 1)
+    inp, planes, stride = {False: (128, 32, 1), True: (64, 32, 2),
+                           "stride1": (64, 32, 1)}[downsample]
     ds = torch.nn.Sequential(Conv2d(inp, planes * 4, 1, stride=stride, bias=False),
                              BatchNorm2d(planes * 4)) if downsample else None
     a = Bottleneck(inp, planes, stride, ds).cuda()
@@ -298,9 +300,11 @@ def test_bottleneck_fused_join_matches_unfused(downsample):
     assert int(a.bn3.num_batches_tracked) == 1
 
 
-@pytest.mark.parametrize("case", ["pad_nchw", "rows_phase", "zero", "transpose"])
+@pytest.mark.parametrize("case", ["pad_nchw", "rows_phase", "zero", "transpose", "acc_rows",
+                                  "acc_generic", "acc_zero"])
 def test_copy4d(case):
-    """csrc/elementwise.hip copy4d: strided copy over dst's shape, zeros outside src."""
+    """csrc/elementwise.hip copy4d: strided copy over dst's shape, zeros outside src;
+    accumulate: dst += src where src has the index."""
     from tutorial_torch_distributed_data_parallel_amd._native import native
 
     C = native()
@@ -319,9 +323,53 @@ def test_copy4d(case):
         dst = torch.ones(2, 8, 5, 6, device="cuda").contiguous(memory_format=torch.channels_last)
         src = torch.empty(0, 0, 0, 0, device="cuda")
         ref = torch.zeros(2, 8, 5, 6, device="cuda")
-    else:
+    elif case == "transpose":
         src = torch.randn(3, 3, 16, 64, device="cuda", generator=g).permute(3, 2, 0, 1)
         dst = torch.empty(64, 16, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
         ref = src
+    elif case == "acc_rows":
+        src = torch.randn(2, 8, 5, 6, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last)
+        big = torch.randn(2, 8, 10, 12, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last)
+        want = big.clone()
+        want[:, :, 1::2, 0::2] += src
+        C.copy4d(big[:, :, 1::2, 0::2], src, accumulate=True)
+        torch.testing.assert_close(big, want)
+        return
+    elif case == "acc_generic":
+        src = torch.randn(4, 3, 9, 7, device="cuda", generator=g)
+        dst = torch.randn(4, 4, 9, 7, device="cuda", generator=g)
+        want = dst.clone()
+        want[:, :3] += src
+        C.copy4d(dst, src, accumulate=True)
+        torch.testing.assert_close(dst, want)
+        return
+    else:
+        dst = torch.randn(2, 8, 5, 6, device="cuda", generator=g)
+        want = dst.clone()
+        C.copy4d(dst, torch.empty(0, 0, 0, 0, device="cuda"), accumulate=True)
+        torch.testing.assert_close(dst, want)
+        return
     C.copy4d(dst, src)
     torch.testing.assert_close(dst, ref)
+
+
+def test_dgrad_w_accumulates_into_out():
+    """conv_nhwc_dgrad_w(out=, beta=1): out = dgrad + out (split-K and direct tilings)."""
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for (B, Cin, H, Cout, R) in [(8, 64, 14, 256, 1), (2, 256, 7, 64, 1), (4, 32, 12, 32, 3)]:
+        w = torch.randn(Cout, Cin, R, R, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last) * 0.1
+        dy = torch.randn(B, Cout, H, H, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last)
+        base = torch.randn(B, Cin, H, H, device="cuda", generator=g).contiguous(
+            memory_format=torch.channels_last)
+        fresh = C.conv_nhwc_dgrad_w(dy, w, [B, Cin, H, H], 1, 1, R // 2, R // 2)
+        out = base.clone()
+        r = C.conv_nhwc_dgrad_w(dy, w, [B, Cin, H, H], 1, 1, R // 2, R // 2, out=out, beta=1.0)
+        assert r.data_ptr() == out.data_ptr()
+        torch.testing.assert_close(out, fresh + base, atol=1e-4, rtol=1e-4)

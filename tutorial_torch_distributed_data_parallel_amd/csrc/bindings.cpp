@@ -552,9 +552,11 @@ void check_weight_cl(const Tensor& w) {
               "conv weight must be channels_last ([Cout][R][S][C] memory)");
 }
 
-// Input gradient straight from the channels_last weight parameter (stride 1)
+// Input gradient straight from the channels_last weight parameter (stride 1); with `out`,
+// written there as out = dgrad + beta * out (a residual block's shared input gradient)
 Tensor conv_nhwc_dgrad_w_op(const Tensor& dy, const Tensor& w, std::vector<int64_t> x_shape,
-                            int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+                            int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                            const c10::optional<Tensor>& out, double beta) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CL(dy);
   check_weight_cl(w);
   const int64_t R = w.size(2), S = w.size(3);
@@ -562,9 +564,17 @@ Tensor conv_nhwc_dgrad_w_op(const Tensor& dy, const Tensor& w, std::vector<int64
   const ConvGeom g = nhwc_geom(x_shape, dy.size(1), R, S, sh, sw, ph, pw);
   TORCH_CHECK(w.size(0) == g.Cout && w.size(1) == g.C, "dgrad_w: weight shape");
   TORCH_CHECK(dy.size(2) == g.P && dy.size(3) == g.Q && dy.size(0) == g.N, "dgrad_w: dy shape");
-  auto dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor dx;
+  if (out.has_value()) {
+    dx = *out;
+    CHECK_GPU(dx); CHECK_F32(dx); CHECK_CL(dx);
+    TORCH_CHECK(dx.sizes().vec() == x_shape, "dgrad_w: out shape");
+  } else {
+    TORCH_CHECK(beta == 0.0, "dgrad_w: beta needs out");
+    dx = at::empty(x_shape, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   const WeightTaps t{(int)R, (int)S, 0, 0, 1, 1};
-  return conv_nhwc_exec(kConvDgrad, g, dy, w, dx, c10::nullopt, false, 0.0, &t);
+  return conv_nhwc_exec(kConvDgrad, g, dy, w, dx, c10::nullopt, false, beta, &t);
 }
 
 // One stride phase of a strided input gradient with the phase's taps read from the weight
@@ -589,8 +599,9 @@ Tensor conv_nhwc_dgrad_phase_w_op(const Tensor& dy, const Tensor& w, int64_t Hp,
 }
 
 // dst = src over dst's logical shape (any strides); where an index is outside src's shape the
-// element is 0 (channel padding / un-padding, layout changes, strided phase scatters)
-void copy4d_op(Tensor& dst, const Tensor& src) {
+// element is 0 (channel padding / un-padding, layout changes, strided phase scatters).
+// accumulate: dst += src where src has the index, dst unchanged elsewhere
+void copy4d_op(Tensor& dst, const Tensor& src, bool accumulate) {
   CHECK_GPU(dst); CHECK_GPU(src); CHECK_F32(dst); CHECK_F32(src);
   TORCH_CHECK(dst.dim() == 4 && src.dim() == 4, "copy4d: 4-D tensors");
   Copy4D c{};
@@ -598,6 +609,7 @@ void copy4d_op(Tensor& dst, const Tensor& src) {
     c.dsz[i] = dst.size(i); c.dst_stride[i] = dst.stride(i);
     c.ssz[i] = src.size(i); c.src_stride[i] = src.stride(i);
   }
+  c.accumulate = accumulate;
   copy4d(src.data_ptr<float>(), dst.data_ptr<float>(), c, cur_stream());
 }
 
@@ -1037,9 +1049,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
   m.def("conv_nhwc_dgrad_phase", &conv_nhwc_dgrad_phase_op);
-  m.def("conv_nhwc_dgrad_w", &conv_nhwc_dgrad_w_op);
+  m.def("conv_nhwc_dgrad_w", &conv_nhwc_dgrad_w_op, py::arg("dy"), py::arg("w"),
+        py::arg("x_shape"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("out") = py::none(), py::arg("beta") = 0.0);
   m.def("conv_nhwc_dgrad_phase_w", &conv_nhwc_dgrad_phase_w_op);
-  m.def("copy4d", &copy4d_op, py::arg("dst"), py::arg("src"));
+  m.def("copy4d", &copy4d_op, py::arg("dst"), py::arg("src"), py::arg("accumulate") = false);
   m.def("conv_wgrad_transposed", [](int64_t cout, int64_t R, int64_t S, int64_t C) {
     ConvGeom g{};
     g.Cout = (int)cout; g.R = (int)R; g.S = (int)S; g.C = (int)C;

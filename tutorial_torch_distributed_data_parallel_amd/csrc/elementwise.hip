@@ -149,6 +149,7 @@ struct Copy4D32 {
   long ds[4], ss[4];
 };
 
+template <bool ACC>
 __global__ __launch_bounds__(256) void copy4d32_kernel(const float* __restrict__ src,
                                                        float* __restrict__ dst, Copy4D32 c,
                                                        uint32_t total) {
@@ -162,10 +163,16 @@ __global__ __launch_bounds__(256) void copy4d32_kernel(const float* __restrict__
     const int i1 = (int)(q2 - i0 * (uint32_t)c.sz1);
     const bool in = (int)i0 < c.ssz[0] && i1 < c.ssz[1] && i2 < c.ssz[2] && i3 < c.ssz[3];
     const float v = in ? src[i0 * c.ss[0] + i1 * c.ss[1] + i2 * c.ss[2] + i3 * c.ss[3]] : 0.f;
-    dst[i0 * c.ds[0] + i1 * c.ds[1] + i2 * c.ds[2] + i3 * c.ds[3]] = v;
+    float* d = dst + i0 * c.ds[0] + i1 * c.ds[1] + i2 * c.ds[2] + i3 * c.ds[3];
+    if (ACC) {
+      if (in) *d += v;
+    } else {
+      *d = v;
+    }
   }
 }
 
+template <bool ACC>
 __global__ __launch_bounds__(256) void copy4d_kernel(const float* __restrict__ src,
                                                      float* __restrict__ dst, Copy4D c,
                                                      long total) {
@@ -185,7 +192,11 @@ __global__ __launch_bounds__(256) void copy4d_kernel(const float* __restrict__ s
       so += idx[d] * c.src_stride[d];
       doff += idx[d] * c.dst_stride[d];
     }
-    dst[doff] = in ? src[so] : 0.f;
+    if (ACC) {
+      if (in) dst[doff] += src[so];
+    } else {
+      dst[doff] = in ? src[so] : 0.f;
+    }
   }
 }
 }  // namespace
@@ -199,6 +210,7 @@ struct RowsCopy {
   long ds0, ds2, ds3, ss0, ss2, ss3;
 };
 
+template <bool ACC>
 __global__ __launch_bounds__(256) void copy4d_rows_kernel(const float* __restrict__ src,
                                                           float* __restrict__ dst, RowsCopy c,
                                                           uint32_t total) {
@@ -213,7 +225,11 @@ __global__ __launch_bounds__(256) void copy4d_rows_kernel(const float* __restric
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (c4 < c.C4s)
       v = *reinterpret_cast<const f32x4*>(src + n * c.ss0 + h * c.ss2 + w * c.ss3 + 4 * c4);
-    *reinterpret_cast<f32x4*>(dst + n * c.ds0 + h * c.ds2 + w * c.ds3 + 4 * c4) = v;
+    else if (ACC)
+      continue;
+    f32x4* d = reinterpret_cast<f32x4*>(dst + n * c.ds0 + h * c.ds2 + w * c.ds3 + 4 * c4);
+    if (ACC) v += *d;
+    *d = v;
   }
 }
 }  // namespace
@@ -221,6 +237,7 @@ __global__ __launch_bounds__(256) void copy4d_rows_kernel(const float* __restric
 void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s) {
   const long total = c.dsz[0] * c.dsz[1] * c.dsz[2] * c.dsz[3];
   if (total <= 0) return;
+  if (c.accumulate && c.ssz[0] * c.ssz[1] * c.ssz[2] * c.ssz[3] == 0) return;  // += nothing
   // rows fast path: unit channel stride, 16-B aligned rows, same spatial extent
   const bool empty_src = c.ssz[0] * c.ssz[1] * c.ssz[2] * c.ssz[3] == 0;
   const bool rows = c.dst_stride[1] == 1 && (empty_src || c.src_stride[1] == 1) &&
@@ -247,7 +264,12 @@ void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s) {
     const uint32_t n4 = (uint32_t)(total / 4);
     long g = ((long)n4 + 255) / 256;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(copy4d_rows_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, r, n4);
+    if (c.accumulate)
+      hipLaunchKernelGGL(copy4d_rows_kernel<true>, dim3((unsigned)g), dim3(256), 0, s, src, dst,
+                         r, n4);
+    else
+      hipLaunchKernelGGL(copy4d_rows_kernel<false>, dim3((unsigned)g), dim3(256), 0, s, src, dst,
+                         r, n4);
     return;
   }
   long g = (total + 255) / 256;
@@ -262,11 +284,20 @@ void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s) {
       k.ds[d] = c.dst_stride[d];
       k.ss[d] = c.src_stride[d];
     }
-    hipLaunchKernelGGL(copy4d32_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, k,
-                       (uint32_t)total);
+    if (c.accumulate)
+      hipLaunchKernelGGL(copy4d32_kernel<true>, dim3((unsigned)g), dim3(256), 0, s, src, dst, k,
+                         (uint32_t)total);
+    else
+      hipLaunchKernelGGL(copy4d32_kernel<false>, dim3((unsigned)g), dim3(256), 0, s, src, dst, k,
+                         (uint32_t)total);
     return;
   }
-  hipLaunchKernelGGL(copy4d_kernel, dim3((unsigned)g), dim3(256), 0, s, src, dst, c, total);
+  if (c.accumulate)
+    hipLaunchKernelGGL(copy4d_kernel<true>, dim3((unsigned)g), dim3(256), 0, s, src, dst, c,
+                       total);
+  else
+    hipLaunchKernelGGL(copy4d_kernel<false>, dim3((unsigned)g), dim3(256), 0, s, src, dst, c,
+                       total);
 }
 
 }  // namespace tdp

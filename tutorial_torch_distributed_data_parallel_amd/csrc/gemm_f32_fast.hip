@@ -784,8 +784,38 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
   float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
   const long ldo = split ? p.N : p.ldc;
+  // beta != 0 reads C: all 16 rows of an f-slab are loaded before any store, so the loads are
+  // in flight together (interleaved with the stores to `out` they would serialise on the
+  // possible aliasing: one memory round trip per row)
+  const bool rmw = !split && p.beta != 0.f;
 #pragma unroll
   for (int f = 0; f < FM; ++f) {
+    float cold[16][2];
+    if (rmw) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+        const float* orow = out + (long)(row < p.M ? row : 0) * ldo;
+        if (BKC || FN == 1) {
+#pragma unroll
+          for (int g = 0; g < FN; ++g) {
+            const int col = n0 + wn * (32 * FN) + g * 32 + l31;
+            cold[r][g] = (row < p.M && col < p.N) ? orow[col] : 0.f;
+          }
+        } else {
+          const int col = n0 + wn * 64 + 2 * l31;
+          if (row < p.M && col + 1 < p.N) {
+            const f32x2 o = *reinterpret_cast<const f32x2*>(orow + col);
+            cold[r][0] = o[0];
+            cold[r][1] = o[1];
+          } else {
+            cold[r][0] = (row < p.M && col < p.N) ? orow[col] : 0.f;
+            cold[r][1] = 0.f;
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -800,7 +830,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
           float v = acc[f][g][r];
           if (!split) {
             if (p.bias) v += p.bias[col];
-            if (p.beta != 0.f) v += p.beta * orow[col];
+            if (rmw) v += p.beta * cold[r][g];
             if (p.relu) v = fmaxf(v, 0.f);
           }
           orow[col] = v;
@@ -811,10 +841,9 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
         if (col + 1 < p.N) {
           if (!split) {
             if (p.bias) { v[0] += p.bias[col]; v[1] += p.bias[col + 1]; }
-            if (p.beta != 0.f) {
-              const f32x2 o = *reinterpret_cast<const f32x2*>(orow + col);
-              v[0] += p.beta * o[0];
-              v[1] += p.beta * o[1];
+            if (rmw) {
+              v[0] += p.beta * cold[r][0];
+              v[1] += p.beta * cold[r][1];
             }
             if (p.relu) { v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); }
           }
@@ -823,7 +852,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
           float x = v[0];
           if (!split) {
             if (p.bias) x += p.bias[col];
-            if (p.beta != 0.f) x += p.beta * orow[col];
+            if (rmw) x += p.beta * cold[r][0];
             if (p.relu) x = fmaxf(x, 0.f);
           }
           orow[col] = x;

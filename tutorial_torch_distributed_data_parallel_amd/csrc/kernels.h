@@ -221,8 +221,10 @@ void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, fl
                       float* db, float beta_db, float* part, int slices, hipStream_t s);
 void fill_f32(float* x, long n, float v, hipStream_t s);
 // 4-D strided copy over dst's logical shape; elements outside src's shape are written as 0
+// (accumulate: dst += src, and elements outside src's shape are left alone)
 struct Copy4D {
   long dsz[4], dst_stride[4], ssz[4], src_stride[4];
+  bool accumulate;
 };
 void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s);
 // xb[b] = x[idx[b]] (rows of F floats), yb[b] = y[idx[b]]: a loader batch in one launch

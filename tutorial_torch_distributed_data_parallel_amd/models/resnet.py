@@ -9,9 +9,11 @@ Weights use torchvision's initialisation (Kaiming-normal fan_out convs, BN gamma
 """
 from __future__ import annotations
 
+import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops._grad import SharedGrad, fork
 from ..nn import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d
 
 
@@ -32,15 +34,40 @@ class Bottleneck(nn.Module):
         self._fused_join = True
 
     def forward(self, x):
+        if self._fused_join and hasattr(self.bn3, "relu_join"):
+            return self._forward_fused(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         identity = self.downsample(x) if self.downsample is not None else x
-        if self._fused_join and hasattr(self.bn3, "relu_join"):
-            # relu(bn3(conv3(.)) + identity) in the normalisation pass; its backward writes the
-            # identity gradient in the same pass as bn3's (no separate add/ReLU-mask kernels)
-            return self.bn3.relu_join(self.conv3(out), identity)
         out = self.bn3(self.conv3(out))
         return ops.add_relu(out, identity)
+
+    def _forward_fused(self, x):
+        # relu(bn3(conv3(.)) + identity) in the normalisation pass; its backward writes the
+        # identity gradient in the same pass as bn3's (no separate add/ReLU-mask kernels).
+        # x's two consumers (conv1, identity path) share ONE gradient buffer (ops/_grad.py
+        # SharedGrad): bn3's backward (or the downsample conv's input gradient) writes it and
+        # conv1's input-gradient GEMM accumulates into it -- no autograd add of the two.
+        sink = None
+        xa = xb = x
+        if torch.is_grad_enabled() and x.requires_grad:
+            sink = SharedGrad()
+            xa, xb = fork(x, sink)
+        out = self.bn1(self.conv1(xa, grad_into=sink) if _takes_sink(self.conv1) else
+                       self.conv1(xa))
+        out = self.bn2(self.conv2(out))
+        ds = self.downsample
+        if ds is None:
+            return self.bn3.relu_join(self.conv3(out), xb, grad_into=sink)
+        if isinstance(ds, nn.Sequential) and len(ds) == 2 and _takes_sink(ds[0]):
+            identity = ds[1](ds[0](xb, grad_into=sink))
+        else:
+            identity = ds(xb)
+        return self.bn3.relu_join(self.conv3(out), identity)
+
+
+def _takes_sink(m) -> bool:
+    return isinstance(m, Conv2d)
 
 
 class ResNet(nn.Module):

@@ -42,8 +42,9 @@ class Conv2d(nn.Conv2d):
         if in_channels % 4 == 0:
             self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
 
-    def forward(self, x):
-        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, relu=self.relu)
+    def forward(self, x, grad_into=None):
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, relu=self.relu,
+                          grad_into=grad_into)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")
@@ -84,11 +85,12 @@ class _NativeBN(nn.modules.batchnorm._BatchNorm):
     def _group(self):
         return None
 
-    def relu_join(self, x, residual):
-        """``relu(bn(x) + residual)`` as one normalisation pass (ResNet's residual join)."""
-        return self.forward(x, residual, relu=True)
+    def relu_join(self, x, residual, grad_into=None):
+        """``relu(bn(x) + residual)`` as one normalisation pass (ResNet's residual join);
+        ``grad_into``: the residual's gradient goes into that ``SharedGrad``."""
+        return self.forward(x, residual, relu=True, residual_grad_into=grad_into)
 
-    def forward(self, x, residual=None, relu=None):
+    def forward(self, x, residual=None, relu=None, residual_grad_into=None):
         """``relu?(bn(x) [+ residual])``; ``residual`` fuses a residual join into the
         normalisation (ResNet's ``relu(bn3(conv3(.)) + identity)``, one pass instead of two)."""
         self._check_input_dim(x)
@@ -108,7 +110,7 @@ class _NativeBN(nn.modules.batchnorm._BatchNorm):
                               momentum=factor, eps=self.eps,
                               relu=self.relu if relu is None else relu,
                               group=self._group() if use_batch else None, residual=residual,
-                              num_batches_tracked=nbt)
+                              num_batches_tracked=nbt, residual_grad_into=residual_grad_into)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")

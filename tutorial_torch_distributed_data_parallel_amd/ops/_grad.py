@@ -62,3 +62,51 @@ def epilogue_target(p: torch.Tensor | None):
 
 def needs(ctx, i: int) -> bool:
     return bool(ctx.needs_input_grad[i])
+
+
+class SharedGrad:
+    """One gradient buffer shared by the consumers of a forked tensor (:func:`fork`).
+
+    A residual block's input ``x`` feeds the block's first convolution and its identity path;
+    autograd would give each consumer its own gradient tensor and add them (one extra
+    read-read-write pass over an activation-sized tensor per block). Consumers that know the sink
+    instead ``deposit`` into ``buf``: the first one writes it, later ones accumulate into it --
+    the input-gradient GEMM with ``beta = 1`` (csrc/gemm_f32_fast.hip epilogue), a strided phase
+    with ``copy4d(accumulate=True)`` -- and all return ``buf`` itself, which ``fork``'s backward
+    then passes on once."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+    def deposit(self, g: torch.Tensor) -> torch.Tensor:
+        """Generic path (consumers without a fused accumulate): ``buf += g``."""
+        if self.buf is None:
+            self.buf = g
+        else:
+            self.buf.add_(g)
+        return self.buf
+
+
+class _Fork(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, sink, n):
+        ctx.sink = sink
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        sink = ctx.sink
+        buf, sink.buf = sink.buf, None
+        total = buf
+        for g in grads:  # consumers that did not deposit: their gradients are added here
+            if g is None or g is buf:
+                continue
+            total = g if total is None else total.add_(g)
+        return total, None, None
+
+
+def fork(x: torch.Tensor, sink: SharedGrad, n: int = 2):
+    """``n`` aliases of ``x`` whose gradients meet in ``sink`` (see :class:`SharedGrad`)."""
+    return _Fork.apply(x, sink, n)

@@ -27,7 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
-from ._grad import grad_dest, needs
+from ._grad import SharedGrad, grad_dest, needs
 
 
 def _pair(v):
@@ -36,11 +36,12 @@ def _pair(v):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, relu: bool):
+    def forward(ctx, x, weight, bias, stride, padding, relu: bool, sink=None):
         C = native()
         sh, sw = stride
         ph, pw = padding
         y = C.conv2d_fwd(x, weight, bias, sh, sw, ph, pw, relu)
+        ctx.sink = sink
         ctx.geom = (sh, sw, ph, pw)
         ctx.relu = relu
         ctx.params = (weight, bias)
@@ -68,7 +69,9 @@ class _Conv2dFn(torch.autograd.Function):
             C.conv2d_wgrad(g, x, dw, sh, sw, ph, pw, 0.0)
         if needs(ctx, 0):
             dx = C.conv2d_dgrad(g, weight, ctx.x_shape, sh, sw, ph, pw)
-        return dx, dw, db, None, None, None
+            if ctx.sink is not None:
+                dx = ctx.sink.deposit(dx)
+        return dx, dw, db, None, None, None, None
 
 
 _CL = torch.channels_last
@@ -99,7 +102,7 @@ class _ConvNHWCFn(torch.autograd.Function):
     the RGB stem (3 channels, padded to 4 for the 16-B DMA chunks) repacks, natively."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, relu: bool):
+    def forward(ctx, x, weight, bias, stride, padding, relu: bool, sink=None):
         C = native()
         N, Cin, H, W = x.shape
         Cout, _, R, S = weight.shape
@@ -110,6 +113,7 @@ class _ConvNHWCFn(torch.autograd.Function):
         wt = _as_cl(C, weight, Cp)  # the parameter itself for every conv but the stem
         y = C.conv_nhwc_fwd(xp, wt.permute(0, 2, 3, 1), bias, R, S, sh, sw, ph, pw, relu)
         ctx.geom = (R, S, sh, sw, ph, pw, Cin, Cp)
+        ctx.sink = sink
         ctx.relu = relu
         ctx.params = (weight, bias)
         ctx.save_for_backward(xp, wt, y if relu else None)
@@ -147,25 +151,33 @@ class _ConvNHWCFn(torch.autograd.Function):
                 C.conv_nhwc_wgrad(g, xp, dwt, R, S, sh, sw, ph, pw, 0.0)
                 C.copy4d(dw, dwt.permute(0, 3, 1, 2))
         if needs(ctx, 0):
+            sink = ctx.sink
+            acc = sink.buf if (sink is not None and Cp == Cin) else None
             if sh == 1 and sw == 1:
-                dx = C.conv_nhwc_dgrad_w(g, wt, list(xp.shape), sh, sw, ph, pw)
+                # with a shared residual-input gradient: accumulated by the GEMM (beta = 1)
+                dx = C.conv_nhwc_dgrad_w(g, wt, list(xp.shape), sh, sw, ph, pw, out=acc,
+                                         beta=0.0 if acc is None else 1.0)
             else:
-                dx = _dgrad_phases(C, g, wt, xp.shape, R, S, sh, sw, ph, pw)
+                dx = _dgrad_phases(C, g, wt, xp.shape, R, S, sh, sw, ph, pw, into=acc)
             if Cp != Cin:
                 dx = dx[:, :Cin]
-        return dx, dw, db, None, None, None
+            if sink is not None:
+                dx = dx if acc is not None else sink.deposit(dx)
+        return dx, dw, db, None, None, None, None
 
 
-def _dgrad_phases(C, g, wt, x_shape, R, S, sh, sw, ph, pw):
+def _dgrad_phases(C, g, wt, x_shape, R, S, sh, sw, ph, pw, into=None):
     """Strided input gradient as sh*sw stride-1 GEMMs, one per output phase.
 
     dx pixels h = a + sh*i only receive taps r = r0 + sh*t with r0 = (a + ph) mod sh, from dy row
     p = i + da - t (da = (a + ph - r0) / sh): a stride-1 convolution over the phase sub-grid with
     the phase's taps, which the kernel gathers from the weight itself. This skips the
     (sh*sw - 1)/(sh*sw) of multiply-adds a direct gather spends on the zeros between strided
-    taps (measured 4x on ResNet's stride-2 layers)."""
+    taps (measured 4x on ResNet's stride-2 layers). ``into``: accumulate into that tensor
+    instead (phases without taps leave it alone)."""
     N, Cp, H, W = x_shape
-    dx = torch.empty(x_shape, device=g.device, dtype=g.dtype, memory_format=_CL)
+    acc = into is not None
+    dx = into if acc else torch.empty(x_shape, device=g.device, dtype=g.dtype, memory_format=_CL)
     none = torch.empty((0, 0, 0, 0), device=g.device, dtype=g.dtype)
     for a in range(sh):
         r0 = (a + ph) % sh
@@ -177,10 +189,11 @@ def _dgrad_phases(C, g, wt, x_shape, R, S, sh, sw, ph, pw):
                 continue
             view = dx[:, :, a::sh, b::sw]
             if Rp == 0 or Sp == 0:
-                C.copy4d(view, none)  # no tap reaches this phase: zeros
+                if not acc:
+                    C.copy4d(view, none)  # no tap reaches this phase: zeros
                 continue
             C.copy4d(view, C.conv_nhwc_dgrad_phase_w(g, wt, Hp, Wp, Rp, Sp, da, db, r0, s0, sh,
-                                                     sw))
+                                                     sw), accumulate=acc)
     return dx
 
 
@@ -196,11 +209,13 @@ def _nhwc_ok(x, weight, stride):
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
-           stride=1, padding=0, relu: bool = False) -> torch.Tensor:
+           stride=1, padding=0, relu: bool = False,
+           grad_into: SharedGrad | None = None) -> torch.Tensor:
     """``relu?(conv2d(x, weight, bias, stride, padding))`` for float32 [N, C, H, W] tensors.
 
     On the GPU the result is channels_last (NHWC memory, logical NCHW shape, as torch does for
-    channels_last inputs)."""
+    channels_last inputs). ``grad_into``: the input gradient goes into that shared buffer (a
+    forked residual input, ops/_grad.py ``fork``)."""
     stride, padding = _pair(stride), _pair(padding)
     if not x.is_cuda:
         y = F.conv2d(x, weight, bias, stride, padding)
@@ -208,8 +223,9 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     if x.dtype != torch.float32:
         raise TypeError(f"native conv2d expects float32 activations, got {x.dtype}")
     if _nhwc_ok(x, weight, stride):
-        return _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu)
-    return _Conv2dFn.apply(x.contiguous(), weight.contiguous(), bias, stride, padding, relu)
+        return _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu, grad_into)
+    return _Conv2dFn.apply(x.contiguous(), weight.contiguous(), bias, stride, padding, relu,
+                           grad_into)
 
 
 def bias_relu_backward_reference(dy, y, bias_needed: bool):

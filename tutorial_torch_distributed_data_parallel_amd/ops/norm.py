@@ -114,7 +114,7 @@ def _kernels(x):
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group,
-                residual, num_batches):
+                residual, num_batches, sink=None):
         K = _kernels(x)
         C = x.shape[1]
         # channels_last (NHWC) activations are a [pixels, C] matrix: the BatchNorm1d kernels
@@ -133,6 +133,7 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.group = group
         ctx.has_res = residual is not None
+        ctx.sink = sink
         ctx.save_for_backward(x, weight, stats, y if relu else None)
         return _unrows(y, ctx.shape4) if ctx.nhwc else y
 
@@ -158,16 +159,19 @@ class _BatchNormFn(torch.autograd.Function):
             if ctx.nhwc:
                 dx = _unrows(dx, ctx.shape4) if dx is not None else None
                 dres = _unrows(dres, ctx.shape4) if dres is not None else None
-        return dx, dw, db, None, None, None, None, None, None, dres, None
+            if dres is not None and ctx.sink is not None:
+                dres = ctx.sink.deposit(dres)  # the forked block input's shared gradient
+        return dx, dw, db, None, None, None, None, None, None, dres, None, None
 
 
 def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
                running_var: torch.Tensor | None, weight: torch.Tensor | None = None,
                bias: torch.Tensor | None = None, training: bool = True, momentum: float = 0.1,
                eps: float = 1e-5, relu: bool = False, group=None, residual=None,
-               num_batches_tracked=None) -> torch.Tensor:
+               num_batches_tracked=None, residual_grad_into=None) -> torch.Tensor:
     """``relu?(batch_norm(x) [+ residual])`` over dim 1 of x ([N, C] or [N, C, *]); ``group``
-    makes it synchronous; ``num_batches_tracked`` (training) is incremented on the device."""
+    makes it synchronous; ``num_batches_tracked`` (training) is incremented on the device;
+    ``residual_grad_into`` (a ``SharedGrad``) receives the residual's gradient."""
     if training:
         if residual is not None and x.is_cuda and not (x.shape[1] % 4 == 0 and (
                 x.dim() == 2 or _is_nhwc(x))):
@@ -177,7 +181,8 @@ def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
             y = y + residual
             return F.relu(y) if relu else y
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, float(momentum),
-                                  float(eps), bool(relu), group, residual, num_batches_tracked)
+                                  float(eps), bool(relu), group, residual, num_batches_tracked,
+                                  residual_grad_into)
     if residual is not None:
         y = batch_norm(x, running_mean, running_var, weight, bias, False, momentum, eps, False)
         y = y + residual
