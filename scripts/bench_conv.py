@@ -49,6 +49,8 @@ def main():
         Cout, _, R, S = ws
         x = torch.randn(B, Cin, H, W, device="cuda")
         w = torch.randn(ws, device="cuda") * 0.05
+        if Cin % 4 == 0:  # the Conv2d module's parameter layout (nn/modules.py)
+            w = w.contiguous(memory_format=torch.channels_last)
         P = (H + 2 * pd[0] - R) // st[0] + 1
         Q = (W + 2 * pd[1] - S) // st[1] + 1
         flops = 2.0 * B * P * Q * Cout * Cin * R * S

@@ -203,7 +203,11 @@ class Accelerator:
     def backward(self, loss, **kwargs):
         self._step += 1
         self.sync_gradients = (self._step % self.gradient_accumulation_steps) == 0
-        (loss / self.gradient_accumulation_steps).backward(**kwargs)
+        if "gradient" in kwargs:
+            (loss / self.gradient_accumulation_steps).backward(**kwargs)
+        else:  # seeded with a cached 1/steps tensor: no fill or division kernel per step
+            from ..ops.loss import backward
+            backward(loss, 1.0 / self.gradient_accumulation_steps, **kwargs)
 
     def clip_grad_norm_(self, parameters, max_norm: float, norm_type: float = 2.0):
         """Clip the (already averaged) gradients: native on MI355X (tdp.nn.utils)."""

@@ -80,6 +80,7 @@ struct FastParams {
   int tiles_n, tiles_m;
   float beta, rowsum_beta;
   int relu;
+  int cvec;  // C (or the split-K workspace) takes 16-B row stores: N % 4 == 0, aligned rows
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
 };
 
@@ -784,6 +785,67 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
   float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
   const long ldo = split ? p.N : p.ldc;
+  if (p.cvec) {
+    // Row-vector store: the tile goes through LDS (the pipeline stages are free once every wave
+    // has left the K loop) and leaves as 16-B-per-lane row segments. The accumulator layout
+    // alone gives each lane one column (or a column pair) of 16 rows: dword stores, 4x the
+    // store instructions, and the store tail is issue-bound (an output-heavy GEMM such as a 1x1
+    // convolution with K = 64 spent most of its time there).
+    constexpr int PAD = (BM * (BN + 8) * 4 <= S * STG) ? 8 : 0;  // 4-row offset = 32 banks
+    constexpr int TS = BN + PAD;
+    float* T = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is done reading the last K stage
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int lr = wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+        if (BKC || FN == 1) {
+#pragma unroll
+          for (int g = 0; g < FN; ++g) T[lr * TS + wn * (32 * FN) + g * 32 + l31] = acc[f][g][r];
+        } else {
+          *reinterpret_cast<f32x2*>(T + lr * TS + wn * 64 + 2 * l31) =
+              f32x2{acc[f][0][r], acc[f][FN - 1][r]};
+        }
+      }
+    __syncthreads();
+    constexpr int C4 = BN / 4;          // float4 per tile row
+    constexpr int IT = BM * C4 / kT;    // float4 per thread (8 or 16)
+    constexpr int HB = 8;               // C loads in flight per batch (beta != 0)
+    const bool rmw = !split && p.beta != 0.f;
+#pragma unroll
+    for (int i0 = 0; i0 < IT; i0 += HB) {
+      f32x4 cold[HB];
+      if (rmw) {
+#pragma unroll
+        for (int i = 0; i < HB; ++i) {
+          const int e = (i0 + i) * kT + threadIdx.x;
+          const int row = m0 + e / C4, col = n0 + (e % C4) * 4;
+          const bool ok = row < p.M && col < p.N;
+          cold[i] = *reinterpret_cast<const f32x4*>(out + (ok ? row * ldo + col : 0));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < HB; ++i) {
+        const int e = (i0 + i) * kT + threadIdx.x;
+        const int lr = e / C4, lc = (e % C4) * 4;
+        const int row = m0 + lr, col = n0 + lc;
+        if (row >= p.M || col >= p.N) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(T + lr * TS + lc);
+        if (!split) {
+          if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
+          if (rmw) v += p.beta * cold[i];
+          if (p.relu) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+          }
+        }
+        *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
+      }
+    }
+    return;  // a persistent loop's barrier protects T before the next tile's DMA
+  }
   // beta != 0 reads C: all 16 rows of an f-slab are loaded before any store, so the loads are
   // in flight together (interleaved with the stores to `out` they would serialise on the
   // possible aliasing: one memory round trip per row)
@@ -978,6 +1040,15 @@ std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wg
 void gemm_f32_set_override(int fn, int splits, int stages) {
   o_fn = fn; o_splits = splits; o_stages = stages;
 }
+// Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
+static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
+void gemm_f32_set_cvec(bool on) { o_no_cvec = !on; }
+static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int splits) {
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (N % 4) return false;
+  if (splits > 1) return true;  // the workspace: N-float rows of an aligned allocation
+  return ldc % 4 == 0 && al(C) && (bias == nullptr || al(bias));
+}
 
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   int fn = (a.M >= 512 && a.N >= 512) ? 2 : 1;
@@ -1025,6 +1096,7 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.beta = plan.splits > 1 ? 0.f : a.beta;
   p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
+  p.cvec = c_vec_ok(a.N, a.ldc, a.C, a.bias, plan.splits) && !o_no_cvec;
   p.opt = a.opt;
   const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
   const bool ak = a.a_kcontig, bk = a.b_kcontig;
@@ -1230,6 +1302,7 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   p.tiles_n = ceil_div(pl.N, 64 * pl.fn);
   p.beta = pl.splits > 1 ? 0.f : beta;
   p.relu = (pl.splits > 1 ? false : relu) ? 1 : 0;
+  p.cvec = c_vec_ok(pl.N, p.ldc, C, bias, pl.splits) && !o_no_cvec;
   const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
   const int fn = pl.fn, st = pl.fm;
   if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s);

@@ -134,6 +134,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
 void gemm_f32_set_mode(int mode);
 // benchmarking knob: force the fast kernel's tile width / split-K / stages (0 = planner's choice)
 void gemm_f32_set_override(int fn, int splits, int stages);
+// row-vector (LDS-staged, 16-B) output stores of the fast GEMM on / off (measurements, tests)
+void gemm_f32_set_cvec(bool on);
 // optimizer-epilogue variant (SGD flags, Adam flags, persistent grid on/off, workgroups per CU);
 // negative = keep. Returns the active {sgd, adam, persist, wgs}.
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs);

@@ -55,6 +55,27 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int 
                                  float(label_smoothing), reduction == "mean", acc)
 
 
+_SEEDS: dict = {}
+
+
+def seed_grad(loss: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """The gradient that seeds ``loss.backward``: a cached device tensor of ``scale`` (no
+    ``ones_like`` fill kernel per step -- what autograd launches when no gradient is passed --
+    and no ATen division for ``loss / accumulation_steps``). Read-only by contract: the native
+    backward kernels only read it."""
+    key = (loss.device, loss.dtype, tuple(loss.shape), float(scale))
+    g = _SEEDS.get(key)
+    if g is None:
+        g = torch.full(loss.shape, float(scale), device=loss.device, dtype=loss.dtype)
+        _SEEDS[key] = g
+    return g
+
+
+def backward(loss: torch.Tensor, scale: float = 1.0, **kwargs) -> None:
+    """``(loss * scale).backward(**kwargs)`` without the seed-gradient fill / scaling kernels."""
+    loss.backward(seed_grad(loss, scale), **kwargs)
+
+
 @torch.no_grad()
 def count_correct(logits: torch.Tensor, target: torch.Tensor, acc: torch.Tensor) -> None:
     """acc[1] += #(argmax == target), acc[2] += #rows (fused argmax+compare+count)."""
