@@ -224,13 +224,15 @@ def test_model_matches_cpu_reference(name, hw, n):
     y_cpu.square().sum().backward()
     y_gpu.square().sum().backward()
     # relative L2 error per parameter: a ReLU whose pre-activation rounds to the other side of 0
-    # in fp32 vs fp64 (it happens ~1 in 1e5 elements) legitimately flips single gradient entries
+    # in fp32 vs fp64 (it happens ~1 in 1e5 elements) legitimately flips single gradient entries.
+    # Noise floor: stock ATen fp32 on the CPU vs this fp64 reference gives 3.6e-3 on ResNet-50's
+    # conv1.weight (2.6e-3 on layer2.2.conv3.weight) for this very input -- the bound sits above it.
     worst = []
     for (pn, pc), (_, pg) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
         err = (pg.grad.double().cpu() - pc.grad).norm().item() / (pc.grad.norm().item() + 1e-12)
         worst.append((err, pn))
     worst.sort(reverse=True)
-    assert worst[0][0] <= 2e-3, worst[:5]
+    assert worst[0][0] <= 5e-3, worst[:5]
 
 
 @pytest.mark.parametrize("orient", [-1, 0, 1])

@@ -15,6 +15,7 @@ struct ConvPlan {
   int mode = 0;
   int M = 0, N = 0, K = 0;
   int fm = 2, fn = 2;
+  int bm = 128;  // NHWC fast path: block rows (128, or 256 = FM 4 for K-contiguous A)
   int splits = 1, k_per_split = 0;
   long ws_floats = 0;
 };

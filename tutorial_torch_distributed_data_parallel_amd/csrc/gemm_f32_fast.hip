@@ -389,12 +389,15 @@ template <int R>
 struct SrcOf<R, kWTap, false> : WTapSrc<R> {};
 
 // One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel.
-template <int FN, int AKIND, int BKIND, int S, int OPTK>
+// FM = 32-row MFMA tiles per wave (block rows BM = 64 * FM): 2, or 4 for a K-contiguous A (twice
+// the MFMAs per barrier and per B fragment read, for the long-M convolution GEMMs).
+template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM>
 __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, lds_char* smem) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
-  constexpr int FM = 2;
-  constexpr int BM = 128, BN = 64 * FN;
+  static_assert(FM == 2 || (FM == 4 && AK && OPTK == 0), "FM 4: K-contiguous A, plain epilogue");
+  constexpr int BM = 64 * FM, BN = 64 * FN;
+  constexpr int WR = 32 * FM;  // rows per wave
   constexpr int A_BYTES = BM * kBK * 4, B_BYTES = BN * kBK * 4;
   constexpr int STG = A_BYTES + B_BYTES;
   constexpr int GA = A_BYTES / 1024 / 4, GB = B_BYTES / 1024 / 4;  // glds per wave per tile
@@ -440,7 +443,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   int a_off[FM], b_off[FN];
 #pragma unroll
   for (int f = 0; f < FM; ++f) {
-    const int row = wm * 64 + f * 32 + l31;
+    const int row = wm * WR + f * 32 + l31;
     a_off[f] = AK ? row * 128 : (wm * 64 + 2 * l31) * 4;
   }
 #pragma unroll
@@ -458,7 +461,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     if (AK) {
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
-        const int row = wm * 64 + f * 32 + l31;
+        const int row = wm * WR + f * 32 + l31;
         const int slot = (2 * q + h) ^ swz(row);
         const f32x4 v = *reinterpret_cast<const f32x4*>(st + a_off[f] + slot * 16);
 #pragma unroll
@@ -714,7 +717,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
         for (int rr = 0; rr < RB; ++rr) {
           const int f = f0 + fb, r = r0 + rr;
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+          const int row = m0 + wm * WR + (AK ? f * 32 + rl : 2 * rl + f);
 #pragma unroll
           for (int g = 0; g < NG; ++g) {
             const int col = PAIR ? n0 + wn * 64 + 2 * l31 : n0 + wn * (32 * FN) + g * 32 + l31;
@@ -785,7 +788,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
   float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
   const long ldo = split ? p.N : p.ldc;
-  if (p.cvec) {
+  if (BM * BN * 4 <= S * STG && p.cvec) {
     // Row-vector store: the tile goes through LDS (the pipeline stages are free once every wave
     // has left the K loop) and leaves as 16-B-per-lane row segments. The accumulator layout
     // alone gives each lane one column (or a column pair) of 16 rows: dword stores, 4x the
@@ -800,7 +803,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int lr = wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+        const int lr = wm * WR + (AK ? f * 32 + rl : 2 * rl + f);
         if (BKC || FN == 1) {
 #pragma unroll
           for (int g = 0; g < FN; ++g) T[lr * TS + wn * (32 * FN) + g * 32 + l31] = acc[f][g][r];
@@ -857,7 +860,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+        const int row = m0 + wm * WR + (AK ? f * 32 + rl : 2 * rl + f);
         const float* orow = out + (long)(row < p.M ? row : 0) * ldo;
         if (BKC || FN == 1) {
 #pragma unroll
@@ -881,7 +884,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int row = m0 + wm * 64 + (AK ? f * 32 + rl : 2 * rl + f);
+      const int row = m0 + wm * WR + (AK ? f * 32 + rl : 2 * rl + f);
       if (row >= p.M) continue;
       float* orow = out + (long)row * ldo;
       if (BKC || FN == 1) {
@@ -924,7 +927,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPTK>
+template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM = 2>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
@@ -950,32 +953,42 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
       __builtin_amdgcn_s_sleep(127);
     }
     for (int lid = t0 + j; lid < t1; lid += per) {
-      gemm_tile<FN, AKIND, BKIND, S, OPTK>(p, lid, smem);
+      gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem);
       __builtin_amdgcn_s_barrier();  // every wave is done with this tile's LDS stages
     }
   } else {
     const int q8 = nwg / 8, r8 = nwg % 8;
     const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-    gemm_tile<FN, AKIND, BKIND, S, OPTK>(p, lid, smem);
+    gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem);
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPT = 0>
+template <int FN, int AKIND, int BKIND, int S, int OPT = 0, int FM = 2>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
-  constexpr int STG = 128 * kBK * 4 + 64 * FN * kBK * 4;
+  constexpr int STG = 64 * FM * kBK * 4 + 64 * FN * kBK * 4;
   const size_t lds = (size_t)S * STG;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT>,
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT>), dim3(nblocks), dim3(kT),
-                     lds, s, p);
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>), dim3(nblocks),
+                     dim3(kT), lds, s, p);
 }
 
+// bm = 256: the FM 4 kernel (64-wide tile, 2 stages = 80 KiB of LDS, two workgroups per CU);
+// instantiated for K-contiguous A operands only
 template <int AKIND, int BKIND, int OPT = 0>
-void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s) {
+void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s,
+                  int bm = 128) {
+  constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
+  if constexpr (AK && OPT == 0) {
+    if (bm == 256) {
+      launch_fast<1, AKIND, BKIND, 2, 0, 4>(p, nblocks, s);
+      return;
+    }
+  }
   if (fn == 1) {
     if (stages == 3) launch_fast<1, AKIND, BKIND, 3, OPT>(p, nblocks, s);
     else launch_fast<1, AKIND, BKIND, 2, OPT>(p, nblocks, s);
@@ -1042,6 +1055,8 @@ void gemm_f32_set_override(int fn, int splits, int stages) {
 }
 // Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
 static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
+static int o_bm = 0;  // 0 auto, 128 / 256 forced (sweeps)
+void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
 void gemm_f32_set_cvec(bool on) { o_no_cvec = !on; }
 static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int splits) {
   auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
@@ -1073,7 +1088,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   }
   int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
   plan.fast = true;
-  plan.bm = 128;
+  plan.bm = (o_bm == 256 && fn == 1 && splits == 1 && a.a_kcontig && a.opt.kind == 0) ? 256 : 128;
   plan.bn = bn;
   plan.tile = fn;
   plan.k_per_split = kps;
@@ -1092,7 +1107,7 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.M = a.M; p.N = a.N; p.K = a.K;
   p.k_per_split = plan.k_per_split;
   p.splits = plan.splits;
-  p.tiles_m = ceil_div(a.M, 128);
+  p.tiles_m = ceil_div(a.M, plan.bm);
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.beta = plan.splits > 1 ? 0.f : a.beta;
   p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
@@ -1137,8 +1152,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
     return;
   }
   p.opt.kind = 0;
-  if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nblocks, s);
-  else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nblocks, s);
+  if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nblocks, s, plan.bm);
+  else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nblocks, s, plan.bm);
   else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nblocks, s);
   else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nblocks, s);
   if (plan.splits > 1)
@@ -1242,6 +1257,13 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
   // 2 with 3 stages); measured faster on 86 of 112 (layer, plan) pairs of AlexNet / ResNet-50
   // and on every forward / input-gradient shape (scripts/sweep_conv_fd.py).
   if (gp.tile == 1 && o_stages == 0) gp.stages = 2;
+  // 256-row tiles (FM 4: half the B traffic and barriers per MFMA) only on request
+  // (gemm_f32_set_bm): measured 3-34 % SLOWER than 128 rows on every ResNet-50 / AlexNet forward
+  // and input-gradient shape with the 64-wide tile (profiles/micro/gemm_bm256_ab.jsonl) -- two
+  // workgroups per CU instead of three hide less of the operand-load latency
+  pl.bm = 128;
+  if (mode != kConvWgrad && gp.tile == 1 && gp.splits == 1 && o_bm == 256) pl.bm = 256;
+  if (pl.bm == 256) gp.stages = 2;
   pl.fn = gp.tile;
   pl.fm = gp.stages;  // pipeline depth (the NHWC path always uses BM = 128)
   pl.splits = gp.splits;
@@ -1298,16 +1320,17 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   else { p.lda = 0; p.ldb = pl.N; p.ldc = pl.N; }
   p.k_per_split = pl.k_per_split;
   p.splits = pl.splits;
-  p.tiles_m = ceil_div(pl.M, 128);
+  p.tiles_m = ceil_div(pl.M, pl.bm);
   p.tiles_n = ceil_div(pl.N, 64 * pl.fn);
   p.beta = pl.splits > 1 ? 0.f : beta;
   p.relu = (pl.splits > 1 ? false : relu) ? 1 : 0;
   p.cvec = c_vec_ok(pl.N, p.ldc, C, bias, pl.splits) && !o_no_cvec;
   const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
   const int fn = pl.fn, st = pl.fm;
-  if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s);
-  else if (pl.mode == kConvDgrad && wtap) launch_kinds<kImDgrad, kWTap>(p, fn, st, nblocks, s);
-  else if (pl.mode == kConvDgrad) launch_kinds<kImDgrad, kDenseMN>(p, fn, st, nblocks, s);
+  if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s, pl.bm);
+  else if (pl.mode == kConvDgrad && wtap)
+    launch_kinds<kImDgrad, kWTap>(p, fn, st, nblocks, s, pl.bm);
+  else if (pl.mode == kConvDgrad) launch_kinds<kImDgrad, kDenseMN>(p, fn, st, nblocks, s, pl.bm);
   else if (!wt) launch_kinds<kDenseMN, kImWgrad>(p, fn, st, nblocks, s);
   else launch_kinds<kImWgradT, kDenseMN>(p, fn, st, nblocks, s);
   if (pl.splits > 1)

@@ -136,6 +136,8 @@ void gemm_f32_set_mode(int mode);
 void gemm_f32_set_override(int fn, int splits, int stages);
 // row-vector (LDS-staged, 16-B) output stores of the fast GEMM on / off (measurements, tests)
 void gemm_f32_set_cvec(bool on);
+// fast-GEMM block rows: 0 auto, 128 or 256 forced (measurements, tests)
+void gemm_f32_set_bm(int bm);
 // optimizer-epilogue variant (SGD flags, Adam flags, persistent grid on/off, workgroups per CU);
 // negative = keep. Returns the active {sgd, adam, persist, wgs}.
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs);

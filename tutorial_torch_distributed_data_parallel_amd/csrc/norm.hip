@@ -13,6 +13,7 @@
 // channels (one per lane, coalesced across the wave) and its 4 waves split the rows; for HW > 1 a
 // workgroup owns one channel (coalesced along HW). Either way the N*HW axis can additionally be
 // split over blockIdx.y so that a small-C layer still puts >= 1 workgroup on every CU.
+#include <cstdlib>
 #include <initializer_list>
 #include <stdexcept>
 
@@ -329,21 +330,34 @@ __global__ __launch_bounds__(256) void bwd_elemt_kernel(
 // workgroup owns CB = min(C, 1024) channels; a thread owns 4 adjacent channels (one 16-B load
 // per row, rows coalesced across lanes) and walks rows with stride RPW = 256 / (CB / 4); the
 // RPW row groups are merged through LDS. One reciprocal per row serves 4 Welford updates.
-__device__ __forceinline__ void rows4_layout(int C, int& CB, int& LPR, int& RPW) {
+__device__ __forceinline__ void rows4_layout(int C, int& CB, int& LPR, int& RPW,
+                                             int threads = 256) {
   CB = C < 1024 ? C : 1024;
   LPR = CB / 4;
-  RPW = 256 / LPR;
+  RPW = threads / LPR;
 }
 
-__global__ __launch_bounds__(256) void moments_rows4(const float* __restrict__ x, int N, int C,
-                                                     int splits, float* __restrict__ ws,
-                                                     float* __restrict__ mean,
-                                                     float* __restrict__ var,
+// The two row reductions run 1024-thread workgroups, one per CU: 16 waves keep enough loads in
+// flight to stream at HBM rate (256-thread workgroups at one per CU read 3.7-4.4 TB/s; more
+// workgroups per CU instead multiply the split partials the final kernels merge serially). The
+// RPW row groups of a workgroup are merged by a tree in LDS.
+constexpr int kRedT = 1024;
+
+__device__ __forceinline__ int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+__global__ __launch_bounds__(kRedT) void moments_rows4(const float* __restrict__ x, int N, int C,
+                                                       int splits, float* __restrict__ ws,
+                                                       float* __restrict__ mean,
+                                                       float* __restrict__ var,
     float* __restrict__ cnt_out, float cnt) {
   if (cnt_out && splits == 1 && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
-  __shared__ float sh[3][1024];
+  __shared__ float sh[3][4096];
   int CB, LPR, RPW;
-  rows4_layout(C, CB, LPR, RPW);
+  rows4_layout(C, CB, LPR, RPW, kRedT);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
   const int c = blockIdx.x * CB + 4 * cq;
   const bool act = rg < RPW && c < C;
@@ -367,19 +381,30 @@ __global__ __launch_bounds__(256) void moments_rows4(const float* __restrict__ x
   if (rg < RPW) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int s = rg * CB + 4 * cq + j;
-      sh[0][s] = n;
-      sh[1][s] = mu[j];
-      sh[2][s] = m2[j];
+      const int q = rg * CB + 4 * cq + j;
+      sh[0][q] = n;
+      sh[1][q] = mu[j];
+      sh[2][q] = m2[j];
+    }
+  }
+  // tree merge of the RPW row groups (Chan), log2(RPW) levels
+  for (int st = pow2_ceil(RPW) >> 1; st > 0; st >>= 1) {
+    __syncthreads();
+    for (int i = t; i < st * CB; i += kRedT) {
+      const int g = i / CB, k = i - g * CB;
+      if (g + st < RPW) {
+        const Wf w = wf_merge(Wf{sh[0][i], sh[1][i], sh[2][i]},
+                              Wf{sh[0][i + st * CB], sh[1][i + st * CB], sh[2][i + st * CB]});
+        sh[0][i] = w.n; sh[1][i] = w.mean; sh[2][i] = w.m2;
+      }
+      (void)k;
     }
   }
   __syncthreads();
-  for (int k = t; k < CB; k += 256) {
+  for (int k = t; k < CB; k += kRedT) {
     const int ch = blockIdx.x * CB + k;
     if (ch >= C) continue;
-    Wf w{0.f, 0.f, 0.f};
-    for (int g = 0; g < RPW; ++g)
-      w = wf_merge(w, Wf{sh[0][g * CB + k], sh[1][g * CB + k], sh[2][g * CB + k]});
+    const Wf w{sh[0][k], sh[1][k], sh[2][k]};
     if (splits == 1) {
       mean[ch] = w.mean;
       var[ch] = w.n > 0.f ? w.m2 / w.n : 0.f;
@@ -390,15 +415,15 @@ __global__ __launch_bounds__(256) void moments_rows4(const float* __restrict__ x
   }
 }
 
-__global__ __launch_bounds__(256) void bwd_reduce_rows4(const float* __restrict__ dy,
-                                                        const float* __restrict__ x,
-                                                        const float* __restrict__ mean,
-                                                        const float* __restrict__ yr, int N,
-                                                        int C, int splits,
-                                                        float* __restrict__ part) {
-  __shared__ float sh[2][1024];
+__global__ __launch_bounds__(kRedT) void bwd_reduce_rows4(const float* __restrict__ dy,
+                                                          const float* __restrict__ x,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ yr, int N,
+                                                          int C, int splits,
+                                                          float* __restrict__ part) {
+  __shared__ float sh[2][4096];
   int CB, LPR, RPW;
-  rows4_layout(C, CB, LPR, RPW);
+  rows4_layout(C, CB, LPR, RPW, kRedT);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
   const int c = blockIdx.x * CB + 4 * cq;
   const bool act = rg < RPW && c < C;
@@ -431,18 +456,22 @@ __global__ __launch_bounds__(256) void bwd_reduce_rows4(const float* __restrict_
       sh[1][rg * CB + 4 * cq + j] = m[j];
     }
   }
+  for (int st = pow2_ceil(RPW) >> 1; st > 0; st >>= 1) {
+    __syncthreads();
+    for (int i = t; i < st * CB; i += kRedT) {
+      if (i / CB + st < RPW) {
+        sh[0][i] += sh[0][i + st * CB];
+        sh[1][i] += sh[1][i + st * CB];
+      }
+    }
+  }
   __syncthreads();
-  for (int k = t; k < CB; k += 256) {
+  for (int k = t; k < CB; k += kRedT) {
     const int ch = blockIdx.x * CB + k;
     if (ch >= C) continue;
-    float sa = 0.f, sm = 0.f;
-    for (int g = 0; g < RPW; ++g) {
-      sa += sh[0][g * CB + k];
-      sm += sh[1][g * CB + k];
-    }
     float* o = part + (long)blockIdx.y * 2 * C;
-    o[ch] = sa;
-    o[C + ch] = sm;
+    o[ch] = sh[0][k];
+    o[C + ch] = sh[1][k];
   }
 }
 
@@ -558,10 +587,17 @@ inline int ew_grid(long total) {
 }  // namespace
 
 int bn_splits(int N, int C, int HW, int num_cus) {
-  if (HW == 1 && C % 4 == 0) {  // rows4 kernels: ~1 workgroup per CU, >= 8 row iterations
-    const int CB = C < 1024 ? C : 1024, RPW = 256 / (CB / 4);
+  if (HW == 1 && C % 4 == 0) {
+    // rows4 reductions (1024-thread workgroups): one workgroup per CU, >= 8 row iterations per
+    // thread; TDP_BN_WG_PER_CU overrides the per-CU count (sweeps)
+    static const int per_cu = [] {
+      const char* e = std::getenv("TDP_BN_WG_PER_CU");
+      const int v = e ? std::atoi(e) : 1;
+      return v >= 1 && v <= 16 ? v : 1;
+    }();
+    const int CB = C < 1024 ? C : 1024, RPW = kRedT / (CB / 4);
     const int nblk = rows4_nblk(C);
-    long s = ((long)num_cus + nblk - 1) / nblk;
+    long s = ((long)per_cu * num_cus + nblk - 1) / nblk;
     const long cap = (N + 8L * RPW - 1) / (8L * RPW);
     if (s > cap) s = cap;
     return s < 1 ? 1 : (int)s;
@@ -585,7 +621,7 @@ void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, flo
                 float* var, float* count_out, hipStream_t s) {
   const float cnt = (float)((double)N * HW);
   if (rows4_ok(C, HW, {x}))
-    hipLaunchKernelGGL(moments_rows4, dim3(rows4_nblk(C), splits), dim3(256), 0, s, x, N, C,
+    hipLaunchKernelGGL(moments_rows4, dim3(rows4_nblk(C), splits), dim3(kRedT), 0, s, x, N, C,
                        splits, ws, mean, var, count_out, cnt);
   else if (HW == 1)
     hipLaunchKernelGGL(moments_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, x, N, C, splits,
@@ -638,7 +674,7 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
                    float* dw, float* db, float grad_beta, hipStream_t s) {
   // partials always go through ws (2*C*splits floats); the final kernel also writes dw/db
   if (rows4_ok(C, HW, {dy, x, y_relu, mean}))
-    hipLaunchKernelGGL(bwd_reduce_rows4, dim3(rows4_nblk(C), splits), dim3(256), 0, s, dy, x,
+    hipLaunchKernelGGL(bwd_reduce_rows4, dim3(rows4_nblk(C), splits), dim3(kRedT), 0, s, dy, x,
                        mean, y_relu, N, C, splits, ws);
   else if (HW == 1)
     hipLaunchKernelGGL(bwd_reduce_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, dy, x, mean,
