@@ -196,6 +196,34 @@ def test_batchnorm_kernels(C, shape):
     _close(ye, torch.nn.functional.batch_norm(x, rm, rv, w, b, False, 0.0, 1e-5), atol=1e-4)
 
 
+@pytest.mark.parametrize("shape", [(128, 4096), (6000, 256), (77, 12), (300, 2048)])
+def test_batchnorm_relu_mask_path(C, shape):
+    """csrc/norm.hip: the forward's 1-byte-per-4-channels ReLU mask (bit j = channel 4q+j > 0)
+    drives the backward exactly as the float output does."""
+    torch.manual_seed(11)
+    x = torch.randn(shape, device="cuda") * 2 + 0.3
+    Cn = shape[1]
+    w, b = torch.randn(Cn, device="cuda"), torch.randn(Cn, device="cuda")
+    res = torch.randn(shape, device="cuda")
+    st = C.bn_moments(x)[0]
+    stats = C.bn_merge(st, Cn, 1e-5, 0.1, None, None)
+    mask = torch.empty((shape[0], Cn // 4), dtype=torch.uint8, device="cuda")
+    y = C.bn_elemt(x, stats, w, b, True, res, mask_out=mask)
+    y_ref = C.bn_elemt(x, stats, w, b, True, res)
+    assert torch.equal(y, y_ref)
+    bits = (y > 0).view(shape[0], Cn // 4, 4).to(torch.int32)
+    packed = (bits * torch.tensor([1, 2, 4, 8], device="cuda", dtype=torch.int32)).sum(-1)
+    assert torch.equal(mask.to(torch.int32), packed)
+    dy = torch.randn(shape, device="cuda")
+    dw1, db1, dw2, db2 = (torch.empty(Cn, device="cuda") for _ in range(4))
+    s1 = C.bn_bwd_reduce(dy, x, stats, y, dw1, db1, 0.0)
+    s2 = C.bn_bwd_reduce(dy, x, stats, None, dw2, db2, 0.0, mask=mask)
+    assert torch.equal(s1, s2) and torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    o1 = C.bn_bwd_elemt(dy, x, stats, w, s1, y, True)
+    o2 = C.bn_bwd_elemt(dy, x, stats, w, s2, None, True, mask=mask)
+    assert torch.equal(o1[0], o2[0]) and torch.equal(o1[1], o2[1])
+
+
 def test_linear_autograd_matches_torch():
     from tutorial_torch_distributed_data_parallel_amd import ops
 

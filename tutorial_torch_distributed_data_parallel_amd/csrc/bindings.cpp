@@ -404,9 +404,20 @@ Tensor bn_merge_op(const Tensor& gathered, int64_t C, double eps, double momentu
   return stats;
 }
 
+// the ReLU mask of the [rows, C % 4 == 0] form: uint8, one byte per 4 channels
+static const uint8_t* mask_ptr(const c10::optional<Tensor>& m, const Tensor& x) {
+  if (!m.has_value() || !m->defined()) return nullptr;
+  CHECK_GPU(*m); CHECK_CONTIG(*m);
+  TORCH_CHECK(m->scalar_type() == at::kByte, "bn ReLU mask must be uint8");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0 && m->numel() == x.numel() / 4,
+              "bn ReLU mask: [rows, C/4] bytes for a [rows, C % 4 == 0] input");
+  return m->data_ptr<uint8_t>();
+}
+
 Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Tensor>& w,
                    const c10::optional<Tensor>& b, bool relu,
-                   const c10::optional<Tensor>& residual) {
+                   const c10::optional<Tensor>& residual,
+                   const c10::optional<Tensor>& mask_out) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
@@ -418,7 +429,8 @@ Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Ten
   auto y = at::empty_like(x);
   const float* sp = stats.data_ptr<float>();
   bn_elemt(x.data_ptr<float>(), sp, sp + C, fptr(w), fptr(b), N, C, HW, relu,
-           y.data_ptr<float>(), cur_stream(), fptr(residual));
+           y.data_ptr<float>(), cur_stream(), fptr(residual),
+           const_cast<uint8_t*>(mask_ptr(mask_out, x)));
   return y;
 }
 
@@ -437,7 +449,8 @@ Tensor bn_eval_op(const Tensor& x, const Tensor& rmean, const Tensor& rvar,
 // returns sums [sum_dy(C) | sum_dy_xmu(C)] ; writes dw/db when given (grad_beta: accumulate)
 Tensor bn_bwd_reduce_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
                         const c10::optional<Tensor>& y_relu, const c10::optional<Tensor>& dw,
-                        const c10::optional<Tensor>& db, double grad_beta) {
+                        const c10::optional<Tensor>& db, double grad_beta,
+                        const c10::optional<Tensor>& mask) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
@@ -447,14 +460,15 @@ Tensor bn_bwd_reduce_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
   const float* sp = stats.data_ptr<float>();
   bn_bwd_reduce(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(y_relu), N, C, HW,
                 splits, ws.data_ptr<float>(), sums.data_ptr<float>(), fptr(dw), fptr(db),
-                (float)grad_beta, cur_stream());
+                (float)grad_beta, cur_stream(), mask_ptr(mask, x));
   return sums;
 }
 
 // returns dx, or [dx, dresidual] when residual_grad (the fused residual input's gradient)
 std::vector<Tensor> bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
                                     const c10::optional<Tensor>& w, const Tensor& sums,
-                                    const c10::optional<Tensor>& y_relu, bool residual_grad) {
+                                    const c10::optional<Tensor>& y_relu, bool residual_grad,
+                                    const c10::optional<Tensor>& mask) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
@@ -464,7 +478,8 @@ std::vector<Tensor> bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Ten
   const float* sp = stats.data_ptr<float>();
   bn_bwd_elemt(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(w),
                sums.data_ptr<float>(), fptr(y_relu), sp + 2 * C, N, C, HW, dx.data_ptr<float>(),
-               cur_stream(), residual_grad ? dres.data_ptr<float>() : nullptr);
+               cur_stream(), residual_grad ? dres.data_ptr<float>() : nullptr,
+               mask_ptr(mask, x));
   if (residual_grad) return {dx, dres};
   return {dx};
 }
@@ -1097,11 +1112,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("momentum"), py::arg("rmean"), py::arg("rvar"),
         py::arg("num_batches") = py::none());
   m.def("bn_elemt", &bn_elemt_op, py::arg("x"), py::arg("stats"), py::arg("w"), py::arg("b"),
-        py::arg("relu"), py::arg("residual") = py::none());
+        py::arg("relu"), py::arg("residual") = py::none(), py::arg("mask_out") = py::none());
   m.def("bn_eval", &bn_eval_op);
-  m.def("bn_bwd_reduce", &bn_bwd_reduce_op);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
+        py::arg("y_relu"), py::arg("dw"), py::arg("db"), py::arg("grad_beta"),
+        py::arg("mask") = py::none());
   m.def("bn_bwd_elemt", &bn_bwd_elemt_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
-        py::arg("w"), py::arg("sums"), py::arg("y_relu"), py::arg("residual_grad") = false);
+        py::arg("w"), py::arg("sums"), py::arg("y_relu"), py::arg("residual_grad") = false,
+        py::arg("mask") = py::none());
 
   m.def("rccl_unique_id", &unique_id_op);
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")

@@ -267,9 +267,11 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
               hipStream_t s);
 // y = (x - mean) * invstd * w + b (optional ReLU). w/b may be null (affine=False).
 // residual (optional, [rows, C] form only): y = relu?(bn(x) + residual), the ResNet join
+// mask_out (optional, [rows, C] form with relu): the ReLU mask as one byte per 4 channels (bit j =
+// channel 4q+j > 0) -- what the backward reads instead of y (1/16 of the bytes)
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
-              const float* residual = nullptr);
+              const float* residual = nullptr, uint8_t* mask_out = nullptr);
 // eval: y = (x - rmean) * rsqrt(rvar + eps) * w + b (optional ReLU)
 void bn_eval(const float* x, const float* rmean, const float* rvar, const float* w,
              const float* b, int N, int C, int HW, float eps, bool relu, float* y, hipStream_t s);
@@ -277,12 +279,14 @@ void bn_eval(const float* x, const float* rmean, const float* rvar, const float*
 // (fused ReLU). dw/db (optional, accumulate when beta != 0): dw = sum_dy_xmu*invstd, db = sum_dy.
 void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const float* invstd,
                    const float* y_relu, int N, int C, int HW, int splits, float* ws, float* sums,
-                   float* dw, float* db, float grad_beta, hipStream_t s);
+                   float* dw, float* db, float grad_beta, hipStream_t s,
+                   const uint8_t* mask = nullptr);
 // dx = w*invstd*(dy - sum_dy/cnt - (x-mean)*invstd^2*sum_dy_xmu/cnt), sums possibly all-reduced.
 // dres (optional, [rows, C] form only): also write the masked dy -- the gradient of a fused
 // residual input
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
-                  int N, int C, int HW, float* dx, hipStream_t s, float* dres = nullptr);
+                  int N, int C, int HW, float* dx, hipStream_t s, float* dres = nullptr,
+                  const uint8_t* mask = nullptr);
 
 }  // namespace tdp

@@ -420,7 +420,8 @@ __global__ __launch_bounds__(kRedT) void bwd_reduce_rows4(const float* __restric
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ yr, int N,
                                                           int C, int splits,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part,
+                                                          const uint8_t* __restrict__ mk) {
   __shared__ float sh[2][4096];
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW, kRedT);
@@ -437,7 +438,11 @@ __global__ __launch_bounds__(kRedT) void bwd_reduce_rows4(const float* __restric
       const long off = r * C + c;
       f32x4 d = *reinterpret_cast<const f32x4*>(dy + off);
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + off);
-      if (yr) {
+      if (mk) {
+        const uint32_t bits = mk[off >> 2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = ((bits >> j) & 1u) ? d[j] : 0.f;
+      } else if (yr) {
         const f32x4 yv = *reinterpret_cast<const f32x4*>(yr + off);
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
@@ -483,7 +488,8 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
                                                    const float* __restrict__ bb, int N, int C,
                                                    int splits, int relu, int eval, float eps,
                                                    const float* __restrict__ res,
-                                                   float* __restrict__ y) {
+                                                   float* __restrict__ y,
+                                                   uint8_t* __restrict__ mk) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
@@ -511,6 +517,10 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
       o[j] = relu ? fmaxf(q, 0.f) : q;
     }
     *reinterpret_cast<f32x4*>(y + r * C + c) = o;
+    // ReLU mask for the backward: one byte per 4 channels (64 lanes: 64 consecutive bytes)
+    if (mk)
+      mk[(r * C + c) >> 2] = (uint8_t)((o[0] > 0.f ? 1 : 0) | (o[1] > 0.f ? 2 : 0) |
+                                       (o[2] > 0.f ? 4 : 0) | (o[3] > 0.f ? 8 : 0));
   }
 }
 
@@ -519,7 +529,8 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ w,
     const float* __restrict__ sums, const float* __restrict__ yr, const float* __restrict__ cnt,
-    int N, int C, int splits, float* __restrict__ dx, float* __restrict__ dres) {
+    int N, int C, int splits, float* __restrict__ dx, float* __restrict__ dres,
+    const uint8_t* __restrict__ mk) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
@@ -545,7 +556,11 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
     const long off = r * C + c;
     f32x4 d = *reinterpret_cast<const f32x4*>(dy + off);
     const f32x4 xv = *reinterpret_cast<const f32x4*>(x + off);
-    if (yr) {
+    if (mk) {
+      const uint32_t bits = mk[off >> 2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = ((bits >> j) & 1u) ? d[j] : 0.f;
+    } else if (yr) {
       const f32x4 yv = *reinterpret_cast<const f32x4*>(yr + off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
@@ -643,14 +658,15 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
 
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
-              const float* residual) {
+              const float* residual, uint8_t* mask_out) {
   if (rows4_ok(C, HW, {x, y, mean, invstd, w, b, residual})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, mean, invstd, w,
-                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, residual, y);
+                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, residual, y, relu ? mask_out : nullptr);
     return;
   }
   if (residual) throw std::runtime_error("bn_elemt: a fused residual needs the [rows, C%4] form");
+  if (mask_out) throw std::runtime_error("bn_elemt: a ReLU mask needs the [rows, C%4] form");
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, mean, invstd, w, b,
                      total, C, HW, relu ? 1 : 0, 0, 0.f, y);
@@ -661,7 +677,8 @@ void bn_eval(const float* x, const float* rmean, const float* rvar, const float*
   if (rows4_ok(C, HW, {x, y})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, rmean, rvar, w,
-                       b, N, C, sp, relu ? 1 : 0, 1, eps, (const float*)nullptr, y);
+                       b, N, C, sp, relu ? 1 : 0, 1, eps, (const float*)nullptr, y,
+                       (uint8_t*)nullptr);
     return;
   }
   const long total = (long)N * C * HW;
@@ -671,11 +688,13 @@ void bn_eval(const float* x, const float* rmean, const float* rvar, const float*
 
 void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const float* invstd,
                    const float* y_relu, int N, int C, int HW, int splits, float* ws, float* sums,
-                   float* dw, float* db, float grad_beta, hipStream_t s) {
+                   float* dw, float* db, float grad_beta, hipStream_t s, const uint8_t* mask) {
   // partials always go through ws (2*C*splits floats); the final kernel also writes dw/db
   if (rows4_ok(C, HW, {dy, x, y_relu, mean}))
     hipLaunchKernelGGL(bwd_reduce_rows4, dim3(rows4_nblk(C), splits), dim3(kRedT), 0, s, dy, x,
-                       mean, y_relu, N, C, splits, ws);
+                       mean, y_relu, N, C, splits, ws, mask);
+  else if (mask)
+    throw std::runtime_error("bn_bwd_reduce: a ReLU mask needs the [rows, C%4] form");
   else if (HW == 1)
     hipLaunchKernelGGL(bwd_reduce_1d, dim3((C + 63) / 64, splits), dim3(256), 0, s, dy, x, mean,
                        y_relu, N, C, splits, ws);
@@ -688,14 +707,16 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
 
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
-                  int N, int C, int HW, float* dx, hipStream_t s, float* dres) {
+                  int N, int C, int HW, float* dx, hipStream_t s, float* dres,
+                  const uint8_t* mask) {
   if (rows4_ok(C, HW, {dy, x, y_relu, dx, dres})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(bwd_elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, dy, x, mean,
-                       invstd, w, sums, y_relu, count, N, C, sp, dx, dres);
+                       invstd, w, sums, y_relu, count, N, C, sp, dx, dres, mask);
     return;
   }
   if (dres) throw std::runtime_error("bn_bwd_elemt: a fused residual needs the [rows, C%4] form");
+  if (mask) throw std::runtime_error("bn_bwd_elemt: a ReLU mask needs the [rows, C%4] form");
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(bwd_elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, dy, x, mean, invstd,
                      w, sums, y_relu, count, total, C, HW, dx);

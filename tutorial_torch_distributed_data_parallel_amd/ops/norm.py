@@ -11,6 +11,8 @@ multi-process tests exercise.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -93,6 +95,9 @@ class _TorchKernels:
 _TORCH_K = _TorchKernels()
 
 
+_MASK = os.environ.get("TDP_BN_MASK", "1") != "0"  # A/B: 0 = the backward reads the float output
+
+
 def _is_nhwc(x) -> bool:
     return x.dim() == 4 and not x.is_contiguous() and \
         x.is_contiguous(memory_format=torch.channels_last)
@@ -128,32 +133,40 @@ class _BatchNormFn(torch.autograd.Function):
         st = K.bn_moments(x)[0]
         gathered = group.all_gather_flat(st) if group is not None else st
         stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var, num_batches)
-        y = K.bn_elemt(x, stats, weight, bias, relu, residual)
+        # [rows, C % 4] form on the GPU: the backward reads a 1-byte-per-4-channels ReLU mask
+        # instead of the float output (1/16 of the bytes, twice per backward)
+        mask = None
+        if relu and x.is_cuda and x.dim() == 2 and C % 4 == 0 and _MASK:
+            mask = torch.empty((x.shape[0], C // 4), dtype=torch.uint8, device=x.device)
+            y = K.bn_elemt(x, stats, weight, bias, relu, residual, mask_out=mask)
+        else:
+            y = K.bn_elemt(x, stats, weight, bias, relu, residual)
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.group = group
         ctx.has_res = residual is not None
         ctx.sink = sink
-        ctx.save_for_backward(x, weight, stats, y if relu else None)
+        ctx.save_for_backward(x, weight, stats, y if (relu and mask is None) else None, mask)
         return _unrows(y, ctx.shape4) if ctx.nhwc else y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, stats, y = ctx.saved_tensors
+        x, weight, stats, y, mask = ctx.saved_tensors
         K = _kernels(x)
         dy = _rows(dy.contiguous(memory_format=torch.channels_last)) if ctx.nhwc \
             else dy.contiguous()
         w_param, b_param = ctx.params
         dw = grad_dest(w_param) if (w_param is not None and needs(ctx, 1)) else None
         db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
-        sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0)
+        mk = {} if mask is None else {"mask": mask}
+        sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0, **mk)
         dx = dres = None
         want_res = ctx.has_res and needs(ctx, 9)
         if needs(ctx, 0) or want_res:
             if ctx.group is not None:
                 ctx.group.all_reduce_sum_(sums)
             # one pass: dx, and the residual input's gradient (the ReLU-masked dy) when fused
-            out = K.bn_bwd_elemt(dy, x, stats, weight, sums, y, want_res)
+            out = K.bn_bwd_elemt(dy, x, stats, weight, sums, y, want_res, **mk)
             dx = out[0] if needs(ctx, 0) else None
             dres = out[1] if want_res else None
             if ctx.nhwc:
