@@ -59,3 +59,33 @@ def test_bottleneck_shared_input_grad_cpu():
         torch.testing.assert_close(xa.grad, xb.grad)
         for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
             torch.testing.assert_close(p.grad, q.grad, msg=lambda m: f"{n}: {m}")
+
+
+def test_conv_plan_db_geometries():
+    """ops/plan_db.py: the GEMM geometries of a pass mirror ops/conv.py (one for forward /
+    weight gradient / stride-1 input gradient, one per stride phase otherwise), and the shipped
+    table parses."""
+    import json
+
+    from tutorial_torch_distributed_data_parallel_amd.ops import plan_db
+
+    g = plan_db.conv_geoms("fwd", (128, 3, 224, 224), (64, 3, 7, 7), (2, 2), (3, 3))
+    assert g == [[128, 4, 224, 224, 64, 7, 7, 112, 112, 2, 2, 3, 3]]
+    ph = plan_db.conv_geoms("dgrad", (128, 256, 28, 28), (256, 256, 3, 3), (2, 2), (1, 1))
+    # 3x3 stride 2: phases (a, b) with Rp x Sp taps 1x1, 1x2, 2x1, 2x2 -- all 14x14 dx pixels
+    assert sorted((p[5], p[6]) for p in ph) == [(1, 1), (1, 2), (2, 1), (2, 2)]
+    assert all(p[2] == 14 and p[3] == 14 and p[7] == 14 and p[8] == 14 for p in ph)
+    with open(plan_db.DEFAULT_DB) as f:
+        table = json.load(f)
+    for e in table["plans"]:
+        assert e["pass"] in ("fwd", "dgrad", "wgrad") and e["fn"] in (1, 2) and e["splits"] >= 1
+        assert e["us"] < e["us_heuristic"]
+
+    class Rec:
+        def __init__(self):
+            self.n = 0
+
+        def conv_plan_db_put(self, mode, geom, fn, splits):
+            assert len(geom) == 13
+            self.n += 1
+    assert plan_db.register(Rec(), table["plans"]) >= len(table["plans"])

@@ -1078,6 +1078,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("cout"), py::arg("R") = 0, py::arg("S") = 0, py::arg("C") = 0);
   m.def("conv_set_wgrad_transposed", &conv_set_wgrad_transposed);
   m.def("conv_set_wgrad_target", &conv_set_wgrad_target);
+  // geom = [N, C, H, W, Cout, R, S, P, Q, sh, sw, ph, pw] of the NHWC GEMM call (mode 0 fwd,
+  // 1 input gradient, 2 weight gradient; an input-gradient stride phase is its own geometry)
+  m.def("conv_plan_db_put", [](int64_t mode, std::vector<int64_t> v, int64_t fn, int64_t splits) {
+    TORCH_CHECK(v.size() == 13, "conv_plan_db_put: geometry of 13 ints");
+    ConvGeom g{(int)v[0], (int)v[1], (int)v[2], (int)v[3], (int)v[4], (int)v[5], (int)v[6],
+               (int)v[7], (int)v[8], (int)v[9], (int)v[10], (int)v[11], (int)v[12]};
+    conv_plan_db_put((int)mode, g, (int)fn, (int)splits);
+  });
+  m.def("conv_plan_db_clear", &conv_plan_db_clear);
+  m.def("conv_plan_db_size", &conv_plan_db_size);
   m.def("conv2d_dgrad", &conv2d_dgrad_op);
   m.def("conv2d_wgrad", &conv2d_wgrad_op);
   m.def("chan_relu_bias_bwd", &chan_relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),

@@ -33,6 +33,10 @@ bool conv_nhwc_ok(int mode, const ConvGeom& g);
 bool conv_wgrad_transposed(const ConvGeom& g);
 void conv_set_wgrad_transposed(int mode);  // -1 auto, 0 / 1 force
 void conv_set_wgrad_target(int per_cu);     // split-K workgroups per CU (<= 0: auto)
+// measured (FN, split-K) per exact geometry + pass (gemm_f32_fast.hip "plan table")
+void conv_plan_db_put(int mode, const ConvGeom& g, int fn, int splits);
+void conv_plan_db_clear();
+long conv_plan_db_size();
 ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
 // Input gradient with B read from the weight's own [Cout][R][S][C] storage (no transposed copy):
 // the (phase) taps of the full R x S filter, (r, s) = (r0 + rp*sh, s0 + sp*sw); see WTap.

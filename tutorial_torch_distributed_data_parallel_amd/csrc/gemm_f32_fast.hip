@@ -29,6 +29,7 @@
 //     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
 #include <cstdlib>
 #include <stdexcept>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -1208,6 +1209,41 @@ static bool wgrad_transposed(const ConvGeom& g) {
 }
 bool conv_wgrad_transposed(const ConvGeom& g) { return wgrad_transposed(g); }
 
+// Measured plan table (tile width, split-K) per exact convolution geometry and pass -- the
+// MIOpen perf-db idea: the heuristic planner above cannot see wave quantisation (a grid of T
+// workgroups on 3 (FN 1) or 2 (FN 2) slots per CU runs ceil(T / slots) rounds; ResNet-50's
+// layer3/4 3x3 convolutions lose up to 20 % to a near-empty last round). Entries come from
+// scripts/tune_conv_plans.py sweeps (pkg/perfdb/*.json, registered at import by ops/conv.py);
+// geometries not in the table use the heuristic. Overrides (gemm_f32_set_override) win.
+struct PlanKey {
+  int v[14];
+  bool operator==(const PlanKey& o) const {
+    for (int i = 0; i < 14; ++i)
+      if (v[i] != o.v[i]) return false;
+    return true;
+  }
+};
+struct PlanKeyHash {
+  size_t operator()(const PlanKey& k) const {
+    size_t h = 1469598103934665603ull;
+    for (int i = 0; i < 14; ++i) h = (h ^ (size_t)(unsigned)k.v[i]) * 1099511628211ull;
+    return h;
+  }
+};
+static std::unordered_map<PlanKey, std::pair<int, int>, PlanKeyHash>& plan_db() {
+  static std::unordered_map<PlanKey, std::pair<int, int>, PlanKeyHash> db;
+  return db;
+}
+static PlanKey plan_key(int mode, const ConvGeom& g) {
+  return PlanKey{{mode, g.N, g.C, g.H, g.W, g.Cout, g.R, g.S, g.P, g.Q, g.sh, g.sw, g.ph, g.pw}};
+}
+void conv_plan_db_put(int mode, const ConvGeom& g, int fn, int splits) {
+  if ((fn != 1 && fn != 2) || splits < 1) throw std::runtime_error("conv plan db: bad plan");
+  plan_db()[plan_key(mode, g)] = {fn, splits};
+}
+void conv_plan_db_clear() { plan_db().clear(); }
+long conv_plan_db_size() { return (long)plan_db().size(); }
+
 bool conv_nhwc_ok(int mode, const ConvGeom& g) {
   if (g.C % 4 || g.Cout % 4) return false;
   if (mode == kConvDgrad && (ilog2_exact(g.sh) < 0 || ilog2_exact(g.sw) < 0)) return false;
@@ -1225,7 +1261,17 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
   a.M = pl.M; a.N = pl.N; a.K = pl.K;
   GemmPlan gp;
   gemm_f32_fast_plan(a, num_cus, gp);
-  if (mode == kConvWgrad && o_fn == 0 && o_splits == 0) {
+  const bool free_plan = o_fn == 0 && o_splits == 0 && o_stages == 0 && o_bm == 0;
+  const auto hit = free_plan ? plan_db().find(plan_key(mode, g)) : plan_db().end();
+  if (hit != plan_db().end()) {
+    const int fn = hit->second.first;
+    const int kps = ceil_div(ceil_div(pl.K, hit->second.second), kBK) * kBK;
+    gp.tile = fn;
+    gp.k_per_split = kps;
+    gp.splits = ceil_div(pl.K, kps);
+    gp.ws_floats = gp.splits > 1 ? (long)gp.splits * pl.M * pl.N : 0;
+    gp.stages = 2;
+  } else if (mode == kConvWgrad && o_fn == 0 && o_splits == 0) {
     const int fn = wgrad_fn(pl.M, pl.N);
     const long tiles = (long)ceil_div(pl.M, 128) * ceil_div(pl.N, 64 * fn);
     const int per_cu = o_wgrad_target > 0 ? o_wgrad_target : (g.R * g.S == 1 ? 2 : 8);

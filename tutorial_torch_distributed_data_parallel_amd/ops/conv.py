@@ -27,6 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
+from . import plan_db
 from ._grad import SharedGrad, grad_dest, needs
 
 
@@ -223,6 +224,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     if x.dtype != torch.float32:
         raise TypeError(f"native conv2d expects float32 activations, got {x.dtype}")
     if _nhwc_ok(x, weight, stride):
+        plan_db.ensure_loaded(native())  # measured per-geometry plans (ops/plan_db.py)
         return _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu, grad_into)
     return _Conv2dFn.apply(x.contiguous(), weight.contiguous(), bias, stride, padding, relu,
                            grad_into)
