@@ -375,3 +375,43 @@ def test_dgrad_w_accumulates_into_out():
         r = C.conv_nhwc_dgrad_w(dy, w, [B, Cin, H, H], 1, 1, R // 2, R // 2, out=out, beta=1.0)
         assert r.data_ptr() == out.data_ptr()
         torch.testing.assert_close(out, fresh + base, atol=1e-4, rtol=1e-4)
+
+
+def test_padded_channels_last_input_and_native_flatten():
+    """data/synthetic.py padded_channels_last: the stem conv reads the zero-padded NHWC storage
+    in place (forward and weight gradient equal the plain NCHW input's); ops.flatten of a
+    channels_last activation equals torch.flatten (values and gradient)."""
+    from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
+        SyntheticDataset, gather_batch, padded_channels_last)
+
+    torch.manual_seed(3)
+    x = torch.randn(6, 3, 33, 31, device="cuda")
+    xp = padded_channels_last(x)
+    assert xp.shape == x.shape and torch.equal(xp, x)
+    w1 = torch.randn(16, 3, 5, 5, device="cuda", requires_grad=True)
+    w2 = w1.detach().clone().requires_grad_()
+    y1 = ops.conv2d(x, w1, None, 2, 2)
+    y2 = ops.conv2d(xp, w2, None, 2, 2)
+    torch.testing.assert_close(y1, y2)
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    y2.backward(g)
+    torch.testing.assert_close(w1.grad, w2.grad)
+    ds = SyntheticDataset(10, (3, 16, 16), device="cuda", seed=1)
+    assert getattr(ds.x, "_tdp_padded_base", None) is not None
+    idx = torch.tensor([3, 1, 7], device="cuda")
+    xb, yb = gather_batch(ds.x, ds.y, idx)
+    torch.testing.assert_close(xb, ds.x[idx.cpu()])
+    assert torch.equal(yb, ds.y[idx])
+    a = torch.randn(4, 8, 6, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+    a1 = a.clone().requires_grad_()
+    a2 = a.clone().requires_grad_()
+    f1 = ops.flatten(a1)
+    f2 = torch.flatten(a2, 1)
+    torch.testing.assert_close(f1, f2)
+    gg = torch.randn_like(f1)
+    f1.backward(gg)
+    f2.backward(gg)
+    torch.testing.assert_close(a1.grad, a2.grad)
+    assert a1.grad.is_contiguous(memory_format=torch.channels_last)

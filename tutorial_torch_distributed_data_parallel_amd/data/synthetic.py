@@ -33,6 +33,9 @@ class SyntheticDataset(torch.utils.data.Dataset):
         else:
             self.y = torch.randint(0, num_classes, (self.n,), generator=g, device=device)
         self.device = device
+        if device.type == "cuda" and dtype == torch.float32 and len(self.shape) == 3 and \
+                self.shape[0] % 4 != 0:
+            self.x = padded_channels_last(self.x)
 
     def __len__(self):
         return self.n
@@ -41,9 +44,35 @@ class SyntheticDataset(torch.utils.data.Dataset):
         return self.x[i], self.y[i]
 
 
+def padded_channels_last(x: torch.Tensor) -> torch.Tensor:
+    """``x`` [n, C, H, W] (C % 4 != 0, e.g. RGB) re-laid out as channels_last with the channel
+    stride rounded up to a multiple of 4 (zero-filled): a [n, C, H, W] view of a
+    [n, H, W, Cp] buffer. The NHWC convolutions read it in place (16-B chunks of 4 channels per
+    pixel, ops/conv.py) instead of re-packing every batch; values and shape are unchanged."""
+    n, c, h, w = x.shape
+    cp = (c + 3) // 4 * 4
+    base = torch.zeros((n, h, w, cp), device=x.device, dtype=x.dtype)
+    base[..., :c] = x.permute(0, 2, 3, 1)
+    return _padded_view(base, c)
+
+
+def _padded_view(base: torch.Tensor, c: int) -> torch.Tensor:
+    n, h, w, cp = base.shape
+    v = base.as_strided((n, c, h, w), (h * w * cp, 1, w * cp, cp))
+    v._tdp_padded_base = base  # the zero-filled [n, H, W, Cp] storage (ops/conv.py reads it)
+    return v
+
+
 def gather_batch(x: torch.Tensor, y: torch.Tensor, idx: torch.Tensor):
     """``(x[idx], y[idx])``: on the GPU one native launch for samples and labels
-    (csrc/elementwise.hip ``gather_batch``), else two ``index_select``."""
+    (csrc/elementwise.hip ``gather_batch``), else two ``index_select``. A channel-padded
+    channels_last dataset (``padded_channels_last``) yields a batch in the same layout."""
+    base = getattr(x, "_tdp_padded_base", None)
+    if base is not None and x.is_cuda and idx.is_cuda and len(idx) > 0:
+        from .._native import native
+
+        xb, yb = native().gather_batch(base, y, idx)
+        return _padded_view(xb, x.shape[1]), yb
     if (x.is_cuda and idx.is_cuda and x.dtype == torch.float32 and y.dtype == torch.long and
             idx.dtype == torch.long and x.is_contiguous() and y.is_contiguous() and
             idx.is_contiguous() and y.device == x.device and len(idx) > 0):

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
+from .. import ops
 from ..nn import AdaptiveAvgPool2d, Conv2d, Dropout, Linear, MaxPool2d
 
 
@@ -48,7 +49,7 @@ class AlexNet(nn.Module):
     def forward(self, x):
         x = self.features(x)
         x = self.avgpool(x)
-        x = x.reshape(x.shape[0], -1)
+        x = ops.flatten(x)  # channels_last -> torch's (C, H, W) feature order, natively
         return self.classifier(x)
 
 

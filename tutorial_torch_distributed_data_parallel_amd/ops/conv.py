@@ -90,6 +90,13 @@ def _as_cl(C, t, channels: int | None = None):
     channels = c if channels is None else channels
     if channels == c and t.is_contiguous(memory_format=_CL):
         return t
+    base = getattr(t, "_tdp_padded_base", None)
+    if base is not None and tuple(base.shape) == (n, h, w, channels) and \
+            t.data_ptr() == base.data_ptr() and t.stride() == (h * w * channels, 1, w * channels,
+                                                                 channels):
+        # a channel-padded channels_last batch (data/synthetic.py): its zero-filled storage IS
+        # the padded NHWC operand
+        return base.permute(0, 3, 1, 2)
     out = torch.empty((n, channels, h, w), device=t.device, dtype=t.dtype, memory_format=_CL)
     C.copy4d(out, t)
     return out

@@ -91,6 +91,37 @@ def adaptive_avg_pool2d(x, output_size):
     return _AvgPoolFn.apply(x.contiguous(memory_format=_fmt(x)), P, Q)
 
 
+class _FlattenNCHWFn(torch.autograd.Function):
+    """channels_last [N, C, H, W] -> [N, C*H*W] in torch's (C, H, W) feature order (what the
+    classifier weights expect, e.g. torchvision AlexNet's fc6), and back in the backward: one
+    native strided copy each way (csrc/elementwise.hip copy4d) instead of ATen's direct_copy."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        out = torch.empty((N, C, H, W), device=x.device, dtype=x.dtype)
+        native().copy4d(out, x)
+        ctx.shape = (N, C, H, W)
+        return out.view(N, C * H * W)
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        gx = torch.empty((N, C, H, W), device=dy.device, dtype=dy.dtype,
+                         memory_format=torch.channels_last)
+        native().copy4d(gx, dy.contiguous().view(N, C, H, W))
+        return gx
+
+
+def flatten(x: torch.Tensor) -> torch.Tensor:
+    """``torch.flatten(x, 1)`` with torch's feature order; a channels_last GPU activation is
+    reordered natively (no ATen copy kernel)."""
+    if x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and not x.is_contiguous() and \
+            x.is_contiguous(memory_format=torch.channels_last):
+        return _FlattenNCHWFn.apply(x)
+    return x.reshape(x.shape[0], -1)
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p, seed):
