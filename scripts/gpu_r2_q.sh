@@ -1,0 +1,12 @@
+#!/bin/bash
+# Conv-epilogue BN statistics: full GPU suite, ResNet-50 x2, kernel stats.
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+fatal() { case "$1" in 0) ;; *) echo "fatal rc=$1 in $2"; exit "$1";; esac; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/r2q_all.log 2>&1
+rc=$?; grep -E "^FAILED|Error" gpurun_out/r2q_all.log | head -10; tail -2 gpurun_out/r2q_all.log; fatal $rc tests
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --model resnet50 --steps 30 --warmup 5 --no-diag > gpurun_out/r2q_r50_$i.json 2>/dev/null; fatal $? r50
+  grep -o '"ms_per_step": [0-9.]*' gpurun_out/r2q_r50_$i.json
+done
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r50_q -o r50 -- python3 bench.py --model resnet50 --steps 6 --warmup 2 --no-diag > gpurun_out/prof_r50_q.log 2>&1
+fatal $? prof

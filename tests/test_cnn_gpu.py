@@ -415,3 +415,42 @@ def test_padded_channels_last_input_and_native_flatten():
     f2.backward(gg)
     torch.testing.assert_close(a1.grad, a2.grad)
     assert a1.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 28, 28, 64, 3, 1), (4, 256, 14, 14, 1024, 1, 1),
+                                   (2, 4, 33, 29, 64, 7, 2), (3, 128, 9, 9, 512, 1, 1)])
+def test_conv_epilogue_bn_stats(shape):
+    """The forward GEMM epilogue's per-tile (count, mean, M2) merged by bn_moments_partials equal
+    the moments pass over the stored output; ops.conv2d(bn_stats=True) -> batch_norm uses them."""
+    from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    B, Cin, H, W, Cout, R, st = shape
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(B, Cin, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last) + 0.7
+    w = (torch.randn(Cout, Cin, R, R, device="cuda", generator=g) * 0.2).contiguous(
+        memory_format=torch.channels_last)
+    C.gemm_f32_set_override(0, 1, 0)  # unsplit: small test shapes would plan split-K
+    try:
+        y = ops.conv2d(x, w, None, st, R // 2, bn_stats=True)
+    finally:
+        C.gemm_f32_set_override(0, 0, 0)
+    tag = getattr(y, "_tdp_bn_part", None)
+    assert tag is not None, "an unsplit forward plan must emit statistics"
+    rows = y.permute(0, 2, 3, 1).reshape(-1, Cout)
+    ref = C.bn_moments(rows)[0]
+    got = C.bn_moments_partials(tag[0], float(rows.shape[0]))
+    torch.testing.assert_close(got[:Cout], ref[:Cout], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(got[Cout:2 * Cout], ref[Cout:2 * Cout], atol=1e-5, rtol=1e-4)
+    assert got[2 * Cout].item() == rows.shape[0]
+    yd = y.double()
+    torch.testing.assert_close(got[:Cout].double(), yd.mean((0, 2, 3)), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(got[Cout:2 * Cout].double(), yd.var((0, 2, 3), unbiased=False),
+                               atol=1e-5, rtol=1e-4)
+    # the batch norm consumes them: same output as when the moments pass runs
+    gamma, beta = torch.randn(Cout, device="cuda"), torch.randn(Cout, device="cuda")
+    o1 = ops.batch_norm(y, None, None, gamma, beta, training=True, relu=True)
+    o2 = ops.batch_norm(y.clone(), None, None, gamma, beta, training=True, relu=True)
+    torch.testing.assert_close(o1, o2, atol=1e-5, rtol=1e-5)

@@ -548,15 +548,20 @@ ConvGeom nhwc_geom(const std::vector<int64_t>& xs, int64_t cout, int64_t R, int6
 
 Tensor conv_nhwc_exec(int mode, const ConvGeom& g, const Tensor& A, const Tensor& B, Tensor C,
                       const c10::optional<Tensor>& bias, bool relu, double beta,
-                      const WeightTaps* wtap = nullptr) {
+                      const WeightTaps* wtap = nullptr, Tensor* stats = nullptr) {
   TORCH_CHECK(conv_nhwc_ok(mode, g), "conv (NHWC): channels must be multiples of 4 and "
               "input-gradient strides powers of two");
   const ConvPlan pl = conv_nhwc_plan(mode, g, num_cus(C.get_device()));
   Tensor ws;
   if (pl.ws_floats > 0) ws = at::empty({pl.ws_floats}, C.options());
-  conv_nhwc_run(pl, g, A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
-                fptr(bias), relu, (float)beta, pl.ws_floats > 0 ? ws.data_ptr<float>() : nullptr,
-                cur_stream(), wtap);
+  Tensor st;
+  if (stats != nullptr && pl.splits == 1)
+    st = at::empty({(pl.M + pl.bm - 1) / pl.bm, 3, (int64_t)pl.N}, C.options());
+  const bool wrote = conv_nhwc_run(pl, g, A.data_ptr<float>(), B.data_ptr<float>(),
+                                   C.data_ptr<float>(), fptr(bias), relu, (float)beta,
+                                   pl.ws_floats > 0 ? ws.data_ptr<float>() : nullptr,
+                                   cur_stream(), wtap, st.defined() ? st.data_ptr<float>() : nullptr);
+  if (stats != nullptr) *stats = wrote ? st : Tensor();
   return C;
 }
 
@@ -638,6 +643,33 @@ Tensor conv_nhwc_fwd_op(const Tensor& x, const Tensor& wt, const c10::optional<T
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == g.Cout, "bias size");
   auto y = at::empty({g.N, g.Cout, g.P, g.Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   return conv_nhwc_exec(kConvFwd, g, x, wt, y, bias, relu, 0.0);
+}
+
+// Forward that also returns the output's per-tile column (count, mean, M2) for a following
+// BatchNorm (bn_moments_partials), or an undefined tensor when the plan cannot produce them
+std::vector<Tensor> conv_nhwc_fwd_stats_op(const Tensor& x, const Tensor& wt, int64_t R,
+                                           int64_t S, int64_t sh, int64_t sw, int64_t ph,
+                                           int64_t pw) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CL(x); CHECK_GPU(wt); CHECK_CONTIG(wt);
+  const ConvGeom g = nhwc_geom(x.sizes().vec(), wt.size(0), R, S, sh, sw, ph, pw);
+  TORCH_CHECK(wt.numel() == (int64_t)g.Cout * R * S * g.C, "conv (NHWC): weight size mismatch");
+  auto y = at::empty({g.N, g.Cout, g.P, g.Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor st;
+  conv_nhwc_exec(kConvFwd, g, x, wt, y, c10::nullopt, false, 0.0, nullptr, &st);
+  return {y, st};
+}
+
+// part [T, 3, C] per-tile (count, mean, M2) -> [mean(C) | var(C) | count], bn_moments' layout
+Tensor bn_moments_partials_op(const Tensor& part, double count) {
+  CHECK_GPU(part); CHECK_F32(part); CHECK_CONTIG(part);
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == 3, "bn_moments_partials: part [T, 3, C]");
+  const int T = (int)part.size(0), C = (int)part.size(2);
+  auto st = at::empty({2 * C + 1}, part.options());
+  auto ws = at::empty({bn_partials_ws_floats(T, C)}, part.options());
+  float* sp = st.data_ptr<float>();
+  bn_moments_partials(part.data_ptr<float>(), T, C, ws.data_ptr<float>(), sp, sp + C,
+                      sp + 2 * C, (float)count, cur_stream());
+  return st;
 }
 
 // dy channels_last [N,Cout,P,Q]; w2 [R*S*Cout, C] -> dx channels_last x_shape
@@ -1066,6 +1098,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nhwc_dgrad", &conv_nhwc_dgrad_op);
   m.def("conv_nhwc_wgrad", &conv_nhwc_wgrad_op);
   m.def("conv_nhwc_dgrad_phase", &conv_nhwc_dgrad_phase_op);
+  m.def("conv_nhwc_fwd_stats", &conv_nhwc_fwd_stats_op);
+  m.def("bn_moments_partials", &bn_moments_partials_op, py::arg("part"), py::arg("count"));
   m.def("conv_nhwc_dgrad_w", &conv_nhwc_dgrad_w_op, py::arg("dy"), py::arg("w"),
         py::arg("x_shape"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("out") = py::none(), py::arg("beta") = 0.0);

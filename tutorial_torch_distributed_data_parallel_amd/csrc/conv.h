@@ -43,9 +43,12 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus);
 struct WeightTaps {
   int R, S, r0, s0, sh, sw;
 };
-void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
+// stats (optional, forward only): [tiles_m][3][N] per-tile column (count, mean, M2) of the
+// output, written when the plan is unsplit with the row-vector epilogue and no bias / ReLU /
+// beta; returns whether it was written
+bool conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,
-                   hipStream_t s, const WeightTaps* wtap = nullptr);
+                   hipStream_t s, const WeightTaps* wtap = nullptr, float* stats = nullptr);
 
 // NCHW ReLU backward + per-channel bias gradient: g = dy*(y>0) (if y), db = sum over n,hw.
 int chan_splits(int N, int C, int HW, int num_cus);

@@ -82,6 +82,7 @@ struct FastParams {
   float beta, rowsum_beta;
   int relu;
   int cvec;  // C (or the split-K workspace) takes 16-B row stores: N % 4 == 0, aligned rows
+  float* stats;  // optional [tiles_m][3][N]: per-tile column (count, mean, M2) of the stored C
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
 };
 
@@ -848,6 +849,47 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
         *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
       }
     }
+    if (p.stats != nullptr && !split) {
+      // Batch-norm statistics of this tile's columns, from the tile still in LDS (a convolution
+      // whose output feeds a BatchNorm: the moments pass over the whole output is skipped).
+      // Shifted sums about the tile's first row keep the one-pass variance exact in practice
+      // (the deviations are O(std)); tiles merge with Chan's formula (bn_moments_partials).
+      const int lc = (threadIdx.x % C4) * 4;
+      const f32x4 k4 = *reinterpret_cast<const f32x4*>(T + lc);
+      f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int lr = (i * kT + threadIdx.x) / C4;
+        if (m0 + lr < p.M) {
+          const f32x4 d = *reinterpret_cast<const f32x4*>(T + lr * TS + lc) - k4;
+          s1 += d;
+          s2 += d * d;
+        }
+      }
+      __syncthreads();  // every T read is done: the LDS becomes the cross-thread scratch
+      float* R = T;
+      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12) = s1;
+      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12 + 4) = s2;
+      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12 + 8) = k4;
+      __syncthreads();
+      constexpr int GRP = kT / C4;  // threads sharing a column quad
+      const float n = (float)min(BM, p.M - m0);
+      for (int c = threadIdx.x; c < BN; c += kT) {
+        const int q = c >> 2, j = c & 3, col = n0 + c;
+        if (col >= p.N) continue;
+        float a = 0.f, b = 0.f;
+#pragma unroll 4
+        for (int g = 0; g < GRP; ++g) {
+          a += R[(g * C4 + q) * 12 + j];
+          b += R[(g * C4 + q) * 12 + 4 + j];
+        }
+        const float mean_d = a / n;
+        float* o = p.stats + (long)(m0 / BM) * 3 * p.N;
+        o[col] = n;
+        o[p.N + col] = R[q * 12 + 8 + j] + mean_d;
+        o[2 * p.N + col] = fmaxf(b - a * mean_d, 0.f);
+      }
+    }
     return;  // a persistent loop's barrier protects T before the next tile's DMA
   }
   // beta != 0 reads C: all 16 rows of an f-slab are loaded before any store, so the loads are
@@ -1322,9 +1364,9 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
 // DGRAD: A = dy (NHWC), B = W2 [R*S*Cout][C], C = dx [N*H*W][C]
 // WGRAD: A = dy [N*P*Q][Cout], B = x (NHWC),  C = dWt [Cout][R*S*C] (beta: accumulate);
 //        when conv_wgrad_transposed(g): C = dWt^T [R*S*C][Cout] (A/B arguments unchanged)
-void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
+bool conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const float* B,
                    float* C, const float* bias, bool relu, float beta, float* ws,
-                   hipStream_t s, const WeightTaps* wtap) {
+                   hipStream_t s, const WeightTaps* wtap, float* stats) {
   FastParams p{};
   if (wtap) {
     if (pl.mode != kConvDgrad) throw std::runtime_error("weight taps are for the input gradient");
@@ -1371,6 +1413,10 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   p.beta = pl.splits > 1 ? 0.f : beta;
   p.relu = (pl.splits > 1 ? false : relu) ? 1 : 0;
   p.cvec = c_vec_ok(pl.N, p.ldc, C, bias, pl.splits) && !o_no_cvec;
+  // column statistics ride on the row-vector epilogue of an unsplit, plain forward GEMM
+  const bool stats_ok = stats != nullptr && pl.mode == kConvFwd && pl.splits == 1 && p.cvec &&
+                        bias == nullptr && !relu && beta == 0.f;
+  p.stats = stats_ok ? stats : nullptr;
   const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
   const int fn = pl.fn, st = pl.fm;
   if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s, pl.bm);
@@ -1381,6 +1427,7 @@ void conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   else launch_kinds<kImWgradT, kDenseMN>(p, fn, st, nblocks, s);
   if (pl.splits > 1)
     splitk_reduce(ws, pl.splits, pl.M, pl.N, C, false, pl.N, bias, beta, relu, s);
+  return p.stats != nullptr;
 }
 
 }  // namespace tdp

@@ -272,6 +272,11 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
               const float* residual = nullptr, uint8_t* mask_out = nullptr);
+// part [T][3][C] per-row-tile (count, mean, M2) -> mean, var (biased), count (= cnt): the
+// moments of a convolution output whose forward GEMM epilogue produced them
+void bn_moments_partials(const float* part, int T, int C, float* ws, float* mean, float* var,
+                         float* count_out, float cnt, hipStream_t s);
+long bn_partials_ws_floats(int T, int C);
 // eval: y = (x - rmean) * rsqrt(rvar + eps) * w + b (optional ReLU)
 void bn_eval(const float* x, const float* rmean, const float* rvar, const float* w,
              const float* b, int N, int C, int HW, float eps, bool relu, float* y, hipStream_t s);

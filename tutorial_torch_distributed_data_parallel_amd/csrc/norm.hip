@@ -157,6 +157,36 @@ __global__ __launch_bounds__(256) void moments_final(const float* __restrict__ w
   if (cnt_out && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
 }
 
+// First level of the per-tile partial merge: block (channel group of 16, chunk of 256 tiles);
+// 16 lane groups take every 16th tile of the chunk, merged through LDS -> ws [chunks][3][C]
+// (moments_final finishes). Parallel over chunks: a 3136-tile layer-1 output is 13 chunks.
+__global__ __launch_bounds__(256) void moments_partials_l1(const float* __restrict__ part, int T,
+                                                           int C, float* __restrict__ ws) {
+  __shared__ Wf sh[16][16];
+  const int lane = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lane;
+  const int z0 = blockIdx.y * 256;
+  Wf w{0.f, 0.f, 0.f};
+  if (c < C) {
+#pragma unroll 4
+    for (int z = z0 + g; z < z0 + 256 && z < T; z += 16) {
+      const float* o = part + (long)z * 3 * C;
+      w = wf_merge(w, Wf{o[c], o[C + c], o[2 * C + c]});
+    }
+  }
+  sh[g][lane] = w;
+  __syncthreads();
+  if (threadIdx.x < 16 && c < C) {
+    Wf a = wf_merge(wf_merge(sh[0][lane], sh[1][lane]), wf_merge(sh[2][lane], sh[3][lane]));
+    Wf b = wf_merge(wf_merge(sh[4][lane], sh[5][lane]), wf_merge(sh[6][lane], sh[7][lane]));
+    Wf d = wf_merge(wf_merge(sh[8][lane], sh[9][lane]), wf_merge(sh[10][lane], sh[11][lane]));
+    Wf e = wf_merge(wf_merge(sh[12][lane], sh[13][lane]), wf_merge(sh[14][lane], sh[15][lane]));
+    w = wf_merge(wf_merge(a, b), wf_merge(d, e));
+    float* o = ws + (long)blockIdx.y * 3 * C;
+    o[c] = w.n; o[C + c] = w.mean; o[2 * C + c] = w.m2;
+  }
+}
+
 // Rows of `g`: [mean(C) | var(C) | count], stride 2C+1. Zero-count ranks drop out, as in
 // batch_norm_gather_stats_with_counts (TORCH/nn/modules/_functions.py:96-115).
 __global__ void merge_kernel(const float* __restrict__ g, int R, int C, float eps, float momentum,
@@ -631,6 +661,17 @@ int bn_splits(int N, int C, int HW, int num_cus) {
 }
 
 long bn_ws_floats(int C, int splits) { return 3L * C * (splits > 0 ? splits : 1); }
+
+long bn_partials_ws_floats(int T, int C) { return 3L * C * ((T + 255) / 256); }
+
+void bn_moments_partials(const float* part, int T, int C, float* ws, float* mean, float* var,
+                         float* count_out, float cnt, hipStream_t s) {
+  const int chunks = (T + 255) / 256;
+  hipLaunchKernelGGL(moments_partials_l1, dim3((C + 15) / 16, chunks), dim3(256), 0, s, part, T,
+                     C, ws);
+  hipLaunchKernelGGL(moments_final, dim3((C + 15) / 16), dim3(256), 0, s, ws, C, chunks, mean,
+                     var, count_out, cnt);
+}
 
 void bn_moments(const float* x, int N, int C, int HW, int splits, float* ws, float* mean,
                 float* var, float* count_out, hipStream_t s) {

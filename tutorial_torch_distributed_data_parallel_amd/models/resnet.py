@@ -83,6 +83,14 @@ class ResNet(nn.Module):
         self.layer4 = self._make_layer(512, layers[3], 2, device)
         self.avgpool = AdaptiveAvgPool2d((1, 1))
         self.fc = Linear(512 * Bottleneck.expansion, num_classes, device=device)
+        # every convolution here feeds a BatchNorm: its GEMM epilogue emits the statistics
+        self.conv1.bn_stats = True
+        for m in self.modules():
+            if isinstance(m, Bottleneck):
+                for c in (m.conv1, m.conv2, m.conv3):
+                    c.bn_stats = True
+                if m.downsample is not None and isinstance(m.downsample[0], Conv2d):
+                    m.downsample[0].bn_stats = True
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

@@ -36,6 +36,7 @@ class Conv2d(nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
                          bias=bias, device=device, dtype=dtype)
         self.relu = relu
+        self.bn_stats = False  # output feeds a BatchNorm: emit its statistics (ops.conv2d)
         # The weight lives in channels_last memory ([Cout][R][S][C]): exactly the operand layout
         # of the implicit-GEMM kernels (forward B, input-gradient taps, weight-gradient output),
         # so no step permutes or copies it. Shape and state_dict keys stay torch's [Cout, C, R, S].
@@ -44,7 +45,7 @@ class Conv2d(nn.Conv2d):
 
     def forward(self, x, grad_into=None):
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, relu=self.relu,
-                          grad_into=grad_into)
+                          grad_into=grad_into, bn_stats=self.bn_stats and self.training)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")

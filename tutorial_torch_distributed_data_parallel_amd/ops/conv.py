@@ -110,7 +110,7 @@ class _ConvNHWCFn(torch.autograd.Function):
     the RGB stem (3 channels, padded to 4 for the 16-B DMA chunks) repacks, natively."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, relu: bool, sink=None):
+    def forward(ctx, x, weight, bias, stride, padding, relu: bool, sink=None, stats_box=None):
         C = native()
         N, Cin, H, W = x.shape
         Cout, _, R, S = weight.shape
@@ -119,7 +119,12 @@ class _ConvNHWCFn(torch.autograd.Function):
         ph, pw = padding
         xp = _as_cl(C, x, Cp)
         wt = _as_cl(C, weight, Cp)  # the parameter itself for every conv but the stem
-        y = C.conv_nhwc_fwd(xp, wt.permute(0, 2, 3, 1), bias, R, S, sh, sw, ph, pw, relu)
+        if stats_box is not None and bias is None and not relu:
+            # the GEMM epilogue also emits the output's per-tile BN statistics (or None)
+            y, st = C.conv_nhwc_fwd_stats(xp, wt.permute(0, 2, 3, 1), R, S, sh, sw, ph, pw)
+            stats_box.append(st)
+        else:
+            y = C.conv_nhwc_fwd(xp, wt.permute(0, 2, 3, 1), bias, R, S, sh, sw, ph, pw, relu)
         ctx.geom = (R, S, sh, sw, ph, pw, Cin, Cp)
         ctx.sink = sink
         ctx.relu = relu
@@ -171,7 +176,7 @@ class _ConvNHWCFn(torch.autograd.Function):
                 dx = dx[:, :Cin]
             if sink is not None:
                 dx = dx if acc is not None else sink.deposit(dx)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def _dgrad_phases(C, g, wt, x_shape, R, S, sh, sw, ph, pw, into=None):
@@ -218,12 +223,14 @@ def _nhwc_ok(x, weight, stride):
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            stride=1, padding=0, relu: bool = False,
-           grad_into: SharedGrad | None = None) -> torch.Tensor:
+           grad_into: SharedGrad | None = None, bn_stats: bool = False) -> torch.Tensor:
     """``relu?(conv2d(x, weight, bias, stride, padding))`` for float32 [N, C, H, W] tensors.
 
     On the GPU the result is channels_last (NHWC memory, logical NCHW shape, as torch does for
     channels_last inputs). ``grad_into``: the input gradient goes into that shared buffer (a
-    forked residual input, ops/_grad.py ``fork``)."""
+    forked residual input, ops/_grad.py ``fork``). ``bn_stats``: the output will be
+    batch-normalised -- the GEMM epilogue also computes its per-channel statistics, attached
+    to the result for ``batch_norm`` (no moments pass over the output)."""
     stride, padding = _pair(stride), _pair(padding)
     if not x.is_cuda:
         y = F.conv2d(x, weight, bias, stride, padding)
@@ -232,7 +239,11 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         raise TypeError(f"native conv2d expects float32 activations, got {x.dtype}")
     if _nhwc_ok(x, weight, stride):
         plan_db.ensure_loaded(native())  # measured per-geometry plans (ops/plan_db.py)
-        return _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu, grad_into)
+        box = [] if bn_stats else None
+        y = _ConvNHWCFn.apply(x, weight, bias, stride, padding, relu, grad_into, box)
+        if box and box[0] is not None:
+            y._tdp_bn_part = (box[0], y._version)  # ops/norm.py batch_norm consumes it
+        return y
     return _Conv2dFn.apply(x.contiguous(), weight.contiguous(), bias, stride, padding, relu,
                            grad_into)
 

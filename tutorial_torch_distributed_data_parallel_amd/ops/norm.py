@@ -119,7 +119,7 @@ def _kernels(x):
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, group,
-                residual, num_batches, sink=None):
+                residual, num_batches, sink=None, part=None):
         K = _kernels(x)
         C = x.shape[1]
         # channels_last (NHWC) activations are a [pixels, C] matrix: the BatchNorm1d kernels
@@ -130,7 +130,11 @@ class _BatchNormFn(torch.autograd.Function):
         if residual is not None:
             residual = _rows(residual.contiguous(memory_format=torch.channels_last)) \
                 if ctx.nhwc else residual.contiguous()
-        st = K.bn_moments(x)[0]
+        if part is not None and ctx.nhwc:
+            # statistics from the producing convolution's GEMM epilogue (per-tile Chan merge)
+            st = native().bn_moments_partials(part, float(x.shape[0]))
+        else:
+            st = K.bn_moments(x)[0]
         gathered = group.all_gather_flat(st) if group is not None else st
         stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var, num_batches)
         # [rows, C % 4] form on the GPU: the backward reads a 1-byte-per-4-channels ReLU mask
@@ -174,7 +178,16 @@ class _BatchNormFn(torch.autograd.Function):
                 dres = _unrows(dres, ctx.shape4) if dres is not None else None
             if dres is not None and ctx.sink is not None:
                 dres = ctx.sink.deposit(dres)  # the forked block input's shared gradient
-        return dx, dw, db, None, None, None, None, None, None, dres, None, None
+        return dx, dw, db, None, None, None, None, None, None, dres, None, None, None
+
+
+def _conv_stats(x):
+    """Per-tile statistics a producing convolution attached to ``x`` (ops/conv.py
+    ``bn_stats``), if they still describe it (same version: not modified in place since)."""
+    tag = getattr(x, "_tdp_bn_part", None)
+    if tag is None or tag[1] != x._version or tag[0].shape[2] != x.shape[1]:
+        return None
+    return tag[0]
 
 
 def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
@@ -195,7 +208,7 @@ def batch_norm(x: torch.Tensor, running_mean: torch.Tensor | None,
             return F.relu(y) if relu else y
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var, float(momentum),
                                   float(eps), bool(relu), group, residual, num_batches_tracked,
-                                  residual_grad_into)
+                                  residual_grad_into, _conv_stats(x))
     if residual is not None:
         y = batch_norm(x, running_mean, running_var, weight, bias, False, momentum, eps, False)
         y = y + residual
