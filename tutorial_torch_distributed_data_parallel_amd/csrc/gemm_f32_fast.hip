@@ -1302,7 +1302,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
 }
 
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
-  FastParams p;
+  FastParams p{};  // zero: every optional pointer (stats, wt, ...) unset unless assigned below
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
   p.rowsum = a.rowsum; p.rowsum_beta = a.rowsum_beta;
   p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
