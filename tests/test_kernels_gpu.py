@@ -337,53 +337,3 @@ def test_gather_batch_matches_index_select(C):
         assert torch.equal(xb, x.index_select(0, idx)) and torch.equal(yb, y.index_select(0, idx))
         xb2, yb2 = gather_batch(x, y, idx[5:20])
         assert torch.equal(xb2, x[idx[5:20]]) and torch.equal(yb2, y[idx[5:20]])
-
-
-@pytest.mark.parametrize("M,N,K", [(70000, 256, 64), (50000, 132, 96), (33333, 64, 256),
-                                   (20000, 512, 128)])
-def test_gemm_persistent_matches_per_tile(C, M, N, K):
-    """The persistent plain GEMM (resident grid, the next tile's first stages prefetched under
-    the epilogue, the output staged through one stage buffer in halves) is bitwise identical to
-    one workgroup per tile: same K order per tile, only the schedule differs."""
-    torch.manual_seed(21)
-    A = torch.randn(M, K, device="cuda")
-    W = torch.randn(N, K, device="cuda")
-    b = torch.randn(N, device="cuda")
-    outs = []
-    for persist in (False, True):
-        C.gemm_f32_set_persist(persist)
-        try:
-            o = torch.empty(M, N, device="cuda")
-            C.gemm_f32(A, W, o, True, True, bias=b, relu=True)
-            outs.append(o)
-        finally:
-            C.gemm_f32_set_persist(False)
-    assert torch.equal(outs[0], outs[1])
-    ref = torch.relu(A.double() @ W.double().t() + b.double())
-    torch.testing.assert_close(outs[1].double(), ref, atol=2e-4 * K ** 0.5, rtol=1e-4)
-
-
-@pytest.mark.parametrize("Cin,H,Cout,R", [(64, 56, 256, 1), (256, 28, 64, 3), (128, 17, 96, 3)])
-def test_conv_persistent_matches_per_tile(C, Cin, H, Cout, R):
-    """Persistent vs per-tile convolution forward (with the BN-statistics epilogue) and input
-    gradient: bitwise identical outputs and statistics."""
-    from tutorial_torch_distributed_data_parallel_amd import ops
-
-    torch.manual_seed(22)
-    x = torch.randn(32, Cin, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(Cout, Cin, R, R, device="cuda") * 0.05).contiguous(
-        memory_format=torch.channels_last)
-    dy = torch.randn(32, Cout, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
-    res = []
-    C.gemm_f32_set_override(0, 1, 0)  # unsplit plans (persistence needs them)
-    try:
-        for persist in (False, True):
-            C.gemm_f32_set_persist(persist)
-            y = ops.conv2d(x, w, None, 1, R // 2, bn_stats=True)
-            dx = C.conv_nhwc_dgrad_w(dy, w, [32, Cin, H, H], 1, 1, R // 2, R // 2)
-            res.append((y, y._tdp_bn_part[0], dx))
-    finally:
-        C.gemm_f32_set_override(0, 0, 0)
-        C.gemm_f32_set_persist(False)
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)

@@ -16,7 +16,6 @@ struct ConvPlan {
   int M = 0, N = 0, K = 0;
   int fm = 2, fn = 2;
   int bm = 128;  // NHWC fast path: block rows (128, or 256 = FM 4 for K-contiguous A)
-  int grid = 0;  // NHWC fast path: > 0 = persistent grid of this many workgroups (splits == 1)
   int splits = 1, k_per_split = 0;
   long ws_floats = 0;
 };

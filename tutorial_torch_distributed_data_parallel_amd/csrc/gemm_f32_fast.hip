@@ -82,7 +82,6 @@ struct FastParams {
   float beta, rowsum_beta;
   int relu;
   int cvec;  // C (or the split-K workspace) takes 16-B row stores: N % 4 == 0, aligned rows
-  int persist;  // plain GEMM, splits == 1: a resident grid walks the tiles (gemm_tile PersistState)
   float* stats;  // optional [tiles_m][3][N]: per-tile column (count, mean, M2) of the stored C
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
 };
@@ -391,23 +390,11 @@ struct SrcOf<R, kImWgradT, true> : ImSrcB<R, true> {};
 template <int R>
 struct SrcOf<R, kWTap, false> : WTapSrc<R> {};
 
-// Cross-tile pipeline state of a persistent workgroup: `gbase` = global K-step count (stage
-// buffer of K step t of the current tile = (gbase + t) % S); `prefetched` = the previous tile
-// already issued this tile's first S-1 stages (during its last K steps), so their HBM latency
-// overlapped its epilogue.
-struct PersistState {
-  int gbase;
-  bool prefetched;
-};
-
-// One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel. With `ps`
-// (persistent plain GEMM, splits == 1) the last K steps prefetch tile `next_lid` and the
-// epilogue stages its output through the one free stage buffer, in two halves.
+// One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel.
 // FM = 32-row MFMA tiles per wave (block rows BM = 64 * FM): 2, or 4 for a K-contiguous A (twice
 // the MFMAs per barrier and per B fragment read, for the long-M convolution GEMMs).
 template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM>
-__device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, lds_char* smem,
-                                          PersistState* ps = nullptr, int next_lid = -1) {
+__device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, lds_char* smem) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
   static_assert(FM == 2 || (FM == 4 && AK && OPTK == 0), "FM 4: K-contiguous A, plain epilogue");
@@ -431,26 +418,12 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   const int ke = min(p.K, kb + p.k_per_split);
   const int nk = (ke - kb + kBK - 1) / kBK;
 
-  const int gb = ps ? ps->gbase : 0;
   SrcOf<BM, AKIND, true> srcA;
   SrcOf<BN, BKIND, false> srcB;
   srcA.init(p, m0, p.M, wid, lane);
   srcB.init(p, n0, p.N, wid, lane);
   auto issue = [&](int t) {
-    lds_char* st = smem + ((gb + t) % S) * STG;
-    if (t >= nk && next_lid >= 0) {
-      // past this tile's K range: the next tile's stage t - nk (persistent, splits == 1: its K
-      // range is [0, K) too). The sources are re-pointed once; this tile issued its last stage.
-      if (t == nk) {
-        const int nt = next_lid % tiles_mn;
-        srcA.init(p, (nt / p.tiles_n) * BM, p.M, wid, lane);
-        srcB.init(p, (nt % p.tiles_n) * BN, p.N, wid, lane);
-      }
-      const int k0 = (t - nk) * kBK;
-      srcA.issue(p, k0, p.K, st, wid);
-      srcB.issue(p, k0, p.K, st + A_BYTES, wid);
-      return;
-    }
+    lds_char* st = smem + (t % S) * STG;
     const int k0 = kb + t * kBK;
     srcA.issue(p, k0, ke, st, wid);
     srcB.issue(p, k0, ke, st + A_BYTES, wid);
@@ -464,10 +437,8 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (!(ps && ps->prefetched)) {
 #pragma unroll
-    for (int t = 0; t < S - 1; ++t) issue(t);
-  }
+  for (int t = 0; t < S - 1; ++t) issue(t);
 
   const int h = lane >> 5, l31 = lane & 31;
   // per-lane LDS byte offsets of the fragment reads (within a stage)
@@ -540,7 +511,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     wait_vmcnt<(S - 2) * G>();
     __builtin_amdgcn_s_barrier();
     issue(kt + S - 1);  // refill the stage every wave finished reading (kt - 1)
-    const lds_char* st = smem + ((gb + kt) % S) * STG;
+    const lds_char* st = smem + (kt % S) * STG;
     const int kvalid = ke - (kb + kt * kBK);  // < 32 only on the K tail
     if (do_rs && threadIdx.x < BM) {
       const int kmax = kvalid < kBK ? kvalid : kBK;
@@ -574,13 +545,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
                                                              0);
     }
   }
-  // no LDS-DMA may outlive the workgroup; a persistent tile with a successor leaves the next
-  // tile's prefetch in flight (into stage buffers the epilogue does not touch)
-  if (!(ps && next_lid >= 0)) wait_vmcnt<0>();
-  if (ps) {
-    ps->gbase = gb + nk;
-    ps->prefetched = next_lid >= 0;
-  }
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
   if (do_rs && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
     float* d = p.rowsum + m0 + threadIdx.x;
     *d = (p.rowsum_beta != 0.f ? p.rowsum_beta * *d : 0.f) + rs;
@@ -825,90 +790,6 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
   float* out = split ? p.ws + (long)z * p.M * p.N : p.C;
   const long ldo = split ? p.N : p.ldc;
-  if (OPTK == 0 && ps != nullptr && p.cvec) {
-    // persistent form of the row-vector store: only the stage buffer of this tile's last K step
-    // is free (the others hold the next tile's prefetch), so the tile goes through it in two
-    // halves -- the rows of wave row 0, then of wave row 1
-    constexpr int HR = BM / 2;
-    constexpr int PADH = (HR * (BN + 8) * 4 <= STG) ? 8 : 0;
-    constexpr int TSH = BN + PADH;
-    static_assert(HR * TSH * 4 <= STG, "half tile must fit one stage buffer");
-    float* T = reinterpret_cast<float*>(smem + ((gb + nk - 1) % S) * STG);
-    constexpr int C4 = BN / 4;
-    constexpr int ITH = HR * C4 / kT;  // float4 per thread per half
-    const bool want_st = p.stats != nullptr;  // (beta == 0 here: the host plans persistence so)
-    const int lcs = (threadIdx.x % C4) * 4;
-    f32x4 k4 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      __syncthreads();  // hh 0: every wave left the K loop; hh 1: half 0 fully read
-      if (wm == hh) {
-#pragma unroll
-        for (int f = 0; f < FM; ++f)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int lr = AK ? f * 32 + rl : 2 * rl + f;  // row within the wave's (= half's) rows
-            if (BKC || FN == 1) {
-#pragma unroll
-              for (int g = 0; g < FN; ++g)
-                T[lr * TSH + wn * (32 * FN) + g * 32 + l31] = acc[f][g][r];
-            } else {
-              *reinterpret_cast<f32x2*>(T + lr * TSH + wn * 64 + 2 * l31) =
-                  f32x2{acc[f][0][r], acc[f][FN - 1][r]};
-            }
-          }
-      }
-      __syncthreads();
-      if (hh == 0 && want_st) k4 = *reinterpret_cast<const f32x4*>(T + lcs);
-#pragma unroll
-      for (int i = 0; i < ITH; ++i) {
-        const int e = i * kT + threadIdx.x;
-        const int lr = e / C4, lc = (e % C4) * 4;
-        const int row = m0 + hh * HR + lr, col = n0 + lc;
-        if (row >= p.M || col >= p.N) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(T + lr * TSH + lc);
-        if (want_st) {
-          const f32x4 d = v - k4;
-          s1 += d;
-          s2 += d * d;
-        }
-        if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
-        if (p.relu) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
-        }
-        *reinterpret_cast<f32x4*>(p.C + row * p.ldc + col) = v;
-      }
-    }
-    if (want_st) {
-      // as in the non-persistent epilogue below (stats only ride on a bias/ReLU/beta-free GEMM)
-      __syncthreads();
-      float* R = T;
-      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12) = s1;
-      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12 + 4) = s2;
-      *reinterpret_cast<f32x4*>(R + threadIdx.x * 12 + 8) = k4;
-      __syncthreads();
-      constexpr int GRP = kT / C4;
-      const float n = (float)min(BM, p.M - m0);
-      for (int c = threadIdx.x; c < BN; c += kT) {
-        const int q = c >> 2, j = c & 3, col = n0 + c;
-        if (col >= p.N) continue;
-        float a = 0.f, b = 0.f;
-#pragma unroll 4
-        for (int g = 0; g < GRP; ++g) {
-          a += R[(g * C4 + q) * 12 + j];
-          b += R[(g * C4 + q) * 12 + 4 + j];
-        }
-        const float mean_d = a / n;
-        float* o = p.stats + (long)(m0 / BM) * 3 * p.N;
-        o[col] = n;
-        o[p.N + col] = R[q * 12 + 8 + j] + mean_d;
-        o[2 * p.N + col] = fmaxf(b - a * mean_d, 0.f);
-      }
-    }
-    return;  // the next tile's first K-loop barrier protects this buffer before its refill
-  }
   if (BM * BN * 4 <= S * STG && p.cvec) {
     // Row-vector store: the tile goes through LDS (the pipeline stages are free once every wave
     // has left the K loop) and leaves as 16-B-per-lane row segments. The accumulator layout
@@ -1089,7 +970,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM = 2, bool PER = false>
+template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM = 2>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
@@ -1118,20 +999,6 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
       gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem);
       __builtin_amdgcn_s_barrier();  // every wave is done with this tile's LDS stages
     }
-  } else if constexpr (PER) {
-    // resident grid (splits == 1): each workgroup walks tiles of its XCD's contiguous range,
-    // prefetching the next tile's first stages under the current tile's epilogue
-    const int T = p.tiles_m * p.tiles_n;
-    const int q8 = nwg / 8, r8 = nwg % 8;
-    const int per = q8 + (xcd < r8 ? 1 : 0);
-    const int before = xcd * q8 + (xcd < r8 ? xcd : r8);
-    const int j = b / 8;
-    const int t0 = (int)((long)T * before / nwg), t1 = (int)((long)T * (before + per) / nwg);
-    PersistState ps{0, false};
-    for (int lid = t0 + j; lid < t1; lid += per) {
-      const int nxt = lid + per < t1 ? lid + per : -1;
-      gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem, &ps, nxt);
-    }
   } else {
     const int q8 = nwg / 8, r8 = nwg % 8;
     const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
@@ -1139,18 +1006,17 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPT = 0, int FM = 2, bool PER = false>
+template <int FN, int AKIND, int BKIND, int S, int OPT = 0, int FM = 2>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
   constexpr int STG = 64 * FM * kBK * 4 + 64 * FN * kBK * 4;
   const size_t lds = (size_t)S * STG;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute(
-        (const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM, PER>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM, PER>), dim3(nblocks),
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>), dim3(nblocks),
                      dim3(kT), lds, s, p);
 }
 
@@ -1163,13 +1029,6 @@ void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStrea
   if constexpr (AK && OPT == 0) {
     if (bm == 256) {
       launch_fast<1, AKIND, BKIND, 2, 0, 4>(p, nblocks, s);
-      return;
-    }
-  }
-  if constexpr (OPT == 0) {
-    if (p.persist) {  // resident grid walking the tiles (2 stages; see PersistState)
-      if (fn == 1) launch_fast<1, AKIND, BKIND, 2, 0, 2, true>(p, nblocks, s);
-      else launch_fast<2, AKIND, BKIND, 2, 0, 2, true>(p, nblocks, s);
       return;
     }
   }
@@ -1240,21 +1099,6 @@ void gemm_f32_set_override(int fn, int splits, int stages) {
 // Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
 static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
 static int o_bm = 0;  // 0 auto, 128 / 256 forced (sweeps)
-// Persistent plain GEMMs (splits == 1, more tiles than resident workgroup slots): the resident
-// grid walks the tiles and hides each tile's first operand loads under the previous tile's
-// epilogue. Off until measured (TDP_GEMM_PERSIST=1 / gemm_f32_set_persist(true) turn it on).
-static bool o_persist = [] {
-  const char* e = std::getenv("TDP_GEMM_PERSIST");
-  return e && e[0] == '1';
-}();
-void gemm_f32_set_persist(bool on) { o_persist = on; }
-static int persist_grid(long tiles, int splits, int fn, int stages, int bm, int num_cus) {
-  // the persistent kernels are instantiated with 2 stages and 128-row tiles; they carry more
-  // registers than the one-tile kernels: 2 resident workgroups per CU
-  if (!o_persist || splits != 1 || stages != 2 || bm != 128) return 0;
-  const long slots = 2L * num_cus;
-  return tiles > slots ? (int)slots : 0;
-}
 void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
 void gemm_f32_set_cvec(bool on) { o_no_cvec = !on; }
 static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int splits) {
@@ -1296,9 +1140,6 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   const int nk = ceil_div(kps, kBK);
   plan.stages = (fn == 1 && nk > 4) ? 3 : 2;
   if (o_stages == 2 || o_stages == 3) plan.stages = o_stages;
-  if (a.opt.kind == 0 && a.rowsum == nullptr)
-    plan.grid = persist_grid((long)ceil_div(a.M, plan.bm) * ceil_div(a.N, bn), plan.splits, fn,
-                             plan.stages, plan.bm, num_cus);
 }
 
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
@@ -1354,13 +1195,10 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
     return;
   }
   p.opt.kind = 0;
-  p.persist = plan.grid > 0 && plan.splits == 1 && a.rowsum == nullptr && a.beta == 0.f &&
-              p.cvec ? 1 : 0;
-  const int nb = p.persist ? plan.grid : nblocks;
-  if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nb, s, plan.bm);
-  else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nb, s, plan.bm);
-  else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nb, s);
-  else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nb, s);
+  if (ak && bk) launch_kinds<kDenseK, kDenseK>(p, fn, st, nblocks, s, plan.bm);
+  else if (ak && !bk) launch_kinds<kDenseK, kDenseMN>(p, fn, st, nblocks, s, plan.bm);
+  else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nblocks, s);
+  else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nblocks, s);
   if (plan.splits > 1)
     splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
   if (a.opt.kind != 0) gemm_opt_fallback(a, s);
@@ -1514,8 +1352,6 @@ ConvPlan conv_nhwc_plan(int mode, const ConvGeom& g, int num_cus) {
   pl.bm = 128;
   if (mode != kConvWgrad && gp.tile == 1 && gp.splits == 1 && o_bm == 256) pl.bm = 256;
   if (pl.bm == 256) gp.stages = 2;
-  pl.grid = persist_grid((long)ceil_div(pl.M, pl.bm) * ceil_div(pl.N, 64 * gp.tile), gp.splits,
-                         gp.tile, gp.stages, pl.bm, num_cus);
   pl.fn = gp.tile;
   pl.fm = gp.stages;  // pipeline depth (the NHWC path always uses BM = 128)
   pl.splits = gp.splits;
@@ -1581,8 +1417,7 @@ bool conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
   const bool stats_ok = stats != nullptr && pl.mode == kConvFwd && pl.splits == 1 && p.cvec &&
                         bias == nullptr && !relu && beta == 0.f;
   p.stats = stats_ok ? stats : nullptr;
-  p.persist = pl.grid > 0 && pl.splits == 1 && beta == 0.f && p.cvec ? 1 : 0;
-  const int nblocks = p.persist ? pl.grid : p.tiles_m * p.tiles_n * pl.splits;
+  const int nblocks = p.tiles_m * p.tiles_n * pl.splits;
   const int fn = pl.fn, st = pl.fm;
   if (pl.mode == kConvFwd) launch_kinds<kImFwd, kDenseK>(p, fn, st, nblocks, s, pl.bm);
   else if (pl.mode == kConvDgrad && wtap)

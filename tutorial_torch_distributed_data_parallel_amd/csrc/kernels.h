@@ -138,8 +138,6 @@ void gemm_f32_set_override(int fn, int splits, int stages);
 void gemm_f32_set_cvec(bool on);
 // fast-GEMM block rows: 0 auto, 128 or 256 forced (measurements, tests)
 void gemm_f32_set_bm(int bm);
-// persistent plain fast GEMMs on / off (A/B measurements, tests)
-void gemm_f32_set_persist(bool on);
 // optimizer-epilogue variant (SGD flags, Adam flags, persistent grid on/off, workgroups per CU);
 // negative = keep. Returns the active {sgd, adam, persist, wgs}.
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs);
