@@ -72,7 +72,18 @@ def main():
             dy = torch.randn_like(y_x)
             Cout, Cin, R, S = ws
             P, Q = y_x.shape[2], y_x.shape[3]
-            passes = [("fwd", lambda: ops.conv2d(x, w, None, st, pd), FD),
+            def fwd_bn():
+                # ResNet: a BatchNorm follows -- an unsplit plan's epilogue emits its statistics,
+                # a split plan leaves a moments pass over the output (price both)
+                y = ops.conv2d(x, w, None, st, pd, bn_stats=True)
+                tag = getattr(y, "_tdp_bn_part", None)
+                if tag is None:
+                    C.bn_moments(y.permute(0, 2, 3, 1).reshape(-1, y.shape[1]))
+                else:
+                    C.bn_moments_partials(tag[0], float(y.numel() // y.shape[1]))
+
+            fwd = fwd_bn if name == "resnet50" else (lambda: ops.conv2d(x, w, None, st, pd))
+            passes = [("fwd", fwd, FD),
                       ("wgrad", lambda: torch.autograd.grad(y_w, wr, dy, retain_graph=True),
                        wgrad_candidates(Cout, R * S * ((Cin + 3) // 4 * 4), xs[0] * P * Q))]
             if xs[1] >= 4:  # the stem's input needs no gradient
