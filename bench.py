@@ -39,6 +39,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -432,13 +433,8 @@ def main():
     value = a.batch * world * a.steps / dt
     base = baseline_for(world, a.impl, a.syncbn, a.model)
     final_loss = round(float(loss.item()), 5)
-    diag = None
-    if a.impl == "tdp" and a.api == "ddp" and use_gpu and not a.no_diag:
-        try:
-            diag = diagnostics(a, ddp, step, ms, world, graph, barrier, build_rehearsal)
-        except Exception as e:  # diagnostics never cost the measurement
-            diag = {"error": repr(e)[:300]}
-    if rank == 0:
+
+    def record(diag):
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
                                           bn=", +SyncBatchNorm" if a.syncbn else "")
         if a.impl == "tdp":
@@ -477,7 +473,30 @@ def main():
         }
         if diag is not None:
             rec["diagnostics"] = diag
-        print(json.dumps(rec), file=out, flush=True)
+        return rec
+
+    diag = None
+    if a.impl == "tdp" and a.api == "ddp" and use_gpu and not a.no_diag:
+        # The measurement is final here. Diagnostics run more collectives, and a peer that
+        # stalls in them must not cost the result: past the deadline every rank exits 0, and
+        # rank 0 first prints the record without them.
+        limit = float(os.environ.get("TDP_DIAG_TIMEOUT_S", "120"))
+
+        def expire():
+            if rank == 0:
+                print(json.dumps(record({"error": f"diagnostics exceeded {limit:g} s"})),
+                      file=out, flush=True)
+            os._exit(0)
+        timer = threading.Timer(limit, expire)
+        timer.daemon = True
+        timer.start()
+        try:
+            diag = diagnostics(a, ddp, step, ms, world, graph, barrier, build_rehearsal)
+        except Exception as e:  # diagnostics never cost the measurement
+            diag = {"error": repr(e)[:300]}
+        timer.cancel()
+    if rank == 0:
+        print(json.dumps(record(diag)), file=out, flush=True)
     finish()
 
 

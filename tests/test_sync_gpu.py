@@ -320,3 +320,25 @@ def test_bucket_rebuild_gpu(pg, fused):
     for n, p in model.named_parameters():
         torch.testing.assert_close(p.detach(), params[n].detach(), atol=5e-5, rtol=1e-4,
                                    msg=lambda m: f"{n}: {m}")
+
+
+@pytest.mark.gpu
+def test_bench_diagnostics_deadline():
+    """bench.py: diagnostics that overrun TDP_DIAG_TIMEOUT_S cannot cost the measurement -- the
+    record is printed (one JSON line, diagnostics marked) and the process exits 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TDP_DIAG_MULTI="1", TDP_DIAG_TIMEOUT_S="0.001")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--mlp-dims",
+                        "256,128,128", "--steps", "3", "--warmup", "1", "--dataset", "512"],
+                       env=env, capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["steps"] == 3 and rec["value"] > 0
+    assert "exceeded" in rec["diagnostics"]["error"]
