@@ -143,6 +143,8 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
   }
   const char* mode = std::getenv("TDP_COMM_STREAM");
   const std::string m = mode ? mode : "auto";
+  const char* fm = std::getenv("TDP_GRAPH_FORK_MARKER");
+  fork_marker_ = !(fm && fm[0] == '0');
   stream_mode_ = m == "side" ? kStreamSide
                  : m == "compute" ? kStreamCompute
                  : m == "hostsync" ? kStreamHostSync
@@ -196,19 +198,24 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute) {
   // queue while the host runs ahead slows every launch on the other queue. Inside a hipGraph the
   // same dependency is a graph edge and the collectives overlap backward. So: side stream while
   // capturing, the compute stream itself otherwise (TDP_COMM_STREAM overrides for measurements).
-  bool side = true;
-  if (stream_mode_ == kStreamAuto) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    check_hip(hipStreamIsCapturing(compute, &cap), "hipStreamIsCapturing");
-    side = cap == hipStreamCaptureStatusActive;
-  } else {
-    side = stream_mode_ != kStreamCompute;
-  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  check_hip(hipStreamIsCapturing(compute, &cap), "hipStreamIsCapturing");
+  const bool capturing = cap == hipStreamCaptureStatusActive;
+  const bool side_wanted = stream_mode_ == kStreamAuto ? capturing : stream_mode_ != kStreamCompute;
+  bool side = side_wanted;
   if (!side && launched_side_) side = true;  // never switch streams within one iteration
   hipStream_t cs = side ? ops_->comm_stream() : compute;
   if (side) {
     launched_side_ = true;
     check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
+    // Captured fork: HIP assigns graph nodes to its replay streams depth first, the first
+    // child edge of a node inheriting the node's stream and every further edge taking the next
+    // one (mod the graph's stream count). Capturing the collective first made it the first
+    // child, so the compute chain moved to a new stream at every bucket and, after a few
+    // buckets, wrapped onto the collectives' stream: backward serialised behind an all-reduce
+    // (profiles/overlap_rehearsal_r3.md). An empty node on the compute stream, captured before
+    // the collective, is the first child instead: compute keeps one stream, collectives another.
+    if (capturing && fork_marker_) graph_fork_marker(compute);
     if (stream_mode_ == kStreamHostSync)
       check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
     else

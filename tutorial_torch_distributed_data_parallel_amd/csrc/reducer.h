@@ -201,6 +201,7 @@ class SyncBackend : public ReducerBackend {
     kStreamHostJoin = 4, kStreamNoJoin = 5
   };
   int stream_mode_ = kStreamAuto;
+  bool fork_marker_ = true;  // TDP_GRAPH_FORK_MARKER=0 disables (A/B)
 };
 
 class Reducer {
