@@ -208,13 +208,12 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute) {
   if (side) {
     launched_side_ = true;
     check_hip(hipEventRecord(ready_[bucket], compute), "hipEventRecord");
-    // Captured fork: HIP assigns graph nodes to its replay streams depth first, the first
-    // child edge of a node inheriting the node's stream and every further edge taking the next
-    // one (mod the graph's stream count). Capturing the collective first made it the first
-    // child, so the compute chain moved to a new stream at every bucket and, after a few
-    // buckets, wrapped onto the collectives' stream: backward serialised behind an all-reduce
-    // (profiles/overlap_rehearsal_r3.md). An empty node on the compute stream, captured before
-    // the collective, is the first child instead: compute keeps one stream, collectives another.
+    // Captured fork: when the collective is captured before the compute chain's next node,
+    // HIP's replay puts the chain on a different stream at every fork and, after a few buckets,
+    // on the collectives' hardware queue -- backward serialised behind an all-reduce (measured:
+    // profiles/graph_fork_order_r3.md; consistent with the first child edge of a node inheriting
+    // its stream). An empty node on the compute stream, captured before the collective, keeps
+    // compute and collectives on separate queues: the probe replays fully concurrent.
     if (capturing && fork_marker_) graph_fork_marker(compute);
     if (stream_mode_ == kStreamHostSync)
       check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
