@@ -27,7 +27,8 @@ into no-ops (``compute_ms``), the share of the collective time hidden behind com
 of the multi-GPU schedule (``rehearsal_ms``: RCCL collectives kept, per-bucket fused update,
 captured step).
 
-Timing: W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
+Timing: a device clock warm-up (``--device-warmup-ms`` of dummy GEMMs, no model state touched),
+then W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
 both sides; the max over ranks is reported; rank 0 prints one JSON line. Native libraries (RCCL
 prints a version banner when a communicator is created) write to file descriptor 1, so the
 process points fd 1 at stderr and writes the JSON line to a private duplicate of the original
@@ -77,6 +78,9 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--split-mb", type=float, default=None,
                     help="cut parameters larger than this into buckets of this size")
+    ap.add_argument("--device-warmup-ms", type=float, default=200.0,
+                    help="GPU clock warm-up (dummy GEMMs, no model state) before the W warm-up "
+                         "steps; 0 = off (see device_warmup)")
     ap.add_argument("--no-diag", action="store_true",
                     help="skip the post-measurement diagnostics (comm / compute / rehearsal)")
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
@@ -126,6 +130,34 @@ MODEL_DESC = {
     "alexnet": "AlexNet (torchvision topology, 10 classes, 3x{s}x{s}{bn})",
     "resnet50": "ResNet-50 (torchvision v1.5 topology, 10 classes, 3x{s}x{s}{bn})",
 }
+
+
+def device_warmup(dev, ms: float, native_gemm: bool):
+    """Bring the GPU to its steady-state clock before the W warm-up steps: ``ms`` of dummy
+    2048^3 GEMMs (no model state is touched). Measured on MI355X (scripts/step_timeline.py,
+    profiles/bench_clock_ramp_r3.md): from a cold start the toy-MLP step needs ~40 steps (~20 ms
+    of load) to settle -- 0.49 ms for steps 10-19, 0.476 for 20-29, 0.455 from step 40 on -- so a
+    5-step warm-up timed the power-management ramp instead of the training step. Both --impl
+    variants get the same warm-up."""
+    if ms <= 0:
+        return
+    a = torch.randn(2048, 2048, device=dev)
+    b = torch.randn(2048, 2048, device=dev)
+    c = torch.empty(2048, 2048, device=dev)
+    if native_gemm:
+        from tutorial_torch_distributed_data_parallel_amd._native import native
+
+        C = native()
+        run = lambda: C.gemm_f32(a, b, c, True, True)  # noqa: E731
+    else:
+        run = lambda: torch.mm(a, b.t(), out=c)  # noqa: E731
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1000.0 < ms:
+        for _ in range(16):
+            run()
+        torch.cuda.synchronize()
+    del a, b, c
 
 
 def _time_steps(step, n):
@@ -409,6 +441,8 @@ def main():
         def step():
             return run_step(*next_batch())
 
+    if use_gpu:
+        device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
     for _ in range(a.warmup):
         step()
     barrier()
@@ -466,6 +500,7 @@ def main():
                 "optimizer": a.optim + (" (fused into the gradient reduction)"
                                         if a.impl == "tdp" and fused else ""),
                 "final_loss": final_loss,
+                "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)
                               for i in range(len(ddp._bounds) - 1)]
                 if a.impl == "tdp" and a.api == "ddp" else None,
