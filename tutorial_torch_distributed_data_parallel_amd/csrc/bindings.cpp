@@ -1137,6 +1137,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout_op);
   m.def("add_relu", &add_relu_op);
   m.def("relu_mask", &relu_mask_op);
+  m.def("factor_stage", [](const Tensor& g, const Tensor& x, Tensor& g_all, Tensor& x_all,
+                          int64_t rank, double alpha) {
+    CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
+    CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+    CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
+    CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
+    const int64_t ng = g.numel(), nx = x.numel();
+    TORCH_CHECK(ng % 4 == 0 && nx % 4 == 0, "factor_stage: sizes must be multiples of 4");
+    TORCH_CHECK((rank + 1) * ng <= g_all.numel() && (rank + 1) * nx <= x_all.numel(),
+                "factor_stage: slot out of range");
+    factor_stage(g.data_ptr<float>(), x.data_ptr<float>(), g_all.data_ptr<float>() + rank * ng,
+                 x_all.data_ptr<float>() + rank * nx, ng, nx, (float)alpha, cur_stream());
+  });
   m.def("gather_batch", &gather_batch_op);
   m.def("image_transform", &image_transform_op, py::arg("x"), py::arg("flip"), py::arg("Ho"),
         py::arg("Wo"), py::arg("mean"), py::arg("std"), py::arg("round_u8") = true,
@@ -1286,6 +1299,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("epilogue_allowed", &SyncBackend::epilogue_allowed)
       .def_property_readonly("collective", &SyncBackend::collective)
       .def("owned_shard", &SyncBackend::owned_shard)
+      .def("arm_factor",
+           [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in) {
+             CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
+             CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
+             const int64_t W = b.ops()->world();
+             TORCH_CHECK(g_all.numel() == W * B * out && x_all.numel() == W * B * in,
+                         "arm_factor: buffers must hold W*B rows of out / in floats");
+             FactorJob j;
+             j.g_all = g_all.data_ptr<float>();
+             j.x_all = x_all.data_ptr<float>();
+             j.B = B; j.out = out; j.in = in;
+             b.arm_factor(bucket, j);
+           })
       .def("begin_iteration", [](SyncBackend& b, bool gpu) {
         b.begin_iteration(gpu ? cur_stream() : nullptr);
       });

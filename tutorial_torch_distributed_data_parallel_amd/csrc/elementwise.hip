@@ -301,3 +301,37 @@ void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s) {
 }
 
 }  // namespace tdp
+
+// ------------------------------------------------------------------ factored gradient staging
+// Factored synchronisation of a Linear weight (reducer.h FactorJob): this rank's factors go into
+// its slots of the all-gather buffers in one launch -- gdst = alpha * g (alpha = 1/W: the GEMM
+// over the gathered factors then yields the AVERAGED gradient) and xdst = x. Both row-contiguous,
+// element counts % 4 == 0: float4 grid-stride copies, the first ng/4 units are g's.
+namespace tdp {
+namespace {
+__global__ __launch_bounds__(256) void factor_stage_kernel(const f32x4* __restrict__ g,
+                                                           const f32x4* __restrict__ x,
+                                                           f32x4* __restrict__ gdst,
+                                                           f32x4* __restrict__ xdst, long ng4,
+                                                           long nx4, float alpha) {
+  const long total = ng4 + nx4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += 256L * gridDim.x) {
+    if (i < ng4) gdst[i] = g[i] * alpha;
+    else xdst[i - ng4] = x[i - ng4];
+  }
+}
+}  // namespace
+
+void factor_stage(const float* g, const float* x, float* gdst, float* xdst, long ng, long nx,
+                  float alpha, hipStream_t s) {
+  const long units = (ng + nx) / 4;
+  long grid = (units + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(factor_stage_kernel, dim3((unsigned)grid), dim3(256), 0, s,
+                     reinterpret_cast<const f32x4*>(g), reinterpret_cast<const f32x4*>(x),
+                     reinterpret_cast<f32x4*>(gdst), reinterpret_cast<f32x4*>(xdst), ng / 4,
+                     nx / 4, alpha);
+}
+
+}  // namespace tdp

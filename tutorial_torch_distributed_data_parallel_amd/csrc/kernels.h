@@ -237,6 +237,9 @@ void copy4d(const float* src, float* dst, const Copy4D& c, hipStream_t s);
 void gather_batch(const float* x, const int64_t* y, const int64_t* idx, long n, long F, int B,
                   float* xb, int64_t* yb, hipStream_t s);
 void f32_to_bf16_copy(const float* x, uint16_t* y, long n, hipStream_t s);
+// gdst[0:ng) = alpha * g, xdst[0:nx) = x (ng, nx % 4 == 0, 16-B aligned): one launch
+void factor_stage(const float* g, const float* x, float* gdst, float* xdst, long ng, long nx,
+                  float alpha, hipStream_t s);
 // uint8 [B][Hs][Ws][C] -> bilinear resize to Ho x Wo (align_corners=False), optional per-sample
 // horizontal flip (flip[b] != 0), optional PIL-style rounding, /255, (v - mean) / std; output
 // channels_last [B][Ho][Wo][C] or NCHW. C in {1, 3, 4}.

@@ -23,6 +23,7 @@ RcclOps::RcclOps(std::shared_ptr<Communicator> comm, float* grad, float* param, 
 
 RcclOps::~RcclOps() {
   if (wire_) (void)hipFree(wire_);
+  if (factor_ws_) (void)hipFree(factor_ws_);
 }
 
 void RcclOps::all_reduce_avg(int64_t off, int64_t n, hipStream_t s) {
@@ -124,12 +125,78 @@ void RcclOps::scale_grads(int b, const Ranges& r, hipStream_t s) {
   for_range_sets(r, [&](const RangeSet& rs) { scale_ranges_by(grad_, rs, blk, s); });
 }
 
+void SyncOps::factor_sync(int64_t, int64_t, int64_t, const FactorJob&, hipStream_t) {
+  throw std::runtime_error("factored gradient synchronisation needs the device backend");
+}
+
+void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+                          hipStream_t s) {
+  const int W = comm_->world(), r = comm_->rank();
+  if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
+  if (!skip_collectives) {
+    // in place: this rank's factor rows already sit at slot r (written on the compute stream)
+    comm_->all_gather(j.g_all + (int64_t)r * j.B * j.out, j.g_all, (size_t)j.B * j.out,
+                      ncclFloat32, s);
+    comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in, ncclFloat32,
+                      s);
+  }
+  // this rank's rows of the averaged gradient: dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all
+  const int64_t m0 = (own - begin) / j.in;
+  GemmF32Args a;
+  a.A = j.g_all + m0;  // stored [K = W*B][out]: MN-contiguous A, column offset m0
+  a.lda = j.out;
+  a.a_kcontig = false;
+  a.B = j.x_all;       // stored [K][in]
+  a.ldb = j.in;
+  a.b_kcontig = false;
+  a.C = grad_ + own;
+  a.ldc = j.in;
+  a.M = (int)(cnt / j.in);
+  a.N = j.in;
+  a.K = W * j.B;
+  if (cus_ == 0) {
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    check_hip(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev),
+              "hipDeviceGetAttribute");
+  }
+  const int cus = cus_;
+  GemmF32Args probe = a;
+  probe.opt.kind = 1;
+  const GemmPlan pp = gemm_f32_plan(probe, cus);
+  const bool epi = fused.kind != 0 && pp.fast && !pp.skinny && pp.splits == 1;
+  if (epi) {
+    // the epilogue updates p / state at C's element index: the arena offset `own`
+    a.opt.kind = fused.kind;
+    a.opt.p = fused.p + own;
+    a.opt.s0 = fused.s0 ? fused.s0 + own : nullptr;
+    a.opt.s1 = fused.s1 ? fused.s1 + own : nullptr;
+    a.opt.s2 = fused.s2 ? fused.s2 + own : nullptr;
+    a.opt.sgd = fused.sgd;
+    a.opt.adam = fused.adam;
+  }
+  const GemmPlan plan = gemm_f32_plan(a, cus);
+  if (plan.ws_floats > factor_ws_floats_) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+    if (cap != hipStreamCaptureStatusNone)
+      throw std::runtime_error("factor_sync: split-K workspace must be sized by an eager step");
+    if (factor_ws_) check_hip(hipFree(factor_ws_), "hipFree");
+    check_hip(hipMalloc(&factor_ws_, sizeof(float) * (size_t)plan.ws_floats), "hipMalloc(ws)");
+    factor_ws_floats_ = plan.ws_floats;
+  }
+  gemm_f32_run(a, plan, factor_ws_, s);
+  if (!epi) opt_update({{own, own + cnt}}, s);
+  all_gather_params(begin, cnt, s);
+}
+
 // ------------------------------------------------------------------------------------------------
 // SyncBackend: the bucket algorithm
 // ------------------------------------------------------------------------------------------------
 SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_buckets,
                          bool timing, bool skip_single_rank)
     : ops_(std::move(ops)), numel_(numel), timing_(timing), skip_single_rank_(skip_single_rank) {
+  factor_.resize(num_buckets);
   if (ops_->on_device()) {
     ready_.resize(num_buckets);
     for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
@@ -183,7 +250,14 @@ Range SyncBackend::owned_shard(int64_t begin, int64_t end) const {
   return {begin + (int64_t)r * cnt, begin + (int64_t)(r + 1) * cnt};
 }
 
+void SyncBackend::arm_factor(int bucket, const FactorJob& j) {
+  if (bucket < 0 || bucket >= (int)factor_.size()) throw std::runtime_error("arm_factor: bucket");
+  if (j.B <= 0 || !j.g_all || !j.x_all) throw std::runtime_error("arm_factor: empty job");
+  factor_[bucket] = j;
+}
+
 void SyncBackend::begin_iteration(hipStream_t compute) {
+  for (auto& f : factor_) f.B = 0;
   epi_done_.clear();
   pending_.clear();
   deferred_.clear();
@@ -296,6 +370,19 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
       deferred_.push_back({begin, end});
       launched_any_ = true;
     }
+    return;
+  }
+  if (bucket < (int)factor_.size() && factor_[bucket].B > 0) {
+    const FactorJob j = factor_[bucket];
+    factor_[bucket].B = 0;
+    const Range own = owned_shard(begin, end);
+    const int64_t cnt = own.second - own.first;
+    if (fused_kind == 0 || clip != ClipMode::NONE || compressed ||
+        cnt * ops_->world() != end - begin || (int64_t)j.out * j.in != end - begin)
+      throw std::runtime_error("factored bucket: needs the fused optimizer, no clipping / "
+                               "compression, and one whole-row-sharded weight per bucket");
+    hipStream_t cs = pick_stream(bucket, compute);
+    ops_->factor_sync(begin, own.first, cnt, j, cs);
     return;
   }
   hipStream_t cs = pick_stream(bucket, compute);

@@ -66,6 +66,18 @@ enum class Compression : int { NONE = 0, BF16 = 1 };
 //           goes on the wire, so one rank's exploding gradient cannot dominate the average.
 enum class ClipMode : int { NONE = 0, GLOBAL = 1, LOCAL = 2 };
 
+// Factored synchronisation of one Linear weight W[out][in] (its own bucket, sharded by rows):
+// the averaged gradient (1/W) sum_r g_r^T x_r has rank <= W*B, so instead of reduce-scattering the
+// out*in gradient every rank all-gathers the factors -- g_r [B][out] (already scaled by 1/W) and
+// x_r [B][in], which the compute stream wrote into this rank's slots of g_all / x_all -- and
+// computes ITS row shard of the averaged gradient with one GEMM of depth W*B, whose epilogue
+// applies the fused optimizer; the updated rows are then all-gathered as in the sharded update.
+struct FactorJob {
+  float* g_all = nullptr;  // [W*B][out], rank r's rows at r*B
+  float* x_all = nullptr;  // [W*B][in]
+  int B = 0, out = 0, in = 0;
+};
+
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
 struct SyncOps {
   virtual ~SyncOps() = default;
@@ -91,6 +103,9 @@ struct SyncOps {
   virtual void scale_grads(int block, const Ranges& r, hipStream_t s) = 0; // g[r] *= coef
   // collective watchdog: the work enqueued on `s` so far must finish within the timeout
   virtual void watch(hipStream_t s, const char* what) { (void)s; (void)what; }
+  // factored weight bucket [begin, begin + W*cnt): this rank owns [own, own + cnt) (FactorJob)
+  virtual void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+                           hipStream_t s);
 };
 
 // Device implementation: RCCL communicator + gfx950 kernels over the device arenas.
@@ -126,6 +141,8 @@ class RcclOps : public SyncOps {
   void clip_coef(int block, hipStream_t s) override;
   void scale_grads(int block, const Ranges& r, hipStream_t s) override;
   void watch(hipStream_t s, const char* what) override { comm_->watch(s, what); }
+  void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+                   hipStream_t s) override;
 
   FusedOptimizer fused;
   float* clip_block = nullptr;  // DDP-owned hyper block for LOCAL clipping
@@ -142,6 +159,9 @@ class RcclOps : public SyncOps {
   int64_t numel_;
   Compression compression_;
   uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
+  float* factor_ws_ = nullptr;  // split-K workspace of factored shard GEMMs (grown eagerly)
+  int64_t factor_ws_floats_ = 0;
+  int cus_ = 0;
 };
 
 // The bucket algorithm (one instance per DDP model).
@@ -170,6 +190,9 @@ class SyncBackend : public ReducerBackend {
 
   // the shard of bucket [begin, end) this rank owns under the sharded update (tail excluded)
   Range owned_shard(int64_t begin, int64_t end) const;
+  // Arm bucket `bucket` (exactly one Linear weight) for factored synchronisation in this
+  // iteration: its launch runs ops.factor_sync instead of reduce-scatter / update / all-gather.
+  void arm_factor(int bucket, const FactorJob& j);
   std::shared_ptr<SyncOps> ops() const { return ops_; }
   bool collective() const { return !(skip_single_rank_ && ops_->world() == 1); }
 
@@ -191,6 +214,7 @@ class SyncBackend : public ReducerBackend {
   Ranges epi_done_;              // ranges updated by GEMM epilogues this iteration (sorted)
   std::vector<Pending> pending_; // buckets reduced but not yet updated (clipping) / not reduced
   Ranges deferred_;              // world size 1: bucket updates deferred to the end of backward
+  std::vector<FactorJob> factor_;  // per bucket, armed for this iteration when B > 0
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;

@@ -40,8 +40,11 @@ def grad_dest(p: torch.Tensor | None) -> torch.Tensor | None:
 
 
 def note_use(p: torch.Tensor | None) -> None:
-    """Forward-time use count of a DDP parameter (the optimizer epilogue needs exactly one)."""
-    ref = getattr(p, "_tdp_epi", None) if p is not None else None
+    """Forward-time use count of a DDP parameter (the optimizer epilogue and the factored
+    synchronisation need exactly one)."""
+    if p is None:
+        return
+    ref = getattr(p, "_tdp_epi", None) or getattr(p, "_tdp_factor", None)
     if ref is not None:
         ddp = ref()
         if ddp is not None:
@@ -58,6 +61,16 @@ def epilogue_target(p: torch.Tensor | None):
         return None
     ddp = ref()
     return ddp.epilogue_slot(p) if ddp is not None else None
+
+
+def factor_target(p: torch.Tensor | None):
+    """The DDP whose factored synchronisation replaces the weight-gradient GEMM of ``p`` in
+    this backward (``DistributedDataParallel.factor_slot``), else None."""
+    ref = getattr(p, "_tdp_factor", None) if p is not None else None
+    if ref is None or p.grad is not None:
+        return None
+    ddp = ref()
+    return ddp.factor_slot(p) if ddp is not None else None
 
 
 def needs(ctx, i: int) -> bool:

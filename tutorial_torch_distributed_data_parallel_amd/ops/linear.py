@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
-from ._grad import epilogue_target, grad_dest, needs, note_use
+from ._grad import epilogue_target, factor_target, grad_dest, needs, note_use
 
 
 class _LinearFn(torch.autograd.Function):
@@ -43,7 +43,8 @@ class _LinearFn(torch.autograd.Function):
         db = grad_dest(b_param) if want_db else None
         # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU)
         g = C.relu_bias_bwd(dy, y) if ctx.relu else dy
-        epi = epilogue_target(w_param) if needs(ctx, 1) else None
+        fac = factor_target(w_param) if needs(ctx, 1) else None
+        epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
@@ -53,7 +54,12 @@ class _LinearFn(torch.autograd.Function):
             dw = grad_dest(w_param)
             # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];
             # the bias gradient (sum over the batch of g) is reduced inside the same kernel
-            if epi is not None:
+            if fac is not None and fac.factor_submit(w_param, g, x2):
+                # world size > 1: the DDP bucket of W computes this rank's rows of the averaged
+                # gradient from the all-gathered factors (g, x) instead; dw stays unwritten
+                if want_db:
+                    C.relu_bias_bwd(g, None, db)
+            elif epi is not None:
                 # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
                 # from the accumulators; the gradient itself is never written to HBM
                 C.gemm_f32_opt(g, x2, dw, False, False, epi[0], epi[1], rowsum=db)

@@ -4,7 +4,9 @@
 stream and reports nccl-tests' bus bandwidth (algbw x 2(n-1)/n for all-reduce, x (n-1)/n for the
 other two), which is what the 7 point-to-point xGMI links of a rank bound. ``ddp_comm_ms`` times
 exactly the collectives one DDP step issues (the bucket plan of a model, sharded or not) with no
-compute around them: the denominator of the overlap figure bench.py reports.
+compute around them: the denominator of the overlap figure bench.py reports. Factored Linear
+weights (DDP._factor_candidates) are timed as what they send: the factor all-gathers and the
+all-gather of the updated parameters.
 Used by ``scripts/rccl_sweep.py`` and, at world size > 1, by ``bench.py`` itself (the driver's
 multi-GPU run is where the measurements come from).
 """
@@ -71,9 +73,17 @@ def ddp_comm_ms(ddp, iters: int = 10, warmup: int = 3) -> float:
     sharded = bool(ddp._fused_opt is not None and ddp._fused_shard)
     plan = []
     b = ddp._bounds
+    # factored weights (DDP._factor_candidates): factor all-gathers + the parameter all-gather
+    factored = {ddp._factor_bucket[i]: (ddp._factor_last_B[i],) + ddp._factor[i]
+                for i in ddp._factor if i in ddp._factor_last_B}
+    fbufs = {k: (torch.zeros(W * B * o, device=g.device), torch.zeros(W * B * n, device=g.device))
+             for k, (B, o, n) in factored.items()}
     for i in range(len(b) - 1):
         lo, hi = b[i], b[i + 1]
-        if sharded:
+        if i in factored:
+            B, o, n = factored[i]
+            plan.append((lo, hi, -(i + 1)))
+        elif sharded:
             s0, s1 = ddp._backend.owned_shard(lo, hi)
             cnt = s1 - s0
             plan.append((lo, hi, cnt))
@@ -82,7 +92,14 @@ def ddp_comm_ms(ddp, iters: int = 10, warmup: int = 3) -> float:
 
     def step():
         for lo, hi, cnt in plan:
-            if cnt > 0:
+            if cnt < 0:  # factored bucket
+                B, o, n = factored[-cnt - 1]
+                ga, xa = fbufs[-cnt - 1]
+                comm.all_gather(ga, ga[r * B * o: (r + 1) * B * o])
+                comm.all_gather(xa, xa[r * B * n: (r + 1) * B * n])
+                c = (hi - lo) // W
+                comm.all_gather(p[lo: lo + W * c], p[lo + r * c: lo + (r + 1) * c])
+            elif cnt > 0:
                 comm.reduce_scatter(g[lo + r * cnt: lo + (r + 1) * cnt], g[lo: lo + W * cnt],
                                     "avg")
                 if lo + W * cnt < hi:
@@ -92,5 +109,5 @@ def ddp_comm_ms(ddp, iters: int = 10, warmup: int = 3) -> float:
                 comm.all_reduce(g[lo:hi], "avg")
 
     ms = _time(step, iters, warmup)
-    del g, p
+    del g, p, fbufs
     return ms

@@ -61,7 +61,8 @@ class DistributedDataParallel(nn.Module):
                  static_graph: bool = False, first_bucket_cap_mb: float | None = None,
                  split_bucket_mb: float | None = None, grad_compression: str | None = None,
                  timing: bool = False, check_replicas_every: int | None = None,
-                 force_collective: bool = False, rebuild_buckets: bool = True):
+                 force_collective: bool = False, rebuild_buckets: bool = True,
+                 factor_sync: bool | None = None):
         super().__init__()
         if process_group is not None:
             raise NotImplementedError("sub-groups are not supported: DDP uses the world group")
@@ -116,6 +117,16 @@ class DistributedDataParallel(nn.Module):
         # issue the collectives even at world size 1 (the single-GPU rehearsal of the multi-GPU
         # schedule; TDP_FORCE_COLLECTIVE=1 does the same from the environment)
         self._force_collective = bool(force_collective)
+        # factored synchronisation of Linear weights (see _factor_candidates); None = auto: on
+        # whenever it applies (GPU, fused optimizer, no clipping / compression); TDP_FACTOR_SYNC=0
+        # turns the auto mode off
+        env_fac = os.environ.get("TDP_FACTOR_SYNC")
+        self._factor_pref = factor_sync if factor_sync is not None else \
+            (None if env_fac is None else env_fac != "0")
+        self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
+        self._factor_bucket = {}   # arena index -> its (dedicated) bucket
+        self._factor_bufs = {}     # (arena index, B) -> (g_all, x_all) all-gather buffers
+        self._factor_last_B = {}   # arena index -> per-rank batch of its last factored step
         self._epi_on = False
         self._epi_index = {}
         self._uses = {}            # id(param) -> forward uses in the current iteration
@@ -173,9 +184,20 @@ class DistributedDataParallel(nn.Module):
 
     def _plan_buckets(self):
         first, cap, split = self._caps
-        return native().Reducer.compute_bucket_bounds(
+        b = list(native().Reducer.compute_bucket_bounds(
             self.arena.offsets, self.arena.numels, self.arena.numel,
-            self.arena.data.element_size(), first, cap, split)
+            self.arena.data.element_size(), first, cap, split))
+        factor = getattr(self, "_factor", None) or {}
+        if factor:
+            # a factored weight is a bucket of its own (its launch replaces the bucket's
+            # collectives, reducer.cpp SyncBackend::launch)
+            cuts = set(b)
+            for i in factor:
+                off, n = self.arena.offsets[i], self.arena.numels[i]
+                cuts.update((off, off + n))
+            b = sorted(cuts)
+            self._factor_bucket = {i: b.index(self.arena.offsets[i]) for i in factor}
+        return b
 
     def _register_hooks(self):
         for h in self._hooks:
@@ -374,8 +396,56 @@ class DistributedDataParallel(nn.Module):
         self.push_fused_hyper(optimizer, initial=True)
         return True
 
+    def _factor_candidates(self) -> dict:
+        """Linear weights W[out][in] whose gradient synchronisation can be factored (reducer.h
+        FactorJob): (1/W) sum_r g_r^T x_r has rank <= W*B, so all-gathering the factors g_r
+        [B][out] and x_r [B][in] and computing this rank's row shard of the average with one
+        depth-W*B GEMM (fused optimizer in its epilogue) replaces the reduce-scatter of the
+        out*in gradient; the updated rows are all-gathered as in the sharded update. Needs a
+        GPU, the fused optimizer with sharding (or the one-GPU rehearsal: world size 1 with
+        collectives forced), no clipping / compression, out % 4W == 0 and whole-row shards that
+        are multiples of 64 elements (SyncBackend.owned_shard). Every rank must run the same
+        per-rank batch size (DistributedSampler guarantees it)."""
+        from ..nn.modules import Linear
+
+        W = self.world_size
+        if not self._gpu or self._fused_opt is None or self._factor_pref is False:
+            return {}
+        if self._clip_global or self._clip_local or self._compression not in (None, "none"):
+            return {}
+        rehearsal = W == 1 and (self._force_collective or
+                                os.environ.get("TDP_FORCE_COLLECTIVE", "0") == "1")
+        if not (self._fused_shard or rehearsal):
+            return {}
+        index = {id(p): i for i, p in enumerate(self.arena.params)}
+        out = {}
+        for m in self.module.modules():
+            if not isinstance(m, Linear) or m.weight.dim() != 2 or id(m.weight) not in index:
+                continue
+            o, n = m.weight.shape
+            if o % (4 * W) or n % 4 or ((o // W) * n) % 64:
+                continue
+            out[index[id(m.weight)]] = (int(o), int(n))
+        return out
+
+    def _configure_factor(self):
+        """Recompute the factored weights; re-plan the buckets (each gets its own) when the set
+        changed. Called from _configure_fused: registration, comm hook, clipping changes."""
+        cand = self._factor_candidates()
+        for i, p in enumerate(self.arena.params):
+            p._tdp_factor = weakref.ref(self) if i in cand else None
+        if cand != self._factor:
+            self._factor = cand
+            self._factor_bufs.clear()
+            self._bounds = self._plan_buckets()
+            return True
+        return False
+
     def _configure_fused(self):
         """(Re-)apply the fused-optimizer configuration to the current backend."""
+        if self._configure_factor():
+            self._build_reducer()  # new bucket bounds (calls back into _configure_fused)
+            return
         opt = self._fused_opt
         b = self._backend
         b.shard = self._fused_shard
@@ -495,6 +565,37 @@ class DistributedDataParallel(nn.Module):
         if i is None or not self.arena.numels[i]:
             return None
         return self._backend, self.arena.offsets[i]
+
+    def factor_slot(self, p):
+        """This DDP when the weight-gradient GEMM of ``p`` should be replaced by the factored
+        synchronisation in the current backward (see _factor_candidates), else None."""
+        i = self._epi_index.get(id(p))
+        if i is None or i not in self._factor or not self.require_backward_grad_sync or \
+                not self.reducer.expecting or self._uses.get(id(p), 0) != 1 or p.grad is not None:
+            return None
+        return self
+
+    def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor) -> bool:
+        """Stage this rank's factors of ``p``'s gradient (g [B][out] = dL/dy, x [B][in]) and
+        arm its bucket; False when factoring does not pay at this batch size (the caller then
+        runs the ordinary weight-gradient GEMM). Must run before ``p``'s gradient hook."""
+        i = self._epi_index[id(p)]
+        o, n = self._factor[i]
+        B = int(g.shape[0])
+        W = self.world_size
+        if g.shape != (B, o) or x.shape != (B, n) or not g.is_contiguous() or \
+                not x.is_contiguous() or 2 * W * B * (o + n) > o * n:
+            return False
+        key = (i, B)
+        bufs = self._factor_bufs.get(key)
+        if bufs is None:
+            bufs = (torch.empty(W * B * o, device=self.device),
+                    torch.empty(W * B * n, device=self.device))
+            self._factor_bufs[key] = bufs
+        native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W)
+        self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], B, o, n)
+        self._factor_last_B[i] = B
+        return True
 
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
