@@ -1300,7 +1300,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("collective", &SyncBackend::collective)
       .def("owned_shard", &SyncBackend::owned_shard)
       .def("arm_factor",
-           [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in) {
+           [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
+              int64_t bias_off, int bias_bucket) {
              CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
              CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
              const int64_t W = b.ops()->world();
@@ -1310,7 +1311,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.g_all = g_all.data_ptr<float>();
              j.x_all = x_all.data_ptr<float>();
              j.B = B; j.out = out; j.in = in;
-             b.arm_factor(bucket, j);
+             j.bias_off = bias_off;
+             b.arm_factor(bucket, j, bias_bucket);
            })
       .def("begin_iteration", [](SyncBackend& b, bool gpu) {
         b.begin_iteration(gpu ? cur_stream() : nullptr);

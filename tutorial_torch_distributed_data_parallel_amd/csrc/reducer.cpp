@@ -24,6 +24,7 @@ RcclOps::RcclOps(std::shared_ptr<Communicator> comm, float* grad, float* param, 
 RcclOps::~RcclOps() {
   if (wire_) (void)hipFree(wire_);
   if (factor_ws_) (void)hipFree(factor_ws_);
+  if (factor_part_) (void)hipFree(factor_part_);
 }
 
 void RcclOps::all_reduce_avg(int64_t off, int64_t n, hipStream_t s) {
@@ -141,6 +142,34 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
                       s);
   }
   // this rank's rows of the averaged gradient: dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all
+  if (cus_ == 0) {
+    int dev = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    check_hip(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev),
+              "hipDeviceGetAttribute");
+  }
+  const int cus = cus_;
+  auto grow = [&](float*& buf, int64_t& have, int64_t want, const char* what) {
+    if (want <= have) return;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+    if (cap != hipStreamCaptureStatusNone)
+      throw std::runtime_error(std::string("factor_sync: ") + what +
+                               " must be sized by an eager step before capture");
+    if (buf) check_hip(hipFree(buf), "hipFree");
+    check_hip(hipMalloc(&buf, sizeof(float) * (size_t)want), "hipMalloc(factor)");
+    have = want;
+  };
+  if (j.bias_off >= 0) {
+    // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
+    // every rank: identical inputs, identical results, no collective
+    const int rows = W * j.B;
+    const int sl = relu_bias_slices(rows, j.out, cus);
+    grow(factor_part_, factor_part_floats_, (int64_t)sl * j.out, "bias workspace");
+    relu_bias_bwd_ws(j.g_all, nullptr, rows, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
+                     factor_part_, sl, s);
+    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
+  }
   const int64_t m0 = (own - begin) / j.in;
   GemmF32Args a;
   a.A = j.g_all + m0;  // stored [K = W*B][out]: MN-contiguous A, column offset m0
@@ -154,13 +183,6 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   a.M = (int)(cnt / j.in);
   a.N = j.in;
   a.K = W * j.B;
-  if (cus_ == 0) {
-    int dev = 0;
-    check_hip(hipGetDevice(&dev), "hipGetDevice");
-    check_hip(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev),
-              "hipDeviceGetAttribute");
-  }
-  const int cus = cus_;
   GemmF32Args probe = a;
   probe.opt.kind = 1;
   const GemmPlan pp = gemm_f32_plan(probe, cus);
@@ -176,15 +198,7 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     a.opt.adam = fused.adam;
   }
   const GemmPlan plan = gemm_f32_plan(a, cus);
-  if (plan.ws_floats > factor_ws_floats_) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
-    if (cap != hipStreamCaptureStatusNone)
-      throw std::runtime_error("factor_sync: split-K workspace must be sized by an eager step");
-    if (factor_ws_) check_hip(hipFree(factor_ws_), "hipFree");
-    check_hip(hipMalloc(&factor_ws_, sizeof(float) * (size_t)plan.ws_floats), "hipMalloc(ws)");
-    factor_ws_floats_ = plan.ws_floats;
-  }
+  grow(factor_ws_, factor_ws_floats_, plan.ws_floats, "split-K workspace");
   gemm_f32_run(a, plan, factor_ws_, s);
   if (!epi) opt_update({{own, own + cnt}}, s);
   all_gather_params(begin, cnt, s);
@@ -197,6 +211,7 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
                          bool timing, bool skip_single_rank)
     : ops_(std::move(ops)), numel_(numel), timing_(timing), skip_single_rank_(skip_single_rank) {
   factor_.resize(num_buckets);
+  factor_skip_.assign(num_buckets, 0);
   if (ops_->on_device()) {
     ready_.resize(num_buckets);
     for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
@@ -250,14 +265,18 @@ Range SyncBackend::owned_shard(int64_t begin, int64_t end) const {
   return {begin + (int64_t)r * cnt, begin + (int64_t)(r + 1) * cnt};
 }
 
-void SyncBackend::arm_factor(int bucket, const FactorJob& j) {
-  if (bucket < 0 || bucket >= (int)factor_.size()) throw std::runtime_error("arm_factor: bucket");
+void SyncBackend::arm_factor(int bucket, const FactorJob& j, int bias_bucket) {
+  const int nb = (int)factor_.size();
+  if (bucket < 0 || bucket >= nb || bias_bucket >= nb) throw std::runtime_error("arm_factor: bucket");
   if (j.B <= 0 || !j.g_all || !j.x_all) throw std::runtime_error("arm_factor: empty job");
+  if ((j.bias_off >= 0) != (bias_bucket >= 0)) throw std::runtime_error("arm_factor: bias");
   factor_[bucket] = j;
+  if (bias_bucket >= 0) factor_skip_[bias_bucket] = 1;
 }
 
 void SyncBackend::begin_iteration(hipStream_t compute) {
   for (auto& f : factor_) f.B = 0;
+  std::fill(factor_skip_.begin(), factor_skip_.end(), 0);
   epi_done_.clear();
   pending_.clear();
   deferred_.clear();
@@ -370,6 +389,10 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
       deferred_.push_back({begin, end});
       launched_any_ = true;
     }
+    return;
+  }
+  if (bucket < (int)factor_skip_.size() && factor_skip_[bucket]) {
+    factor_skip_[bucket] = 0;  // a factored bias: its weight's job averages and updates it
     return;
   }
   if (bucket < (int)factor_.size() && factor_[bucket].B > 0) {

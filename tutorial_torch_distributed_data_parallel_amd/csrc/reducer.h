@@ -76,6 +76,10 @@ struct FactorJob {
   float* g_all = nullptr;  // [W*B][out], rank r's rows at r*B
   float* x_all = nullptr;  // [W*B][in]
   int B = 0, out = 0, in = 0;
+  // arena offset of the layer's bias (-1: none): its averaged gradient is the column sum of
+  // g_all, which every rank holds after the all-gather, so every rank updates the whole bias
+  // itself -- the bias bucket issues no collective at all
+  int64_t bias_off = -1;
 };
 
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
@@ -161,6 +165,8 @@ class RcclOps : public SyncOps {
   uint16_t* wire_ = nullptr;  // bf16 staging buffer for compressed buckets
   float* factor_ws_ = nullptr;  // split-K workspace of factored shard GEMMs (grown eagerly)
   int64_t factor_ws_floats_ = 0;
+  float* factor_part_ = nullptr;  // column-sum partials of the factored biases
+  int64_t factor_part_floats_ = 0;
   int cus_ = 0;
 };
 
@@ -192,7 +198,8 @@ class SyncBackend : public ReducerBackend {
   Range owned_shard(int64_t begin, int64_t end) const;
   // Arm bucket `bucket` (exactly one Linear weight) for factored synchronisation in this
   // iteration: its launch runs ops.factor_sync instead of reduce-scatter / update / all-gather.
-  void arm_factor(int bucket, const FactorJob& j);
+  // `bias_bucket` (>= 0): the bucket holding exactly the layer's bias, updated by the job.
+  void arm_factor(int bucket, const FactorJob& j, int bias_bucket);
   std::shared_ptr<SyncOps> ops() const { return ops_; }
   bool collective() const { return !(skip_single_rank_ && ops_->world() == 1); }
 
@@ -215,6 +222,7 @@ class SyncBackend : public ReducerBackend {
   std::vector<Pending> pending_; // buckets reduced but not yet updated (clipping) / not reduced
   Ranges deferred_;              // world size 1: bucket updates deferred to the end of backward
   std::vector<FactorJob> factor_;  // per bucket, armed for this iteration when B > 0
+  std::vector<char> factor_skip_;  // per bucket: a factored bias, handled by its weight's job
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;

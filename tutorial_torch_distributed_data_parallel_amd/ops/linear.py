@@ -56,9 +56,9 @@ class _LinearFn(torch.autograd.Function):
             # the bias gradient (sum over the batch of g) is reduced inside the same kernel
             if fac is not None and fac.factor_submit(w_param, g, x2):
                 # world size > 1: the DDP bucket of W computes this rank's rows of the averaged
-                # gradient from the all-gathered factors (g, x) instead; dw stays unwritten
-                if want_db:
-                    C.relu_bias_bwd(g, None, db)
+                # gradient from the all-gathered factors (g, x), and the averaged bias gradient
+                # from the gathered g; dw / db are handed to autograd unwritten
+                pass
             elif epi is not None:
                 # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
                 # from the accumulators; the gradient itself is never written to HBM

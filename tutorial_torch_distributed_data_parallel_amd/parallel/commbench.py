@@ -74,14 +74,17 @@ def ddp_comm_ms(ddp, iters: int = 10, warmup: int = 3) -> float:
     plan = []
     b = ddp._bounds
     # factored weights (DDP._factor_candidates): factor all-gathers + the parameter all-gather
-    factored = {ddp._factor_bucket[i]: (ddp._factor_last_B[i],) + ddp._factor[i]
+    factored = {ddp._factor_bucket[i]: (ddp._factor_last_B[i],) + ddp._factor[i][:2]
                 for i in ddp._factor if i in ddp._factor_last_B}
+    quiet = {ddp._factor_bias_bucket[i] for i in ddp._factor
+             if i in ddp._factor_last_B and i in ddp._factor_bias_bucket}
     fbufs = {k: (torch.zeros(W * B * o, device=g.device), torch.zeros(W * B * n, device=g.device))
              for k, (B, o, n) in factored.items()}
     for i in range(len(b) - 1):
         lo, hi = b[i], b[i + 1]
+        if i in quiet:  # a factored bias: averaged from the gathered factors, no collective
+            continue
         if i in factored:
-            B, o, n = factored[i]
             plan.append((lo, hi, -(i + 1)))
         elif sharded:
             s0, s1 = ddp._backend.owned_shard(lo, hi)

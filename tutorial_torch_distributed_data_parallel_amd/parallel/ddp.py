@@ -125,6 +125,7 @@ class DistributedDataParallel(nn.Module):
             (None if env_fac is None else env_fac != "0")
         self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
         self._factor_bucket = {}   # arena index -> its (dedicated) bucket
+        self._factor_bias_bucket = {}  # arena index -> the (dedicated) bucket of its bias
         self._factor_bufs = {}     # (arena index, B) -> (g_all, x_all) all-gather buffers
         self._factor_last_B = {}   # arena index -> per-rank batch of its last factored step
         self._epi_on = False
@@ -192,11 +193,14 @@ class DistributedDataParallel(nn.Module):
             # a factored weight is a bucket of its own (its launch replaces the bucket's
             # collectives, reducer.cpp SyncBackend::launch)
             cuts = set(b)
-            for i in factor:
-                off, n = self.arena.offsets[i], self.arena.numels[i]
-                cuts.update((off, off + n))
+            for i, (_, _, bi) in factor.items():
+                for j in (i,) if bi is None else (i, bi):
+                    off, n = self.arena.offsets[j], self.arena.numels[j]
+                    cuts.update((off, off + n))
             b = sorted(cuts)
             self._factor_bucket = {i: b.index(self.arena.offsets[i]) for i in factor}
+            self._factor_bias_bucket = {i: b.index(self.arena.offsets[bi])
+                                        for i, (_, _, bi) in factor.items() if bi is not None}
         return b
 
     def _register_hooks(self):
@@ -425,7 +429,9 @@ class DistributedDataParallel(nn.Module):
             o, n = m.weight.shape
             if o % (4 * W) or n % 4 or ((o // W) * n) % 64:
                 continue
-            out[index[id(m.weight)]] = (int(o), int(n))
+            bias = m.bias if m.bias is not None and id(m.bias) in index else None
+            out[index[id(m.weight)]] = (int(o), int(n), index[id(bias)] if bias is not None
+                                        else None)
         return out
 
     def _configure_factor(self):
@@ -578,9 +584,11 @@ class DistributedDataParallel(nn.Module):
     def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor) -> bool:
         """Stage this rank's factors of ``p``'s gradient (g [B][out] = dL/dy, x [B][in]) and
         arm its bucket; False when factoring does not pay at this batch size (the caller then
-        runs the ordinary weight-gradient GEMM). Must run before ``p``'s gradient hook."""
+        runs the ordinary weight-gradient GEMM). Must run before ``p``'s gradient hook. When
+        True, the layer's bias (if any) is averaged and updated by the same job: the caller
+        must not compute its gradient."""
         i = self._epi_index[id(p)]
-        o, n = self._factor[i]
+        o, n, bi = self._factor[i]
         B = int(g.shape[0])
         W = self.world_size
         if g.shape != (B, o) or x.shape != (B, n) or not g.is_contiguous() or \
@@ -593,7 +601,9 @@ class DistributedDataParallel(nn.Module):
                     torch.empty(W * B * n, device=self.device))
             self._factor_bufs[key] = bufs
         native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W)
-        self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], B, o, n)
+        self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], B, o, n,
+                                 -1 if bi is None else self.arena.offsets[bi],
+                                 self._factor_bias_bucket.get(i, -1))
         self._factor_last_B[i] = B
         return True
 
