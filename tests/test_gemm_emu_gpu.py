@@ -1,0 +1,125 @@
+"""fp32 GEMM on the bf16 matrix core (exact 3-way bf16 split, six products: csrc/gemm_f32_fast.hip
+`split3_pair` / `mfma_emu6`) against a float64 reference, side by side with the native
+v_mfma_f32_32x32x2_f32 path. The emulated path must carry fp32 accuracy: its error, measured
+against |A| @ |B| (the scale of the rounding error any fp32 summation order makes), stays within a
+small multiple of the native f32 MFMA path's error and within an absolute fp32 bound."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+U = 2.0 ** -24  # fp32 unit roundoff
+
+
+@pytest.fixture(scope="module")
+def C():
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    c = native()
+    yield c
+    c.gemm_f32_set_emu(True)
+
+
+def _run(C, A, B, a_k, b_k, emu, **kw):
+    M = A.shape[0] if a_k else A.shape[1]
+    N = B.shape[0] if b_k else B.shape[1]
+    out = torch.empty(M, N, device="cuda")
+    C.gemm_f32_set_emu(emu)
+    try:
+        C.gemm_f32(A, B, out, a_k, b_k, **kw)
+    finally:
+        C.gemm_f32_set_emu(True)
+    torch.cuda.synchronize()
+    return out
+
+
+def _scaled_err(out, A, B, a_k, b_k):
+    A2 = (A if a_k else A.t()).double()
+    B2 = (B.t() if b_k else B).double()
+    ref = A2 @ B2
+    scale = A2.abs() @ B2.abs()
+    return ((out.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+
+
+SHAPES = [(128, 4096, 9216, True, True),    # toy-MLP fc1 forward (split-K)
+          (128, 4096, 4096, True, False),   # fc2 input gradient
+          (4096, 4096, 128, False, False),  # fc2 weight gradient (FN=2 tiles)
+          (512, 384, 256, True, True),
+          (130, 66, 257, True, True),       # ragged edges, K tail (257 % 32 != 0)
+          (260, 136, 44, False, True),
+          (64, 8, 4, True, True)]
+
+
+@pytest.mark.parametrize("M,N,K,a_k,b_k", SHAPES)
+@pytest.mark.parametrize("dist", ["normal", "wide"])
+def test_emu_matches_fp64_like_native_f32(C, M, N, K, a_k, b_k, dist):
+    torch.manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn((M, K) if a_k else (K, M), device="cuda")
+    B = torch.randn((N, K) if b_k else (K, N), device="cuda")
+    if dist == "wide":  # 2^[-20, 20] magnitudes: every split term is exercised, none underflows
+        A = A * torch.exp2(torch.randint(-20, 21, A.shape, device="cuda").float())
+        B = B * torch.exp2(torch.randint(-20, 21, B.shape, device="cuda").float())
+    e_emu = _scaled_err(_run(C, A, B, a_k, b_k, True), A, B, a_k, b_k)
+    e_nat = _scaled_err(_run(C, A, B, a_k, b_k, False), A, B, a_k, b_k)
+    # fp32 summation of K products: worst case ~K*u, typical ~sqrt(K)*u; the six-term split
+    # adds <= ~3u per product. Both paths must sit inside the fp32 bound.
+    bound = (8 + 2 * K ** 0.5) * U
+    assert e_nat < bound, (e_nat, bound)
+    assert e_emu < bound, (e_emu, bound)
+    assert e_emu < 4 * e_nat + 16 * U, (e_emu, e_nat)
+
+
+def test_emu_split_is_exact_on_representable_products(C):
+    # 12-bit A (split into hi + mid) times 6-bit B: 18-bit products, 32 of them sum to <= 23
+    # bits, exact in fp32 -- the split path must reproduce them bit for bit
+    g = torch.Generator(device="cpu").manual_seed(3)
+    M = N = 64
+    K = 32
+    A = (torch.randint(-(2 ** 11), 2 ** 11, (M, K), generator=g).float() * 2.0 ** -5).cuda()
+    B = (torch.randint(-(2 ** 5), 2 ** 5, (N, K), generator=g).float() * 2.0 ** -7).cuda()
+    ref = (A.double() @ B.double().t()).float()
+    out = _run(C, A, B, True, True, True)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+def test_emu_epilogues_and_identity(C):
+    n = 64
+    A = torch.eye(n, device="cuda")
+    B = torch.randn(n, n, device="cuda")  # full-mantissa values survive the split exactly
+    out = _run(C, A, B, True, False, True)
+    torch.testing.assert_close(out, B, rtol=0, atol=0)
+    x = torch.randn(256, 320, device="cuda")
+    w = torch.randn(192, 320, device="cuda") / 18
+    b = torch.randn(192, device="cuda")
+    out = _run(C, x, w, True, True, True, bias=b, relu=True)
+    ref = torch.relu(x.double() @ w.double().t() + b.double()).float()
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("emu", [True, False])
+def test_conv_paths_under_both_products(emu):
+    # implicit-GEMM forward / input-gradient / weight-gradient kernels share the split path
+    import torch.nn.functional as F
+
+    from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    Cn = native()
+    Cn.gemm_f32_set_emu(emu)
+    try:
+        torch.manual_seed(5)
+        x = torch.randn(4, 64, 14, 14, device="cuda", requires_grad=True)
+        w = (torch.randn(128, 64, 3, 3, device="cuda") / 24).requires_grad_()
+        y = ops.conv2d(x, w, None, 1, 1)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        torch.cuda.synchronize()
+    finally:
+        Cn.gemm_f32_set_emu(True)
+    xr = x.detach().double().cpu().requires_grad_()
+    wr = w.detach().double().cpu().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 1, 1)
+    yr.backward(dy.double().cpu())
+    torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-5, atol=1e-4)

@@ -88,6 +88,62 @@ struct FastParams {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef char lds_char;  // generic pointer into the dynamic LDS array (reads infer ds_read)
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// ---- fp32 GEMM on the bf16 matrix core (EMU kernels) ----------------------------------------
+// gfx950 runs v_mfma_f32_32x32x2_f32 at 1/16 of the bf16 rate (64 vs 1024 FLOP/clk/SIMD). An
+// fp32 operand splits EXACTLY into three bf16 terms x = x0 + x1 + x2 (x0 = RNE_bf16(x),
+// x1 = RNE_bf16(x - x0), x2 = x - x0 - x1: 24 significand bits = 3 x 8, every subtraction exact),
+// so a*b = sum_ij a_i b_j with the six terms of weight >= 2^-16 kept and a1b2 + a2b1 + a2b2
+// (<= ~2^-24 |a||b|, the size of one fp32 rounding of the product) dropped. Each bf16 x bf16
+// product is exact in the fp32 accumulator, so the result carries fp32 accuracy (error bound
+// tested against fp64 next to the native f32 MFMA path: tests/test_gemm_emu_gpu.py) at 6 x 32
+// instead of 8 x 64 cycles per 32x32x16 step: a 2.67x higher matrix-core ceiling. The split
+// runs on the VALU from the SAME fp32 LDS fragments the f32 path reads (v_cvt_pk_bf16_f32 does
+// the RNE pair conversion), and overlaps the previous step's MFMAs.
+// K order: the bf16 MFMA gives lane half h the k-slots 8h..8h+7; the f32 fragment reads give
+// lane half h the k = 8q + 4h + s (s < 4) of two consecutive q -- the same permutation for A and
+// B, so the dot products are unchanged.
+__device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& h, unsigned& m,
+                                            unsigned& l) {
+  const f32x2 v = {x0, x1};
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf2));
+  const f32x2 r = v - f32x2{__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf2));
+  const f32x2 r2 = r - f32x2{__uint_as_float(mu << 16), __uint_as_float(mu & 0xffff0000u)};
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, bf2));
+}
+// 8 fp32 (two f32 k-steps of 4) -> three bf16x8 MFMA operands
+__device__ __forceinline__ void split3_x8(const float (&x0)[4], const float (&x1)[4], bf8& h,
+                                          bf8& m, bf8& l) {
+  unsigned hs[4], ms[4], ls[4];
+  split3_pair(x0[0], x0[1], hs[0], ms[0], ls[0]);
+  split3_pair(x0[2], x0[3], hs[1], ms[1], ls[1]);
+  split3_pair(x1[0], x1[1], hs[2], ms[2], ls[2]);
+  split3_pair(x1[2], x1[3], hs[3], ms[3], ls[3]);
+  const u32x4 hv = {hs[0], hs[1], hs[2], hs[3]};
+  const u32x4 mv = {ms[0], ms[1], ms[2], ms[3]};
+  const u32x4 lv = {ls[0], ls[1], ls[2], ls[3]};
+  h = __builtin_bit_cast(bf8, hv);
+  m = __builtin_bit_cast(bf8, mv);
+  l = __builtin_bit_cast(bf8, lv);
+}
+// acc += a*b over the six kept split terms (smallest first)
+__device__ __forceinline__ f32x16 mfma_emu6(const bf8& ah, const bf8& am, const bf8& al,
+                                            const bf8& bh, const bf8& bm, const bf8& bl,
+                                            f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  return acc;
+}
 
 // optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
 constexpr int kOptWide = 4;  // SGD with paired columns: one batch covers both row tiles
@@ -393,7 +449,7 @@ struct SrcOf<R, kWTap, false> : WTapSrc<R> {};
 // One output tile (logical id `lid`): the workgroup body of gemm_f32_fast_kernel.
 // FM = 32-row MFMA tiles per wave (block rows BM = 64 * FM): 2, or 4 for a K-contiguous A (twice
 // the MFMAs per barrier and per B fragment read, for the long-M convolution GEMMs).
-template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM>
+template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM, bool EMU>
 __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, lds_char* smem) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   constexpr bool BKC = BKIND == kDenseK;
@@ -517,6 +573,38 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
       const int kmax = kvalid < kBK ? kvalid : kBK;
       for (int k = 0; k < kmax; ++k)
         rs += *reinterpret_cast<const float*>(st + k * (BM * 4) + threadIdx.x * 4);
+    }
+    if constexpr (EMU) {
+      // two bf16 K16 steps per K tile: q pair (2j, 2j+1) feeds one 32x32x16 step
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        read_frag(st, 2 * j, av[0], bv[0]);
+        read_frag(st, 2 * j + 1, av[1], bv[1]);
+        if (kvalid < kBK) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              if (8 * (2 * j + u) + 4 * h + s >= kvalid) {
+#pragma unroll
+                for (int f = 0; f < FM; ++f) av[u][f][s] = 0.f;
+#pragma unroll
+                for (int g = 0; g < FN; ++g) bv[u][g][s] = 0.f;
+              }
+            }
+        }
+        bf8 ah[FM], am[FM], al[FM], bh[FN], bm[FN], bl[FN];
+#pragma unroll
+        for (int f = 0; f < FM; ++f) split3_x8(av[0][f], av[1][f], ah[f], am[f], al[f]);
+#pragma unroll
+        for (int g = 0; g < FN; ++g) split3_x8(bv[0][g], bv[1][g], bh[g], bm[g], bl[g]);
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int g = 0; g < FN; ++g)
+            acc[f][g] = mfma_emu6(ah[f], am[f], al[f], bh[g], bm[g], bl[g], acc[f][g]);
+      }
+      continue;
     }
     read_frag(st, 0, av[0], bv[0]);
 #pragma unroll
@@ -970,7 +1058,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM = 2>
+template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM, bool EMU>
 __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
@@ -996,49 +1084,61 @@ __global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
       __builtin_amdgcn_s_sleep(127);
     }
     for (int lid = t0 + j; lid < t1; lid += per) {
-      gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem);
+      gemm_tile<FN, AKIND, BKIND, S, OPTK, FM, EMU>(p, lid, smem);
       __builtin_amdgcn_s_barrier();  // every wave is done with this tile's LDS stages
     }
   } else {
     const int q8 = nwg / 8, r8 = nwg % 8;
     const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-    gemm_tile<FN, AKIND, BKIND, S, OPTK, FM>(p, lid, smem);
+    gemm_tile<FN, AKIND, BKIND, S, OPTK, FM, EMU>(p, lid, smem);
   }
 }
 
-template <int FN, int AKIND, int BKIND, int S, int OPT = 0, int FM = 2>
+template <int FN, int AKIND, int BKIND, int S, int OPT, int FM, bool EMU>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
   constexpr int STG = 64 * FM * kBK * 4 + 64 * FN * kBK * 4;
   const size_t lds = (size_t)S * STG;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>,
+    (void)hipFuncSetAttribute((const void*)gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM, EMU>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM>), dim3(nblocks),
+  hipLaunchKernelGGL((gemm_f32_fast_kernel<FN, AKIND, BKIND, S, OPT, FM, EMU>), dim3(nblocks),
                      dim3(kT), lds, s, p);
 }
 
+// fp32 products on the bf16 matrix core (split3 emulation, see split3_pair) unless
+// TDP_GEMM_EMU=0 (or gemm_f32_set_emu(false)) selects the native v_mfma_f32_32x32x2_f32 path
+bool o_emu = [] {
+  const char* e = std::getenv("TDP_GEMM_EMU");
+  return !(e && e[0] == '0');
+}();
+
 // bm = 256: the FM 4 kernel (64-wide tile, 2 stages = 80 KiB of LDS, two workgroups per CU);
 // instantiated for K-contiguous A operands only
-template <int AKIND, int BKIND, int OPT = 0>
-void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s,
-                  int bm = 128) {
+template <int AKIND, int BKIND, int OPT, bool EMU>
+void launch_kinds_t(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s, int bm) {
   constexpr bool AK = AKIND != kDenseMN && AKIND != kImWgradT;
   if constexpr (AK && OPT == 0) {
     if (bm == 256) {
-      launch_fast<1, AKIND, BKIND, 2, 0, 4>(p, nblocks, s);
+      launch_fast<1, AKIND, BKIND, 2, 0, 4, EMU>(p, nblocks, s);
       return;
     }
   }
   if (fn == 1) {
-    if (stages == 3) launch_fast<1, AKIND, BKIND, 3, OPT>(p, nblocks, s);
-    else launch_fast<1, AKIND, BKIND, 2, OPT>(p, nblocks, s);
+    if (stages == 3) launch_fast<1, AKIND, BKIND, 3, OPT, 2, EMU>(p, nblocks, s);
+    else launch_fast<1, AKIND, BKIND, 2, OPT, 2, EMU>(p, nblocks, s);
   } else {
-    if (stages == 3) launch_fast<2, AKIND, BKIND, 3, OPT>(p, nblocks, s);
-    else launch_fast<2, AKIND, BKIND, 2, OPT>(p, nblocks, s);
+    if (stages == 3) launch_fast<2, AKIND, BKIND, 3, OPT, 2, EMU>(p, nblocks, s);
+    else launch_fast<2, AKIND, BKIND, 2, OPT, 2, EMU>(p, nblocks, s);
   }
+}
+template <int AKIND, int BKIND, int OPT = 0>
+void launch_kinds(const FastParams& p, int fn, int stages, int nblocks, hipStream_t s,
+                  int bm = 128) {
+  if (o_emu) launch_kinds_t<AKIND, BKIND, OPT, true>(p, fn, stages, nblocks, s, bm);
+  else launch_kinds_t<AKIND, BKIND, OPT, false>(p, fn, stages, nblocks, s, bm);
 }
 
 }  // namespace
@@ -1099,6 +1199,8 @@ void gemm_f32_set_override(int fn, int splits, int stages) {
 // Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
 static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
 static int o_bm = 0;  // 0 auto, 128 / 256 forced (sweeps)
+void gemm_f32_set_emu(bool on) { o_emu = on; }
+bool gemm_f32_emu() { return o_emu; }
 void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
 void gemm_f32_set_cvec(bool on) { o_no_cvec = !on; }
 static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int splits) {

@@ -138,6 +138,9 @@ void gemm_f32_set_mode(int mode);
 void gemm_f32_set_override(int fn, int splits, int stages);
 // row-vector (LDS-staged, 16-B) output stores of the fast GEMM on / off (measurements, tests)
 void gemm_f32_set_cvec(bool on);
+// fast GEMM products: split-bf16 emulation on the bf16 matrix core (default) or native f32 MFMA
+void gemm_f32_set_emu(bool on);
+bool gemm_f32_emu();
 // fast-GEMM block rows: 0 auto, 128 or 256 forced (measurements, tests)
 void gemm_f32_set_bm(int bm);
 // optimizer-epilogue variant (SGD flags, Adam flags, persistent grid on/off, workgroups per CU);
