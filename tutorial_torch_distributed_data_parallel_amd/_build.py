@@ -77,8 +77,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     for s in hip_srcs:
         o = BUILD / (s.stem + ".hip.o")
         if force or _needs(o, s, headers):
+            # the split-bf16 GEMM keeps its f32 residual subtractions scalar: packed f32 VALU
+            # (v_pk_add_f32) costs ~4x a v_sub_f32's issue slot beside MFMAs
+            extra = ["-fno-slp-vectorize"] if s.name == "gemm_f32_fast.hip" else []
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, "-ffp-contract=fast",
-                              "-c", str(s), "-o", str(o)])
+                              *extra, "-c", str(s), "-o", str(o)])
     for s in cpp_srcs:
         o = BUILD / (s.stem + ".cpp.o")
         if force or _needs(o, s, headers):

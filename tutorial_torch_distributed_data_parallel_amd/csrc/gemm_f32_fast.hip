@@ -28,6 +28,7 @@
 //     taps that fall into the zero padding read a 16-B zero page. With C % 32 == 0 a K tile
 //     never straddles a filter tap, so the tap decomposition is one scalar computation per tile.
 #include <cstdlib>
+#include <type_traits>
 #include <stdexcept>
 #include <unordered_map>
 #include <vector>
@@ -108,14 +109,14 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // B, so the dot products are unchanged.
 __device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& h, unsigned& m,
                                             unsigned& l) {
-  const f32x2 v = {x0, x1};
-  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf2));
-  const f32x2 r = v - f32x2{__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
-  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf2));
-  const f32x2 r2 = r - f32x2{__uint_as_float(mu << 16), __uint_as_float(mu & 0xffff0000u)};
+  // scalar f32 subtractions (built with -fno-slp-vectorize: no v_pk_add_f32)
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf2));
+  const float r0 = x0 - __uint_as_float(hu << 16), r1 = x1 - __uint_as_float(hu & 0xffff0000u);
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{r0, r1}, bf2));
+  const float s0 = r0 - __uint_as_float(mu << 16), s1 = r1 - __uint_as_float(mu & 0xffff0000u);
   h = hu;
   m = mu;
-  l = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, bf2));
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{s0, s1}, bf2));
 }
 // 8 fp32 (two f32 k-steps of 4) -> three bf16x8 MFMA operands
 __device__ __forceinline__ void split3_x8(const float (&x0)[4], const float (&x1)[4], bf8& h,
@@ -563,7 +564,10 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   // bias gradient: the workgroups of the first column tile also sum their A tiles over K
   const bool do_rs = !AK && p.rowsum != nullptr && tn == 0;
   float rs = 0.f;
-  for (int kt = 0; kt < nk; ++kt) {
+  // K loop with the tail tile peeled: only the last tile can be partial, so every other
+  // iteration is one branch-free basic block (no per-lane tail zeroing, no merge copies)
+  auto ktile = [&](const int kt, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
     wait_vmcnt<(S - 2) * G>();
     __builtin_amdgcn_s_barrier();
     issue(kt + S - 1);  // refill the stage every wave finished reading (kt - 1)
@@ -575,12 +579,66 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
         rs += *reinterpret_cast<const float*>(st + k * (BM * 4) + threadIdx.x * 4);
     }
     if constexpr (EMU) {
-      // two bf16 K16 steps per K tile: q pair (2j, 2j+1) feeds one 32x32x16 step
+      if (!TAIL || kvalid >= kBK) {
+        // Full K tile, one basic block: read all four q fragments, split step 0 (exposed), then
+        // issue step 0's MFMAs with step 1's split VALU interleaved (1 MFMA : ~6 VALU -- the
+        // VALU of an in-order wave only co-executes with MFMAs it issues in between them), then
+        // step 1's MFMAs (the co-resident wave's split runs beside them).
+        constexpr int NF = FM + FN, NB = FM * FN;
+        // register budget (two waves per SIMD: <= 256 VGPR + AGPR): step 1's fp32 fragments are
+        // read only after step 0's are split (dead)
+        float a4[4][FM][4], b4[4][FN][4];
+        bf8 xh[2][NF], xm[2][NF], xl[2][NF];  // fragment i: A tile i (< FM) or B tile i - FM
+        auto split_frag = [&](int j, int i) {
+          if (i < FM) split3_x8(a4[2 * j][i], a4[2 * j + 1][i], xh[j][i], xm[j][i], xl[j][i]);
+          else split3_x8(b4[2 * j][i - FM], b4[2 * j + 1][i - FM], xh[j][i], xm[j][i], xl[j][i]);
+        };
+        read_frag(st, 0, a4[0], b4[0]);
+        read_frag(st, 1, a4[1], b4[1]);
+#pragma unroll
+        for (int i = 0; i < NF; ++i) split_frag(0, i);
+        __builtin_amdgcn_sched_barrier(0);
+        read_frag(st, 2, a4[2], b4[2]);
+        read_frag(st, 3, a4[3], b4[3]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          const int f = c / FN, g = c % FN;
+          acc[f][g] = mfma_emu6(xh[0][f], xm[0][f], xl[0][f], xh[0][FM + g], xm[0][FM + g],
+                                xl[0][FM + g], acc[f][g]);
+#pragma unroll
+          for (int i = c; i < NF; i += NB) split_frag(1, i);
+          // 36 VALU per split fragment (4 pairs x 9), spread over the chunk's 6 MFMAs; chunk 0
+          // carries two fragments when NF > NB
+          if (c == 0 && NF > NB) {
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int g = 0; g < FN; ++g)
+            acc[f][g] = mfma_emu6(xh[1][f], xm[1][f], xl[1][f], xh[1][FM + g], xm[1][FM + g],
+                                  xl[1][FM + g], acc[f][g]);
+        return;
+      }
+      // K tail: two bf16 K16 steps, q pair (2j, 2j+1) feeds one 32x32x16 step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         read_frag(st, 2 * j, av[0], bv[0]);
         read_frag(st, 2 * j + 1, av[1], bv[1]);
-        if (kvalid < kBK) {
+        if (TAIL && kvalid < kBK) {
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -604,7 +662,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
           for (int g = 0; g < FN; ++g)
             acc[f][g] = mfma_emu6(ah[f], am[f], al[f], bh[g], bm[g], bl[g], acc[f][g]);
       }
-      continue;
+      return;
     }
     read_frag(st, 0, av[0], bv[0]);
 #pragma unroll
@@ -612,7 +670,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
       if (q < 3) read_frag(st, q + 1, av[(q + 1) & 1], bv[(q + 1) & 1]);
       float (&a)[FM][4] = av[q & 1];
       float (&bb)[FN][4] = bv[q & 1];
-      if (kvalid < kBK) {
+      if (TAIL && kvalid < kBK) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           if (8 * q + 4 * h + s >= kvalid) {
@@ -632,7 +690,9 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             acc[f][g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[f][s], bb[g][s], acc[f][g], 0, 0,
                                                              0);
     }
-  }
+  };
+  for (int kt = 0; kt < nk - 1; ++kt) ktile(kt, std::false_type{});
+  if (nk > 0) ktile(nk - 1, std::true_type{});
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
   if (do_rs && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
     float* d = p.rowsum + m0 + threadIdx.x;
@@ -1059,7 +1119,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 }
 
 template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM, bool EMU>
-__global__ __launch_bounds__(kT) void gemm_f32_fast_kernel(FastParams p) {
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_f32_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
   // XCD-aware tile order (bijective): hardware ids b and b+8 share an XCD; each XCD gets a
