@@ -132,6 +132,18 @@ MODEL_DESC = {
 }
 
 
+def _gemm_products(impl: str, use_gpu: bool):
+    """How the fp32 GEMMs form their products (tdp fast GEMM: csrc/gemm_f32_fast.hip)."""
+    if impl != "tdp" or not use_gpu:
+        return None
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    if native().gemm_f32_emu():
+        return ("fp32 operands split exactly into 3 bf16 terms (RNE), 6 bf16 MFMA products with "
+                "fp32 accumulation: error within the native f32 bound (tests/test_gemm_emu_gpu.py)")
+    return "native v_mfma_f32_32x32x2_f32"
+
+
 def device_warmup(dev, ms: float, native_gemm: bool):
     """Bring the GPU to its steady-state clock before the W warm-up steps: ``ms`` of dummy
     2048^3 GEMMs (no model state is touched). Measured on MI355X (scripts/step_timeline.py,
@@ -504,6 +516,7 @@ def main():
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)
                               for i in range(len(ddp._bounds) - 1)]
                 if a.impl == "tdp" and a.api == "ddp" else None,
+                "gemm_products": _gemm_products(a.impl, use_gpu),
             },
         }
         if diag is not None:
