@@ -1271,7 +1271,11 @@ static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int spl
 }
 
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
-  int fn = (a.M >= 512 && a.N >= 512) ? 2 : 1;
+  // 128-wide tiles split the fewest fragments per MFMA; with split-bf16 products (VALU-heavy
+  // per fragment) they win on the skinny-M GEMMs too (toy-MLP fc1 forward 84.5 -> 68.4 us,
+  // fc2 forward 40.7 -> 38.4, fc2 input gradient 45.0 -> 39.6: profiles/micro/gemm_plan_sweep_emu_r4f.log)
+  static const bool skinny_fn1 = std::getenv("TDP_GEMM_SKINNY_FN1") != nullptr;  // A/B
+  int fn = (a.N >= 512 && (a.M >= 512 || (o_emu && !skinny_fn1))) ? 2 : 1;
   if (o_fn == 1 || o_fn == 2) fn = o_fn;
   const int bn = 64 * fn;
   const long tiles = (long)ceil_div(a.M, 128) * ceil_div(a.N, bn);
