@@ -137,3 +137,28 @@ def test_factored_skips_when_not_profitable(pg):
     assert not d1._factor_last_B
     for a, b in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_replicated_factored_update_matches_sharded(pg, opt_name):
+    """FactorJob.replicate: every rank computes all rows of the averaged gradient and updates
+    them itself (no parameter all-gather). Rehearsed at world size 1 (where the shard is the
+    whole weight) it must train bit-for-bit like the sharded job; the auto policy picks it for
+    W*B <= 768 only."""
+    tdp = pg
+    m1, d1, o1 = _build(tdp, opt_name, True, seed=21)
+    m2, d2, o2 = _build(tdp, opt_name, True, seed=21)
+    d1.factor_replicate, d2.factor_replicate = True, False
+    for _ in range(4):
+        x = torch.randn(64, DIMS[0], device="cuda")
+        y = torch.randint(0, 10, (64,), device="cuda")
+        for d, o in ((d1, o1), (d2, o2)):
+            o.zero_grad(set_to_none=True)
+            tdp.ops.cross_entropy(d(x), y).backward()
+            o.step()
+    torch.cuda.synchronize()
+    assert set(d1._factor_last_B.values()) == {64}
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, atol=0, rtol=0)
+    assert d1._replicate_pays(2, 128) and d1._replicate_pays(4, 128)
+    assert not d1._replicate_pays(8, 128) and not d1._replicate_pays(1, 128)

@@ -1303,7 +1303,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("owned_shard", &SyncBackend::owned_shard)
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
-              int64_t bias_off, int bias_bucket) {
+              int64_t bias_off, int bias_bucket, bool replicate) {
              CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
              CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
              const int64_t W = b.ops()->world();
@@ -1314,8 +1314,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.x_all = x_all.data_ptr<float>();
              j.B = B; j.out = out; j.in = in;
              j.bias_off = bias_off;
+             j.replicate = replicate;
              b.arm_factor(bucket, j, bias_bucket);
-           })
+           },
+           py::arg("bucket"), py::arg("g_all"), py::arg("x_all"), py::arg("B"), py::arg("out"),
+           py::arg("in"), py::arg("bias_off"), py::arg("bias_bucket"),
+           py::arg("replicate") = false)
       .def("begin_iteration", [](SyncBackend& b, bool gpu) {
         b.begin_iteration(gpu ? cur_stream() : nullptr);
       });

@@ -201,7 +201,7 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   grow(factor_ws_, factor_ws_floats_, plan.ws_floats, "split-K workspace");
   gemm_f32_run(a, plan, factor_ws_, s);
   if (!epi) opt_update({{own, own + cnt}}, s);
-  all_gather_params(begin, cnt, s);
+  if (!j.replicate) all_gather_params(begin, cnt, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -398,10 +398,12 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   if (bucket < (int)factor_.size() && factor_[bucket].B > 0) {
     const FactorJob j = factor_[bucket];
     factor_[bucket].B = 0;
-    const Range own = owned_shard(begin, end);
+    // replicated jobs own the whole weight; sharded ones this rank's 1/W of its rows
+    const Range own = j.replicate ? Range{begin, end} : owned_shard(begin, end);
     const int64_t cnt = own.second - own.first;
     if (fused_kind == 0 || clip != ClipMode::NONE || compressed ||
-        cnt * ops_->world() != end - begin || (int64_t)j.out * j.in != end - begin)
+        (!j.replicate && cnt * ops_->world() != end - begin) ||
+        (int64_t)j.out * j.in != end - begin)
       throw std::runtime_error("factored bucket: needs the fused optimizer, no clipping / "
                                "compression, and one whole-row-sharded weight per bucket");
     hipStream_t cs = pick_stream(bucket, compute);

@@ -80,6 +80,11 @@ struct FactorJob {
   // g_all, which every rank holds after the all-gather, so every rank updates the whole bias
   // itself -- the bias bucket issues no collective at all
   int64_t bias_off = -1;
+  // replicated: every rank computes ALL rows of the averaged gradient (GEMM depth W*B over the
+  // whole weight) and updates them itself -- identical inputs and kernel, identical parameters --
+  // so no parameter all-gather follows. Chosen when W*B is small enough that the extra GEMM rows
+  // cost less than the out*in*(W-1)/W all-gather on xGMI (parallel/ddp.py factor_replicate).
+  bool replicate = false;
 };
 
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.

@@ -123,6 +123,10 @@ class DistributedDataParallel(nn.Module):
         env_fac = os.environ.get("TDP_FACTOR_SYNC")
         self._factor_pref = factor_sync if factor_sync is not None else \
             (None if env_fac is None else env_fac != "0")
+        # replicated factored update (reducer.h FactorJob.replicate): None = auto (_replicate_pays),
+        # TDP_FACTOR_REPLICATE=0/1 forces it off / on
+        env_rep = os.environ.get("TDP_FACTOR_REPLICATE")
+        self.factor_replicate = None if env_rep in (None, "", "auto") else env_rep != "0"
         self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
         self._factor_bucket = {}   # arena index -> its (dedicated) bucket
         self._factor_bias_bucket = {}  # arena index -> the (dedicated) bucket of its bias
@@ -601,11 +605,24 @@ class DistributedDataParallel(nn.Module):
                     torch.empty(W * B * n, device=self.device))
             self._factor_bufs[key] = bufs
         native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W)
+        rep = self._replicate_pays(W, B) if self.factor_replicate is None else \
+            self.factor_replicate
         self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], B, o, n,
                                  -1 if bi is None else self.arena.offsets[bi],
-                                 self._factor_bias_bucket.get(i, -1))
+                                 self._factor_bias_bucket.get(i, -1), replicate=bool(rep))
         self._factor_last_B[i] = B
         return True
+
+    # Price model of the replicated factored update (per weight element, per rank): the extra GEMM
+    # rows cost 2*W*B*(1 - 1/W) FLOP at ~150 TF/s (split-bf16 fp32 GEMM, profiles/micro) plus
+    # (1 - 1/W) * 16 B of optimizer-state HBM traffic at ~5 TB/s; the all-gather they replace moves
+    # 4 * (W - 1)/W B per element at an assumed ~300 GB/s ring bus bandwidth on 7 xGMI links.
+    # Replication pays while W*B*2/150e12 + 16/5e12 < 4/300e9, i.e. W*B below ~760: at B = 128
+    # for 2 and 4 ranks, not at 8 (scripts/rccl_sweep.py measures the bandwidth on a node).
+    _REPLICATE_MAX_WB = 768
+
+    def _replicate_pays(self, W: int, B: int) -> bool:
+        return W > 1 and W * B <= self._REPLICATE_MAX_WB
 
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
