@@ -161,7 +161,8 @@ std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus)
 
 // ----------------------------------------------------------------------------------------- loss
 std::vector<Tensor> ce_fwd_op(const Tensor& logits, const Tensor& labels, int64_t ignore_index,
-                              double smoothing, bool mean, const c10::optional<Tensor>& acc) {
+                              double smoothing, bool mean, const c10::optional<Tensor>& acc,
+                              bool with_grad) {
   CHECK_GPU(logits); CHECK_F32(logits); CHECK_ROWMAJOR(logits);
   CHECK_GPU(labels); CHECK_CONTIG(labels);
   TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
@@ -175,9 +176,18 @@ std::vector<Tensor> ce_fwd_op(const Tensor& logits, const Tensor& labels, int64_
     TORCH_CHECK(acc->numel() >= 3, "acc needs 3 floats");
     accp = acc->data_ptr<float>();
   }
+  // with_grad: also the logits gradient for an upstream gradient of 1 (one launch for the
+  // training step's loss forward + backward; single workgroup, so bounded to small B*C)
+  Tensor d;
+  if (with_grad) {
+    TORCH_CHECK((int64_t)B * C <= (1 << 16), "ce_fwd with_grad: B*C too large");
+    d = at::empty({B, C}, logits.options());
+  }
   cross_entropy_fwd(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), B, C, logits.stride(0),
                     (int)ignore_index, (float)smoothing, mean, loss.data_ptr<float>(),
-                    lse.data_ptr<float>(), accp, cur_stream());
+                    lse.data_ptr<float>(), accp, cur_stream(),
+                    with_grad ? d.data_ptr<float>() : nullptr);
+  if (with_grad) return {loss, lse, d};
   return {loss, lse};
 }
 
@@ -1059,7 +1069,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_emu", &gemm_f32_emu);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
-  m.def("ce_fwd", &ce_fwd_op);
+  m.def("ce_fwd", &ce_fwd_op, py::arg("logits"), py::arg("labels"), py::arg("ignore_index"),
+        py::arg("smoothing"), py::arg("mean"), py::arg("acc"), py::arg("with_grad") = false);
   m.def("ce_bwd", &ce_bwd_op);
   m.def("count_correct", &count_correct_op);
   m.def("sgd_flat", &sgd_flat_op, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"),

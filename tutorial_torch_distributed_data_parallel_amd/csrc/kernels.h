@@ -178,7 +178,7 @@ void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf
 //   lse_out[B] (optional) saves log-sum-exp per row for the backward.
 void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, long ld,
                        int ignore_index, float label_smoothing, bool mean, float* out_loss,
-                       float* lse_out, float* acc, hipStream_t s);
+                       float* lse_out, float* acc, hipStream_t s, float* dpre = nullptr);
 // dlogits = gout[0] * d(loss)/d(logits)
 void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* lse,
                        const float* gout, int B, int C, long ld, int ignore_index,

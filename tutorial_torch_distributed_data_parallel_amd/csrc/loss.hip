@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
                                                      const int64_t* __restrict__ labels, int B,
                                                      int C, long ld, int ignore_index, float eps,
                                                      int mean, float* out_loss, float* lse,
-                                                     float* acc, int count_only) {
+                                                     float* acc, int count_only,
+                                                     float* __restrict__ dpre) {
   __shared__ float red[4];
   float ls = 0.f, cr = 0.f, vd = 0.f;
   if (C <= 32) {
@@ -101,6 +102,23 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
   ls = block_sum<256>(ls, red);
   cr = block_sum<256>(cr, red);
   vd = block_sum<256>(vd, red);
+  if (dpre) {
+    // the logits gradient for an upstream gradient of exactly 1 (the loss.backward() seed):
+    // the backward then needs no kernel (ops/loss.py). lse[r] was written by this workgroup
+    // before block_sum's barriers.
+    const float g = mean ? 1.f / vd : 1.f;
+    for (int i = threadIdx.x; i < B * C; i += 256) {
+      const int r = i / C, c = i % C;
+      const int64_t y = labels[r];
+      const bool valid = (y != ignore_index) && y >= 0 && y < C;
+      float v = 0.f;
+      if (valid) {
+        const float p = __expf(logits[(long)r * ld + c] - lse[r]);
+        v = g * (p - (c == (int)y ? (1.f - eps) : 0.f) - eps / C);
+      }
+      dpre[i] = v;
+    }
+  }
   if (threadIdx.x == 0) {
     if (!count_only) {
       if (out_loss) out_loss[0] = mean ? (vd > 0.f ? ls / vd : NAN) : ls;
@@ -137,9 +155,10 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
 
 void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, long ld,
                        int ignore_index, float label_smoothing, bool mean, float* out_loss,
-                       float* lse_out, float* acc, hipStream_t s) {
+                       float* lse_out, float* acc, hipStream_t s, float* dpre) {
   hipLaunchKernelGGL(ce_fwd_kernel, dim3(1), dim3(256), 0, s, logits, labels, B, C, ld,
-                     ignore_index, label_smoothing, mean ? 1 : 0, out_loss, lse_out, acc, 0);
+                     ignore_index, label_smoothing, mean ? 1 : 0, out_loss, lse_out, acc, 0,
+                     dpre);
 }
 
 void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* lse,
@@ -156,7 +175,7 @@ void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* 
 void count_correct(const float* logits, const int64_t* labels, int B, int C, long ld, float* acc,
                    hipStream_t s) {
   hipLaunchKernelGGL(ce_fwd_kernel, dim3(1), dim3(256), 0, s, logits, labels, B, C, ld, -100,
-                     0.f, 0, (float*)nullptr, (float*)nullptr, acc, 1);
+                     0.f, 0, (float*)nullptr, (float*)nullptr, acc, 1, (float*)nullptr);
 }
 
 }  // namespace tdp
