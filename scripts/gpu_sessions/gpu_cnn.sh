@@ -1,7 +1,7 @@
 #!/bin/bash
 # CNN iteration: conv/pool kernel numerics, then AlexNet / ResNet-50 step time tdp vs stock torch.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${B:-128}

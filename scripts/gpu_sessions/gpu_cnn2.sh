@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests/test_cnn_gpu.py -x -q > gpurun_out/pytest_cnn.log 2>&1 && \

@@ -2,7 +2,7 @@
 # Optimizer-in-GEMM-epilogue (world size 1): GPU tests, bench default (fused auto = epilogue) vs
 # the per-bucket / unfused paths, Adam, and a kernel-stats profile of the new default step.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/e8
 export TMPDIR=/tmp
 O=gpurun_out/e8

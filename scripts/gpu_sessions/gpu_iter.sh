@@ -1,7 +1,7 @@
 #!/bin/bash
 # Iteration call: GPU tests, GEMM microbench, flagship bench variants + kernel profile.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-100}

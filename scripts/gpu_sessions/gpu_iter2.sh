@@ -1,7 +1,7 @@
 #!/bin/bash
 # Iteration: CNN numerics, ResNet-50 graph/eager timing + kernel profile, MLP eager host profile.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${B:-128}

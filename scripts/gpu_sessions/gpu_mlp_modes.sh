@@ -2,7 +2,7 @@
 # Toy-MLP step time under every execution mode on one GPU (graph/eager x fused/unfused x
 # real RCCL all-reduce), plus a kernel trace of the eager rehearsal of the multi-GPU schedule.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 run() { local name=$1; shift; timeout -k 10 300 python bench.py --steps 200 --warmup 30 "$@" > gpurun_out/mode_$name.json 2> gpurun_out/mode_$name.err; }

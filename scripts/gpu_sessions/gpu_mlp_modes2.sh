@@ -1,7 +1,7 @@
 #!/bin/bash
 # Stream-hop penalty experiments for the eager multi-GPU schedule (rehearsed at world size 1).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export TDP_FORCE_COLLECTIVE=1

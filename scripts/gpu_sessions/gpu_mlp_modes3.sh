@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export TDP_FORCE_COLLECTIVE=1

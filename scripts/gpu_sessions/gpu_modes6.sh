@@ -4,7 +4,7 @@
 # optimizer, AlexNet native vs stock, and kernel traces (with timestamps, for idle-gap analysis)
 # of the default eager step and of the rehearsal.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/m6
 export TMPDIR=/tmp
 O=gpurun_out/m6

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Persistent optimizer-epilogue wgrad kernel (TDP_OPT_PERSIST) vs one-tile-per-workgroup launch.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/p10; mkdir -p $O; export TMPDIR=/tmp
 B="python bench.py --steps 300 --warmup 30"
 timeout -k 10 300 python -u -m pytest tests/test_ddp_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \

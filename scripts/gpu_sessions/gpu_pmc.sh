@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC counters for the GEMM microbenchmark (own run: --pmc with --kernel-trace only).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true

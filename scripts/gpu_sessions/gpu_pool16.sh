@@ -1,7 +1,7 @@
 #!/bin/bash
 # 4-channel max-pool kernels: tests, benches, AlexNet kernel stats.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/b16; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_cnn_gpu.py tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 120 python bench.py --steps 300 --warmup 30 > $O/mlp.json 2> $O/mlp.err && \

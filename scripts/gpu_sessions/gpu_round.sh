@@ -2,7 +2,7 @@
 # One gpurun call: GPU tests, smoke, benches (native vs stock torch), rocprof kernel stats.
 # Every GPU step has its own time limit; steps are chained so the first failure ends the call.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-100}

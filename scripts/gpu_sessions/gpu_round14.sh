@@ -2,7 +2,7 @@
 # After the wgrad planner / split-K combine changes: full GPU tests + smoke, headline bench,
 # AlexNet / ResNet-50 ours vs stock torch, kernel stats of the AlexNet step.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r14; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \

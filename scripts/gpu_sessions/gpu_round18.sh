@@ -1,7 +1,7 @@
 #!/bin/bash
 # Conv planner: 2 stages for FN=1, FN=2 fwd/dgrad when N%128==0: tests, benches, AlexNet stats, ResNet-50.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r18; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_cnn_gpu.py tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 120 python bench.py --steps 300 --warmup 30 > $O/mlp.json 2> $O/mlp.err && \

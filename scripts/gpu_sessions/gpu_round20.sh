@@ -2,7 +2,7 @@
 # SGD optimizer-epilogue variants (TDP_OPT_VARIANT: 4 = whole-tile batch, 8 = non-temporal, 12 = both):
 # numerics through the fused-optimizer tests, then headline bench + epilogue microbench per variant.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r20; mkdir -p $O; export TMPDIR=/tmp
 for v in 4 8 12; do
   TDP_OPT_VARIANT=$v timeout -k 10 200 python -u -m pytest tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_v$v.log 2>&1 || exit $?

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Host-side (Python) cost of the eager toy-MLP step: cProfile of bench.py, top functions by self time.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r21; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 180 python -m cProfile -o $O/bench.prof bench.py --steps 1000 --warmup 30 > $O/mlp.json 2> $O/mlp.err && \
 python -c "

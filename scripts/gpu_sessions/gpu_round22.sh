@@ -1,7 +1,7 @@
 #!/bin/bash
 # Eager vs hipGraph-replayed toy-MLP step at world size 1 (current kernels, SGD epilogue default).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r22; mkdir -p $O; export TMPDIR=/tmp
 for i in 1 2; do
   timeout -k 10 120 python bench.py --steps 500 --warmup 30 >> $O/eager.json 2>> $O/eager.err && \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Lean optimizer step/zero_grad wrappers: GPU tests, headline bench x2, kernel trace of the step.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r24; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 120 python bench.py --steps 500 --warmup 30 >> $O/mlp.json 2>> $O/mlp.err && \

@@ -2,7 +2,7 @@
 # Re-measure the CNN configs (AlexNet = the reference's model, ResNet-50 = BASELINE config 5) and the
 # stock torch DDP path on the same box; toy MLP + SyncBN and the Accelerate-facade configs.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r25; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 200 python bench.py --model alexnet --steps 50 --warmup 10 > $O/alex.json 2> $O/alex.err && \
 timeout -k 10 200 python bench.py --model alexnet --steps 50 --warmup 10 --impl torch > $O/alex_torch.json 2> $O/alex_torch.err && \

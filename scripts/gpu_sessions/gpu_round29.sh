@@ -2,7 +2,7 @@
 # LDS-staged SGD epilogue (TDP_OPT_VARIANT 16 / 24 = +non-temporal) vs the default (8): numerics
 # through the fused-optimizer + kernel tests, headline bench x2 each, epilogue micro-benchmark.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r29; mkdir -p $O; export TMPDIR=/tmp
 for v in 16 24; do
   TDP_OPT_VARIANT=$v timeout -k 10 200 python -u -m pytest tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_v$v.log 2>&1 || exit $?

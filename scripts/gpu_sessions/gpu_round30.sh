@@ -1,7 +1,7 @@
 #!/bin/bash
 # LDS-staged SGD epilogue as the default: full GPU suite, smoke, bench default, variants 16/24 x3, kernel stats.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r30; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \

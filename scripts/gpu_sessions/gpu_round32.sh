@@ -2,7 +2,7 @@
 # LDS-staged Adam epilogue (TDP_OPT_ADAM_VARIANT 16 / 24) vs the register epilogue (0): fused-optimizer
 # tests per variant, Adam bench x2 each.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r32; mkdir -p $O; export TMPDIR=/tmp
 for v in 16 24; do
   TDP_OPT_ADAM_VARIANT=$v timeout -k 10 200 python -u -m pytest tests/test_ddp_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_v$v.log 2>&1 || exit $?

@@ -2,7 +2,7 @@
 # 4-way unrolled non-temporal flat SGD (the world > 1 sharded update): kernel + optimizer tests, the
 # epilogue micro-benchmark's sgd_us column (flat SGD over fc1 / fc2), headline bench.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/r34; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 150 python scripts/bench_opt_epilogue.py > $O/epi.jsonl 2> $O/epi.err && \

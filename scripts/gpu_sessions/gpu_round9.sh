@@ -2,7 +2,7 @@
 # Full GPU tests + smoke, headline bench (stdout must be ONE JSON line), Accelerate-API bench,
 # stock torch, eager side-stream join variants (1-rank collective rehearsal), AlexNet per-layer.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/r9
 export TMPDIR=/tmp
 O=gpurun_out/r9

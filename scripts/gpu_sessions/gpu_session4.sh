@@ -2,7 +2,7 @@
 # Re-validate HEAD on a fresh MI355X: GPU tests, smoke, MLP + ResNet-50 benches (native vs stock
 # torch), then a 2-ranks-on-one-GPU RCCL probe (last: its failure only tells whether RCCL allows it).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \

@@ -2,7 +2,7 @@
 # Why does an eager side comm stream cost ~1 ms/step? Stream priority variants + kernel and HIP
 # runtime traces of the side-stream rehearsal (GPU idle gaps vs host-side blocking calls).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/s7
 export TMPDIR=/tmp
 O=gpurun_out/s7

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU test suite + flagship bench (graph and eager) + rehearsal of the multi-GPU comm path.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \

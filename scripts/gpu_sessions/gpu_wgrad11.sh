@@ -1,7 +1,7 @@
 #!/bin/bash
 # Weight-gradient plan sweep (AlexNet + ResNet-50 conv shapes), CNN numerics, AlexNet per-layer.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/w11; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_cnn_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 300 python scripts/sweep_wgrad.py alexnet 128 > $O/sweep_alexnet.jsonl 2> $O/sweep_alexnet.err && \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Weight-gradient planner v2 (FN=2 when it does not pad, split-K target per CU): numerics, target sweep, AlexNet per-layer + step.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 O=gpurun_out/w13; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_cnn_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 300 python scripts/sweep_wgrad.py alexnet 128 targets > $O/tg_alexnet.jsonl 2> $O/tg_alexnet.err && \
