@@ -85,6 +85,7 @@ struct FastParams {
   int cvec;  // C (or the split-K workspace) takes 16-B row stores: N % 4 == 0, aligned rows
   float* stats;  // optional [tiles_m][3][N]: per-tile column (count, mean, M2) of the stored C
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
+  int prio;         // EMU: static wave priority for every other hardware slot (A/B knob)
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -1122,6 +1123,12 @@ template <int FN, int AKIND, int BKIND, int S, int OPTK, int FM, bool EMU>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_f32_fast_kernel(FastParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = smem_raw;
+  if constexpr (EMU) {
+    // two workgroups share each SIMD and run the same VALU-split / MFMA sequence; equal priority
+    // keeps them in lockstep (both split, then both wait on the matrix pipe). A static priority
+    // for every other hardware slot lets one wave's split run beside the other's MFMAs.
+    if (p.prio && ((blockIdx.x >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
+  }
   // XCD-aware tile order (bijective): hardware ids b and b+8 share an XCD; each XCD gets a
   // contiguous range of logical tiles, ordered split-major so an XCD shares one K slice.
   const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
@@ -1170,6 +1177,12 @@ void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
 
 // fp32 products on the bf16 matrix core (split3 emulation, see split3_pair) unless
 // TDP_GEMM_EMU=0 (or gemm_f32_set_emu(false)) selects the native v_mfma_f32_32x32x2_f32 path
+// same-box A/B (profiles/micro/gemm_emu_prio_ab_r4l.txt): toy MLP 0.4069 -> 0.3975 ms/step,
+// ResNet-50 35.57 -> 35.43; the isolated GEMMs do not move. TDP_GEMM_EMU_PRIO=0 turns it off.
+static const int o_emu_prio = [] {
+  const char* e = std::getenv("TDP_GEMM_EMU_PRIO");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
 bool o_emu = [] {
   const char* e = std::getenv("TDP_GEMM_EMU");
   return !(e && e[0] == '0');
@@ -1310,6 +1323,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
 
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   FastParams p{};  // zero: every optional pointer (stats, wt, ...) unset unless assigned below
+  p.prio = o_emu_prio;
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
   p.rowsum = a.rowsum; p.rowsum_beta = a.rowsum_beta;
   p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
@@ -1534,6 +1548,7 @@ bool conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
                    float* C, const float* bias, bool relu, float beta, float* ws,
                    hipStream_t s, const WeightTaps* wtap, float* stats) {
   FastParams p{};
+  p.prio = o_emu_prio;
   if (wtap) {
     if (pl.mode != kConvDgrad) throw std::runtime_error("weight taps are for the input gradient");
     p.wt.Cout = g.Cout; p.wt.Sp = g.S;
