@@ -1271,7 +1271,10 @@ void gemm_f32_set_override(int fn, int splits, int stages) {
 }
 // Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
 static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
-static int o_bm = 0;  // 0 auto, 128 / 256 forced (sweeps)
+static int o_bm = [] {  // 0 auto, 128 / 256 forced (sweeps; TDP_GEMM_BM=256 from the environment)
+  const char* e = std::getenv("TDP_GEMM_BM");
+  return e ? ((std::atoi(e) == 256 || std::atoi(e) == 128) ? std::atoi(e) : 0) : 0;
+}();
 void gemm_f32_set_emu(bool on) { o_emu = on; }
 bool gemm_f32_emu() { return o_emu; }
 void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
