@@ -27,7 +27,8 @@ into no-ops (``compute_ms``), the share of the collective time hidden behind com
 of the multi-GPU schedule (``rehearsal_ms``: RCCL collectives kept, per-bucket fused update,
 captured step).
 
-Timing: a device clock warm-up (``--device-warmup-ms`` of dummy GEMMs, no model state touched),
+Timing: a device warm-up (``--device-warmup-ms`` of dummy GEMMs; ``--warmup-mode scratch``:
+training steps of a scratch replica of the model -- no state of the measured model touched),
 then W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
 both sides; the max over ranks is reported; rank 0 prints one JSON line. Native libraries (RCCL
 prints a version banner when a communicator is created) write to file descriptor 1, so the
@@ -81,6 +82,9 @@ def parse():
     ap.add_argument("--device-warmup-ms", type=float, default=200.0,
                     help="GPU clock warm-up (dummy GEMMs, no model state) before the W warm-up "
                          "steps; 0 = off (see device_warmup)")
+    ap.add_argument("--warmup-mode", choices=["scratch", "gemm"], default="gemm",
+                    help="device warm-up before the W warm-up steps: training steps of a scratch "
+                         "replica of the model (tdp) or dummy GEMMs")
     ap.add_argument("--no-diag", action="store_true",
                     help="skip the post-measurement diagnostics (comm / compute / rehearsal)")
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
@@ -142,6 +146,42 @@ def _gemm_products(impl: str, use_gpu: bool):
         return ("fp32 operands split exactly into 3 bf16 terms (RNE), 6 bf16 MFMA products with "
                 "fp32 accumulation: error within the native f32 bound (tests/test_gemm_emu_gpu.py)")
     return "native v_mfma_f32_32x32x2_f32"
+
+
+def scratch_warmup(a, dims, in_shape, dev):
+    """Device warm-up on a SCRATCH replica of the benchmarked model (same architecture, its own
+    random weights, optimizer and random batch; no DDP, no collectives, nothing shared with the
+    measured model): ``--device-warmup-ms`` of real training steps before the W warm-up steps.
+    Motivation (profiles/micro/bench_warmup_r4o.txt): after 200 ms of dummy GEMMs a 20-step
+    window ran at 0.401 ms/step against 0.375 for steps 20-119 (1000 ms of GEMMs: 0.398). The
+    scratch replica did not close that gap reliably in a same-box A/B (bench_warmup_r4p.txt), so
+    the dummy GEMMs stay the default."""
+    import tutorial_torch_distributed_data_parallel_amd as tdp
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
+
+    if a.device_warmup_ms <= 0:
+        return
+    g = torch.Generator(device=dev).manual_seed(7)
+    if a.model == "toy_mlp":
+        m = ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
+    else:
+        m = build_model(a.model, device=dev)
+    opt = (tdp.optim.SGD(m.parameters(), lr=0.01, momentum=0.9) if a.optim == "sgd"
+           else tdp.optim.Adam(m.parameters(), lr=1e-3))
+    x = torch.randn((a.batch,) + tuple(in_shape), device=dev, generator=g)
+    if x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (a.batch,), device=dev, generator=g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1000.0 < a.device_warmup_ms:
+        for _ in range(4):
+            opt.zero_grad(set_to_none=True)
+            tdp.ops.backward(tdp.ops.cross_entropy(m(x), y))
+            opt.step()
+        torch.cuda.synchronize()
+    del m, opt, x, y
 
 
 def device_warmup(dev, ms: float, native_gemm: bool):
@@ -454,7 +494,10 @@ def main():
             return run_step(*next_batch())
 
     if use_gpu:
-        device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
+        if a.impl == "tdp" and a.warmup_mode == "scratch":
+            scratch_warmup(a, dims, in_shape, dev)
+        else:
+            device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
     for _ in range(a.warmup):
         step()
     barrier()

@@ -454,3 +454,33 @@ def test_conv_epilogue_bn_stats(shape):
     o1 = ops.batch_norm(y, None, None, gamma, beta, training=True, relu=True)
     o2 = ops.batch_norm(y.clone(), None, None, gamma, beta, training=True, relu=True)
     torch.testing.assert_close(o1, o2, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_optimizer_on_channels_last_conv_weights_without_ddp(opt_name):
+    """The native convolutions keep their weights channels_last; the multi-tensor optimizer path
+    (no DDP arena) updates them in storage order, grads in either layout, like torch.optim."""
+    import tutorial_torch_distributed_data_parallel_amd as tdp
+
+    torch.manual_seed(0)
+    w = torch.randn(8, 4, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+    b = torch.randn(8, device="cuda")
+    p1 = [torch.nn.Parameter(w.clone(memory_format=torch.channels_last)),
+          torch.nn.Parameter(b.clone())]
+    p2 = [torch.nn.Parameter(w.clone()), torch.nn.Parameter(b.clone())]
+    o1 = (tdp.optim.SGD(p1, lr=0.1, momentum=0.9) if opt_name == "sgd"
+          else tdp.optim.Adam(p1, lr=1e-2))
+    o2 = (torch.optim.SGD(p2, lr=0.1, momentum=0.9) if opt_name == "sgd"
+          else torch.optim.Adam(p2, lr=1e-2))
+    for i in range(3):
+        gw = torch.randn(8, 4, 3, 3, device="cuda")
+        gb = torch.randn(8, device="cuda")
+        # alternate the gradient layout: channels_last and plain contiguous
+        p1[0].grad = gw.contiguous(memory_format=torch.channels_last) if i % 2 else gw.clone()
+        p1[1].grad = gb.clone()
+        p2[0].grad, p2[1].grad = gw.clone(), gb.clone()
+        o1.step()
+        o2.step()
+    assert p1[0].is_contiguous(memory_format=torch.channels_last)
+    for a, r in zip(p1, p2):
+        torch.testing.assert_close(a.detach(), r.detach(), rtol=1e-5, atol=1e-6)

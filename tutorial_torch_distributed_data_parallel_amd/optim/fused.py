@@ -83,6 +83,25 @@ def sync_all_hyper() -> None:
         opt.sync_hyper()
 
 
+
+def _dense(t: torch.Tensor) -> torch.Tensor:
+    """A 1-D view of ``t``'s memory in storage order (no copy): the elementwise optimizer kernels
+    only need p, grad and state to share one element order. Dense row-major tensors and
+    channels_last conv weights (the native convolutions' parameter layout) qualify."""
+    if t.is_contiguous():
+        return t.view(-1)
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return t.permute(0, 2, 3, 1).view(-1)
+    raise RuntimeError(f"optimizer tensor with unsupported strides {tuple(t.stride())}")
+
+
+def _grad_like(p: torch.Tensor) -> torch.Tensor:
+    """``p.grad`` flattened in ``p``'s element order (converted only if its layout differs)."""
+    g = p.grad
+    if p.is_contiguous():
+        return g.contiguous().view(-1)
+    return _dense(g.contiguous(memory_format=torch.channels_last))
+
 class _FusedBase(Optimizer):
     _state_keys: tuple = ()
     _kind = 0  # hyper-block kind: 1 SGD, 2 Adam
@@ -309,8 +328,9 @@ class SGD(_FusedBase):
             for lst, first in ((new, True), (old, False)):
                 if lst:
                     bufs = [self.state[p]["momentum_buffer"] for p in lst] if mom else []
-                    C.sgd_multi([p.data for p in lst], [p.grad.contiguous() for p in lst], bufs,
-                                *hyper[:5], hyper[5], first, g["grad_scale"])
+                    C.sgd_multi([_dense(p.data) for p in lst], [_grad_like(p) for p in lst],
+                                [_dense(b) for b in bufs], *hyper[:5], hyper[5], first,
+                                g["grad_scale"])
         return loss
 
     def _cpu_step(self, g, ps):
@@ -429,9 +449,9 @@ class Adam(_FusedBase):
                 by_step.setdefault(int(self.state[p]["step"].item()), []).append(p)
             for step, lst in by_step.items():
                 st = [self.state[p] for p in lst]
-                C.adam_multi([p.data for p in lst], [p.grad.contiguous() for p in lst],
-                             [s["exp_avg"] for s in st], [s["exp_avg_sq"] for s in st],
-                             [s["max_exp_avg_sq"] for s in st] if g["amsgrad"] else [],
+                C.adam_multi([_dense(p.data) for p in lst], [_grad_like(p) for p in lst],
+                             [_dense(s["exp_avg"]) for s in st], [_dense(s["exp_avg_sq"]) for s in st],
+                             [_dense(s["max_exp_avg_sq"]) for s in st] if g["amsgrad"] else [],
                              *args, step, g["grad_scale"])
         return loss
 
