@@ -27,8 +27,9 @@ into no-ops (``compute_ms``), the share of the collective time hidden behind com
 of the multi-GPU schedule (``rehearsal_ms``: RCCL collectives kept, per-bucket fused update,
 captured step).
 
-Timing: a device warm-up (``--device-warmup-ms`` of dummy GEMMs; ``--warmup-mode scratch``:
-training steps of a scratch replica of the model -- no state of the measured model touched),
+Timing: a device warm-up (``--device-warmup-ms`` of training steps on a scratch replica of the
+model for the toy MLP, dummy GEMMs for the CNNs; ``--warmup-mode``) that touches no state of the
+measured model,
 then W untimed warm-up steps, then exactly K steps bracketed by barrier + device sync on
 both sides; the max over ranks is reported; rank 0 prints one JSON line. Native libraries (RCCL
 prints a version banner when a communicator is created) write to file descriptor 1, so the
@@ -82,9 +83,10 @@ def parse():
     ap.add_argument("--device-warmup-ms", type=float, default=200.0,
                     help="GPU clock warm-up (dummy GEMMs, no model state) before the W warm-up "
                          "steps; 0 = off (see device_warmup)")
-    ap.add_argument("--warmup-mode", choices=["scratch", "gemm"], default="gemm",
+    ap.add_argument("--warmup-mode", choices=["auto", "scratch", "gemm"], default="auto",
                     help="device warm-up before the W warm-up steps: training steps of a scratch "
-                         "replica of the model (tdp) or dummy GEMMs")
+                         "replica of the model (tdp) or dummy GEMMs; auto = scratch for the toy "
+                         "MLP, GEMMs for the CNNs")
     ap.add_argument("--no-diag", action="store_true",
                     help="skip the post-measurement diagnostics (comm / compute / rehearsal)")
     ap.add_argument("--syncbn", action="store_true", help="toy MLP + SyncBatchNorm config")
@@ -153,9 +155,10 @@ def scratch_warmup(a, dims, in_shape, dev):
     random weights, optimizer and random batch; no DDP, no collectives, nothing shared with the
     measured model): ``--device-warmup-ms`` of real training steps before the W warm-up steps.
     Motivation (profiles/micro/bench_warmup_r4o.txt): after 200 ms of dummy GEMMs a 20-step
-    window ran at 0.401 ms/step against 0.375 for steps 20-119 (1000 ms of GEMMs: 0.398). The
-    scratch replica did not close that gap reliably in a same-box A/B (bench_warmup_r4p.txt), so
-    the dummy GEMMs stay the default."""
+    window ran at 0.401 ms/step against 0.375 for steps 20-119 (1000 ms of GEMMs: 0.398); the
+    window length, not the dataset, matters (bench_warmup_r4q.txt). With the scratch replica the
+    20-step toy-MLP window ran at 0.385-0.391 vs 0.396-0.408 (r4p round 1, r4q; r4p round 2 was a
+    noisy box); the CNNs do not move, so ``auto`` uses it for the toy MLP only."""
     import tutorial_torch_distributed_data_parallel_amd as tdp
     from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
     from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
@@ -494,7 +497,9 @@ def main():
             return run_step(*next_batch())
 
     if use_gpu:
-        if a.impl == "tdp" and a.warmup_mode == "scratch":
+        mode = a.warmup_mode if a.warmup_mode != "auto" else \
+            ("scratch" if a.model == "toy_mlp" else "gemm")
+        if a.impl == "tdp" and mode == "scratch":
             scratch_warmup(a, dims, in_shape, dev)
         else:
             device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
