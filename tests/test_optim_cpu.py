@@ -60,3 +60,36 @@ def test_profiler_sees_optimizer_step():
         opt.step()
     names = {e.name for e in prof.events()}
     assert any(n.startswith("Optimizer.step#SGD.step") for n in names), names
+
+
+def test_dense_views_follow_storage_order():
+    """The multi-tensor kernels see p, grad and state as 1-D views in the PARAMETER's storage
+    order: channels_last conv weights stay views (no copy), a gradient of the other layout is
+    converted to the parameter's order."""
+    from tutorial_torch_distributed_data_parallel_amd.optim.fused import _dense, _grad_like
+
+    w = torch.randn(4, 3, 2, 2).contiguous(memory_format=torch.channels_last)
+    w.grad = torch.randn(4, 3, 2, 2)  # plain contiguous gradient
+    v = _dense(w)
+    assert v.data_ptr() == w.data_ptr() and v.dim() == 1
+    assert torch.equal(v, w.permute(0, 2, 3, 1).reshape(-1))
+    assert torch.equal(_grad_like(w), w.grad.permute(0, 2, 3, 1).reshape(-1))
+    b = torch.randn(5)
+    b.grad = torch.randn(5)
+    assert _dense(b).data_ptr() == b.data_ptr() and torch.equal(_grad_like(b), b.grad)
+    try:
+        _dense(torch.randn(4, 6)[:, ::2])
+    except RuntimeError:
+        pass
+    else:
+        raise AssertionError("strided tensors must be rejected")
+
+
+def test_replicated_factored_update_price_model():
+    """parallel/ddp.py: the replicated factored update is chosen for W*B <= 768 only (2 and 4
+    ranks at the reference's per-rank batch of 128, never at one rank or eight)."""
+    from tutorial_torch_distributed_data_parallel_amd.parallel.ddp import DistributedDataParallel
+
+    pays = DistributedDataParallel._replicate_pays
+    assert pays(2, 128) and pays(4, 128)
+    assert not pays(1, 128) and not pays(8, 128) and pays(8, 64)

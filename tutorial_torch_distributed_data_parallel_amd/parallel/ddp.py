@@ -621,8 +621,9 @@ class DistributedDataParallel(nn.Module):
     # for 2 and 4 ranks, not at 8 (scripts/rccl_sweep.py measures the bandwidth on a node).
     _REPLICATE_MAX_WB = 768
 
-    def _replicate_pays(self, W: int, B: int) -> bool:
-        return W > 1 and W * B <= self._REPLICATE_MAX_WB
+    @classmethod
+    def _replicate_pays(cls, W: int, B: int) -> bool:
+        return W > 1 and W * B <= cls._REPLICATE_MAX_WB
 
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
