@@ -581,10 +581,13 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     }
     if constexpr (EMU) {
       if (!TAIL || kvalid >= kBK) {
-        // Full K tile, one basic block: read all four q fragments, split step 0 (exposed), then
-        // issue step 0's MFMAs with step 1's split VALU interleaved (1 MFMA : ~6 VALU -- the
-        // VALU of an in-order wave only co-executes with MFMAs it issues in between them), then
-        // step 1's MFMAs (the co-resident wave's split runs beside them).
+        // Full K tile, one basic block: split step 0 (exposed), then step 0's MFMAs with step 1's
+        // split VALU requested in between (sched_group_barrier, 1 MFMA : ~6 VALU -- an in-order
+        // wave's VALU only co-executes with MFMAs it issues in between them), then step 1's MFMAs
+        // (the co-resident wave's split runs beside them). The scheduler honours the hint only in
+        // part (ISA: most of the split still runs as blocks between MFMA runs); the measured
+        // levers were the scalar subtractions, the peeled tail and the static priority
+        // (profiles/micro/gemm_emu_pmc_r4.md, gemm_emu_prio_ab_r4l.txt).
         constexpr int NF = FM + FN, NB = FM * FN;
         // register budget (two waves per SIMD: <= 256 VGPR + AGPR): step 1's fp32 fragments are
         // read only after step 0's are split (dead)
