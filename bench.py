@@ -279,8 +279,7 @@ def main():
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_gpu = torch.cuda.is_available() and not a.cpu
-    graph = use_gpu and not a.eager and (a.graph or world > 1) and a.impl == "tdp" and \
-        a.api == "ddp"
+    graph = use_gpu and not a.eager and (a.graph or world > 1) and a.impl == "tdp"
     in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
     fused = False
 
@@ -330,11 +329,12 @@ def main():
             data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
             loader = DeviceLoader(data, a.batch, drop_last=True)
             model, opt, loader = accel.prepare(model, opt, loader)
-            if use_gpu and want_fused and world > 1:
+            ddp = model if isinstance(model, tdp.DDP) else None
+            if use_gpu and want_fused and ddp is not None:
                 fused = model.register_fused_optimizer(opt.optimizer)
             sampler = loader  # set_epoch lives on the prepared loader
 
-            def run_step(x, y):
+            def body(x, y):  # REF/multi-GPU-training-accelerate.py:45-55
                 opt.zero_grad(set_to_none=True)
                 loss = loss_fn(model(x), y)
                 accel.backward(loss)
@@ -350,6 +350,13 @@ def main():
             data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
             sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
             loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+
+            def body(x, y):  # REF/multi-GPU-training-torch.py:118-126
+                opt.zero_grad(set_to_none=True)
+                loss = loss_fn(ddp(x), y)
+                tdp.ops.backward(loss)  # loss.backward() seeded by a cached 1: no fill kernel
+                opt.step()
+                return loss
     else:
         import torch.distributed as dist
         import torch.nn as nn
@@ -432,7 +439,7 @@ def main():
             return next(it[0])
 
     build_rehearsal = None
-    if a.impl == "tdp" and a.api == "ddp":
+    if a.impl == "tdp":
         def build_rehearsal():
             """World size 1: the multi-GPU schedule on one GPU (RCCL collectives kept at world
             size 1, per-bucket fused update instead of the GEMM epilogue, captured step)."""
@@ -474,11 +481,7 @@ def main():
         def tdp_step():
             b = idx_static if graph else cur["b"]
             x, y = gather_batch(data.x, data.y, b)
-            opt.zero_grad(set_to_none=True)
-            loss = loss_fn(ddp(x), y)
-            tdp.ops.backward(loss)  # loss.backward() seeded by a cached 1: no fill kernel
-            opt.step()
-            return loss
+            return body(x, y)
 
         advance()
         run = tdp_step
@@ -492,6 +495,8 @@ def main():
             advance()
             return run()
         step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
+        if a.api == "accelerate":
+            build_rehearsal = None
     else:
         def step():
             return run_step(*next_batch())
@@ -527,6 +532,19 @@ def main():
     value = a.batch * world * a.steps / dt
     base = baseline_for(world, a.impl, a.syncbn, a.model)
     final_loss = round(float(loss.item()), 5)
+    sync = None
+    if a.impl == "tdp" and ddp is not None:
+        # self-report for the multi-GPU record: did every rank end with bit-identical
+        # parameters, did the step run as a captured graph, how was each gradient synchronised
+        from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+        try:
+            ddp.check_replicas()
+            ident = True
+        except RuntimeError:
+            ident = False
+        sync = {"replicas_identical": ident, "captured": isinstance(run, CapturedStep),
+                "backend": rt.get_backend(), "modes": ddp.sync_plan()}
 
     def record(diag):
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
@@ -563,8 +581,9 @@ def main():
                 "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)
                               for i in range(len(ddp._bounds) - 1)]
-                if a.impl == "tdp" and a.api == "ddp" else None,
+                if a.impl == "tdp" and ddp is not None else None,
                 "gemm_products": _gemm_products(a.impl, use_gpu),
+                "sync": sync,
             },
         }
         if diag is not None:
@@ -572,7 +591,7 @@ def main():
         return rec
 
     diag = None
-    if a.impl == "tdp" and a.api == "ddp" and use_gpu and not a.no_diag:
+    if a.impl == "tdp" and ddp is not None and use_gpu and not a.no_diag:
         # The measurement is final here. Diagnostics run more collectives, and a peer that
         # stalls in them must not cost the result: past the deadline every rank exits 0, and
         # rank 0 first prints the record without them.

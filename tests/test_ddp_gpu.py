@@ -219,3 +219,55 @@ def test_optimizer_epilogue_matches_bucket_update(pg, opt_name, monkeypatch):
     for m, _, _ in runs[1:]:
         for a, b in zip(ref, m.parameters()):
             torch.testing.assert_close(b, a, atol=2e-6, rtol=1e-5)
+
+
+def test_capture_right_after_first_step_with_pending_rebuild(pg):
+    """a bucket rebuild planned by iteration 0 must not be recorded into the graph
+    (every replay would restore the pre-capture buffers). CapturedStep(warmup=1) settles it
+    eagerly first: replays must keep changing the parameters, exactly like eager steps."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    class Shuffled(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = tdp.nn.Linear(64, 128, relu=True)
+            self.c = tdp.nn.Linear(128, 10)          # registered second, runs last
+            self.b = tdp.nn.Linear(128, 128, relu=True)
+
+        def forward(self, x):
+            return self.c(self.b(self.a(x)))
+
+    def build():
+        torch.manual_seed(5)
+        m = Shuffled().cuda()
+        d = tdp.DDP(m, device_ids=[0], bucket_cap_mb=100 / 2 ** 20,
+                    first_bucket_cap_mb=100 / 2 ** 20)
+        return m, d, tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+
+    x = torch.randn(32, 64, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+
+    def make(d, o):
+        def step():
+            o.zero_grad(set_to_none=True)
+            loss = tdp.ops.cross_entropy(d(x), y)
+            loss.backward()
+            o.step()
+            return loss
+        return step
+
+    m1, d1, o1 = build()
+    m2, d2, o2 = build()
+    eager = make(d1, o1)
+    eager()
+    graph = CapturedStep(make(d2, o2), warmup=1)
+    assert d2._rebuilt, "the warm-up step should have planned a rebuild, settled before capture"
+    before = [p.detach().clone() for p in m2.parameters()]
+    for _ in range(3):
+        eager()
+        graph.replay()
+    torch.cuda.synchronize()
+    assert any(not torch.equal(a, b) for a, b in zip(before, m2.parameters()))
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)

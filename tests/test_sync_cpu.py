@@ -60,3 +60,23 @@ def test_ddp_logger_runtime_stats(tmp_path):
 @pytest.mark.parametrize("fused", [True, False])
 def test_bucket_rebuild_from_ready_order(tmp_path, fused):
     run(SW.bucket_rebuild, tmp_path, n=2, fused=fused)
+
+
+@pytest.mark.parametrize("world,kind,replicate", [
+    (2, "sgd", True), (2, "adam", False), (3, "sgd", False), (3, "adam", True),
+    (4, "sgd", False), (4, "adam", True)])
+def test_factored_sync_matches_torch_ddp(tmp_path, world, kind, replicate):
+    run(SW.factored_parity, tmp_path, n=world, kind=kind, replicate=replicate)
+
+
+def test_factored_sync_refuses_foreign_gradient(tmp_path):
+    run(SW.factored_foreign_gradient, tmp_path, n=2)
+
+
+def test_capture_failure_on_one_rank_makes_all_eager(tmp_path):
+    run(SW.capture_agreement, tmp_path, n=2)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_gradient_accumulation_skips_communication(tmp_path, fused):
+    run(SW.accumulation_parity, tmp_path, n=2, fused=fused)

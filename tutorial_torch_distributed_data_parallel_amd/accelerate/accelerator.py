@@ -17,6 +17,7 @@ gating as AcceleratedOptimizer does).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -79,9 +80,23 @@ class ShardedLoader:
                                even_batches=self.even, order=order)
         return DeviceLoader(b.dataset, b.batch_size, batch_sampler=bs, device=self.acc.device)
 
+    def epoch_indices(self) -> torch.Tensor:
+        """This rank's whole epoch of sample indices as one device tensor (its batches, in
+        order): callers that gather batches themselves (bench.py's captured step)."""
+        if not isinstance(self.base, DeviceLoader):
+            raise TypeError("epoch_indices needs a DeviceLoader base")
+        return self._device_loader().epoch_indices()
+
     def __iter__(self):
+        # Accelerate's GradientState.end_of_dataloader: the last batch of an epoch always syncs
+        # gradients inside accumulate() (ACC/data_loader.py DataLoaderShard look-ahead)
+        self.acc.end_of_dataloader = False
         if isinstance(self.base, DeviceLoader):
-            yield from self._device_loader()
+            dl = self._device_loader()
+            n = len(dl)
+            for i, batch in enumerate(dl):
+                self.acc.end_of_dataloader = i == n - 1
+                yield batch
             return
         W, r = self.acc.num_processes, self.acc.process_index
         dev = self.acc.device
@@ -130,6 +145,7 @@ class Accelerator:
         self.ddp_kwargs = ddp_kwargs or {}
         self._step = 0
         self.sync_gradients = True
+        self.end_of_dataloader = False
         self._models = []
 
     # ------------------------------------------------------------------ process state
@@ -200,9 +216,35 @@ class Accelerator:
         return out[0] if len(out) == 1 else tuple(out)
 
     # ------------------------------------------------------------------ training
-    def backward(self, loss, **kwargs):
+    @contextlib.contextmanager
+    def accumulate(self, *models):
+        """Gradient accumulation (ACC/accelerator.py ``accumulate`` / ``_do_sync``): every call
+        is one micro-step; gradients are synchronised on every
+        ``gradient_accumulation_steps``-th one (and on an epoch's last batch). The other
+        micro-steps run the DDP models under ``no_sync()`` -- the reducer issues no collective
+        and gradients accumulate locally in the arena -- and the prepared optimizer's ``step`` /
+        ``zero_grad`` are skipped. With a fused optimizer registered, its in-reduction update
+        happens on the synchronising micro-step only (the accumulated gradient goes through the
+        bucket path)."""
         self._step += 1
-        self.sync_gradients = (self._step % self.gradient_accumulation_steps) == 0
+        self.sync_gradients = (self._step % self.gradient_accumulation_steps == 0 or
+                               self.end_of_dataloader)
+        with contextlib.ExitStack() as stack:
+            if not self.sync_gradients:
+                for m in models or self._models:
+                    if isinstance(m, DistributedDataParallel):
+                        stack.enter_context(m.no_sync())
+            yield
+
+    @contextlib.contextmanager
+    def no_sync(self, model):
+        with (model.no_sync() if isinstance(model, DistributedDataParallel)
+              else contextlib.nullcontext()):
+            yield
+
+    def backward(self, loss, **kwargs):
+        """``loss / gradient_accumulation_steps`` then backward (ACC/accelerator.py:2818-2850);
+        whether this backward synchronises is decided by :meth:`accumulate`."""
         if "gradient" in kwargs:
             (loss / self.gradient_accumulation_steps).backward(**kwargs)
         else:  # seeded with a cached 1/steps tensor: no fill or division kernel per step

@@ -75,6 +75,13 @@ def _optimizer(t, params):
     return optim.Adam(params, lr=t["lr"])
 
 
+def _want_fused(t, device) -> bool:
+    from .utils.config import tristate
+
+    v = tristate(t.get("fused_optimizer"))
+    return device.type == "cuda" if v is None else (v and device.type == "cuda")
+
+
 # ----------------------------------------------------------------------------- native DDP
 def basic_ddp_training_loop(rank: int, world_size: int, save_dir: str, optional_args: dict,
                             train_cfg: dict):
@@ -84,6 +91,7 @@ def basic_ddp_training_loop(rank: int, world_size: int, save_dir: str, optional_
     from .parallel import DDP, destroy_process_group, init_process_group
     from .parallel import runtime as rt
     from .train import run_training_loop
+    from .utils.config import tristate
     from .utils.seed import set_seed_based_on_rank
 
     print(f"Running DDP checkpoint example on rank {rank}.")
@@ -104,8 +112,13 @@ def basic_ddp_training_loop(rank: int, world_size: int, save_dir: str, optional_
                     bucket_cap_mb=train_cfg.get("bucket_cap_mb"))
     criterion = tnn.CrossEntropyLoss()
     optimizer = _optimizer(train_cfg, ddp_model.parameters())
+    if _want_fused(train_cfg, device):
+        # the update runs inside the gradient reduction (per bucket, sharded over ranks; in the
+        # weight-gradient GEMM epilogues at world size 1); optimizer.step() becomes a no-op
+        ddp_model.register_fused_optimizer(optimizer)
     run_training_loop(ddp_model, train_loader, train_sampler, test_loader, criterion, optimizer,
                       device, rank, save_dir, num_epochs=train_cfg["num_epochs"],
+                      capture=tristate(train_cfg.get("capture")),
                       checkpoint_epoch=train_cfg["checkpoint_epoch"],
                       set_epoch=optional_args.get("set_epoch", True),
                       print_rand=optional_args.get("print_rand", False),
@@ -125,8 +138,8 @@ def train_ddp(argv=None):
                                 s["out_dir"], optional_args, s["train"])
         return 0
     world = world_size_from(s)
-    if torch.cuda.is_available():
-        world = min(world, torch.cuda.device_count())
+    if torch.cuda.is_available() and os.environ.get("TDP_GPU_RELAY", "0") != "1":
+        world = min(world, torch.cuda.device_count())  # the relay shares one GPU among ranks
     spawn(basic_ddp_training_loop, world, args=(world, s["out_dir"], optional_args, s["train"]))
     return 0
 
@@ -138,6 +151,8 @@ def train_accelerate(argv=None):
     from .data import DeviceLoader
     from .models.registry import build_model
     from .ops import count_correct
+    from .train.graph import GraphedStep
+    from .utils.config import tristate
 
     _, s = _settings(argv, "Run script based on local_settings.yaml file.")
     t = s["train"]
@@ -151,18 +166,32 @@ def train_accelerate(argv=None):
     criterion = tnn.CrossEntropyLoss()
     optimizer = _optimizer(t, model.parameters())
     model, optimizer, train_loader = accelerator.prepare(model, optimizer, train_loader)
+    world = accelerator.num_processes
+    if world > 1 and _want_fused(t, device):
+        model.register_fused_optimizer(optimizer.optimizer)
+    run = torch.zeros(1, device=device)  # persistent: the captured step accumulates into it
+
+    def body(inputs, labels):  # the reference's step (REF/multi-GPU-training-accelerate.py:45-55)
+        optimizer.zero_grad()
+        loss = criterion(model(inputs), labels)
+        accelerator.backward(loss)
+        optimizer.step()
+        run.add_(loss.detach())
+        return loss
+
+    cap = tristate(t.get("capture"))
+    cap = (device.type == "cuda" and world > 1) if cap is None else cap
+    # a captured step replays accelerator.backward's host bookkeeping once: no accumulation
+    step = GraphedStep(body, warmup=2,
+                       capture=cap and accelerator.gradient_accumulation_steps == 1)
     for epoch in range(t["num_epochs"]):
         model.train()
-        run = torch.zeros(1, device=device)
+        run.zero_()
         nb = 0
         for i, (inputs, labels) in enumerate(train_loader):
             if t.get("max_steps_per_epoch") and i >= t["max_steps_per_epoch"]:
                 break
-            optimizer.zero_grad()
-            loss = criterion(model(inputs), labels)
-            accelerator.backward(loss)
-            optimizer.step()
-            run += loss.detach()
+            step(inputs, labels)
             nb += 1
         train_loss = (run / max(nb, 1)).item()  # per-rank mean of batch means, not reduced (R12)
         model.eval()

@@ -913,6 +913,114 @@ std::shared_ptr<Communicator> make_comm(py::bytes uid, int rank, int world, int 
   return std::make_shared<Communicator>(v, rank, world, device);
 }
 
+// Host-relay communicator: the Communicator interface with every collective carried by a Python
+// object (parallel/relay.py: device -> host copy, torch.distributed/gloo, host -> device copy).
+// RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so this is how W processes that
+// share ONE MI355X run the production device path -- RcclOps, the sharded / factored / replicated
+// updates, SyncBatchNorm, the DDP constructor broadcast -- with real rank != 0 slots, row shards
+// and cross-rank bit-identity checks (tests/test_relay_gpu.py). Each call drains the stream the
+// collective was ordered on, hands the relay tensors aliasing the device buffers, and returns
+// after the relay has written the result back and synchronised the device, so the work enqueued
+// on that stream afterwards sees it. Eager only: a collective issued while the stream is being
+// captured raises (hipGraph capture then falls back to eager on every rank, train/graph.py).
+at::ScalarType at_dtype(ncclDataType_t dt) {
+  switch (dt) {
+    case ncclFloat32: return at::kFloat;
+    case ncclFloat64: return at::kDouble;
+    case ncclFloat16: return at::kHalf;
+    case ncclBfloat16: return at::kBFloat16;
+    case ncclInt32: return at::kInt;
+    case ncclInt64: return at::kLong;
+    case ncclUint8: return at::kByte;
+    case ncclInt8: return at::kChar;
+    default: TORCH_CHECK(false, "relay: unsupported RCCL dtype");
+  }
+  return at::kFloat;
+}
+
+const char* op_name(ncclRedOp_t op) {
+  switch (op) {
+    case ncclSum: return "sum";
+    case ncclAvg: return "avg";
+    case ncclMax: return "max";
+    case ncclMin: return "min";
+    case ncclProd: return "prod";
+    default: TORCH_CHECK(false, "relay: unsupported reduce op");
+  }
+  return "sum";
+}
+
+class RelayCommunicator : public Communicator {
+ public:
+  RelayCommunicator(int rank, int world, int device, py::object relay)
+      : Communicator(rank, world, device), relay_(std::move(relay)) {}
+  ~RelayCommunicator() override {
+    py::gil_scoped_acquire g;
+    relay_ = py::object();
+  }
+  bool native_rccl() const override { return false; }
+
+  void all_reduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
+                  hipStream_t s) override {
+    drain(s, "all_reduce");
+    py::gil_scoped_acquire g;
+    relay_.attr("all_reduce")(view(send, count, dt), view(recv, count, dt), op_name(op));
+  }
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override {
+    drain(s, "broadcast");
+    py::gil_scoped_acquire g;
+    relay_.attr("broadcast")(view(buf, count, dt), root);
+  }
+  void all_gather(const void* send, void* recv, size_t send_count, ncclDataType_t dt,
+                  hipStream_t s) override {
+    drain(s, "all_gather");
+    py::gil_scoped_acquire g;
+    relay_.attr("all_gather")(view(send, send_count, dt),
+                              view(recv, send_count * (size_t)world(), dt));
+  }
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, ncclDataType_t dt,
+                      ncclRedOp_t op, hipStream_t s) override {
+    drain(s, "reduce_scatter");
+    py::gil_scoped_acquire g;
+    relay_.attr("reduce_scatter")(view(send, recv_count * (size_t)world(), dt),
+                                  view(recv, recv_count, dt), op_name(op));
+  }
+  void send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s) override {
+    drain(s, "send");
+    py::gil_scoped_acquire g;
+    relay_.attr("send")(view(buf, count, dt), peer);
+  }
+  void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s) override {
+    drain(s, "recv");
+    py::gil_scoped_acquire g;
+    relay_.attr("recv")(view(buf, count, dt), peer);
+  }
+  void group_start() override {}
+  void group_end() override {}
+  void abort() override {}
+
+ private:
+  void drain(hipStream_t s, const char* what) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+    if (cap != hipStreamCaptureStatusNone)
+      throw std::runtime_error(std::string("host-relay communicator: ") + what +
+                               " cannot be captured into a hipGraph (eager only)");
+    py::gil_scoped_release nogil;
+    check_hip(hipStreamSynchronize(s), "hipStreamSynchronize(relay)");
+  }
+  Tensor view(const void* p, size_t n, ncclDataType_t dt) const {
+    auto opts = at::TensorOptions().dtype(at_dtype(dt)).device(at::kCUDA, device());
+    return at::from_blob(const_cast<void*>(p), {(int64_t)n}, opts);
+  }
+  py::object relay_;
+};
+
+std::shared_ptr<RelayCommunicator> make_relay_comm(int rank, int world, int device,
+                                                   py::object relay) {
+  return std::make_shared<RelayCommunicator>(rank, world, device, std::move(relay));
+}
+
 // SyncOps over Python callables: torch.distributed (gloo) collectives and torch math on CPU arenas
 // (parallel/ddp.py _cpu_sync_ops). The C++ SyncBackend algorithm -- bucket order, sharding, tails,
 // clipping, deferred updates -- runs unchanged on top, so the multi-rank logic is exercised by
@@ -949,6 +1057,12 @@ struct PyOps : SyncOps {
   void clip_coef(int b, hipStream_t) override { fns.attr("clip_coef")(b); }
   void scale_grads(int b, const Ranges& r, hipStream_t) override {
     fns.attr("scale_grads")(b, pylist(r));
+  }
+  void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+                   hipStream_t) override {
+    fns.attr("factor_sync")(begin, own, cnt, j.B, j.out, j.in, j.bias_off, j.replicate,
+                            reinterpret_cast<intptr_t>(j.g_all),
+                            reinterpret_cast<intptr_t>(j.x_all));
   }
 };
 
@@ -1150,19 +1264,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout_op);
   m.def("add_relu", &add_relu_op);
   m.def("relu_mask", &relu_mask_op);
+  // this rank's factors of a factored Linear weight into slot `rank` of the all-gather buffers:
+  // g [B][out] * alpha and x [B][in]; each slot holds `slot_rows` >= B rows (the batch size the
+  // ranks agreed on) and rows B.. are zeroed, so a smaller (ragged last) batch on some rank
+  // still issues the same collectives and contributes exactly its own rows to g_all^T x_all
   m.def("factor_stage", [](const Tensor& g, const Tensor& x, Tensor& g_all, Tensor& x_all,
-                          int64_t rank, double alpha) {
+                          int64_t rank, double alpha, int64_t slot_rows) {
     CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
     CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
     CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
     CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
-    const int64_t ng = g.numel(), nx = x.numel();
-    TORCH_CHECK(ng % 4 == 0 && nx % 4 == 0, "factor_stage: sizes must be multiples of 4");
-    TORCH_CHECK((rank + 1) * ng <= g_all.numel() && (rank + 1) * nx <= x_all.numel(),
+    TORCH_CHECK(g.dim() == 2 && x.dim() == 2 && g.size(0) == x.size(0), "factor_stage: [B][*]");
+    const int64_t B = g.size(0), out = g.size(1), in = x.size(1);
+    const int64_t rows = slot_rows < 0 ? B : slot_rows;
+    TORCH_CHECK(B <= rows, "factor_stage: batch larger than the agreed slot");
+    const int64_t ng = B * out, nx = B * in, sg = rows * out, sx = rows * in;
+    TORCH_CHECK(ng % 4 == 0 && nx % 4 == 0 && sg % 4 == 0 && sx % 4 == 0,
+                "factor_stage: sizes must be multiples of 4");
+    TORCH_CHECK((rank + 1) * sg <= g_all.numel() && (rank + 1) * sx <= x_all.numel(),
                 "factor_stage: slot out of range");
-    factor_stage(g.data_ptr<float>(), x.data_ptr<float>(), g_all.data_ptr<float>() + rank * ng,
-                 x_all.data_ptr<float>() + rank * nx, ng, nx, (float)alpha, cur_stream());
-  });
+    float* gd = g_all.data_ptr<float>() + rank * sg;
+    float* xd = x_all.data_ptr<float>() + rank * sx;
+    hipStream_t s = cur_stream();
+    if (B > 0) factor_stage(g.data_ptr<float>(), x.data_ptr<float>(), gd, xd, ng, nx, (float)alpha, s);
+    if (rows > B) {
+      check_hip(hipMemsetAsync(gd + ng, 0, sizeof(float) * (size_t)(sg - ng), s), "memset(pad)");
+      check_hip(hipMemsetAsync(xd + nx, 0, sizeof(float) * (size_t)(sx - nx), s), "memset(pad)");
+    }
+  }, py::arg("g"), py::arg("x"), py::arg("g_all"), py::arg("x_all"), py::arg("rank"),
+     py::arg("alpha"), py::arg("slot_rows") = -1);
   m.def("gather_batch", &gather_batch_op);
   m.def("image_transform", &image_transform_op, py::arg("x"), py::arg("flip"), py::arg("Ho"),
         py::arg("Wo"), py::arg("mean"), py::arg("std"), py::arg("round_u8") = true,
@@ -1197,6 +1327,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world", &Communicator::world)
       .def_property_readonly("device", &Communicator::device)
+      .def_property_readonly("native_rccl", &Communicator::native_rccl)
       // collectives enqueued on the CURRENT stream (ordered with surrounding PyTorch work)
       .def("all_reduce",
            [](Communicator& c, Tensor& t, const std::string& op) {
@@ -1243,6 +1374,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::gil_scoped_release nogil;
         check_hip(hipStreamSynchronize(cur_stream()), "hipStreamSynchronize");
       });
+
+  py::class_<RelayCommunicator, Communicator, std::shared_ptr<RelayCommunicator>>(
+      m, "RelayCommunicator")
+      .def(py::init(&make_relay_comm), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("relay"));
 
   py::class_<ReducerBackend, std::shared_ptr<ReducerBackend>>(m, "ReducerBackend")
       .def("last_comm_ms", &ReducerBackend::last_comm_ms);
@@ -1315,8 +1451,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
               int64_t bias_off, int bias_bucket, bool replicate) {
-             CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
-             CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
+             // device buffers for RcclOps; host buffers for PyOps (the CPU twin looks them up by
+             // address in parallel/ddp.py _CpuSyncOps.factor_sync)
+             TORCH_CHECK(g_all.is_cuda() == b.ops()->on_device() &&
+                         x_all.is_cuda() == b.ops()->on_device(),
+                         "arm_factor: buffers must live where the sync ops run");
+             CHECK_F32(g_all); CHECK_CONTIG(g_all);
+             CHECK_F32(x_all); CHECK_CONTIG(x_all);
              const int64_t W = b.ops()->world();
              TORCH_CHECK(g_all.numel() == W * B * out && x_all.numel() == W * B * in,
                          "arm_factor: buffers must hold W*B rows of out / in floats");

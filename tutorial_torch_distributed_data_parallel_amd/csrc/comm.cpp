@@ -35,7 +35,17 @@ Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world,
     throw std::runtime_error("RCCL unique id must be " + std::to_string(sizeof(id.internal)) +
                              " bytes");
   std::memcpy(id.internal, uid.data(), sizeof(id.internal));
-  check_hip(hipSetDevice(device), "hipSetDevice");
+  make_stream();
+  check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+Communicator::Communicator(int rank, int world, int device)
+    : rank_(rank), world_(world), device_(device) {
+  make_stream();
+}
+
+void Communicator::make_stream() {
+  check_hip(hipSetDevice(device_), "hipSetDevice");
   // Highest priority for the comm stream: bucket all-reduces should not queue behind backward
   // GEMMs on the hardware queues (GPU_MAX_HW_QUEUES=4 per process on this pool).
   // TDP_COMM_PRIORITY=normal selects a default-priority stream instead (measurement knob).
@@ -47,7 +57,6 @@ Communicator::Communicator(const std::vector<uint8_t>& uid, int rank, int world,
   check_hip(hipStreamCreateWithPriority(&stream_, blocking ? hipStreamDefault : hipStreamNonBlocking,
                                         (normal || blocking) ? lo : hi),
             "hipStreamCreateWithPriority");
-  check_nccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
   // TDP_TIMEOUT_S (seconds) or TDP_TIMEOUT_MIN (minutes); torch's NCCL default is 10 minutes
   if (const char* t = std::getenv("TDP_TIMEOUT_S")) timeout_s_ = std::atof(t);
   else if (const char* m = std::getenv("TDP_TIMEOUT_MIN")) timeout_s_ = 60.0 * std::atof(m);

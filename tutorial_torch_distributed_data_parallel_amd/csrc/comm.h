@@ -28,7 +28,7 @@ class Communicator {
   // 128-byte ncclUniqueId as bytes (rank 0 creates it, the store distributes it)
   static std::vector<uint8_t> unique_id();
   Communicator(const std::vector<uint8_t>& uid, int rank, int world, int device);
-  ~Communicator();
+  virtual ~Communicator();
   Communicator(const Communicator&) = delete;
   Communicator& operator=(const Communicator&) = delete;
 
@@ -38,18 +38,18 @@ class Communicator {
   hipStream_t comm_stream() const { return stream_; }
   ncclComm_t handle() const { return comm_; }
 
-  void all_reduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
-                  hipStream_t s);
-  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s);
-  void all_gather(const void* send, void* recv, size_t send_count, ncclDataType_t dt,
-                  hipStream_t s);
-  void reduce_scatter(const void* send, void* recv, size_t recv_count, ncclDataType_t dt,
-                      ncclRedOp_t op, hipStream_t s);
-  void send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s);
-  void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s);
-  void group_start();
-  void group_end();
-  void abort();
+  virtual void all_reduce(const void* send, void* recv, size_t count, ncclDataType_t dt,
+                          ncclRedOp_t op, hipStream_t s);
+  virtual void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s);
+  virtual void all_gather(const void* send, void* recv, size_t send_count, ncclDataType_t dt,
+                          hipStream_t s);
+  virtual void reduce_scatter(const void* send, void* recv, size_t recv_count,
+                              ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
+  virtual void send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s);
+  virtual void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t s);
+  virtual void group_start();
+  virtual void group_end();
+  virtual void abort();
 
   // Collective watchdog (torch's ProcessGroupNCCL watchdog, TORCH/distributed/constants.py:21
   // default 10 min): watch(s, what) records an event on `s` behind the work
@@ -62,6 +62,13 @@ class Communicator {
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   double timeout() const { return timeout_s_; }
   int pending_watches();
+  // true when collectives really run on RCCL (false: the host relay of bindings.cpp)
+  virtual bool native_rccl() const { return true; }
+
+ protected:
+  // for subclasses that move the bytes themselves: creates the comm stream, no RCCL communicator
+  Communicator(int rank, int world, int device);
+  void make_stream();
 
  private:
   struct Watch {

@@ -275,6 +275,9 @@ void SyncBackend::arm_factor(int bucket, const FactorJob& j, int bias_bucket) {
 }
 
 void SyncBackend::begin_iteration(hipStream_t compute) {
+  // an iteration that never reached wait_all (an exception, an aborted capture) must not leak
+  // its stream choice into this one
+  launched_side_ = launched_any_ = false;
   for (auto& f : factor_) f.B = 0;
   std::fill(factor_skip_.begin(), factor_skip_.end(), 0);
   epi_done_.clear();

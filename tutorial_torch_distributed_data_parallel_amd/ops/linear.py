@@ -54,7 +54,7 @@ class _LinearFn(torch.autograd.Function):
             dw = grad_dest(w_param)
             # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];
             # the bias gradient (sum over the batch of g) is reduced inside the same kernel
-            if fac is not None and fac.factor_submit(w_param, g, x2):
+            if fac is not None and fac.factor_submit(w_param, g, x2, dw):
                 # world size > 1: the DDP bucket of W computes this rank's rows of the averaged
                 # gradient from the all-gathered factors (g, x), and the averaged bias gradient
                 # from the gathered g; dw / db are handed to autograd unwritten
@@ -70,10 +70,53 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _LinearCpuFn(torch.autograd.Function):
+    """The CPU twin of _LinearFn's gradient routing (torch math): used for parameters of a DDP
+    running the factored synchronisation on CPU arenas (the gloo tests of that algorithm)."""
+
+    @staticmethod
+    def forward(ctx, x2, weight, bias, relu: bool):
+        y = F.linear(x2, weight, bias)
+        if relu:
+            y = F.relu(y)
+        ctx.relu = relu
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, y = ctx.saved_tensors
+        w_param, b_param = ctx.params
+        g = dy * (y > 0) if ctx.relu else dy
+        dx = dw = db = None
+        want_db = b_param is not None and needs(ctx, 2)
+        db = grad_dest(b_param) if want_db else None
+        if needs(ctx, 0):
+            dx = g @ weight
+        fac = factor_target(w_param) if needs(ctx, 1) else None
+        if needs(ctx, 1):
+            dw = grad_dest(w_param)
+            if fac is not None and fac.factor_submit(w_param, g, x2, dw):
+                pass  # dw / db handed to autograd unwritten (see _LinearFn)
+            else:
+                dw.copy_(g.t() @ x2)
+                if db is not None:
+                    db.copy_(g.sum(0))
+        elif db is not None:
+            db.copy_(g.sum(0))
+        return dx, dw, db, None
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            relu: bool = False) -> torch.Tensor:
     """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
     if not x.is_cuda:
+        if getattr(weight, "_tdp_factor", None) is not None and torch.is_grad_enabled():
+            note_use(weight)
+            lead = x.shape[:-1]
+            y = _LinearCpuFn.apply(x.reshape(-1, x.shape[-1]), weight, bias, relu)
+            return y.reshape(*lead, weight.shape[0])
         y = F.linear(x, weight, bias)
         return F.relu(y) if relu else y
     if x.dtype != torch.float32:

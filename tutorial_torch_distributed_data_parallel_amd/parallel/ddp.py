@@ -32,6 +32,8 @@ from . import runtime as rt
 from .arena import BufferArena, flatten_module
 
 _MB = 1024 * 1024
+# every live DDP instance (hipGraph capture settles pending bucket rebuilds first)
+_LIVE = weakref.WeakSet()
 
 
 def _param_signature(params) -> str:
@@ -130,8 +132,15 @@ class DistributedDataParallel(nn.Module):
         self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
         self._factor_bucket = {}   # arena index -> its (dedicated) bucket
         self._factor_bias_bucket = {}  # arena index -> the (dedicated) bucket of its bias
-        self._factor_bufs = {}     # (arena index, B) -> (g_all, x_all) all-gather buffers
+        self._factor_bufs = {}     # (arena index, rows) -> (g_all, x_all) all-gather buffers
         self._factor_last_B = {}   # arena index -> per-rank batch of its last factored step
+        # arena index -> factor slot rows every rank agreed on (max over ranks of the first
+        # factored step's batch, one all-reduce); smaller batches are zero-padded to it
+        self._factor_cap = {}
+        self._factor_mode = {}     # arena index -> sync mode of its last step (sync_plan)
+        # arena index -> address of the weight gradient handed to autograd unwritten this step:
+        # anything else in p.grad at the hook means another op contributed to the gradient
+        self._factor_handed = {}
         self._epi_on = False
         self._epi_index = {}
         self._uses = {}            # id(param) -> forward uses in the current iteration
@@ -156,6 +165,7 @@ class DistributedDataParallel(nn.Module):
         env_every = int(os.environ.get("TDP_CHECK_REPLICAS", "0") or 0)
         self.check_replicas_every = check_replicas_every if check_replicas_every is not None \
             else env_every
+        _LIVE.add(self)
 
     # --------------------------------------------------------------------------- reducer
     def _build_reducer(self):
@@ -238,10 +248,25 @@ class DistributedDataParallel(nn.Module):
         self._register_hooks()
         self._rebuilt = True
 
+    def settle(self) -> None:
+        """Apply a pending bucket rebuild now (eagerly). hipGraph capture calls it first: a
+        relayout recorded into a graph would restore stale buffers at every replay."""
+        if self._rebuild_order is not None:
+            self._rebuild_buckets()
+
     def _make_hook(self, idx):
         arena = self.arena
 
         def hook(p):
+            if self._factor_handed:
+                ptr = self._factor_handed.pop(idx, None)
+                if ptr is not None and (p.grad is None or p.grad.data_ptr() != ptr):
+                    raise RuntimeError(
+                        "DDP factored synchronisation: the gradient of a factored Linear weight "
+                        f"(arena index {idx}, shape {tuple(p.shape)}) received a contribution "
+                        "from an op other than its Linear layer (a weight penalty, tied weights, "
+                        "x @ w.t() ...); the factored job would drop it. Construct DDP with "
+                        "factor_sync=False for this model.")
             if not arena.is_arena_grad(idx):
                 # a gradient produced outside the native ops: move it into its bucket slot
                 slot = arena.grad_view(idx)
@@ -263,7 +288,12 @@ class DistributedDataParallel(nn.Module):
             ev["bwd1"] = self._event()
         self.reducer.finalize(self._gpu, self.find_unused_parameters)
         if self._iter == 0 and self._rebuild_enabled and self.reducer.iteration == 1:
-            self._plan_rebuild()
+            if self._gpu and torch.cuda.is_current_stream_capturing():
+                # iteration 0 captured (CapturedStep warmup=0): planning needs a broadcast and a
+                # host read; keep the initial layout
+                self._rebuild_enabled = False
+            else:
+                self._plan_rebuild()
         if ev is not None:
             ev["comm1"] = self._event()
             self._pending_samples.append(ev)
@@ -334,7 +364,14 @@ class DistributedDataParallel(nn.Module):
         if sample:
             self._cur_ev = {"fwd0": self._event()}
         if self._rebuild_order is not None:
+            if self._gpu and torch.cuda.is_current_stream_capturing():
+                # the relayout allocates and copies: inside a capture it would be recorded into
+                # the graph and every replay would restore the pre-capture parameters
+                raise RuntimeError("DDP bucket rebuild pending while a hipGraph is being "
+                                   "captured: call ddp.settle() (CapturedStep does) before "
+                                   "capturing")
             self._rebuild_buckets()
+        self._factor_handed.clear()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             if self._fused_opt is not None:
                 # hyper-parameters as they are NOW (after any LR-scheduler step) drive this
@@ -342,6 +379,9 @@ class DistributedDataParallel(nn.Module):
                 # when something changed, before the block is advanced by prepare_for_backward
                 self._fused_opt.sync_hyper()
             self._uses.clear()
+            # a backward that never finished (an exception, a failed hipGraph capture) left its
+            # end-of-backward callback unqueued-but-flagged: this iteration queues its own
+            self._callback_queued = False
             self.reducer.prepare_for_backward(self._gpu)
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
@@ -409,15 +449,25 @@ class DistributedDataParallel(nn.Module):
         FactorJob): (1/W) sum_r g_r^T x_r has rank <= W*B, so all-gathering the factors g_r
         [B][out] and x_r [B][in] and computing this rank's row shard of the average with one
         depth-W*B GEMM (fused optimizer in its epilogue) replaces the reduce-scatter of the
-        out*in gradient; the updated rows are all-gathered as in the sharded update. Needs a
-        GPU, the fused optimizer with sharding (or the one-GPU rehearsal: world size 1 with
-        collectives forced), no clipping / compression, out % 4W == 0 and whole-row shards that
-        are multiples of 64 elements (SyncBackend.owned_shard). Every rank must run the same
-        per-rank batch size (DistributedSampler guarantees it)."""
+        out*in gradient; the updated rows are all-gathered as in the sharded update. Needs the
+        fused optimizer with sharding (or the one-GPU rehearsal: world size 1 with collectives
+        forced), no clipping / compression, out % 4W == 0 and whole-row shards that are
+        multiples of 64 elements (SyncBackend.owned_shard); on CPU arenas only when requested
+        explicitly (the gloo twin). Per-rank batches may differ: the slot size is agreed once
+        (factor_submit) and smaller batches are zero-padded.
+
+        Gradient note: a factored weight's ``p.grad`` is NOT its gradient after backward -- the
+        job computes this rank's rows of the averaged gradient straight into the update (sharded:
+        only the owned rows hold it; the rest of the slot is stale arena memory). Read
+        gradients with factor_sync=False when you need them."""
         from ..nn.modules import Linear
 
         W = self.world_size
-        if not self._gpu or self._fused_opt is None or self._factor_pref is False:
+        if self._fused_opt is None or self._factor_pref is False:
+            return {}
+        if not self._gpu and self._factor_pref is not True:
+            # CPU arenas: the gloo twin (_CpuSyncOps.factor_sync) only when asked for explicitly
+            # (factor_sync=True / TDP_FACTOR_SYNC=1) -- the multi-rank tests of the algorithm
             return {}
         if self._clip_global or self._clip_local or self._compression not in (None, "none"):
             return {}
@@ -585,33 +635,98 @@ class DistributedDataParallel(nn.Module):
             return None
         return self
 
-    def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor) -> bool:
+    def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor, dw=None) -> bool:
         """Stage this rank's factors of ``p``'s gradient (g [B][out] = dL/dy, x [B][in]) and
-        arm its bucket; False when factoring does not pay at this batch size (the caller then
-        runs the ordinary weight-gradient GEMM). Must run before ``p``'s gradient hook. When
-        True, the layer's bias (if any) is averaged and updated by the same job: the caller
-        must not compute its gradient."""
+        arm its bucket; False when factoring does not pay at the agreed batch size (the caller
+        then runs the ordinary weight-gradient GEMM). Must run before ``p``'s gradient hook.
+        When True, the layer's bias (if any) is averaged and updated by the same job: the caller
+        must not compute its gradient, and ``dw`` (the tensor handed to autograd unwritten) must
+        be what reaches ``p.grad`` -- the hook raises if another op added to it.
+
+        Cross-rank agreement: whether a weight is factored and with how many rows per rank must
+        be identical everywhere (the all-gathers are collectives). The first factored step
+        agrees the slot size (max per-rank batch, one all-reduce; it must run eagerly); later
+        steps zero-pad smaller batches into it (a ragged last batch on one rank contributes only
+        its rows), so the decision depends on agreed values only. A batch larger than the slot
+        raises (the launcher's fail-fast then ends every rank)."""
         i = self._epi_index[id(p)]
         o, n, bi = self._factor[i]
         B = int(g.shape[0])
         W = self.world_size
-        if g.shape != (B, o) or x.shape != (B, n) or not g.is_contiguous() or \
-                not x.is_contiguous() or 2 * W * B * (o + n) > o * n:
+        if g.shape != (B, o) or x.shape != (B, n):
+            raise RuntimeError(f"factor_submit: factors {tuple(g.shape)} / {tuple(x.shape)} do "
+                               f"not match the weight [{o}, {n}]")
+        cap = self._factor_cap.get(i)
+        if cap is None:
+            if self._gpu and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("DDP factored synchronisation: the first step must run "
+                                   "eagerly (it agrees the per-rank batch across ranks) before "
+                                   "a hipGraph capture")
+            t = torch.tensor([B], dtype=torch.int64, device=self.device)
+            rt.all_reduce(t, "max")
+            cap = int(t.item())
+            self._factor_cap[i] = cap
+        if B > cap:
+            raise RuntimeError(
+                f"DDP factored synchronisation: per-rank batch {B} exceeds the {cap} rows agreed "
+                "at the first step (keep later batches <= the first one, or factor_sync=False)")
+        if 2 * W * cap * (o + n) > o * n:
+            self._factor_mode[i] = "bucket"
             return False
-        key = (i, B)
+        g = g if g.is_contiguous() else g.contiguous()
+        x = x if x.is_contiguous() else x.contiguous()
+        key = (i, cap)
         bufs = self._factor_bufs.get(key)
         if bufs is None:
-            bufs = (torch.empty(W * B * o, device=self.device),
-                    torch.empty(W * B * n, device=self.device))
+            bufs = (torch.empty(W * cap * o, device=self.device),
+                    torch.empty(W * cap * n, device=self.device))
             self._factor_bufs[key] = bufs
-        native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W)
-        rep = self._replicate_pays(W, B) if self.factor_replicate is None else \
+            if not self._gpu:
+                for t in bufs:
+                    self._cpu_ops.factor_bufs[t.data_ptr()] = t
+        if self._gpu:
+            native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W, cap)
+        else:
+            with torch.no_grad():
+                gs = bufs[0].view(W, cap, o)[self.rank]
+                xs = bufs[1].view(W, cap, n)[self.rank]
+                gs[:B].copy_(g).mul_(1.0 / W)
+                gs[B:].zero_()
+                xs[:B].copy_(x)
+                xs[B:].zero_()
+        rep = self._replicate_pays(W, cap) if self.factor_replicate is None else \
             self.factor_replicate
-        self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], B, o, n,
+        self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], cap, o, n,
                                  -1 if bi is None else self.arena.offsets[bi],
                                  self._factor_bias_bucket.get(i, -1), replicate=bool(rep))
         self._factor_last_B[i] = B
+        self._factor_mode[i] = "factored-replicated" if rep else "factored-sharded"
+        if dw is not None:
+            self._factor_handed[i] = dw.data_ptr()
         return True
+
+    def sync_plan(self) -> dict:
+        """How each parameter's gradient was synchronised in the last step, by name:
+        "factored-replicated" / "factored-sharded" (Linear weights, see _factor_candidates),
+        "factored-bias" (averaged and updated by its weight's job), "bucket" (a factor
+        candidate whose job did not pay at this batch size), "sharded" (reduce-scatter ->
+        update 1/W -> all-gather), "allreduce", or "local" (one rank: no collective)."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        biases = {bi: i for i, (_, _, bi) in self._factor.items() if bi is not None}
+        if not self._backend.collective:
+            default = "local"
+        elif self._fused_shard and self._fused_opt is not None and not self._compression:
+            default = "sharded"
+        else:
+            default = "allreduce"
+        plan = {}
+        for i, p in enumerate(self.arena.params):
+            mode = self._factor_mode.get(i, default if i not in self._factor else "bucket")
+            if i in biases:
+                w = self._factor_mode.get(biases[i], "")
+                mode = "factored-bias" if w.startswith("factored") else default
+            plan[names.get(id(p), f"param{i}")] = mode
+        return plan
 
     # Price model of the replicated factored update (per weight element, per rank): the extra GEMM
     # rows cost 2*W*B*(1 - 1/W) FLOP at ~150 TF/s (split-bf16 fp32 GEMM, profiles/micro) plus
@@ -716,6 +831,7 @@ class _CpuSyncOps:
         self.blk = None
         self.clip_block = None
         self.bufs = {}
+        self.factor_bufs = {}  # address -> host all-gather buffer of a factored weight
         self.poison = os.environ.get("TDP_POISON_UNOWNED", "0") == "1"
         if self.poison:
             # alignment gaps between parameters hold no gradient: they must stay zero (no
@@ -822,6 +938,28 @@ class _CpuSyncOps:
                         torch.maximum(vm, v, out=vm)
                         vv = vm
                     p.addcdiv_(m, vv.sqrt() / bc2 + eps, value=-lr / bc1)
+
+    # factored Linear weights (csrc/reducer.cpp RcclOps::factor_sync, step for step)
+    def factor_sync(self, begin, own, cnt, B, out, in_, bias_off, replicate, gptr, xptr):
+        g_all, x_all = self.factor_bufs[gptr], self.factor_bufs[xptr]
+        W, r = self.W, self.r
+        if W > 1:  # in place: this rank's factor rows already sit at slot r
+            _all_gather_inplace(g_all, r, B * out)
+            _all_gather_inplace(x_all, r, B * in_)
+        G, X = g_all.view(W * B, out), x_all.view(W * B, in_)
+        with torch.no_grad():
+            if bias_off >= 0:
+                # the whole averaged bias gradient on every rank: no collective
+                self.arena.grad[bias_off: bias_off + out].copy_(G.sum(0))
+                self.opt_update([(bias_off, bias_off + out)])
+            m0, rows = (own - begin) // in_, cnt // in_
+            self.arena.grad[own: own + cnt].copy_((G[:, m0: m0 + rows].t() @ X).reshape(-1))
+            if self.poison and not replicate:
+                self.arena.grad[begin: own].fill_(float("nan"))
+                self.arena.grad[own + cnt: begin + W * cnt].fill_(float("nan"))
+        self.opt_update([(own, own + cnt)])
+        if not replicate:
+            self.all_gather_params(begin, cnt)
 
     # clipping
     def _block(self, which):

@@ -31,7 +31,7 @@ from .._native import native
 @dataclass
 class _State:
     initialized: bool = False
-    backend: str = "gloo"  # "rccl" | "gloo"
+    backend: str = "gloo"  # "rccl" | "relay" | "gloo"
     rank: int = 0
     world: int = 1
     local_rank: int = 0
@@ -85,7 +85,9 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
                        world_size: int | None = None, local_rank: int | None = None,
                        master_addr: str | None = None, master_port: int | None = None,
                        timeout: _dt.timedelta | None = None) -> None:
-    """Join the job. ``backend``: "nccl"/"rccl" (GPU), "gloo" (CPU) or None (auto).
+    """Join the job. ``backend``: "nccl"/"rccl" (GPU), "gloo" (CPU), "relay" (GPU tensors and
+    kernels, collectives relayed through the host over gloo: several ranks sharing one GPU,
+    parallel/relay.py) or None (auto). ``TDP_GPU_RELAY=1`` turns a GPU backend into "relay".
 
     Auto picks RCCL when a GPU is visible, else gloo (the reference's NCCL-else-gloo rule,
     REF/multi-GPU-training-torch.py:34-42, decided on what can actually run).
@@ -102,7 +104,13 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
         os.environ["MASTER_PORT"] = str(master_port)
     os.environ.setdefault("MASTER_PORT", "29500")
     want = (backend or "auto").lower()
-    if want in ("nccl", "rccl"):
+    relay = want == "relay" or (os.environ.get("TDP_GPU_RELAY", "0") == "1" and
+                                want in ("nccl", "rccl", "auto") and torch.cuda.is_available())
+    if relay:
+        if not torch.cuda.is_available():
+            raise RuntimeError("backend 'relay' needs a GPU")
+        use_gpu = True
+    elif want in ("nccl", "rccl"):
         if not torch.cuda.is_available():
             raise RuntimeError("backend 'nccl' (RCCL) requested but no GPU is visible")
         use_gpu = True
@@ -128,14 +136,18 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
     owns = False
     # a single-rank job needs no rendezvous at all (and must not grab MASTER_PORT)
     if world > 1 and not dist.is_initialized():
-        pg_backend = "cpu:gloo,cuda:nccl" if use_gpu else "gloo"
+        pg_backend = "cpu:gloo,cuda:nccl" if use_gpu and not relay else "gloo"
         dist.init_process_group(backend=pg_backend, rank=rank, world_size=world, timeout=timeout)
         owns = True
     _S.initialized = True
-    _S.backend = "rccl" if use_gpu else "gloo"
+    _S.backend = ("relay" if relay else "rccl") if use_gpu else "gloo"
     _S.rank, _S.world, _S.local_rank, _S.device = rank, world, local_rank, dev
     _S.owns_torch_pg = owns
-    if use_gpu:
+    if use_gpu and relay:
+        from .relay import HostRelay
+
+        _S.comm = native().RelayCommunicator(rank, world, dev.index, HostRelay(world))
+    elif use_gpu:
         C = native()
         if world == 1:
             uid = C.rccl_unique_id()

@@ -27,13 +27,31 @@ construction the model has taken exactly ``warmup`` steps.
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+
+class CaptureFailed(RuntimeError):
+    """The hipGraph capture itself failed (the warm-up steps ran fine)."""
+
+
+def _capture_fault_injected() -> bool:
+    """TDP_FAULT_CAPTURE=<rank>: make that rank's capture fail (the agreement tests)."""
+    spec = os.environ.get("TDP_FAULT_CAPTURE")
+    if not spec:
+        return False
+    from ..parallel import runtime as rt
+
+    return int(spec) == rt.get_rank()
 
 
 class CapturedStep:
     def __init__(self, step_fn, warmup: int = 3, pool=None):
         if not torch.cuda.is_available():
             raise RuntimeError("CapturedStep needs a GPU")
+        from ..parallel.ddp import _LIVE
+
         self.step_fn = step_fn
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -41,10 +59,19 @@ class CapturedStep:
             for _ in range(warmup):  # allocator warm-up, lazy kernel attributes, momentum init
                 step_fn()
         torch.cuda.current_stream().wait_stream(side)
+        # a bucket rebuild planned by the warm-up must happen now, eagerly: recorded into the
+        # graph, its relayout would restore the pre-capture buffers at every replay
+        for d in list(_LIVE):
+            d.settle()
         torch.cuda.synchronize()
+        if _capture_fault_injected():
+            raise CaptureFailed("injected capture fault (TDP_FAULT_CAPTURE)")
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
-            self.output = step_fn()
+        try:
+            with torch.cuda.graph(self.graph, pool=pool):
+                self.output = step_fn()
+        except Exception as e:
+            raise CaptureFailed(repr(e)) from e
         torch.cuda.synchronize()
 
     def replay(self):
@@ -62,11 +89,119 @@ class CapturedStep:
     __call__ = replay
 
 
-def try_capture(step_fn, warmup: int = 3, log=print):
-    """Capture if possible; on any capture error fall back to eager (returns step_fn)."""
+def agree(ok: bool) -> bool:
+    """True only if ``ok`` holds on EVERY rank (a 1-element MIN all-reduce over gloo on the host:
+    independent of the GPU stream state a failed capture may leave behind)."""
+    from ..parallel import runtime as rt
+
+    if not rt.is_initialized() or rt.get_world_size() == 1:
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    rt.all_reduce(t, "min")
+    return bool(int(t[0]))
+
+
+def try_capture(step_fn, warmup: int = 3, log=print, capture=CapturedStep):
+    """Capture if possible, else run eagerly -- decided for ALL ranks together: one rank
+    replaying a graph while another runs eagerly would issue collectives in a different order
+    (a deadlock or silent corruption). Warm-up errors propagate; a capture error on any rank
+    makes every rank return the eager ``step_fn``. Returns the replayable step or ``step_fn``."""
+    graph, err = None, None
     try:
-        return CapturedStep(step_fn, warmup=warmup)
-    except Exception as e:  # pragma: no cover - depends on runtime support
-        log(f"[tdp] hipGraph capture failed, running eagerly: {e!r}")
-        torch.cuda.synchronize()
-        return step_fn
+        graph = capture(step_fn, warmup=warmup)
+    except CaptureFailed as e:
+        err = e
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    if agree(graph is not None):
+        return graph
+    if err is not None:
+        log(f"[tdp] hipGraph capture failed, running eagerly on every rank: {err}")
+    else:
+        log("[tdp] hipGraph capture failed on another rank: running eagerly on every rank")
+    del graph
+    return step_fn
+
+
+def _static_like(t: torch.Tensor) -> torch.Tensor:
+    """An uninitialised buffer with ``t``'s shape, dtype and memory layout (a channel-padded
+    channels_last batch keeps its padded base: the NHWC convolutions read that)."""
+    base = getattr(t, "_tdp_padded_base", None)
+    if base is not None:
+        from ..data.synthetic import _padded_view
+
+        return _padded_view(torch.empty_like(base), t.shape[1])
+    return torch.empty_like(t)  # preserve_format: channels_last stays channels_last
+
+
+def _layout(t: torch.Tensor):
+    base = getattr(t, "_tdp_padded_base", None)
+    return (tuple(t.shape), t.dtype, t.device, tuple(t.stride()),
+            None if base is None else tuple(base.shape))
+
+
+def _fill(dst: torch.Tensor, src: torch.Tensor) -> None:
+    db, sb = getattr(dst, "_tdp_padded_base", None), getattr(src, "_tdp_padded_base", None)
+    if db is not None and sb is not None:
+        db.copy_(sb, non_blocking=True)
+    else:
+        dst.copy_(src, non_blocking=True)
+
+
+class GraphedStep:
+    """A training step ``body(x, y)`` replayed as a hipGraph fed by static input buffers.
+
+    This is how the reference's own entry points (REF/multi-GPU-training-torch.py:104-133
+    ``train``; REF/multi-GPU-training-accelerate.py:39-57) get their gradient all-reduce
+    overlapped with backward, as stock DDP gives it to them: inside a captured step the
+    reducer's bucket collectives run on the communicator's side stream behind graph edges
+    (csrc/reducer.cpp pick_stream), whereas eagerly they run on the compute stream.
+
+    The first ``warmup`` calls run ``body`` eagerly -- each on its own real batch, so training
+    is step-for-step the eager computation: these steps agree the factored-sync slot sizes,
+    trigger the one-time bucket rebuild and initialise optimizer state -- then the step is
+    captured (try_capture: the decision is agreed across ranks) and every later call copies its
+    batch into the static buffers and replays. A batch whose shape or layout differs (a ragged
+    last batch; identical on every rank under DistributedSampler / even_batches) runs eagerly.
+    ``capture=False`` (or no GPU) runs everything eagerly. The returned loss of a replay is the
+    graph's static output tensor: read it before the next call."""
+
+    def __init__(self, body, warmup: int = 2, capture: bool = True, log=print):
+        self.body = body
+        self.warmup = max(0, int(warmup))
+        self.want = bool(capture) and torch.cuda.is_available()
+        self.log = log
+        self.sx = self.sy = None
+        self.graph = None
+        self.calls = 0
+        self.replayed = 0
+        self.eager = 0
+
+    @property
+    def captured(self) -> bool:
+        return self.graph is not None
+
+    def _eager(self, x, y):
+        self.eager += 1
+        return self.body(x, y)
+
+    def __call__(self, x, y):
+        self.calls += 1
+        if not self.want:
+            return self._eager(x, y)
+        if self.sx is None:
+            self.sx, self.sy = _static_like(x), _static_like(y)
+        if _layout(x) != _layout(self.sx) or _layout(y) != _layout(self.sy):
+            return self._eager(x, y)
+        _fill(self.sx, x)
+        _fill(self.sy, y)
+        if self.graph is None:
+            if self.calls <= self.warmup:
+                return self._eager(self.sx, self.sy)
+            g = try_capture(lambda: self.body(self.sx, self.sy), warmup=0, log=self.log)
+            if not isinstance(g, CapturedStep):
+                self.want = False
+                return self._eager(self.sx, self.sy)
+            self.graph = g
+        self.replayed += 1
+        return self.graph.replay()

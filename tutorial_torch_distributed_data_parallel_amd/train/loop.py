@@ -11,6 +11,7 @@ device by the sampler's indices.
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import torch
@@ -23,6 +24,7 @@ from ..utils import profiling as prof
 from ..utils.checkpoint import save_ddp_checkpoint
 from ..utils.metrics import EpochMeter, epoch_line
 from ..utils.seed import rng_report
+from .graph import GraphedStep
 
 
 def _loss(criterion, outputs, labels, acc):
@@ -45,11 +47,33 @@ def _sample_repr(inputs):
     return inputs.reshape(inputs.shape[0], -1)[0, :4]
 
 
+def make_step(model, criterion, optimizer, meter: EpochMeter):
+    """One training step ``body(inputs, labels) -> loss`` (the reference's hot loop body,
+    REF/multi-GPU-training-torch.py:118-126): zero_grad -> forward -> loss (accumulated into the
+    device meter) -> backward (the DDP reducer syncs buckets here) -> optimizer step. Safe to
+    capture: every tensor it touches persists across calls."""
+
+    def body(inputs, labels):
+        optimizer.zero_grad(set_to_none=True)
+        with prof.range("forward"):
+            outputs = model(inputs)
+            loss = _loss(criterion, outputs, labels, meter.train)
+        with prof.range("backward+reduce"):
+            ops.backward(loss)  # loss.backward() seeded with a cached 1 (no fill kernel per step)
+        with prof.range("optimizer"):
+            optimizer.step()
+        return loss
+    return body
+
+
 def train(model, train_loader, criterion, optimizer, device, meter: EpochMeter | None = None,
           print_every: int = 100, max_steps: int | None = None, global_step: int = 0,
-          verbose: bool = True):
+          verbose: bool = True, stepper=None):
+    """One epoch. ``stepper(inputs, labels)`` runs the step (a :class:`GraphedStep` replaying a
+    captured hipGraph, train/graph.py); None = ``make_step`` eagerly."""
     model.train()
     meter = meter or EpochMeter(device)
+    step = stepper or make_step(model, criterion, optimizer, meter)
     steps = 0
     for batch_idx, (inputs, labels) in enumerate(train_loader):
         if max_steps is not None and batch_idx >= max_steps:
@@ -59,14 +83,7 @@ def train(model, train_loader, criterion, optimizer, device, meter: EpochMeter |
         if verbose and print_every and batch_idx % print_every == 0:
             print(f"TRAIN: Device {device}, Batch {batch_idx}, Data {_sample_repr(inputs)}")
         fault.maybe_inject(rt.get_rank(), global_step + batch_idx)
-        optimizer.zero_grad(set_to_none=True)
-        with prof.range("forward"):
-            outputs = model(inputs)
-            loss = _loss(criterion, outputs, labels, meter.train)
-        with prof.range("backward+reduce"):
-            ops.backward(loss)  # loss.backward() seeded with a cached 1 (no fill kernel per step)
-        with prof.range("optimizer"):
-            optimizer.step()
+        step(inputs, labels)
         steps += 1
     meter.steps += steps
     return meter.train[0:1].clone(), meter.train[2:3].clone()
@@ -95,9 +112,19 @@ def run_training_loop(model, train_loader, train_sampler, test_loader, criterion
                       device, rank: int, save_dir: str | None, num_epochs: int = 20,
                       checkpoint_epoch: int = 5, set_epoch: bool = True,
                       print_rand: bool = False, max_steps_per_epoch: int | None = None,
-                      json_log: str | None = None, verbose: bool = True):
+                      json_log: str | None = None, verbose: bool = True,
+                      capture: bool | None = None):
+    """``capture``: run the training step as a captured hipGraph (GraphedStep) -- None = auto:
+    on a GPU with more than one rank, where it is what overlaps the gradient collectives with
+    backward; TDP_CAPTURE=0/1 overrides auto."""
     print(f"Training on {len(train_loader)} samples, test on {len(test_loader)} samples")
     meter = EpochMeter(device)
+    if capture is None:
+        env = os.environ.get("TDP_CAPTURE")
+        capture = (env == "1") if env in ("0", "1") else \
+            (device.type == "cuda" and rt.get_world_size() > 1)
+    stepper = GraphedStep(make_step(model, criterion, optimizer, meter), warmup=2,
+                          capture=capture and device.type == "cuda")
     history = []
     global_step = 0
     for epoch in range(num_epochs):
@@ -112,7 +139,8 @@ def run_training_loop(model, train_loader, train_sampler, test_loader, criterion
         meter.reset()
         t0 = time.perf_counter()
         train(model, train_loader, criterion, optimizer, device, meter,
-              max_steps=max_steps_per_epoch, global_step=global_step, verbose=verbose)
+              max_steps=max_steps_per_epoch, global_step=global_step, verbose=verbose,
+              stepper=stepper)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         t_train = time.perf_counter() - t0
@@ -132,6 +160,7 @@ def run_training_loop(model, train_loader, train_sampler, test_loader, criterion
         m = meter.reduce()
         m["epoch"] = epoch
         m["train_samples_per_s"] = m["train_n"] / t_train if t_train > 0 else None
+        m["captured_step"] = stepper.captured
         history.append(m)
         if rank == 0:
             print(epoch_line(epoch, num_epochs, m))

@@ -29,6 +29,11 @@ TRAIN_DEFAULTS = {
     "data": "synthetic",         # synthetic (device-resident) | cifar_uint8 (host pipeline)
     "base_seed": None,
     "max_steps_per_epoch": None,
+    # MI355X execution (not in the reference): apply the optimizer inside the gradient
+    # reduction (DDP.register_fused_optimizer) and replay the step as a captured hipGraph so the
+    # bucket collectives overlap backward; "auto" = on a GPU (capture: with more than one rank)
+    "fused_optimizer": "auto",
+    "capture": "auto",
 }
 
 
@@ -51,6 +56,15 @@ def copy_settings_to_out_dir(settings_path: str, settings: dict) -> str:
     with open(dst, "w") as f:
         yaml.dump(settings, f)
     return dst
+
+
+def tristate(v):
+    """YAML "auto" / true / false -> None / True / False."""
+    if v is None or (isinstance(v, str) and v.lower() == "auto"):
+        return None
+    if isinstance(v, str):
+        return v.lower() in ("1", "true", "yes", "on")
+    return bool(v)
 
 
 def world_size_from(settings: dict, default: int = 1) -> int:
