@@ -437,3 +437,46 @@ def accumulation_parity(rank, out_dir, fused=False, gas=4, steps=8):
     _check_replicas(model)
     rddp = None  # noqa: F841
     _teardown()
+
+
+def rebuild_moves_shards(rank, out_dir, kind="sgd"):
+    """A bucket rebuild under the SHARDED fused optimizer moves parameters across shard owners
+    (layers registered in a different order than they run, several parameters per bucket):
+    optimizer state that was current only on the old owner must reach the new one (the rebuild
+    consolidates it first). Oracle: torch DDP + torch.optim."""
+    tdp.init_process_group("gloo")
+    r = rt.get_rank()
+
+    class Shuffled(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = tdp.nn.Linear(24, 40, relu=True)
+            self.c = tdp.nn.Linear(40, 6)           # registered second, runs last
+            self.b = tdp.nn.Linear(40, 40, relu=True)
+
+        def forward(self, x):
+            return self.c(self.b(self.a(x)))
+
+    torch.manual_seed(0)
+    model = Shuffled()
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, bucket_cap_mb=250 * 4 / 2 ** 20, first_bucket_cap_mb=200 * 4 / 2 ** 20)
+    opt, ropt = _make_opts(kind, ddp.parameters(), ref.parameters(), 0.05 if kind == "sgd"
+                           else 1e-2)
+    ddp.register_fused_optimizer(opt)
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    for step in range(5):
+        g = torch.Generator().manual_seed(100 * step + r)
+        x, y = torch.randn(8, 24, generator=g), torch.randint(0, 6, (8,), generator=g)
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        ropt.zero_grad()
+        F.cross_entropy(rddp(x), y).backward()
+        ropt.step()
+        if step == 0:
+            assert ddp._rebuild_order is not None, "expected a rebuild"
+    assert ddp._rebuilt
+    _check_close(model, ref, f"rebuild moves shards {kind}")
+    _check_replicas(model)
+    rddp = None  # noqa: F841
+    _teardown()

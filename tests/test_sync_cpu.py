@@ -80,3 +80,8 @@ def test_capture_failure_on_one_rank_makes_all_eager(tmp_path):
 @pytest.mark.parametrize("fused", [False, True])
 def test_gradient_accumulation_skips_communication(tmp_path, fused):
     run(SW.accumulation_parity, tmp_path, n=2, fused=fused)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_rebuild_moves_sharded_optimizer_state(tmp_path, kind):
+    run(SW.rebuild_moves_shards, tmp_path, n=2, kind=kind)

@@ -71,8 +71,9 @@ class _LinearFn(torch.autograd.Function):
 
 
 class _LinearCpuFn(torch.autograd.Function):
-    """The CPU twin of _LinearFn's gradient routing (torch math): used for parameters of a DDP
-    running the factored synchronisation on CPU arenas (the gloo tests of that algorithm)."""
+    """The CPU twin of _LinearFn's gradient routing in torch math: gradients written straight
+    into arena slots, the factored synchronisation of a DDP on CPU arenas (the gloo tests of that
+    algorithm), and the device op's gradient-ready order (weight before bias)."""
 
     @staticmethod
     def forward(ctx, x2, weight, bias, relu: bool):
@@ -112,7 +113,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
            relu: bool = False) -> torch.Tensor:
     """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
     if not x.is_cuda:
-        if getattr(weight, "_tdp_factor", None) is not None and torch.is_grad_enabled():
+        if torch.is_grad_enabled() and x.dtype == torch.float32:
+            # the device op's gradient routing (arena slots, factored sync, hook order) in torch
+            # math: the CPU/gloo tests see the same parameter-ready order as MI355X
             note_use(weight)
             lead = x.shape[:-1]
             y = _LinearCpuFn.apply(x.reshape(-1, x.shape[-1]), weight, bias, relu)

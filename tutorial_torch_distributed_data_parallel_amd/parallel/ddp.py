@@ -240,6 +240,19 @@ class DistributedDataParallel(nn.Module):
 
     def _rebuild_buckets(self):
         order, self._rebuild_order = self._rebuild_order, None
+        # under the sharded update, optimizer state is current only in this rank's shards of the
+        # OLD buckets; the new layout hands shards to other owners, so every rank first gathers
+        # the complete state (one all-gather per bucket, once per job)
+        self.consolidate_optimizer_state()
+        # per-parameter factored-sync state follows its parameter to the new arena index (the
+        # agreed slot sizes must not be re-agreed: that may happen inside a capture)
+        new_of = {old: new for new, old in enumerate(order)}
+        self._factor_cap = {new_of[i]: v for i, v in self._factor_cap.items()}
+        self._factor_mode = {new_of[i]: v for i, v in self._factor_mode.items()}
+        self._factor_last_B = {new_of[i]: v for i, v in self._factor_last_B.items()}
+        self._factor_bufs = {(new_of[i], b): v for (i, b), v in self._factor_bufs.items()}
+        self._factor = {new_of[i]: (o, n, None if bi is None else new_of[bi])
+                        for i, (o, n, bi) in self._factor.items()}
         remap = self.arena.relayout(order)
         for opt in list(getattr(self.arena, "_optimizers", ())):
             opt._relayout(self.arena, remap)
@@ -681,9 +694,9 @@ class DistributedDataParallel(nn.Module):
             bufs = (torch.empty(W * cap * o, device=self.device),
                     torch.empty(W * cap * n, device=self.device))
             self._factor_bufs[key] = bufs
-            if not self._gpu:
-                for t in bufs:
-                    self._cpu_ops.factor_bufs[t.data_ptr()] = t
+        if not self._gpu:  # the CPU twin finds its host buffers by address
+            for t in bufs:
+                self._cpu_ops.factor_bufs[t.data_ptr()] = t
         if self._gpu:
             native().factor_stage(g, x, bufs[0], bufs[1], self.rank, 1.0 / W, cap)
         else:
