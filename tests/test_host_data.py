@@ -104,3 +104,42 @@ def test_prefetch_loader_gpu_trains():
             opt.step()
             losses.append(float(loss))
     assert losses[-1] < losses[0]
+
+
+def test_cifar10_binary_reader_roundtrip(tmp_path):
+    """The CIFAR-10 binary record layout (label byte + R/G/B 32x32 planes) read by memmap into
+    HostImageDataset, through PrefetchLoader + the transform, against reference_transform.
+    A fixture in the real layout (no download here); parity with torchvision is unpinned."""
+    from tutorial_torch_distributed_data_parallel_amd.data import (load_cifar10_bin,
+                                                                    write_cifar10_bin)
+
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    g = torch.Generator().manual_seed(5)
+    parts = []
+    for name in [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]:
+        img = torch.randint(0, 256, (7, 32, 32, 3), generator=g, dtype=torch.uint8)
+        lab = torch.randint(0, 10, (7,), generator=g)
+        write_cifar10_bin(str(d / name), img, lab)
+        parts.append((img, lab))
+    # the on-disk bytes really are CHW planes after the label
+    raw = (d / "data_batch_1.bin").read_bytes()
+    assert len(raw) == 7 * 3073 and raw[0] == int(parts[0][1][0])
+    assert raw[1] == int(parts[0][0][0, 0, 0, 0]) and raw[1 + 1024] == int(parts[0][0][0, 0, 0, 1])
+    train = load_cifar10_bin(str(tmp_path), train=True)
+    test = load_cifar10_bin(str(d), train=False)
+    assert train.images.shape == (35, 32, 32, 3) and len(test) == 7
+    assert torch.equal(train.images, torch.cat([p[0] for p in parts[:5]]))
+    assert torch.equal(train.labels, torch.cat([p[1] for p in parts[:5]]))
+    assert torch.equal(test.images, parts[5][0])
+    tf = ImageTransform(size=64, flip_p=0.0)
+    loader = PrefetchLoader(train, 8, transform=tf)
+    for x, y in loader:
+        # no sampler: the first batch is rows 0..7 in order
+        assert torch.equal(y, train.labels[: len(y)])
+        want = reference_transform(train.images[: len(y)], None, (64, 64), CIFAR_MEAN, CIFAR_STD)
+        torch.testing.assert_close(x, want)
+        break
+    with pytest.raises(FileNotFoundError):
+        load_cifar10_bin(str(tmp_path / "missing"))
+

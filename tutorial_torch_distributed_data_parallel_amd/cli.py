@@ -38,15 +38,21 @@ def _settings(argv, desc):
 
 
 def _datasets(t, device):
-    """``train.data``: "synthetic" (default: model-shaped float tensors resident on the device)
-    or "cifar_uint8" (CIFAR-10-layout uint8 32x32x3 host images through the native prefetcher
-    and the on-device Resize / Flip / Normalize, the reference's input pipeline)."""
-    from .data import SyntheticDataset, cifar_like_uint8
+    """``train.data``: "synthetic" (default: model-shaped float tensors resident on the device),
+    "cifar10_bin" (the real CIFAR-10 binary files under ``train.data_dir``, default ./data as in
+    REF/data_and_toy_model.py:31-36) or "cifar_uint8" (synthetic CIFAR-10-layout uint8 images);
+    host images go through the native prefetcher and the on-device Resize / Flip / Normalize,
+    the reference's input pipeline."""
+    from .data import SyntheticDataset, cifar_like_uint8, load_cifar10_bin
     from .models.registry import input_shape
 
-    if t.get("data", "synthetic") == "cifar_uint8":
+    kind = t.get("data", "synthetic")
+    if kind in ("cifar_uint8", "cifar10_bin"):
         if t["model"].lower().startswith(("toy_mlp", "mlp")):
-            raise ValueError("data: cifar_uint8 feeds image models (alexnet, resnet50)")
+            raise ValueError(f"data: {kind} feeds image models (alexnet, resnet50)")
+        if kind == "cifar10_bin":  # the real dataset, CIFAR-10 binary files under data_dir
+            root = t.get("data_dir") or "./data"
+            return load_cifar10_bin(root, train=True), load_cifar10_bin(root, train=False)
         return (cifar_like_uint8(t["n_train"], seed=0), cifar_like_uint8(t["n_test"], seed=1))
     shape = input_shape(t["model"], t["image_size"])
     return (SyntheticDataset(t["n_train"], shape, 10, seed=0, device=device),

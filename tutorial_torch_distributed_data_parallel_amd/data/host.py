@@ -71,6 +71,62 @@ def cifar_like_uint8(n: int = 50000, hw: int = 32, num_classes: int = 10, seed: 
     return HostImageDataset(img, labels)
 
 
+CIFAR10_TRAIN_FILES = tuple(f"data_batch_{i}.bin" for i in range(1, 6))
+CIFAR10_TEST_FILES = ("test_batch.bin",)
+_CIFAR_RECORD = 1 + 3 * 32 * 32  # label byte + R, G, B planes of 32x32, row-major
+
+
+def _cifar_dir(root: str) -> str:
+    """``root`` itself or the ``cifar-10-batches-bin`` directory the binary archive unpacks to
+    (torchvision's CIFAR10(root=...) layout, REF/data_and_toy_model.py:31-36)."""
+    import os
+
+    for d in (root, os.path.join(root, "cifar-10-batches-bin")):
+        if os.path.isfile(os.path.join(d, "test_batch.bin")) or \
+                os.path.isfile(os.path.join(d, "data_batch_1.bin")):
+            return d
+    raise FileNotFoundError(
+        f"no CIFAR-10 binary batches (data_batch_1.bin ... / test_batch.bin) under {root!r} or "
+        f"{root!r}/cifar-10-batches-bin: there is no download here -- place the binary archive's "
+        "files there (the python-pickle archive is not read: loading pickles executes code)")
+
+
+def load_cifar10_bin(root: str = "./data", train: bool = True) -> HostImageDataset:
+    """CIFAR-10 from its binary distribution: every record is 1 label byte followed by 3072
+    bytes (R, G, B planes of 32x32). The files are memory-mapped (no pickle, nothing executed)
+    and transposed once to the uint8 [n, 32, 32, 3] layout the native prefetcher gathers from
+    (150 MB for the training set)."""
+    import os
+
+    d = _cifar_dir(root)
+    names = CIFAR10_TRAIN_FILES if train else CIFAR10_TEST_FILES
+    imgs, labels = [], []
+    for name in names:
+        path = os.path.join(d, name)
+        raw = np.memmap(path, dtype=np.uint8, mode="r")
+        if raw.size % _CIFAR_RECORD:
+            raise ValueError(f"{path}: {raw.size} bytes is not a whole number of "
+                             f"{_CIFAR_RECORD}-byte CIFAR-10 records")
+        rec = raw.reshape(-1, _CIFAR_RECORD)
+        labels.append(np.asarray(rec[:, 0], dtype=np.int64))
+        imgs.append(np.asarray(rec[:, 1:]).reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1))
+        del raw, rec
+    if not imgs:
+        raise FileNotFoundError(f"no CIFAR-10 files in {d}")
+    lab = np.concatenate(labels)
+    if lab.size and (lab.min() < 0 or lab.max() > 9):
+        raise ValueError("CIFAR-10 labels must be in [0, 9]")
+    return HostImageDataset(np.ascontiguousarray(np.concatenate(imgs)), lab)
+
+
+def write_cifar10_bin(path: str, images: torch.Tensor, labels: torch.Tensor) -> None:
+    """Write uint8 [n, 32, 32, 3] images + labels in the CIFAR-10 binary record layout (test
+    fixtures, and converting other sources to what load_cifar10_bin reads)."""
+    x = images.to(torch.uint8).permute(0, 3, 1, 2).reshape(len(images), -1).numpy()
+    rec = np.concatenate([labels.to(torch.uint8).numpy().reshape(-1, 1), x], axis=1)
+    rec.astype(np.uint8).tofile(path)
+
+
 def reference_transform(x_u8: torch.Tensor, flip: torch.Tensor | None, size, mean, std,
                         round_u8: bool = True) -> torch.Tensor:
     """torch implementation of image_transform (CPU path and test oracle); [B,H,W,C] uint8 ->

@@ -26,7 +26,8 @@ TRAIN_DEFAULTS = {
     "n_train": 50000,            # CIFAR-10 sizes
     "n_test": 10000,
     "image_size": 224,           # Resize(224), REF/data_and_toy_model.py:13
-    "data": "synthetic",         # synthetic (device-resident) | cifar_uint8 (host pipeline)
+    "data": "synthetic",         # synthetic (device-resident) | cifar10_bin | cifar_uint8
+    "data_dir": "./data",        # cifar10_bin: CIFAR-10 binary batches (REF root="./data")
     "base_seed": None,
     "max_steps_per_epoch": None,
     # MI355X execution (not in the reference): apply the optimizer inside the gradient
