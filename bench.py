@@ -113,6 +113,9 @@ def parse():
                          "the optimizer's HBM traffic); with world_size 1 in the weight-gradient "
                          "GEMM epilogues (no gradient write/re-read). auto = on")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
+    ap.add_argument("--comm-cus", type=int, default=None,
+                    help="CUs left to RCCL: grid-sized kernels (persistent GEMMs, split-K "
+                         "planners) plan for (CUs - N) (TDP_COMM_CUS; default 0)")
     return ap.parse_args()
 
 
@@ -148,6 +151,14 @@ def _gemm_products(impl: str, use_gpu: bool):
         return ("fp32 operands split exactly into 3 bf16 terms (RNE), 6 bf16 MFMA products with "
                 "fp32 accumulation: error within the native f32 bound (tests/test_gemm_emu_gpu.py)")
     return "native v_mfma_f32_32x32x2_f32"
+
+
+def _reserved_cus(impl: str, use_gpu: bool):
+    if impl != "tdp" or not use_gpu:
+        return None
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    return int(native().reserved_cus())
 
 
 def scratch_warmup(a, dims, in_shape, dev):
@@ -293,6 +304,10 @@ def main():
         from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
 
+        if a.comm_cus is not None and use_gpu:
+            from tutorial_torch_distributed_data_parallel_amd._native import native as _nat
+
+            _nat().set_reserved_cus(a.comm_cus)
         tdp.init_process_group("nccl" if use_gpu else "gloo")
         rank, world, dev = rt.get_rank(), rt.get_world_size(), rt.device()
         torch.manual_seed(1234 + rank)
@@ -485,6 +500,17 @@ def main():
 
         advance()
         run = tdp_step
+        if a.impl == "tdp" and ddp is not None and world > 1 and use_gpu:
+            # measured replicated-vs-sharded choice for the factored Linear weights (untimed
+            # training steps, agreed over ranks) before the step is captured
+            def eager_step():
+                advance()
+                tdp_step_eager()
+
+            def tdp_step_eager():
+                x, y = gather_batch(data.x, data.y, cur["b"])
+                return body(x, y)
+            ddp.tune_factor_replicate(eager_step, iters=3)
         if graph:
             from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
 
@@ -544,7 +570,8 @@ def main():
         except RuntimeError:
             ident = False
         sync = {"replicas_identical": ident, "captured": isinstance(run, CapturedStep),
-                "backend": rt.get_backend(), "modes": ddp.sync_plan()}
+                "backend": rt.get_backend(), "modes": ddp.sync_plan(),
+                "factor_tuning": ddp.factor_tuning}
 
     def record(diag):
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
@@ -579,6 +606,7 @@ def main():
                                         if a.impl == "tdp" and fused else ""),
                 "final_loss": final_loss,
                 "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,
+                "comm_cus": _reserved_cus(a.impl, use_gpu),
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)
                               for i in range(len(ddp._bounds) - 1)]
                 if a.impl == "tdp" and ddp is not None else None,

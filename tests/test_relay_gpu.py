@@ -54,7 +54,7 @@ def test_bench_world2_record(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "2", "--mlp-dims", "1024,512,512",
-           "--dataset", "1024", "--no-diag", "--device-warmup-ms", "0"]
+           "--dataset", "1024", "--batch", "32", "--no-diag", "--device-warmup-ms", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
@@ -63,6 +63,7 @@ def test_bench_world2_record(tmp_path):
     assert sync["replicas_identical"] is True, sync
     assert sync["captured"] is False  # relayed collectives cannot be captured: agreed eager
     assert sync["modes"]["fc1.weight"].startswith("factored"), sync
+    assert sync["factor_tuning"]["chosen"] in ("replicated", "sharded"), sync
 
 
 def _port():

@@ -27,18 +27,8 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-int num_cus(int device) {
-  static std::mutex mu;
-  static std::map<int, int> cache;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(device);
-  if (it != cache.end()) return it->second;
-  int v = 0;
-  check_hip(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device),
-            "hipDeviceGetAttribute");
-  cache[device] = v;
-  return v;
-}
+// CUs the compute kernels plan for (comm.h compute_cus: physical minus TDP_COMM_CUS)
+int num_cus(int device) { return compute_cus(device); }
 
 #define CHECK_GPU(x) TORCH_CHECK((x).is_cuda(), #x " must be on the GPU")
 #define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be float32")
@@ -1167,6 +1157,8 @@ float* block_ptr(const c10::optional<Tensor>& blk) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950-native kernels, RCCL communicator and gradient reducer";
   m.def("num_cus", &num_cus);
+  m.def("reserved_cus", &reserved_cus);
+  m.def("set_reserved_cus", &set_reserved_cus);
   m.def("gemm_f32", &gemm_f32_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("mask") = py::none(),
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none(), py::arg("beta") = 0.0,

@@ -1,6 +1,8 @@
 #include "comm.h"
 
+#include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 
 #include <chrono>
@@ -18,6 +20,36 @@ void check_hip(hipError_t e, const char* what) {
 void check_nccl(ncclResult_t r, const char* what) {
   if (r != ncclSuccess)
     throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+
+static std::atomic<int> g_reserved_cus{-1};
+
+int reserved_cus() {
+  int v = g_reserved_cus.load();
+  if (v < 0) {
+    const char* e = std::getenv("TDP_COMM_CUS");
+    v = e ? std::max(0, std::atoi(e)) : 0;
+    g_reserved_cus.store(v);
+  }
+  return v;
+}
+
+void set_reserved_cus(int n) { g_reserved_cus.store(std::max(0, n)); }
+
+int compute_cus(int device) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  int phys = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if ((int)cache.size() <= device) cache.resize(device + 1, 0);
+    if (cache[device] == 0)
+      check_hip(hipDeviceGetAttribute(&cache[device], hipDeviceAttributeMultiprocessorCount,
+                                      device),
+                "hipDeviceGetAttribute");
+    phys = cache[device];
+  }
+  return std::max(1, phys - reserved_cus());
 }
 
 std::vector<uint8_t> Communicator::unique_id() {

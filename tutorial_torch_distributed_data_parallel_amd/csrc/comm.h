@@ -23,6 +23,14 @@ namespace tdp {
 void check_hip(hipError_t e, const char* what);
 void check_nccl(ncclResult_t r, const char* what);
 
+// CUs left to the collectives: kernels that size their grid to the chip (persistent GEMMs,
+// split-K / stream planners) plan for (physical CUs - reserved) so concurrently running RCCL
+// kernels on the comm stream do not stretch their last wave (TDP_COMM_CUS, default 0).
+int reserved_cus();
+void set_reserved_cus(int n);
+// physical CU count of `device` minus reserved_cus(), at least 1
+int compute_cus(int device);
+
 class Communicator {
  public:
   // 128-byte ncclUniqueId as bytes (rank 0 creates it, the store distributes it)

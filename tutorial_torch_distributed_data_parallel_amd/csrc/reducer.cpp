@@ -142,13 +142,9 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
                       s);
   }
   // this rank's rows of the averaged gradient: dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all
-  if (cus_ == 0) {
-    int dev = 0;
-    check_hip(hipGetDevice(&dev), "hipGetDevice");
-    check_hip(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, dev),
-              "hipDeviceGetAttribute");
-  }
-  const int cus = cus_;
+  int dev = 0;
+  check_hip(hipGetDevice(&dev), "hipGetDevice");
+  const int cus = compute_cus(dev);
   auto grow = [&](float*& buf, int64_t& have, int64_t want, const char* what) {
     if (want <= have) return;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -172,7 +172,6 @@ class RcclOps : public SyncOps {
   int64_t factor_ws_floats_ = 0;
   float* factor_part_ = nullptr;  // column-sum partials of the factored biases
   int64_t factor_part_floats_ = 0;
-  int cus_ = 0;
 };
 
 // The bucket algorithm (one instance per DDP model).

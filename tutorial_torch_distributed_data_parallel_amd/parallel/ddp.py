@@ -129,6 +129,7 @@ class DistributedDataParallel(nn.Module):
         # TDP_FACTOR_REPLICATE=0/1 forces it off / on
         env_rep = os.environ.get("TDP_FACTOR_REPLICATE")
         self.factor_replicate = None if env_rep in (None, "", "auto") else env_rep != "0"
+        self.factor_tuning = None  # measured replicate-vs-shard timings (tune_factor_replicate)
         self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
         self._factor_bucket = {}   # arena index -> its (dedicated) bucket
         self._factor_bias_bucket = {}  # arena index -> the (dedicated) bucket of its bias
@@ -752,6 +753,40 @@ class DistributedDataParallel(nn.Module):
     @classmethod
     def _replicate_pays(cls, W: int, B: int) -> bool:
         return W > 1 and W * B <= cls._REPLICATE_MAX_WB
+
+    def tune_factor_replicate(self, step_fn, iters: int = 3):
+        """Measure, don't guess: time ``step_fn`` (one full training step, eager) with the
+        factored weights replicated and sharded, take the max over ranks of each, keep the
+        faster mode for every factored weight, and record the timings in ``factor_tuning``.
+        The price model behind the default (_REPLICATE_MAX_WB) assumes an xGMI bus bandwidth
+        and a GEMM rate; on a node both are measured here. Runs 2 * (iters + 1) real training
+        steps; every rank must call it at the same point (it issues collectives). Replicated
+        runs first (its optimizer state is complete on every rank); choosing it after the
+        sharded runs gathers the sharded state first. No-op (returns None) without factored
+        weights, at world size 1, on CPU, or when TDP_FACTOR_REPLICATE forces a mode."""
+        if not self._factor or self.world_size == 1 or not self._gpu or \
+                os.environ.get("TDP_FACTOR_REPLICATE") not in (None, "", "auto"):
+            return None
+        times = {}
+        for rep in (True, False):
+            self.factor_replicate = rep
+            step_fn()  # one step in this mode before timing it
+            rt.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                step_fn()
+            torch.cuda.synchronize()
+            times[rep] = (time.perf_counter() - t0) * 1000.0 / iters
+        t = torch.tensor([times[True], times[False]], dtype=torch.float64, device=self.device)
+        rt.all_reduce(t, "max")
+        rep_ms, shard_ms = (float(v) for v in t.tolist())
+        choice = rep_ms <= shard_ms
+        if choice:
+            self.consolidate_optimizer_state()  # the sharded steps left state in owned rows only
+        self.factor_replicate = choice
+        self.factor_tuning = {"replicated_ms": round(rep_ms, 4), "sharded_ms": round(shard_ms, 4),
+                              "chosen": "replicated" if choice else "sharded"}
+        return choice
 
     def consolidate_optimizer_state(self) -> None:
         """Make every rank's fused-optimizer state complete after sharded updates: all-gather
