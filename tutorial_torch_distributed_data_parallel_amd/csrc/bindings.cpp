@@ -1172,6 +1172,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_set_cvec", &gemm_f32_set_cvec);
   m.def("gemm_f32_set_bm", &gemm_f32_set_bm);
   m.def("gemm_f32_set_emu", &gemm_f32_set_emu);
+  m.def("gemm_f32_set_exp", &gemm_f32_set_exp);
   m.def("gemm_f32_emu", &gemm_f32_emu);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
