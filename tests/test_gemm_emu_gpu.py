@@ -123,3 +123,58 @@ def test_conv_paths_under_both_products(emu):
     torch.testing.assert_close(y.double().cpu(), yr, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(w.grad.double().cpu(), wr.grad, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("ea,eb", [(-100, 90), (110, -100), (-20, -60)])
+def test_emu_extreme_exponents(C, ea, eb):
+    """Operands around 2^ea and 2^eb (products normal): every split term of the small operand is
+    itself a normal fp32 number down to ~2^-110, so the six-product sum keeps fp32 accuracy;
+    checked against fp64 next to the native f32 MFMA path."""
+    torch.manual_seed(abs(ea) * 31 + abs(eb))
+    M, N, K = 130, 96, 160
+    A = torch.randn(M, K, device="cuda") * 2.0 ** ea
+    B = torch.randn(N, K, device="cuda") * 2.0 ** eb
+    e_emu = _scaled_err(_run(C, A, B, True, True, True), A, B, True, True)
+    e_nat = _scaled_err(_run(C, A, B, True, True, False), A, B, True, True)
+    bound = (8 + 2 * K ** 0.5) * U
+    assert e_nat < bound and e_emu < bound, (e_emu, e_nat, bound)
+
+
+def test_emu_subnormal_operands_follow_native(C):
+    """Subnormal entries (2^-130 .. 2^-127) times ~2^+120: whatever the hardware does with
+    subnormal inputs, the split path must do the same as the native f32 MFMA (flush or keep)."""
+    torch.manual_seed(9)
+    M, N, K = 64, 64, 64
+    A = torch.randn(M, K, device="cuda") * 2.0 ** -128
+    A[:, ::2] *= 4.0  # half the columns normal (2^-126), half subnormal
+    B = torch.randn(N, K, device="cuda") * 2.0 ** 118
+    emu = _run(C, A, B, True, True, True)
+    nat = _run(C, A, B, True, True, False)
+    assert torch.isfinite(emu).all() and torch.isfinite(nat).all()
+    scale = (A.double().abs() @ B.double().abs().t()).float()
+    # the two paths agree to fp32 accuracy relative to the product scale, or both flush the same
+    assert ((emu - nat).abs() <= 64 * U * scale + 1e-30).float().mean() > 0.99, \
+        ((emu - nat).abs() / scale).max()
+
+
+def test_emu_non_finite_inputs_stay_non_finite(C):
+    """inf / NaN operands: the split path turns inf into NaN (x - bf16(x) = inf - inf), so the
+    pinned contract is finiteness: an output is finite exactly when the native f32 MFMA's is.
+    Finite operands up to 3e38 (below bf16's 3.39e38 maximum) stay finite and accurate; above
+    3.39e38 the bf16 head term overflows (documented in docs/PARITY.md)."""
+    torch.manual_seed(4)
+    M, N, K = 64, 64, 64
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(N, K, device="cuda")
+    A[3, 5] = float("inf")
+    A[7, 1] = float("-inf")
+    A[9, 2] = float("nan")
+    B[11, 5] = 0.0  # inf * 0 = NaN in both paths
+    emu = _run(C, A, B, True, True, True)
+    nat = _run(C, A, B, True, True, False)
+    assert torch.equal(torch.isfinite(emu), torch.isfinite(nat))
+    assert not torch.isfinite(emu[3]).any() and not torch.isfinite(emu[9]).any()
+    big = torch.randn(M, K, device="cuda") * 3.0e38 / 4
+    small = torch.randn(N, K, device="cuda") * 1e-12
+    e_emu = _scaled_err(_run(C, big, small, True, True, True), big, small, True, True)
+    assert e_emu < (8 + 2 * K ** 0.5) * U, e_emu

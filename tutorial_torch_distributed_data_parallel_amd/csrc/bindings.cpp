@@ -45,7 +45,7 @@ float* fptr(const c10::optional<Tensor>& t) {
 void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
                  const c10::optional<Tensor>& mask, const c10::optional<Tensor>& bias,
                  const c10::optional<Tensor>& rowsum, double beta, double rowsum_beta,
-                 bool relu) {
+                 bool relu, const c10::optional<Tensor>& gate) {
   CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
   CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
   CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_ROWMAJOR(C);
@@ -78,10 +78,23 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
   a.beta = (float)beta;
   a.rowsum_beta = (float)rowsum_beta;
   a.relu = relu;
-  const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  bool gate_after = false;
+  if (gate.has_value() && gate->defined()) {
+    CHECK_GPU(*gate); CHECK_F32(*gate); CHECK_ROWMAJOR(*gate);
+    TORCH_CHECK(gate->size(0) == M && gate->size(1) == N, "gemm: gate must have C's shape");
+    a.gate = gate->data_ptr<float>();
+    a.ldgate = gate->stride(0);
+    // the fast kernel's row-vector epilogue reads the gate as 16-B rows
+    gate_after = (((uintptr_t)a.gate & 15) != 0 || a.ldgate % 4 != 0);
+  }
+  GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  const float* g = a.gate;
+  if (gate_after && plan.fast) a.gate = nullptr;
+  else gate_after = false;
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
   gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  if (gate_after) gate_inplace(a.C, a.ldc, g, gate->stride(0), M, N, cur_stream());
 }
 
 // Returns whether the epilogue ran. Weight-gradient GEMM whose epilogue applies the DDP's fused optimizer to arena elements
@@ -1162,7 +1175,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32", &gemm_f32_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("mask") = py::none(),
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none(), py::arg("beta") = 0.0,
-        py::arg("rowsum_beta") = 0.0, py::arg("relu") = false);
+        py::arg("rowsum_beta") = 0.0, py::arg("relu") = false, py::arg("gate") = py::none());
   m.def("gemm_f32_opt", &gemm_f32_opt_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
         py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0);

@@ -17,6 +17,8 @@
 // single ds_read_b128 feeds four MFMAs. K-contiguous LDS rows are padded by 16 B (row stride
 // 36 dwords) which makes those reads bank-conflict-free. f32-in MFMA is exact f32 (a k-ordered
 // fmaf chain), so results match torch's fp32 Linear to rounding of the summation order.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -231,7 +233,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             int splits, int M, int N, void* Cv,
                                                             int c_bf16, long ldc,
                                                             const float* __restrict__ bias,
-                                                            float beta, int relu, int zt_log2) {
+                                                            float beta, int relu, int zt_log2,
+                                                            const float* __restrict__ gate,
+                                                            long ldgate) {
   constexpr int W = VEC ? 4 : 1;
   const int ZT = 1 << zt_log2, G = 256 >> zt_log2;
   const int g = threadIdx.x % G, zt = threadIdx.x / G;
@@ -278,6 +282,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       float* C = reinterpret_cast<float*>(Cv) + (long)row * ldc + col + e;
       if (beta != 0.f) x += beta * *C;
       if (relu) x = fmaxf(x, 0.f);
+      if (gate && !(gate[(long)row * ldgate + col + e] > 0.f)) x = 0.f;
       *C = x;
     }
   }
@@ -312,7 +317,24 @@ void launch_tile(int tile, const Params& p, dim3 grid, bool ak, bool bk, hipStre
 
 inline bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
+__global__ __launch_bounds__(256) void gate_kernel(float* __restrict__ C, long ldc,
+                                                   const float* __restrict__ gate, long ldg, int M,
+                                                   int N) {
+  const long n = (long)M * N;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int row = (int)(e / N), col = (int)(e % N);
+    if (!(gate[row * ldg + col] > 0.f)) C[row * ldc + col] = 0.f;
+  }
+}
+
 }  // namespace
+
+void gate_inplace(float* C, long ldc, const float* gate, long ldg, int M, int N, hipStream_t s) {
+  const long n = (long)M * N;
+  if (n <= 0) return;
+  const unsigned grid = (unsigned)std::min<long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(gate_kernel, dim3(grid), dim3(256), 0, s, C, ldc, gate, ldg, M, N);
+}
 
 static int g_mode = 0;  // 0 auto, 1 generic, 2 fast, 3 auto (skinny allowed; = 0)
 void gemm_f32_set_mode(int mode) { g_mode = mode; }
@@ -373,7 +395,10 @@ void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStre
   if (vec) launch_tile<true>(plan.tile, p, grid, a.a_kcontig, a.b_kcontig, s);
   else launch_tile<false>(plan.tile, p, grid, a.a_kcontig, a.b_kcontig, s);
   if (plan.splits > 1)
-    splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+    splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s,
+                  a.gate, a.ldgate);
+  else if (a.gate)  // the generic tile kernel has no gate epilogue: one masking pass
+    gate_inplace(a.C, a.ldc, a.gate, a.ldgate, a.M, a.N, s);
   if (a.opt.kind != 0) gemm_opt_fallback(a, s);
 }
 
@@ -386,7 +411,8 @@ void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s) {
 }
 
 void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf16, long ldc,
-                   const float* bias, float beta, bool relu, hipStream_t s) {
+                   const float* bias, float beta, bool relu, hipStream_t s, const float* gate,
+                   long ldgate) {
   const bool vec = (N % 4 == 0) && (ldc % 4 == 0) && aligned16(C) &&
                    (bias == nullptr || aligned16(bias));
   const long groups = vec ? (long)M * N / 4 : (long)M * N;
@@ -398,10 +424,10 @@ void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf
   const dim3 grid((unsigned)((groups + G - 1) / G));
   if (vec)
     hipLaunchKernelGGL(splitk_reduce_kernel<true>, grid, dim3(256), 0, s, ws, splits, M, N, C,
-                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl);
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl, gate, ldgate);
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<false>, grid, dim3(256), 0, s, ws, splits, M, N, C,
-                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl);
+                       c_bf16 ? 1 : 0, ldc, bias, beta, relu ? 1 : 0, zl, gate, ldgate);
 }
 
 }  // namespace tdp

@@ -90,6 +90,8 @@ struct FastParams {
   // A fragments' split by one conversion, bit 1 the B fragments' -- the bound a pre-split
   // operand would reach (scripts/bench_gemm_emu.py --exp)
   int exp;
+  const float* gate;  // optional C-shaped gate (GemmF32Args::gate), non-split epilogues
+  long ldg;
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -1013,6 +1015,11 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
             for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
           }
+          if (p.gate) {
+            const f32x4 gv = *reinterpret_cast<const f32x4*>(p.gate + row * p.ldg + col);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = gv[c] > 0.f ? v[c] : 0.f;
+          }
         }
         *reinterpret_cast<f32x4*>(out + row * ldo + col) = v;
       }
@@ -1108,6 +1115,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             if (p.bias) v += p.bias[col];
             if (rmw) v += p.beta * cold[r][g];
             if (p.relu) v = fmaxf(v, 0.f);
+            if (p.gate && !(p.gate[(long)row * p.ldg + col] > 0.f)) v = 0.f;
           }
           orow[col] = v;
         }
@@ -1122,6 +1130,11 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
               v[1] += p.beta * cold[r][1];
             }
             if (p.relu) { v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); }
+            if (p.gate) {
+              const float* gr = p.gate + (long)row * p.ldg + col;
+              if (!(gr[0] > 0.f)) v[0] = 0.f;
+              if (!(gr[1] > 0.f)) v[1] = 0.f;
+            }
           }
           *reinterpret_cast<f32x2*>(orow + col) = v;
         } else if (col < p.N) {
@@ -1130,6 +1143,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             if (p.bias) x += p.bias[col];
             if (rmw) x += p.beta * cold[r][0];
             if (p.relu) x = fmaxf(x, 0.f);
+            if (p.gate && !(p.gate[(long)row * p.ldg + col] > 0.f)) x = 0.f;
           }
           orow[col] = x;
         }
@@ -1353,6 +1367,7 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.prio = o_emu_prio;
   p.exp = o_emu_exp;
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
+  p.gate = a.gate; p.ldg = a.ldgate;
   p.rowsum = a.rowsum; p.rowsum_beta = a.rowsum_beta;
   p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
   p.M = a.M; p.N = a.N; p.K = a.K;
@@ -1408,7 +1423,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   else if (!ak && !bk) launch_kinds<kDenseMN, kDenseMN>(p, fn, st, nblocks, s);
   else launch_kinds<kDenseMN, kDenseK>(p, fn, st, nblocks, s);
   if (plan.splits > 1)
-    splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s);
+    splitk_reduce(ws, plan.splits, a.M, a.N, a.C, false, a.ldc, a.bias, a.beta, a.relu, s,
+                  a.gate, a.ldgate);
   if (a.opt.kind != 0) gemm_opt_fallback(a, s);
 }
 

@@ -33,12 +33,16 @@ struct SkinnyParams {
   int M, N, K;
   float beta, rowsum_beta;
   int relu;
+  const float* gate;  // optional C-shaped gate (GemmF32Args::gate)
+  long ldg;
 };
 
-__device__ __forceinline__ float epi(float v, const SkinnyParams& p, const float* crow, int col) {
+__device__ __forceinline__ float epi(float v, const SkinnyParams& p, const float* crow, int col,
+                                     int row) {
   if (p.bias) v += p.bias[col];
   if (p.beta != 0.f) v += p.beta * crow[col];
   if (p.relu) v = fmaxf(v, 0.f);
+  if (p.gate && !(p.gate[(long)row * p.ldg + col] > 0.f)) v = 0.f;
   return v;
 }
 
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(256) void skinny_n_kernel(SkinnyParams p) {
     const int n = threadIdx.x;
     const float v = red[0][n] + red[1][n] + red[2][n] + red[3][n];
     float* crow = p.C + (long)row * p.ldc;
-    crow[n] = epi(v, p, crow, n);
+    crow[n] = epi(v, p, crow, n, row);
   }
 }
 
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(256) void skinny_k_kernel(SkinnyParams p) {
   float* crow = p.C + (long)row * p.ldc;
   f32x4 out;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) out[e] = epi(acc[e], p, crow, col + e);
+  for (int e = 0; e < 4; ++e) out[e] = epi(acc[e], p, crow, col + e, row);
   *reinterpret_cast<f32x4*>(crow + col) = out;
 }
 
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(256) void skinny_m_kernel(SkinnyParams p) {
       const float v = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
                       red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
       float* crow = p.C + (long)m * p.ldc;
-      crow[gc] = epi(v, p, crow, gc);
+      crow[gc] = epi(v, p, crow, gc, m);
     }
   }
   if (p.rowsum && blockIdx.x == 0 && threadIdx.x < p.M) {
@@ -168,6 +172,7 @@ SkinnyParams params_of(const GemmF32Args& a) {
   p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc;
   p.M = a.M; p.N = a.N; p.K = a.K;
   p.beta = a.beta; p.rowsum_beta = a.rowsum_beta; p.relu = a.relu ? 1 : 0;
+  p.gate = a.gate; p.ldg = a.ldgate;
   return p;
 }
 

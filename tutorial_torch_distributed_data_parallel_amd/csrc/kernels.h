@@ -108,6 +108,11 @@ struct GemmF32Args {
   float beta = 0.f, rowsum_beta = 0.f;
   bool relu = false;
   OptEpilogue opt;  // kind != 0: apply the optimizer instead of storing C (needs splits == 1)
+  // optional C-shaped gate, applied last: C = epilogue(C) * (gate > 0). The input gradient of a
+  // Linear whose input is a ReLU output leaves already masked, so the producer's backward
+  // needs no separate mask pass (ops/linear.py)
+  const float* gate = nullptr;
+  long ldgate = 0;
 };
 
 struct GemmPlan {
@@ -123,6 +128,8 @@ struct GemmPlan {
 };
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
+// C[M][N] = 0 where !(gate > 0) (the generic GEMM path's gate epilogue)
+void gate_inplace(float* C, long ldc, const float* gate, long ldg, int M, int N, hipStream_t s);
 void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
 bool gemm_f32_fast_ok(const GemmF32Args& a);
 // skinny GEMM kind for a dimension <= 16 (1: N, 2: K, 3: M; 0: not applicable), and its launch
@@ -168,7 +175,8 @@ void gemm_bf16_run(const GemmBF16Args& a, const GemmPlan& plan, float* ws, hipSt
 
 // split-K combine + epilogue: C = epi(sum_z ws[z]) ; C fp32 or bf16
 void splitk_reduce(const float* ws, int splits, int M, int N, void* C, bool c_bf16, long ldc,
-                   const float* bias, float beta, bool relu, hipStream_t s);
+                   const float* bias, float beta, bool relu, hipStream_t s,
+                   const float* gate = nullptr, long ldgate = 0);
 
 // ------------------------------------------------------------------------------------------------
 // Loss / metrics

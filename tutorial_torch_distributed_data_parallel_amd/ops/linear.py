@@ -20,13 +20,25 @@ from .._native import native
 from ._grad import epilogue_target, factor_target, grad_dest, needs, note_use
 
 
+def _pregated(dy: torch.Tensor, y: torch.Tensor) -> bool:
+    """``dy`` was already multiplied by (y > 0) by the consumer that produced it (its
+    input-gradient epilogue gated by this layer's ReLU output, see _LinearFn.backward)."""
+    return getattr(dy, "_tdp_gated_by", None) == (y.data_ptr(), tuple(y.shape)) and \
+        dy.shape == y.shape and dy.stride() == y.stride()
+
+
+def _mark_gated(dx: torch.Tensor, gate: torch.Tensor) -> None:
+    dx._tdp_gated_by = (gate.data_ptr(), tuple(gate.shape))
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool):
         C = native()
         y = torch.empty((x2.shape[0], weight.shape[0]), device=x2.device, dtype=torch.float32)
         C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
         ctx.relu = relu
+        ctx.gate_in = gate_in
         ctx.params = (weight, bias)
         ctx.save_for_backward(x2, weight, y if relu else None)
         return y
@@ -41,15 +53,21 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
-        # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU)
-        g = C.relu_bias_bwd(dy, y) if ctx.relu else dy
+        # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU) -- unless the
+        # consumer's input-gradient epilogue already applied this mask (idempotent either way)
+        g = C.relu_bias_bwd(dy, y) if ctx.relu and not _pregated(dy, y) else dy
         fac = factor_target(w_param) if needs(ctx, 1) else None
         epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
-            # (before the weight-gradient GEMM: with an optimizer epilogue that one updates W)
-            C.gemm_f32(g, weight, dx, True, False)
+            # (before the weight-gradient GEMM: with an optimizer epilogue that one updates W).
+            # When the input is a ReLU output (the previous fused Linear+ReLU), the epilogue
+            # also applies that layer's mask (x > 0): its backward then skips its mask pass
+            gate = x2 if ctx.gate_in else None
+            C.gemm_f32(g, weight, dx, True, False, gate=gate)
+            if gate is not None:
+                _mark_gated(dx, x2)
         if needs(ctx, 1):
             dw = grad_dest(w_param)
             # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];
@@ -67,7 +85,7 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class _LinearCpuFn(torch.autograd.Function):
@@ -76,11 +94,12 @@ class _LinearCpuFn(torch.autograd.Function):
     algorithm), and the device op's gradient-ready order (weight before bias)."""
 
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool):
         y = F.linear(x2, weight, bias)
         if relu:
             y = F.relu(y)
         ctx.relu = relu
+        ctx.gate_in = gate_in
         ctx.params = (weight, bias)
         ctx.save_for_backward(x2, weight, y if relu else None)
         return y
@@ -89,12 +108,15 @@ class _LinearCpuFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, weight, y = ctx.saved_tensors
         w_param, b_param = ctx.params
-        g = dy * (y > 0) if ctx.relu else dy
+        g = dy * (y > 0) if ctx.relu and not _pregated(dy, y) else dy
         dx = dw = db = None
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
         if needs(ctx, 0):
             dx = g @ weight
+            if ctx.gate_in:
+                dx = dx * (x2 > 0)
+                _mark_gated(dx, x2)
         fac = factor_target(w_param) if needs(ctx, 1) else None
         if needs(ctx, 1):
             dw = grad_dest(w_param)
@@ -106,29 +128,39 @@ class _LinearCpuFn(torch.autograd.Function):
                     db.copy_(g.sum(0))
         elif db is not None:
             db.copy_(g.sum(0))
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            relu: bool = False) -> torch.Tensor:
     """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
+    # the input is the ReLU output of a previous fused Linear(+ReLU): this layer's input-gradient
+    # epilogue applies that ReLU's mask (see _LinearFn.backward)
+    gate_in = bool(getattr(x, "_tdp_relu_out", False)) and x.dim() == 2
     if not x.is_cuda:
         if torch.is_grad_enabled() and x.dtype == torch.float32:
             # the device op's gradient routing (arena slots, factored sync, hook order) in torch
             # math: the CPU/gloo tests see the same parameter-ready order as MI355X
             note_use(weight)
             lead = x.shape[:-1]
-            y = _LinearCpuFn.apply(x.reshape(-1, x.shape[-1]), weight, bias, relu)
-            return y.reshape(*lead, weight.shape[0])
+            y = _LinearCpuFn.apply(x.reshape(-1, x.shape[-1]), weight, bias, relu, gate_in)
+            if relu and x.dim() == 2:
+                y._tdp_relu_out = True
+            return y if x.dim() == 2 else y.reshape(*lead, weight.shape[0])
         y = F.linear(x, weight, bias)
         return F.relu(y) if relu else y
     if x.dtype != torch.float32:
         raise TypeError(f"native linear expects float32 activations, got {x.dtype}")
     lead = x.shape[:-1]
-    x2 = x.reshape(-1, x.shape[-1])
+    x2 = x if x.dim() == 2 else x.reshape(-1, x.shape[-1])
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
+        gate_in = False
     if torch.is_grad_enabled():
         note_use(weight)
-    y = _LinearFn.apply(x2, weight, bias, relu)
+    y = _LinearFn.apply(x2, weight, bias, relu, gate_in)
+    if x.dim() == 2:
+        if relu:
+            y._tdp_relu_out = True
+        return y
     return y.reshape(*lead, weight.shape[0])
