@@ -161,4 +161,4 @@ def test_replicated_factored_update_matches_sharded(pg, opt_name):
     for a, b in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(a, b, atol=0, rtol=0)
     assert d1._replicate_pays(2, 128) and d1._replicate_pays(4, 128)
-    assert not d1._replicate_pays(8, 128) and not d1._replicate_pays(1, 128)
+    assert not d1._replicate_pays(8, 128) and d1._replicate_pays(1, 128)

@@ -752,7 +752,9 @@ class DistributedDataParallel(nn.Module):
 
     @classmethod
     def _replicate_pays(cls, W: int, B: int) -> bool:
-        return W > 1 and W * B <= cls._REPLICATE_MAX_WB
+        # world size 1 (the one-GPU rehearsal): every row is this rank's anyway; replicating
+        # skips the in-place parameter all-gather a sharded job would still issue
+        return W * B <= cls._REPLICATE_MAX_WB
 
     def tune_factor_replicate(self, step_fn, iters: int = 3):
         """Measure, don't guess: time ``step_fn`` (one full training step, eager) with the
