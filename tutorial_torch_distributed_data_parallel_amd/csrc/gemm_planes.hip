@@ -11,11 +11,13 @@
 // laid out K-contiguous and zero-padded to a multiple of 32 in K; the GEMM then runs no VALU on
 // its operands at all:
 //   * 256 threads = 4 waves (2 x 2), block tile 256 x 128, a wave owns 128 x 64 = 4 x 2 32x32
-//     tiles, K step 32 (64-B plane rows); per 16-deep step a wave reads 18 ds_read_b128 operands
-//     (one per plane per tile, MFMA-ready: no conversion) and issues 48 v_mfma_f32_32x32x16_bf16.
-//   * Global -> LDS by global_load_lds_dwordx4, two stages of 72 KiB (A 48 + B 24): one
-//     workgroup per CU, the next stage's DMA in flight while the current one is consumed.
-//   * 64-B rows are XOR-swizzled through the DMA SOURCE address (slot = chunk ^ ((row >> 2) & 3)):
+//     tiles, K step 16 (32-B plane rows); per step a wave reads 18 ds_read_b128 operands (one per
+//     plane per tile, MFMA-ready: no conversion) and issues 48 v_mfma_f32_32x32x16_bf16.
+//   * Global -> LDS by global_load_lds_dwordx4 into four stages of 36 KiB (A 24 + B 12): one
+//     workgroup per CU, three stages in flight behind a counted vmcnt (never 0 inside the loop:
+//     a vmcnt(0) at every barrier exposed the DMA latency -- the first, two-stage version of this
+//     kernel ran at ~170 TF/s, profiles/micro/gemm_planes_r5h.jsonl).
+//   * Rows are XOR-swizzled through the DMA SOURCE address (slot = chunk ^ ((row >> 3) & 1)):
 //     every 16-lane group of a fragment read covers all 64 banks once (conflict-free).
 //   * XCD-aware bijective block order (consecutive tiles of one XCD share the A row panel).
 // Products per 32x32x16 step: a2b0, a0b2, a1b1, a1b0, a0b1, a0b0 (smallest first), as the fast
@@ -36,13 +38,15 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef char lds_char;
 
 constexpr int kT = 256;
-constexpr int kBM = 256, kBN = 128, kBK = 32;  // tile; K step in bf16 elements
-constexpr int kRow = kBK * 2;                  // 64 B per plane row per stage
-constexpr int kAB = 3 * kBM * kRow;            // 48 KiB: three A planes
-constexpr int kBB = 3 * kBN * kRow;            // 24 KiB: three B planes
+constexpr int kBM = 256, kBN = 128, kBK = 16;  // tile; K step (one 32x32x16 MFMA depth)
+constexpr int kRow = kBK * 2;                  // 32 B per plane row per stage
+constexpr int kAB = 3 * kBM * kRow;            // 24 KiB: three A planes
+constexpr int kBB = 3 * kBN * kRow;            // 12 KiB: three B planes
 constexpr int kStg = kAB + kBB;
-constexpr int kS = 2;
+constexpr int kS = 4;                          // 144 KiB: three stages in flight
 constexpr int kUA = kAB / 1024 / 4, kUB = kBB / 1024 / 4;  // 1-KiB DMA units per wave per stage
+constexpr int kG = kUA + kUB;                  // DMA instructions per wave per stage
+constexpr int kPad = 32;                       // planes are padded in K to a multiple of this
 
 struct PlanesParams {
   const uint16_t* A;  // planes [3][a_rows][ldp] (plane stride a_plane elements)
@@ -57,7 +61,9 @@ struct PlanesParams {
   int tiles_m, tiles_n;
 };
 
-__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+// 32-B rows hold two 16-B chunks; rows r and r + 8 share a 32-B bank group, so the chunk slot is
+// flipped by row bit 3: a fragment read's 16-lane groups then cover all 64 banks once
+__device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
 
 __device__ __forceinline__ void glds16(const void* src, lds_char* dst) {
   __builtin_amdgcn_global_load_lds(src, (void __attribute__((address_space(3)))*)(
@@ -76,21 +82,21 @@ __device__ __forceinline__ f32x16 emu6(const bf8 (&a)[3], const bf8 (&b)[3], f32
 }
 
 // Per-lane DMA sources of one operand's share of a stage: unit j of this wave covers plane
-// j / (R/16), rows (j % (R/16)) * 16 + lane / 4, 16-B slot lane % 4 (chunk = slot ^ swz(row)).
+// j / (R/32), rows (j % (R/32)) * 32 + lane / 2, 16-B slot lane % 2 (chunk = slot ^ swz(row)).
 template <int R, int U>
 struct PlaneSrc {
   const uint16_t* src[U];
   __device__ __forceinline__ void init(const uint16_t* base, long plane, long ld, int r0,
                                        int rlim, int wid, int lane) {
-    constexpr int UPP = R / 16;  // units per plane
+    constexpr int UPP = R / 32;  // units per plane
 #pragma unroll
     for (int i = 0; i < U; ++i) {
       const int j = wid * U + i;
       const int pl = j / UPP;
-      const int row = (j % UPP) * 16 + (lane >> 2);
+      const int row = (j % UPP) * 32 + (lane >> 1);
       int gr = r0 + row;
       gr = gr < rlim ? gr : rlim - 1;
-      const int chunk = (lane & 3) ^ swz(row);
+      const int chunk = (lane & 1) ^ swz(row);
       src[i] = base + pl * plane + (long)gr * ld + chunk * 8;
     }
   }
@@ -136,11 +142,11 @@ void gemm_planes_kernel(PlanesParams p) {
 #pragma unroll
   for (int g = 0; g < 2; ++g) b_row[g] = wn * 64 + g * 32 + l31;
 
-  auto read = [&](const lds_char* st, int j, bf8 (&fa)[4][3], bf8 (&fb)[2][3]) {
+  auto read = [&](const lds_char* st, bf8 (&fa)[4][3], bf8 (&fb)[2][3]) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       const int row = a_row[f];
-      const int off = row * kRow + (((2 * j + h) ^ swz(row)) * 16);
+      const int off = row * kRow + ((h ^ swz(row)) * 16);
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         fa[f][pl] = *reinterpret_cast<const bf8*>(st + pl * (kBM * kRow) + off);
@@ -148,34 +154,38 @@ void gemm_planes_kernel(PlanesParams p) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       const int row = b_row[g];
-      const int off = kAB + row * kRow + (((2 * j + h) ^ swz(row)) * 16);
+      const int off = kAB + row * kRow + ((h ^ swz(row)) * 16);
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         fb[g][pl] = *reinterpret_cast<const bf8*>(st + pl * (kBN * kRow) + off);
     }
   };
+  auto issue = [&](int t) {
+    lds_char* st = smem + (t % kS) * kStg;
+    sa.issue(t * kBK, st, wid);
+    sb.issue(t * kBK, st + kAB, wid);
+  };
 
-  sa.issue(0, smem, wid);
-  sb.issue(0, smem + kAB, wid);
+  // S-1 stages in flight ahead of the one being consumed; a counted vmcnt (never 0 inside the
+  // loop) keeps the newer stages' DMA outstanding across the barrier
+#pragma unroll
+  for (int t = 0; t < kS - 1; ++t)
+    if (t < nk) issue(t);
   for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed (only its DMA is outstanding here) and every wave left stage kt - 1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ahead = nk - 1 - kt;  // stages issued after kt that may still be in flight
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kG) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kG) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage kt landed for every wave; every wave left stage kt - 1 (the buffer refilled next)
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) {
-      lds_char* nx = smem + ((kt + 1) % kS) * kStg;
-      sa.issue((kt + 1) * kBK, nx, wid);
-      sb.issue((kt + 1) * kBK, nx + kAB, wid);
-    }
+    if (kt + kS - 1 < nk) issue(kt + kS - 1);
     const lds_char* st = smem + (kt % kS) * kStg;
-    bf8 fa[2][4][3], fb[2][2][3];
-    read(st, 0, fa[0], fb[0]);
-    read(st, 1, fa[1], fb[1]);
+    bf8 fa[4][3], fb[2][3];
+    read(st, fa, fb);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int f = 0; f < 4; ++f)
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) acc[f][g] = emu6(fa[j][f], fb[j][g], acc[f][g]);
+      for (int g = 0; g < 2; ++g) acc[f][g] = emu6(fa[f], fb[g], acc[f][g]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(256) void split_planes_t_kernel(const float* __rest
 
 }  // namespace
 
-long planes_depth(int K) { return (long)ceil_div(K, kBK) * kBK; }
+long planes_depth(int K) { return (long)ceil_div(K, kPad) * kPad; }
 
 void split_planes(const float* src, long ld, bool kcontig, int R, int K, uint16_t* dst,
                   hipStream_t s) {
