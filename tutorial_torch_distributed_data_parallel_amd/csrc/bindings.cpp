@@ -97,51 +97,6 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
   if (gate_after) gate_inplace(a.C, a.ldc, g, gate->stride(0), M, N, cur_stream());
 }
 
-// fp32 operand -> three bf16 planes [3][R][planes_depth(K)] (gemm_planes.hip)
-Tensor split_planes_op(const Tensor& x, bool kcontig) {
-  CHECK_GPU(x); CHECK_F32(x); CHECK_ROWMAJOR(x);
-  const int R = (int)(kcontig ? x.size(0) : x.size(1));
-  const int K = (int)(kcontig ? x.size(1) : x.size(0));
-  const long Kp = planes_depth(K);
-  auto out = at::empty({3, R, Kp}, x.options().dtype(at::kBFloat16));
-  split_planes(x.data_ptr<float>(), x.stride(0), kcontig, R, K,
-               reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
-  return out;
-}
-
-// C = A . B (A [M][K] if a_kcontig else [K][M]; B [N][K] if b_kcontig else [K][N]) through
-// pre-split planes: one split pass per operand, then the planes GEMM. For GEMMs whose operands
-// are re-read by many output tiles (large square shapes, the factored weight gradient of W ranks).
-void gemm_f32_planes_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig,
-                        bool b_kcontig, const c10::optional<Tensor>& bias, double beta,
-                        bool relu) {
-  CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
-  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
-  CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_ROWMAJOR(C);
-  const int M = (int)C.size(0), N = (int)C.size(1);
-  const int K = (int)(a_kcontig ? A.size(1) : A.size(0));
-  TORCH_CHECK((a_kcontig ? A.size(0) : A.size(1)) == M, "gemm: A rows != C rows");
-  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm: B cols != C cols");
-  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm: inner dims differ");
-  const float* bp = nullptr;
-  if (bias.has_value() && bias->defined()) {
-    CHECK_GPU(*bias); CHECK_F32(*bias); CHECK_CONTIG(*bias);
-    TORCH_CHECK(bias->numel() == N, "gemm: bias must have N elements");
-    bp = bias->data_ptr<float>();
-  }
-  const long Kp = planes_depth(K);
-  auto opts = A.options().dtype(at::kBFloat16);
-  Tensor pa = at::empty({3, M, Kp}, opts), pb = at::empty({3, N, Kp}, opts);
-  hipStream_t s = cur_stream();
-  split_planes(A.data_ptr<float>(), A.stride(0), a_kcontig, M, K,
-               reinterpret_cast<uint16_t*>(pa.data_ptr()), s);
-  split_planes(B.data_ptr<float>(), B.stride(0), b_kcontig, N, K,
-               reinterpret_cast<uint16_t*>(pb.data_ptr()), s);
-  gemm_planes_run(reinterpret_cast<const uint16_t*>(pa.data_ptr()),
-                  reinterpret_cast<const uint16_t*>(pb.data_ptr()), M, N, K, C.data_ptr<float>(),
-                  C.stride(0), bp, (float)beta, relu, s);
-}
-
 // Returns whether the epilogue ran. Weight-gradient GEMM whose epilogue applies the DDP's fused optimizer to arena elements
 // [offset, offset + M*N) instead of storing the gradient into C (world size 1, see
 // RcclBackend::epilogue_opt). C must be that contiguous arena slice (its contents are left as
@@ -1225,10 +1180,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
         py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0);
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
-  m.def("split_planes", &split_planes_op, py::arg("x"), py::arg("kcontig"));
-  m.def("gemm_f32_planes", &gemm_f32_planes_op, py::arg("A"), py::arg("B"), py::arg("C"),
-        py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("bias") = py::none(),
-        py::arg("beta") = 0.0, py::arg("relu") = false);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);
   m.def("gemm_f32_set_cvec", &gemm_f32_set_cvec);

@@ -127,18 +127,6 @@ struct GemmPlan {
   int grid = 0;         // fast kernel: > 0 = persistent launch of this many workgroups
 };
 
-// ---- fp32 GEMM from pre-split bf16 planes (gemm_planes.hip) ----
-// padded depth of a planes operand (K rounded up to the 32-deep K step; the pad holds zeros)
-long planes_depth(int K);
-// fp32 operand of R rows x K (kcontig: stored [R][K], else [K][R]; row stride ld) -> three RNE
-// bf16 planes [3][R][planes_depth(K)], K-contiguous: x = plane0 + plane1 + plane2 exactly
-void split_planes(const float* src, long ld, bool kcontig, int R, int K, uint16_t* dst,
-                  hipStream_t s);
-// C[M][N] (+bias, beta * C, ReLU) = A[M][K] . B[N][K]^T from planes of A and B (six bf16
-// products per step: fp32 accuracy)
-void gemm_planes_run(const uint16_t* A, const uint16_t* B, int M, int N, int K, float* C,
-                     long ldc, const float* bias, float beta, bool relu, hipStream_t s);
-
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
 // C[M][N] = 0 where !(gate > 0) (the generic GEMM path's gate epilogue)
 void gate_inplace(float* C, long ldc, const float* gate, long ldg, int M, int N, hipStream_t s);
