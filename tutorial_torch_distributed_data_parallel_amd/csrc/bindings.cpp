@@ -1446,6 +1446,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("fused_kind", &SyncBackend::fused_kind)
       .def_readwrite("shard", &SyncBackend::shard)
       .def_readwrite("compressed", &SyncBackend::compressed)
+      .def_readwrite("skip_opt_begin", &SyncBackend::skip_opt_begin)
       .def_property("clip", [](SyncBackend& b) { return (int)b.clip; },
                     [](SyncBackend& b, int v) {
                       TORCH_CHECK(v >= 0 && v <= 2, "clip mode 0 none | 1 global | 2 local");

@@ -279,7 +279,8 @@ void SyncBackend::begin_iteration(hipStream_t compute) {
   epi_done_.clear();
   pending_.clear();
   deferred_.clear();
-  if (fused_kind != 0) ops_->opt_begin(compute);
+  if (fused_kind != 0 && !(skip_opt_begin && fused_kind == 1 && clip == ClipMode::NONE))
+    ops_->opt_begin(compute);
   if (clip == ClipMode::LOCAL) ops_->clip_begin(1, compute);
 }
 

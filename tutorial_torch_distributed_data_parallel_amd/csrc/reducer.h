@@ -191,6 +191,9 @@ class SyncBackend : public ReducerBackend {
   bool shard = false;     // world > 1: reduce-scatter / update own 1/W / all-gather
   ClipMode clip = ClipMode::NONE;
   bool compressed = false;  // wire compression active (sharding needs the plain fp32 path)
+  // SGD in steady state (first-step flags consumed, no clipping): the per-iteration hyper-block
+  // advance changes nothing the update reads, so its launch is skipped (set by parallel/ddp.py)
+  bool skip_opt_begin = false;
 
   // Optimizer-in-GEMM-epilogue (world size 1 only: the local gradient IS the averaged one): the
   // weight-gradient GEMM of arena elements [off, off + n) applies the fused optimizer instead of

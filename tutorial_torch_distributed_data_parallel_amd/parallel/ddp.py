@@ -144,6 +144,7 @@ class DistributedDataParallel(nn.Module):
         self._factor_handed = {}
         self._epi_on = False
         self._epi_index = {}
+        self._opt_begin_countdown = 0
         self._uses = {}            # id(param) -> forward uses in the current iteration
         # DDP Logger: every `_sample_every`-th iteration is timed with device
         # events -- forward compute, backward compute (first gradient ready -> end of backward),
@@ -397,6 +398,10 @@ class DistributedDataParallel(nn.Module):
             # end-of-backward callback unqueued-but-flagged: this iteration queues its own
             self._callback_queued = False
             self.reducer.prepare_for_backward(self._gpu)
+            if self._fused_opt is not None and self._opt_begin_countdown > 0:
+                self._opt_begin_countdown -= 1
+                if self._opt_begin_countdown == 0:
+                    self._backend.skip_opt_begin = True
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._sync_buffers()
@@ -522,6 +527,10 @@ class DistributedDataParallel(nn.Module):
             return
         opt = self._fused_opt
         b = self._backend
+        # SGD: the hyper block's per-iteration advance (first-step flags) matters for the first
+        # two iterations after (re)binding only; then its launch is skipped (SyncBackend)
+        b.skip_opt_begin = False
+        self._opt_begin_countdown = 2
         b.shard = self._fused_shard
         b.clip = 1 if self._clip_global else (2 if self._clip_local else 0)
         self._bind_fused_buffers(opt)
