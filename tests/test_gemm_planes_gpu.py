@@ -1,0 +1,149 @@
+"""Skinny GEMM from pre-split bf16 planes of A (csrc/gemm_planes.hip) against a float64 reference,
+next to the split-bf16 fast GEMM it replaces on the toy-MLP's forward / input-gradient shapes.
+The split itself must be exact (hi + mid + lo == x), and the GEMM must carry fp32 accuracy:
+error / (|A| @ |B|) within the fp32 bound of tests/test_gemm_emu_gpu.py."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+U = 2.0 ** -24
+
+
+@pytest.fixture(scope="module")
+def C():
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    return native()
+
+
+def _scaled_err(out, A, Bm):
+    ref = A.double() @ Bm.double()
+    scale = A.double().abs() @ Bm.double().abs()
+    return ((out.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+
+
+def test_split_planes_exact(C):
+    torch.manual_seed(0)
+    x = torch.randn(37, 64, device="cuda") * torch.exp2(
+        torch.randint(-30, 31, (37, 64), device="cuda").float())
+    p = C.split_planes(x)
+    assert p.dtype == torch.bfloat16 and p.shape == (3, 37, 64)
+    s = p[0].double() + p[1].double() + p[2].double()
+    assert torch.equal(s, x.double())
+    # the head term is the RNE bf16 of x, the middle term that of the residual
+    assert torch.equal(p[0], x.bfloat16())
+    assert torch.equal(p[1], (x - p[0].float()).bfloat16())
+
+
+SHAPES = [(128, 4096, 9216, True),   # toy-MLP fc1 forward
+          (128, 4096, 4096, True),   # fc2 forward
+          (128, 4096, 4096, False),  # fc2 input gradient (W stored [out][in])
+          (130, 200, 64, True),      # ragged M / N edges
+          (32, 128, 256, False),
+          (300, 256, 512, True)]     # several row tiles
+
+
+@pytest.mark.parametrize("M,N,K,bk", SHAPES)
+def test_planes_gemm_matches_fp64(C, M, N, K, bk):
+    torch.manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn((N, K) if bk else (K, N), device="cuda")
+    Bm = B.t() if bk else B
+    out = torch.empty(M, N, device="cuda")
+    C.gemm_planes(C.split_planes(A), B, out, bk)
+    ref_fast = torch.empty(M, N, device="cuda")
+    C.gemm_f32(A, B, ref_fast, True, bk)
+    torch.cuda.synchronize()
+    e = _scaled_err(out, A, Bm)
+    e_fast = _scaled_err(ref_fast, A, Bm)
+    bound = (8 + 2 * K ** 0.5) * U
+    assert e < bound, (e, bound)
+    assert e < 4 * e_fast + 16 * U, (e, e_fast)
+
+
+def test_planes_gemm_epilogues_and_out_planes(C):
+    torch.manual_seed(1)
+    M, N, K = 128, 512, 1024
+    A = torch.randn(M, K, device="cuda")
+    W = torch.randn(N, K, device="cuda") / 32
+    b = torch.randn(N, device="cuda")
+    gate = torch.randn(M, N, device="cuda")
+    y = torch.empty(M, N, device="cuda")
+    op = torch.empty(3, M, N, device="cuda", dtype=torch.bfloat16)
+    C.gemm_planes(C.split_planes(A), W, y, True, bias=b, relu=True, gate=gate, out_planes=op)
+    ref = torch.relu(A.double() @ W.double().t() + b.double()) * (gate > 0).double()
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(op, C.split_planes(y))
+    # single split (no workspace): the in-kernel epilogue path
+    A2 = torch.randn(256, 128, device="cuda")
+    W2 = torch.randn(1024, 128, device="cuda")
+    b2 = torch.randn(1024, device="cuda")
+    y2 = torch.empty(256, 1024, device="cuda")
+    op2 = torch.empty(3, 256, 1024, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_planes_plan(256, 1024, 128, 256)[0] == 1
+    C.gemm_planes(C.split_planes(A2), W2, y2, True, bias=b2, relu=True, out_planes=op2)
+    ref2 = torch.relu(A2.double() @ W2.double().t() + b2.double())
+    torch.testing.assert_close(y2.double(), ref2, rtol=1e-5, atol=1e-5)
+    assert torch.equal(op2, C.split_planes(y2))
+
+
+def test_planes_gemm_rejects_bad_shapes(C):
+    A = torch.randn(16, 48, device="cuda")  # K % 32 != 0
+    with pytest.raises(RuntimeError):
+        C.gemm_planes(C.split_planes(A), torch.randn(64, 48, device="cuda"),
+                      torch.empty(16, 64, device="cuda"), True)
+
+
+def test_gather_batch_emits_planes(C):
+    torch.manual_seed(2)
+    x = torch.randn(64, 512, device="cuda")
+    y = torch.randint(0, 10, (64,), device="cuda")
+    idx = torch.randint(0, 64, (32,), device="cuda")
+    xb, yb, p = C.gather_batch(x, y, idx, planes=True)
+    assert torch.equal(xb, x[idx]) and torch.equal(yb, y[idx])
+    assert torch.equal(p, C.split_planes(x[idx]))
+
+
+def test_mlp_linear_chain_planes_vs_split_path():
+    """fc1 -> fc2 -> fc3 of the toy MLP shape family (smaller widths) through ops.linear with the
+    planes path on and off: the forward / gradients agree to fp32 accuracy and both match fp64."""
+    from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import gather_batch
+    import importlib
+
+    L = importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear")
+
+    torch.manual_seed(3)
+    data = torch.randn(256, 1024, device="cuda")
+    lab = torch.randint(0, 10, (256,), device="cuda")
+    idx = torch.randperm(256, device="cuda")[:128]
+    ws = [torch.randn(1024, 1024, device="cuda") / 32, torch.randn(512, 1024, device="cuda") / 32,
+          torch.randn(10, 512, device="cuda") / 22]
+    bs = [torch.randn(w.shape[0], device="cuda") / 10 for w in ws]
+    res = {}
+    for on in (True, False):
+        old = L.set_planes(on)
+        try:
+            x, _ = gather_batch(data, lab, idx)
+            assert (getattr(x, "_tdp_planes", None) is not None) == on
+            p = [t.clone().requires_grad_() for t in ws + bs]
+            h = ops.linear(x.reshape(128, -1), p[0], p[3], relu=True)
+            h = ops.linear(h, p[1], p[4], relu=True)
+            out = ops.linear(h, p[2], p[5])
+            out.backward(torch.linspace(-1, 1, out.numel(), device="cuda").view_as(out))
+            torch.cuda.synchronize()
+            res[on] = [out.detach()] + [t.grad for t in p]
+        finally:
+            L.set_planes(old)
+    xd = data[idx].double()
+    pd = [t.double().requires_grad_() for t in ws + bs]
+    h = torch.relu(xd @ pd[0].t() + pd[3])
+    h = torch.relu(h @ pd[1].t() + pd[4])
+    out = h @ pd[2].t() + pd[5]
+    out.backward(torch.linspace(-1, 1, out.numel(), device="cuda", dtype=torch.float64)
+                 .view_as(out))
+    ref = [out.detach()] + [t.grad for t in pd]
+    for a, b, r in zip(res[True], res[False], ref):
+        torch.testing.assert_close(a.double(), r, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)

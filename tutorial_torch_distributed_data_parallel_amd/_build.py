@@ -46,11 +46,25 @@ def _headers():
     return sorted(CSRC.glob("*.h"))
 
 
+def _includes(src: Path, seen=None) -> set:
+    """The in-tree headers ``src`` includes, transitively (``#include "x.h"`` lines)."""
+    seen = set() if seen is None else seen
+    for line in src.read_text().splitlines():
+        line = line.strip()
+        if line.startswith('#include "'):
+            h = CSRC / line.split('"')[1]
+            if h.exists() and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+    return seen
+
+
 def _needs(obj: Path, src: Path, headers) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+    deps = _includes(src) & set(headers)
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in deps)
 
 
 def _run(cmd):
@@ -79,7 +93,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _needs(o, s, headers):
             # the split-bf16 GEMM keeps its f32 residual subtractions scalar: packed f32 VALU
             # (v_pk_add_f32) costs ~4x a v_sub_f32's issue slot beside MFMAs
-            extra = ["-fno-slp-vectorize"] if s.name == "gemm_f32_fast.hip" else []
+            extra = ["-fno-slp-vectorize"] if s.name in ("gemm_f32_fast.hip", "gemm_planes.hip") else []
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, "-ffp-contract=fast",
                               *extra, "-c", str(s), "-o", str(o)])
     for s in cpp_srcs:

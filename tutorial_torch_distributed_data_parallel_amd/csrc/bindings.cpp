@@ -15,6 +15,7 @@
 #include "comm.h"
 #include "conv.h"
 #include "kernels.h"
+#include "planes.h"
 #include "loader.h"
 #include "pool.h"
 #include "reducer.h"
@@ -149,6 +150,74 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
   gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
   return epi;
+}
+
+// Skinny GEMM from the bf16 split planes of A (csrc/gemm_planes.hip):
+//   Ap [3][M][K] bf16 (contiguous), B [N][K] (b_kcontig) or [K][N] fp32, C [M][N] fp32;
+//   out_planes (optional) [3][M][N] bf16 receives the planes of the finished C.
+void gemm_planes_op(const Tensor& Ap, const Tensor& B, Tensor& C, bool b_kcontig,
+                    const c10::optional<Tensor>& bias, bool relu,
+                    const c10::optional<Tensor>& gate, const c10::optional<Tensor>& out_planes) {
+  CHECK_GPU(Ap); CHECK_GPU(B); CHECK_GPU(C);
+  TORCH_CHECK(Ap.scalar_type() == at::kBFloat16 && Ap.dim() == 3 && Ap.size(0) == 3 &&
+                  Ap.is_contiguous(), "gemm_planes: Ap must be a contiguous [3, M, K] bf16 tensor");
+  CHECK_F32(B); CHECK_F32(C); CHECK_ROWMAJOR(B); CHECK_ROWMAJOR(C);
+  const int M = (int)C.size(0), N = (int)C.size(1), K = (int)Ap.size(2);
+  TORCH_CHECK(Ap.size(1) == M, "gemm_planes: A rows != C rows");
+  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm_planes: B cols != C cols");
+  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm_planes: inner dims differ");
+  GemmPlanesArgs a;
+  a.Ap = reinterpret_cast<const uint16_t*>(Ap.data_ptr());
+  a.ps = Ap.stride(0); a.lda = Ap.stride(1);
+  a.B = B.data_ptr<float>(); a.ldb = B.stride(0); a.b_kcontig = b_kcontig;
+  a.C = C.data_ptr<float>(); a.ldc = C.stride(0);
+  a.M = M; a.N = N; a.K = K;
+  a.relu = relu;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_GPU(*bias); CHECK_F32(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == N, "gemm_planes: bias must have N elements");
+    a.bias = bias->data_ptr<float>();
+  }
+  if (gate.has_value() && gate->defined()) {
+    CHECK_GPU(*gate); CHECK_F32(*gate); CHECK_ROWMAJOR(*gate);
+    TORCH_CHECK(gate->size(0) == M && gate->size(1) == N, "gemm_planes: gate must have C's shape");
+    a.gate = gate->data_ptr<float>();
+    a.ldgate = gate->stride(0);
+  }
+  if (out_planes.has_value() && out_planes->defined()) {
+    const Tensor& o = *out_planes;
+    CHECK_GPU(o);
+    TORCH_CHECK(o.scalar_type() == at::kBFloat16 && o.is_contiguous() && o.dim() == 3 &&
+                    o.size(0) == 3 && o.size(1) == M && o.size(2) == N,
+                "gemm_planes: out_planes must be a contiguous [3, M, N] bf16 tensor");
+    a.out_planes = reinterpret_cast<uint16_t*>(o.data_ptr());
+    a.out_ps = o.stride(0);
+  }
+  TORCH_CHECK(gemm_planes_ok(a), "gemm_planes: unsupported shape / alignment (K % 32, N % 4, "
+              "16-B aligned rows)");
+  const GemmPlan plan = gemm_planes_plan(a, num_cus(C.get_device()));
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
+  gemm_planes_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+}
+
+// x [rows, cols] fp32 (unit inner stride) -> its exact bf16 split planes [3, rows, cols]
+Tensor split_planes_op(const Tensor& x) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_ROWMAJOR(x);
+  const int rows = (int)x.size(0), cols = (int)x.size(1);
+  TORCH_CHECK(cols % 4 == 0 && x.stride(0) % 4 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0,
+              "split_planes: cols % 4 == 0 and 16-B aligned rows required");
+  Tensor p = at::empty({3, rows, cols}, x.options().dtype(at::kBFloat16));
+  split_planes(x.data_ptr<float>(), x.stride(0), rows, cols,
+               reinterpret_cast<uint16_t*>(p.data_ptr()), p.stride(0), cur_stream());
+  return p;
+}
+
+std::vector<int64_t> gemm_planes_plan_op(int M, int N, int K, int cus) {
+  GemmPlanesArgs a;
+  a.M = M; a.N = N; a.K = K;
+  const GemmPlan p = gemm_planes_plan(a, cus);
+  return {p.splits, p.k_per_split, p.ws_floats};
 }
 
 std::vector<int64_t> gemm_f32_plan_op(int M, int N, int K, bool rowsum, int cus) {
@@ -860,7 +929,8 @@ Tensor relu_mask_op(const Tensor& dy, const Tensor& y) {
 }
 
 // x [n, ...] fp32 contiguous, y [n] int64, idx [B] int64 (all on the GPU) -> (x[idx], y[idx])
-std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tensor& idx) {
+std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tensor& idx,
+                                    bool planes) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_GPU(y); CHECK_CONTIG(y); CHECK_GPU(idx);
   CHECK_CONTIG(idx);
   TORCH_CHECK(y.scalar_type() == at::kLong && idx.scalar_type() == at::kLong && idx.dim() == 1,
@@ -873,6 +943,14 @@ std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tens
   xs[0] = B;
   auto xb = at::empty(xs, x.options());
   auto yb = at::empty({B}, y.options());
+  if (planes && F % 4 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0) {
+    // also the bf16 split planes of the batch rows [3][B][F] (the planes GEMM's A operand)
+    auto p = at::empty({3, (long)B, F}, x.options().dtype(at::kBFloat16));
+    gather_batch_planes(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F,
+                        B, xb.data_ptr<float>(), yb.data_ptr<int64_t>(),
+                        reinterpret_cast<uint16_t*>(p.data_ptr()), cur_stream());
+    return {xb, yb, p};
+  }
   gather_batch(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F, B,
                xb.data_ptr<float>(), yb.data_ptr<int64_t>(), cur_stream());
   return {xb, yb};
@@ -1180,6 +1258,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
         py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0);
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
+  m.def("gemm_planes", &gemm_planes_op, py::arg("Ap"), py::arg("B"), py::arg("C"),
+        py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,
+        py::arg("gate") = py::none(), py::arg("out_planes") = py::none());
+  m.def("split_planes", &split_planes_op);
+  m.def("gemm_planes_plan", &gemm_planes_plan_op);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);
   m.def("gemm_f32_set_cvec", &gemm_f32_set_cvec);
@@ -1299,7 +1382,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
   }, py::arg("g"), py::arg("x"), py::arg("g_all"), py::arg("x_all"), py::arg("rank"),
      py::arg("alpha"), py::arg("slot_rows") = -1);
-  m.def("gather_batch", &gather_batch_op);
+  m.def("gather_batch", &gather_batch_op, py::arg("x"), py::arg("y"), py::arg("idx"),
+        py::arg("planes") = false);
   m.def("image_transform", &image_transform_op, py::arg("x"), py::arg("flip"), py::arg("Ho"),
         py::arg("Wo"), py::arg("mean"), py::arg("std"), py::arg("round_u8") = true,
         py::arg("channels_last") = true);

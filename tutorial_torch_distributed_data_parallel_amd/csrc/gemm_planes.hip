@@ -1,0 +1,596 @@
+// Skinny-M fp32 GEMM whose A operand arrives pre-split into three bf16 planes (gfx950).
+//
+// Why (profiles/micro/gemm_split_cost_exp_r5d.jsonl, gemm_emu_pmc_r4.md): the split-bf16 fast GEMM
+// (gemm_f32_fast.hip) splits every fp32 fragment on the VALU inside the K loop, once per wave that
+// reads it. For the toy-MLP's skinny GEMMs (M = batch = 128 rows against 4096-9216 columns and
+// K = 4096-9216) the small operand A is re-read by every column tile -- 32 tiles x 2 column waves
+// = 64 redundant splits of each activation -- while the weight B is streamed from HBM once. Here
+// A is split ONCE (by its producer: the gather / split-K reduce / loss head, or split_planes) into
+// exact bf16 hi / mid / lo planes x = x0 + x1 + x2 (csrc/gemm_f32_fast.hip split3_pair: the same
+// RNE conversions, so the planes are bit-identical to the in-kernel split), and the kernel is
+// laid out so that each weight fragment is split by exactly ONE wave:
+//   * block tile 128 (all batch rows) x 128 columns, 4 waves side by side (1 x 4): wave w owns
+//     columns 32w..32w+31 and all four 32-row MFMA tiles, so its one B fragment per 16-deep K step
+//     feeds 4 x 6 v_mfma_f32_32x32x16_bf16 (the six kept split products, smallest first) and its
+//     split (~36 VALU) hides under 24 MFMAs (the fast kernel's 2 x 2 waves split 4 fragments per
+//     24 MFMAs);
+//   * both operands go global -> LDS by global_load_lds_dwordx4 (no VGPR staging), 2 stages of
+//     40 KiB (A planes 3 x 8 KiB + B 16 KiB), two workgroups per CU (80 KiB each, 160 KiB LDS);
+//     one `s_waitcnt vmcnt(0)` + raw barrier per 32-deep K tile, the next tile's DMA in flight
+//     behind the current tile's MFMAs;
+//   * A plane rows are 64 B ([128 rows][32 k] bf16): 16-B chunk c of row r sits in slot
+//     c ^ ((r >> 2) & 3), so the 16 lanes of a ds_read_b128 phase (rows r..r+15) hit all 64 banks;
+//     K-contiguous B rows are 128 B with the fast kernel's (r ^ r >> 3) & 7 swizzle;
+//     MN-contiguous B ([32 k][128 cols], the input gradient's W [out][in]) is read per column;
+//   * split-K fills the chip (tiles x splits ~ 2 per CU); partial tiles go to a workspace combined
+//     by planes_reduce_kernel, whose epilogue (bias, ReLU, C-shaped gate) can also emit the bf16
+//     planes of the finished output for the NEXT skinny GEMM (fc1 forward -> fc2 forward).
+// Numerics equal the fast kernel's split path (same six products of the same exact terms; only
+// the fp32 summation order differs): tests/test_gemm_planes_gpu.py checks both against fp64.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+
+#include "common.h"
+#include "kernels.h"
+#include "planes.h"
+
+namespace tdp {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kBK = 32;
+constexpr int kBM = 128, kBN = 128;
+constexpr int kAPlane = kBM * kBK * 2;  // 8 KiB: [128 rows][32 k] bf16
+constexpr int kABytes = 3 * kAPlane;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef char lds_char;
+
+struct PParams {
+  const uint16_t* Ap;
+  long ps, lda;
+  const float* B;
+  long ldb;
+  float* C;
+  long ldc;
+  float* ws;
+  const float* bias;
+  const float* gate;
+  long ldg;
+  uint16_t* op;  // optional planes of the finished C: [3][M][N], plane stride ops
+  long ops;
+  int relu;
+  int M, N, K, kps, splits, tiles_n, tiles_mn;
+  int prio;
+  int exp;  // timing experiments only (TDP_PLANES_EXP, numerically WRONG when set): bit 0 skips
+            // the MFMA step, bit 1 the B DMA, bit 2 the A DMA, bit 3 the epilogue stores
+};
+
+// exact 3-way bf16 split of a pair (identical instruction sequence to gemm_f32_fast.hip
+// split3_pair: RNE v_cvt_pk_bf16_f32, scalar f32 residuals)
+__device__ __forceinline__ void split_pair(float x0, float x1, unsigned& h, unsigned& m,
+                                           unsigned& l) {
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf2));
+  const float r0 = x0 - __uint_as_float(hu << 16), r1 = x1 - __uint_as_float(hu & 0xffff0000u);
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{r0, r1}, bf2));
+  const float s0 = r0 - __uint_as_float(mu << 16), s1 = r1 - __uint_as_float(mu & 0xffff0000u);
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{s0, s1}, bf2));
+}
+
+__device__ __forceinline__ void split_x8(const float (&x)[8], bf8& h, bf8& m, bf8& l) {
+  unsigned hs[4], ms[4], ls[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split_pair(x[2 * i], x[2 * i + 1], hs[i], ms[i], ls[i]);
+  h = __builtin_bit_cast(bf8, u32x4{hs[0], hs[1], hs[2], hs[3]});
+  m = __builtin_bit_cast(bf8, u32x4{ms[0], ms[1], ms[2], ms[3]});
+  l = __builtin_bit_cast(bf8, u32x4{ls[0], ls[1], ls[2], ls[3]});
+}
+
+// acc += a*b over the six kept split terms (smallest first; a1b2 + a2b1 + a2b2 dropped)
+__device__ __forceinline__ f32x16 mfma6(const bf8& ah, const bf8& am, const bf8& al, const bf8& bh,
+                                        const bf8& bm, const bf8& bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ void glds16(const void* src, lds_char* dst) {
+  __builtin_amdgcn_global_load_lds(
+      src, (void __attribute__((address_space(3)))*)(
+               (__attribute__((address_space(3))) char*)dst), 16, 0, 0);
+}
+
+__device__ __forceinline__ int aswz(int row) { return (row >> 2) & 3; }
+__device__ __forceinline__ int bswz(int row) { return (row ^ (row >> 3)) & 7; }
+
+// bias, ReLU, gate of four adjacent finished outputs, then C (16-B store) and, when requested,
+// the three bf16 planes of the result (8-B stores)
+__device__ __forceinline__ void finish4(const PParams& p, int row, int col, f32x4 v) {
+  if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
+  if (p.relu) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+  }
+  if (p.gate) {
+    const f32x4 g = *reinterpret_cast<const f32x4*>(p.gate + (long)row * p.ldg + col);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = g[c] > 0.f ? v[c] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + col) = v;
+  if (p.op) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
+    uint16_t* o = p.op + (long)row * p.N + col;
+    *reinterpret_cast<u32x2*>(o) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(o + p.ops) = u32x2{m0, m1};
+    *reinterpret_cast<u32x2*>(o + 2 * p.ops) = u32x2{l0, l1};
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// S pipeline stages; WN 32-column MFMA tiles per wave (block tile 128 x 128*WN: WN = 2 halves
+// the A (L2) traffic per MFMA at 112 KiB of LDS, one workgroup per CU)
+template <bool BKC, int S, int WN, int PF>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(WN == 1 ? 2 : 1))) void gemm_planes_kernel(
+    PParams p) {
+  constexpr int BN = kBN * WN;
+  constexpr int BBYTES = BN * kBK * 4;
+  constexpr int STG = kABytes + BBYTES;
+  constexpr int GB = BBYTES / 1024 / 4;  // B chunks per wave per tile
+  constexpr int G = 6 + GB;              // LDS-DMA loads per wave per tile
+  static_assert(PF == 0 || S == 2, "the B prefetch's counted waits assume two stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l31 = lane & 31;
+  // two workgroups share each SIMD running the same read / split / MFMA sequence; a static
+  // priority for every other hardware slot keeps them out of lockstep (TDP_PLANES_PRIO=0: off)
+  if (p.prio && ((blockIdx.x >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
+  // XCD-aware order (bijective): hardware ids b and b + 8 share an XCD; each XCD takes a
+  // contiguous range of logical tiles, split-major, so an XCD's workgroups share A's K slices
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  const int z = lid / p.tiles_mn, t = lid % p.tiles_mn;
+  const int m0 = (t / p.tiles_n) * kBM, n0 = (t % p.tiles_n) * BN;
+  const int kb = z * p.kps;
+  const int ke = min(p.K, kb + p.kps);
+  const int nk = (ke - kb) / kBK;  // K and kps are multiples of 32 (host-checked)
+
+  // per-lane DMA sources: A = 24 1-KiB chunks (3 planes x 8 row blocks of 16 rows), 6 per wave;
+  // B = BN/8 chunks, GB per wave. Out-of-range rows / columns are clamped (discarded outputs).
+  const uint16_t* abase[6];
+  int adst[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int j = w * 6 + i, plane = j >> 3, rb = j & 7;
+    const int row = rb * 16 + (lane >> 2);
+    const int gr = min(m0 + row, p.M - 1);
+    const int c = (lane & 3) ^ aswz(row);
+    abase[i] = p.Ap + plane * p.ps + (long)gr * p.lda + c * 8;
+    adst[i] = plane * kAPlane + rb * 1024;
+  }
+  const float* bbase[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int j = w * GB + i;
+    if (BKC) {  // [BN rows][32 k] fp32, 128-B rows, 8 rows per chunk
+      const int row = j * 8 + (lane >> 3);
+      const int gr = min(n0 + row, p.N - 1);
+      bbase[i] = p.B + (long)gr * p.ldb + ((lane & 7) ^ bswz(row)) * 4;
+    } else {    // [32 k][BN cols] fp32, BN*4-B rows, 1024 / (BN*4) rows per chunk
+      constexpr int LPR = BN / 4, RPC = 1024 / (BN * 4);
+      const int krow = RPC * j + lane / LPR;
+      const int gc = min(n0 + (lane % LPR) * 4, p.N - 4);
+      bbase[i] = p.B + (long)krow * p.ldb + gc;
+    }
+  }
+  // tiles past the end are re-issued at the last tile (same addresses, a stage nobody reads):
+  // every iteration then has the same loads in flight, so one counted vmcnt fits all
+  auto issue = [&](int kt) {
+    lds_char* st = smem + (kt % S) * STG;
+    const int k0 = kb + min(kt, nk - 1) * kBK;
+    if (!(p.exp & 4)) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) glds16(abase[i] + k0, st + adst[i]);
+    }
+    if (p.exp & 2) return;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const float* src = BKC ? bbase[i] + k0 : bbase[i] + (long)k0 * p.ldb;
+      glds16(src, st + kABytes + (w * GB + i) * 1024);
+    }
+  };
+
+  f32x16 acc[4][WN];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int g = 0; g < WN; ++g)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][g][r] = 0.f;
+
+  // B prefetch into L2 (PF > 0, two stages only): one dword per 128-B line of the B tile PF
+  // tiles beyond the one being DMA'd, so the HBM latency of B is paid PF tiles early and the
+  // LDS-DMA hits L2. The load lands in a dummy VGPR that must stay allocated until the load has
+  // completed: the counted wait two iterations later covers it (in-order vmcnt), so two dummies
+  // alternate (d0 even iterations, d1 odd) and each is consumed (kept live) until then.
+  auto prefetch = [&](int kt, float& d) {
+    const int k0 = kb + min(kt, nk - 1) * kBK;
+    const int line = w * 32 + l31;  // 128 lines of 128 B per B tile (lanes 32-63 duplicate)
+    const float* src;
+    if (BKC) src = p.B + (long)min(n0 + line, p.N - 1) * p.ldb + k0;
+    else src = p.B + (long)(k0 + (line >> 2)) * p.ldb + min(n0 + (line & 3) * 32, p.N - 4);
+    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(src) : "memory");
+  };
+  // One 32-deep tile = two 16-deep MFMA steps. Software-pipelined by hand (the compiler's own
+  // schedule re-used one register set and waited for every 3-fragment LDS read before each
+  // group of 6 MFMAs): both steps' B fragments and step 0's A fragments are read up front, step
+  // 1's A fragments are in flight while step 0's 24 MFMAs issue, and step 1's B split runs on
+  // the VALU between them (1 MFMA : 2 VALU groups).
+  auto read_b = [&](const lds_char* st, int s, float (&bv)[8]) {
+    const int bcol = w * 32 + l31;
+    if (BKC) {
+      const int c0 = 4 * s + 2 * h;
+      const f32x4 v0 =
+          *reinterpret_cast<const f32x4*>(st + kABytes + bcol * 128 + ((c0 ^ bswz(bcol)) * 16));
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(st + kABytes + bcol * 128 +
+                                                       (((c0 + 1) ^ bswz(bcol)) * 16));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bv[j] = v0[j];
+        bv[4 + j] = v1[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bv[j] = *reinterpret_cast<const float*>(st + kABytes +
+                                                ((16 * s + 8 * h + j) * BN + bcol) * 4);
+    }
+  };
+  auto read_a = [&](const lds_char* st, int s, bf8 (&a)[4][3]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int row = f * 32 + l31;
+      const int off = row * 64 + (((2 * s + h) ^ aswz(row)) * 16);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[f][q] = *reinterpret_cast<const bf8*>(st + q * kAPlane + off);
+    }
+  };
+  auto compute = [&](int kt) {
+    static_assert(WN == 1, "the hand-pipelined step is written for 32 columns per wave");
+    const lds_char* st = smem + (kt % S) * STG;
+    float b0[8], b1[8];
+    bf8 a0[4][3], a1[4][3];
+    bf8 x0[3];
+    unsigned h1[4], m1[4], l1[4];
+    // B of both steps and half of step 0's A, then step 0's B split (a counted lgkmcnt: at most
+    // 15 reads may be outstanding), then the rest of step 0's A
+    read_b(st, 0, b0);
+    read_b(st, 1, b1);
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int row = f * 32 + l31;
+        a0[f][q] = *reinterpret_cast<const bf8*>(st + q * kAPlane + row * 64 +
+                                                 ((h ^ aswz(row)) * 16));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    split_x8(b0, x0[0], x0[1], x0[2]);
+#pragma unroll
+    for (int f = 2; f < 4; ++f)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int row = f * 32 + l31;
+        a0[f][q] = *reinterpret_cast<const bf8*>(st + q * kAPlane + row * 64 +
+                                                 ((h ^ aswz(row)) * 16));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    // step 0: row tile f's six MFMAs, then step 1's A reads of tile f and a quarter of step 1's
+    // B split (in-order LDS returns keep every wait a counted lgkmcnt <= 9)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      acc[f][0] = mfma6(a0[f][0], a0[f][1], a0[f][2], x0[0], x0[1], x0[2], acc[f][0]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int row = f * 32 + l31;
+        a1[f][q] = *reinterpret_cast<const bf8*>(st + q * kAPlane + row * 64 +
+                                                 (((2 + h) ^ aswz(row)) * 16));
+      }
+      split_pair(b1[2 * f], b1[2 * f + 1], h1[f], m1[f], l1[f]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bf8 y0 = __builtin_bit_cast(bf8, u32x4{h1[0], h1[1], h1[2], h1[3]});
+    const bf8 y1 = __builtin_bit_cast(bf8, u32x4{m1[0], m1[1], m1[2], m1[3]});
+    const bf8 y2 = __builtin_bit_cast(bf8, u32x4{l1[0], l1[1], l1[2], l1[3]});
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f][0] = mfma6(a1[f][0], a1[f][1], a1[f][2], y0, y1, y2, acc[f][0]);
+  };
+  float d0 = 0.f, d1 = 0.f;
+  auto step = [&](int kt, float& d) {
+    // tile kt has landed when at most the S - 2 younger tiles' loads (and the newest prefetch)
+    // are still in flight
+    if constexpr (PF > 0) {
+      wait_vmcnt<1>();
+      asm volatile("" ::"v"(d));  // the prefetch of two iterations ago has completed
+    } else {
+      wait_vmcnt<(S - 2) * G>();
+    }
+    // every LDS read of the stage the next DMA overwrites has returned (the scheduler may sink
+    // the MFMAs that consume the last reads below the barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(kt + S - 1);
+    if constexpr (PF > 0) prefetch(kt + S - 1 + PF, d);
+    if (!(p.exp & 1)) compute(kt);
+  };
+  if (nk > 0) {
+#pragma unroll
+    for (int t = 0; t < S - 1; ++t) issue(t);
+    if constexpr (PF > 0) prefetch(S - 1 + PF - 1, d1);
+  }
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, d0);
+    step(kt + 1, d1);
+  }
+  if (kt < nk) step(kt, d0);
+  asm volatile("" ::"v"(d0), "v"(d1));
+
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+  // Epilogue through LDS (the stages are free once every wave has left the K loop): the MFMA
+  // layout gives a lane one column of 16 rows -- dword stores, and the store tail of 512
+  // workgroups writing 64 KiB each was issue-bound (18 us of a 57-us fc1 forward with the K loop
+  // emptied, TDP_PLANES_EXP=7). Staged, every thread stores 16-B row segments: a partial tile to
+  // the workspace, or the finished tile (bias / ReLU / gate / planes).
+  static_assert(WN == 1 && kBM * (BN + 4) * 4 <= S * STG, "the C tile must fit in the stages");
+  constexpr int TS = BN + 4;  // padded LDS row (floats)
+  float* T = reinterpret_cast<float*>(smem);
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      T[(f * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * TS + w * 32 + l31] = acc[f][0][r];
+  __syncthreads();
+  constexpr int C4 = BN / 4;             // float4 per tile row
+  constexpr int IT = kBM * C4 / kT;      // float4 per thread
+  float* ws = p.ws + (long)z * p.M * p.N;
+#pragma unroll 4
+  for (int i = 0; i < IT; ++i) {
+    const int e = i * kT + threadIdx.x;
+    const int lr = e / C4, lc = (e % C4) * 4;
+    const int row = m0 + lr, col = n0 + lc;
+    if (row >= p.M || col >= p.N || (p.exp & 8)) continue;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + lr * TS + lc);
+    if (p.splits > 1) *reinterpret_cast<f32x4*>(ws + (long)row * p.N + col) = v;
+    else finish4(p, row, col, v);
+  }
+}
+
+// C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread
+__global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
+  const long ng = (long)p.M * p.N / 4;
+  const long idx = (long)blockIdx.x * kT + threadIdx.x;
+  if (idx >= ng) return;
+  const f32x4* src = reinterpret_cast<const f32x4*>(p.ws) + idx;
+  f32x4 a = src[0];
+#pragma unroll 4
+  for (int z = 1; z < p.splits; ++z) a += src[z * ng];
+  const long e0 = idx * 4;
+  const int row = (int)(e0 / p.N), col = (int)(e0 - (long)row * p.N);
+  finish4(p, row, col, a);
+}
+
+// x [rows][cols] (row stride ldx) -> planes [3][rows][cols] (plane stride ps), cols % 4 == 0
+__global__ __launch_bounds__(kT) void split_planes_kernel(const float* __restrict__ x, long ldx,
+                                                          int rows, int cols, uint16_t* planes,
+                                                          long ps) {
+  const long ng = (long)rows * cols / 4;
+  for (long idx = (long)blockIdx.x * kT + threadIdx.x; idx < ng; idx += (long)gridDim.x * kT) {
+    const long e0 = idx * 4;
+    const int row = (int)(e0 / cols), col = (int)(e0 - (long)row * cols);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + (long)row * ldx + col);
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
+    uint16_t* o = planes + (long)row * cols + col;
+    *reinterpret_cast<u32x2*>(o) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(o + ps) = u32x2{m0, m1};
+    *reinterpret_cast<u32x2*>(o + 2 * ps) = u32x2{l0, l1};
+  }
+}
+
+// gather_batch_kernel (elementwise.hip) + the planes of every gathered float4: the toy-MLP's
+// first Linear reads its input batch as planes without a separate split pass
+__global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restrict__ x,
+                                                           const int64_t* __restrict__ y,
+                                                           const int64_t* __restrict__ idx, long n,
+                                                           long F, float* __restrict__ xb,
+                                                           int64_t* __restrict__ yb,
+                                                           uint16_t* __restrict__ planes,
+                                                           long ps) {
+  const int b = blockIdx.x;
+  long i = idx[b];
+  i = i < 0 ? 0 : (i >= n ? n - 1 : i);  // indices checked on the host; clamped so none faults
+  const f32x4* src = reinterpret_cast<const f32x4*>(x + i * F);
+  f32x4* dst = reinterpret_cast<f32x4*>(xb + (long)b * F);
+  uint16_t* o = planes + (long)b * F;
+  const long F4 = F >> 2, step = (long)kT * gridDim.y;
+  for (long k = threadIdx.x + (long)kT * blockIdx.y; k < F4; k += step) {
+    const f32x4 v = src[k];
+    dst[k] = v;
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
+    *reinterpret_cast<u32x2*>(o + 4 * k) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(o + ps + 4 * k) = u32x2{m0, m1};
+    *reinterpret_cast<u32x2*>(o + 2 * ps + 4 * k) = u32x2{l0, l1};
+  }
+  if (threadIdx.x == 0 && blockIdx.y == 0) yb[b] = y[i];
+}
+
+inline bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+// variant: pipeline depth (2 stages: 80 KiB, two workgroups per CU; 3: 120 KiB, one) and the
+// B prefetch distance in tiles (0 = off; two stages only). TDP_PLANES_CFG = "S,PF"
+// (measurements); default 2,0
+struct PlanesCfg {
+  int stages, pf;
+};
+PlanesCfg& planes_cfg() {
+  static PlanesCfg c = [] {
+    PlanesCfg v{2, 0};
+    if (const char* e = std::getenv("TDP_PLANES_CFG")) {
+      int a = 0, b = 0;
+      if (std::sscanf(e, "%d,%d", &a, &b) == 2 && (a == 2 || a == 3) && b >= 0 && b <= 4 &&
+          (a == 2 || b == 0))
+        v = {a, b};
+    }
+    return v;
+  }();
+  return c;
+}
+
+template <bool BKC, int S, int PF>
+void launch_planes(const PParams& p, int nblocks, hipStream_t s) {
+  const size_t lds = (size_t)S * (kABytes + kBN * kBK * 4);
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)gemm_planes_kernel<BKC, S, 1, PF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    configured = true;
+  }
+  hipLaunchKernelGGL((gemm_planes_kernel<BKC, S, 1, PF>), dim3(nblocks), dim3(kT), lds, s, p);
+}
+
+template <bool BKC>
+void launch_cfg(const PParams& p, const PlanesCfg& c, int nblocks, hipStream_t s) {
+  if (c.stages == 3) launch_planes<BKC, 3, 0>(p, nblocks, s);
+  else if (c.pf == 1) launch_planes<BKC, 2, 1>(p, nblocks, s);
+  else if (c.pf == 2) launch_planes<BKC, 2, 2>(p, nblocks, s);
+  else if (c.pf >= 3) launch_planes<BKC, 2, 3>(p, nblocks, s);
+  else launch_planes<BKC, 2, 0>(p, nblocks, s);
+}
+
+}  // namespace
+
+void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
+                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s) {
+  if (F % 4 || !al16(x) || !al16(xb) || ((uintptr_t)planes & 7))
+    throw std::runtime_error("gather_batch_planes: F % 4 == 0 and aligned buffers required");
+  if (B <= 0) return;
+  // row slices: B = 128 rows alone would leave half of the 256 CUs idle
+  const long F4 = F / 4;
+  const int slices = (int)std::max<long>(1, std::min<long>(8, (F4 + kT - 1) / kT));
+  hipLaunchKernelGGL(gather_planes_kernel, dim3(B, slices), dim3(kT), 0, s, x, y, idx, n, F, xb,
+                     yb, planes, (long)B * F);
+}
+
+bool gemm_planes_ok(const GemmPlanesArgs& a) {
+  if (a.M <= 0 || a.N < 4 || a.K < kBK || a.K % kBK) return false;
+  if (!al16(a.Ap) || a.lda % 8 || a.ps % 8 || !al16(a.B) || a.ldb % 4) return false;
+  if (a.N % 4 || a.ldc % 4 || !al16(a.C)) return false;
+  if (a.bias && !al16(a.bias)) return false;
+  if (a.gate && (!al16(a.gate) || a.ldgate % 4)) return false;
+  if (a.out_planes && (((uintptr_t)a.out_planes & 7) || a.out_ps % 4)) return false;
+  return true;
+}
+
+GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus) {
+  GemmPlan plan;
+  plan.fast = true;
+  plan.bm = kBM;
+  const PlanesCfg cfg = planes_cfg();
+  plan.bn = kBN;
+  plan.stages = cfg.stages;
+  const long tiles = (long)ceil_div(a.M, kBM) * ceil_div(a.N, plan.bn);
+  // two workgroups per CU when both fit (2 stages), else one
+  const long target = (cfg.stages == 2 ? 2L : 1L) * num_cus;
+  int splits = 1;
+  static const int force = [] {  // TDP_PLANES_SPLITS: split-K override (measurements)
+    const char* e = std::getenv("TDP_PLANES_SPLITS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (force > 0) {
+    splits = force;
+  } else if (tiles < target) {
+    const int want = (int)((target + tiles - 1) / tiles);
+    const int kmax = a.K / (kBK * 4);  // >= 4 K tiles per split
+    splits = want < kmax ? want : kmax;
+    if (splits < 1) splits = 1;
+  }
+  const int kps = ceil_div(ceil_div(a.K, splits), kBK) * kBK;
+  plan.k_per_split = kps;
+  plan.splits = ceil_div(a.K, kps);
+  plan.ws_floats = plan.splits > 1 ? (long)plan.splits * a.M * a.N : 0;
+  return plan;
+}
+
+void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+  if (!gemm_planes_ok(a)) throw std::runtime_error("gemm_planes: unsupported operands");
+  PParams p{};
+  p.Ap = a.Ap; p.ps = a.ps; p.lda = a.lda;
+  p.B = a.B; p.ldb = a.ldb;
+  p.C = a.C; p.ldc = a.ldc;
+  p.ws = ws;
+  p.bias = a.bias; p.gate = a.gate; p.ldg = a.ldgate;
+  p.op = a.out_planes; p.ops = a.out_ps;
+  p.relu = a.relu ? 1 : 0;
+  p.M = a.M; p.N = a.N; p.K = a.K;
+  static const int exp = [] {
+    const char* e = std::getenv("TDP_PLANES_EXP");
+    return e ? std::atoi(e) : 0;
+  }();
+  p.exp = exp;
+  static const int prio = [] {
+    const char* e = std::getenv("TDP_PLANES_PRIO");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  p.prio = prio;
+  p.kps = plan.k_per_split;
+  p.splits = plan.splits;
+  p.tiles_n = ceil_div(a.N, plan.bn);
+  p.tiles_mn = ceil_div(a.M, kBM) * p.tiles_n;
+  if (plan.splits > 1 && ws == nullptr) throw std::runtime_error("gemm_planes: workspace missing");
+  const int nblocks = p.tiles_mn * plan.splits;
+  if (a.b_kcontig) launch_cfg<true>(p, planes_cfg(), nblocks, s);
+  else launch_cfg<false>(p, planes_cfg(), nblocks, s);
+  if (plan.splits > 1) {
+    const long ng = (long)a.M * a.N / 4;
+    hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
+                       p);
+  }
+}
+
+void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,
+                  hipStream_t s) {
+  if (cols % 4 || ldx % 4 || !al16(x) || ((uintptr_t)planes & 7) || ps % 4)
+    throw std::runtime_error("split_planes: needs cols % 4 == 0 and aligned rows");
+  const long ng = (long)rows * cols / 4;
+  if (ng <= 0) return;
+  const unsigned grid = (unsigned)std::min<long>((ng + kT - 1) / kT, 8192);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(grid), dim3(kT), 0, s, x, ldx, rows, cols, planes,
+                     ps);
+}
+
+}  // namespace tdp

@@ -1,0 +1,42 @@
+// Host API of the bf16-split-planes kernels (csrc/gemm_planes.hip): the skinny GEMM that reads
+// its activation operand as exact bf16 hi / mid / lo planes, and the producers of such planes.
+#pragma once
+#include "kernels.h"
+
+namespace tdp {
+
+// Skinny-M fp32 GEMM from pre-split bf16 planes of A (csrc/gemm_planes.hip):
+//   C[M,N] = A[M,K] . op(B)[K,N] (+bias)(ReLU)(* (gate > 0)), A given as its exact bf16 split
+//   planes Ap [3][M][K] (x = hi + mid + lo, plane stride ps, row stride lda; split_planes or a
+//   producer's epilogue makes them), B fp32 [N][K] (b_kcontig) or [K][N]. K % 32 == 0.
+//   out_planes (optional): the planes of the finished C ([3][M][N], plane stride out_ps) for the
+//   next skinny GEMM that reads C as its A.
+struct GemmPlanesArgs {
+  const uint16_t* Ap = nullptr;
+  long ps = 0, lda = 0;
+  const float* B = nullptr;
+  long ldb = 0;
+  bool b_kcontig = true;
+  float* C = nullptr;
+  long ldc = 0;
+  const float* bias = nullptr;
+  bool relu = false;
+  const float* gate = nullptr;
+  long ldgate = 0;
+  uint16_t* out_planes = nullptr;
+  long out_ps = 0;
+  int M = 0, N = 0, K = 0;
+};
+bool gemm_planes_ok(const GemmPlanesArgs& a);
+GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus);
+void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s);
+// x [rows][cols] (row stride ldx, cols % 4 == 0) -> planes [3][rows][cols] (plane stride ps)
+void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,
+                  hipStream_t s);
+
+// gather_batch (kernels.h) that also writes the planes of the gathered rows: planes [3][B][F]
+// (plane stride B*F), F % 4 == 0
+void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
+                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s);
+
+}  // namespace tdp

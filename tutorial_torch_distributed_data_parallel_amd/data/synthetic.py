@@ -77,7 +77,15 @@ def gather_batch(x: torch.Tensor, y: torch.Tensor, idx: torch.Tensor):
             idx.dtype == torch.long and x.is_contiguous() and y.is_contiguous() and
             idx.is_contiguous() and y.device == x.device and len(idx) > 0):
         from .._native import native
+        from ..ops.linear import attach_planes, planes_input_fit
 
+        if x.dim() == 2 and planes_input_fit(len(idx), x.shape[1]):
+            # a feature batch for a skinny Linear: its bf16 split planes come out of the same
+            # launch (ops/linear.py planes GEMM)
+            r = native().gather_batch(x, y, idx, planes=True)
+            if len(r) == 3:
+                attach_planes(r[0], r[2])
+            return r[0], r[1]
         xb, yb = native().gather_batch(x, y, idx)
         return xb, yb
     return x.index_select(0, idx), y.index_select(0, idx)

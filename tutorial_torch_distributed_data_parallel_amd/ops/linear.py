@@ -16,8 +16,57 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+import os
+
 from .._native import native
 from ._grad import epilogue_target, factor_target, grad_dest, needs, note_use
+
+# Skinny GEMMs (batch rows against thousands of features) read their activation operand from
+# its exact bf16 split planes (csrc/gemm_planes.hip): split once by the producer instead of once
+# per column tile inside the GEMM. TDP_PLANES=0 keeps the in-kernel split (A/B measurements).
+_PLANES = os.environ.get("TDP_PLANES", "1") != "0"
+
+
+def planes_fit(M: int, N: int, K: int) -> bool:
+    """The planes GEMM applies: few rows (a batch), K a multiple of its 32-deep tile, wide N."""
+    return _PLANES and M <= 256 and K % 32 == 0 and K >= 256 and N % 4 == 0 and N >= 512
+
+
+def planes_input_fit(M: int, K: int) -> bool:
+    """A [M, K] activation may feed a planes GEMM (its producer should emit the planes)."""
+    return _PLANES and M <= 256 and K % 32 == 0 and K >= 256
+
+
+def _al16(*ts) -> bool:
+    """Every given tensor (None skipped) has 16-B aligned rows (the planes GEMM's 16-B loads)."""
+    return all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() < 2 or t.stride(0) % 4 == 0))
+               for t in ts)
+
+
+def set_planes(on: bool) -> bool:
+    """Turn the planes path on/off (tests, A/B); returns the previous setting."""
+    global _PLANES
+    old, _PLANES = _PLANES, bool(on)
+    return old
+
+
+def attach_planes(t: torch.Tensor, planes: torch.Tensor) -> None:
+    """Record that ``planes`` are the bf16 split of ``t``'s current contents."""
+    t._tdp_planes = (planes, t._version, t.data_ptr(), tuple(t.shape))
+
+
+def planes_of(t: torch.Tensor) -> torch.Tensor:
+    """The split planes of a 2-D fp32 tensor: the producer's (attach_planes) when they still
+    describe it, else one split_planes pass."""
+    for src in (t, t._base):  # a reshape view of the producer's tensor shares its planes
+        rec = getattr(src, "_tdp_planes", None) if src is not None else None
+        if rec is not None and rec[1] == src._version and rec[2] == t.data_ptr() and \
+                rec[0][0].numel() == t.numel() and rec[0].shape[1] == t.shape[0] and \
+                t.is_contiguous():
+            return rec[0] if rec[0].shape[1:] == t.shape else rec[0].view(3, *t.shape)
+    if t.stride(-1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        t = t.contiguous()
+    return native().split_planes(t)
 
 
 def _pregated(dy: torch.Tensor, y: torch.Tensor) -> bool:
@@ -35,8 +84,18 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool):
         C = native()
-        y = torch.empty((x2.shape[0], weight.shape[0]), device=x2.device, dtype=torch.float32)
-        C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
+        M, K = x2.shape
+        N = weight.shape[0]
+        y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
+        if planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
+            # a hidden layer's output also leaves as planes: the next skinny GEMM's A operand
+            op = torch.empty((3, M, N), device=x2.device, dtype=torch.bfloat16) \
+                if relu and N % 32 == 0 else None
+            C.gemm_planes(planes_of(x2), weight, y, True, bias=bias, relu=relu, out_planes=op)
+            if op is not None:
+                attach_planes(y, op)
+        else:
+            C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
         ctx.relu = relu
         ctx.gate_in = gate_in
         ctx.params = (weight, bias)
@@ -65,7 +124,12 @@ class _LinearFn(torch.autograd.Function):
             # When the input is a ReLU output (the previous fused Linear+ReLU), the epilogue
             # also applies that layer's mask (x > 0): its backward then skips its mask pass
             gate = x2 if ctx.gate_in else None
-            C.gemm_f32(g, weight, dx, True, False, gate=gate)
+            M, K = g.shape
+            if planes_fit(M, x2.shape[1], K) and weight.stride(1) == 1 and \
+                    _al16(weight, gate, dx):
+                C.gemm_planes(planes_of(g), weight, dx, False, gate=gate)
+            else:
+                C.gemm_f32(g, weight, dx, True, False, gate=gate)
             if gate is not None:
                 _mark_gated(dx, x2)
         if needs(ctx, 1):
