@@ -17,8 +17,10 @@ Execution: at world size > 1 the whole step is captured into a hipGraph and repl
 bucket collectives run on the communicator's side stream and overlap backward (inside a graph the
 cross-stream dependency is free; eagerly it slows every launch, profiles/side_stream_eager.md).
 Optimizer scalars live in device hyper blocks, so the captured step stays exact (LR changes,
-Adam's step count). World size 1 runs eagerly (nothing to overlap: no collective at all, the
-optimizer runs in the weight-gradient GEMM epilogues). ``--graph`` / ``--eager`` force a mode.
+Adam's step count). At world size 1 the toy-MLP step is captured as well (no collective, the
+optimizer runs in the weight-gradient GEMM epilogues; replay removes the host-side launch work
+the ~15-kernel eager step is bound by); the CNNs run eagerly. ``--graph`` / ``--eager`` force a
+mode.
 
 Diagnostics (after the timed region, in the JSON line's "diagnostics"): at world size > 1 the
 collectives of one step alone (``comm_ms``), the same captured step with its collectives turned
@@ -290,7 +292,11 @@ def main():
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_gpu = torch.cuda.is_available() and not a.cpu
-    graph = use_gpu and not a.eager and (a.graph or world > 1) and a.impl == "tdp"
+    # captured by default at world size > 1 (collective overlap) and for the toy MLP at world
+    # size 1 too: its eager step is bound by host-side launch work (r6j: eager 0.375-0.47 ms,
+    # captured 0.371-0.374 ms on one box, profiles/r6/bench_modes_r6j.txt)
+    graph = use_gpu and not a.eager and (a.graph or world > 1 or a.model == "toy_mlp") and \
+        a.impl == "tdp"
     in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
     fused = False
 

@@ -453,13 +453,17 @@ inline bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 // variant: pipeline depth (2 stages: 80 KiB, two workgroups per CU; 3: 120 KiB, one) and the
 // B prefetch distance in tiles (0 = off; two stages only). TDP_PLANES_CFG = "S,PF"
-// (measurements); default 2,0
+// (measurements). Default 3,0: one workgroup per CU halves the split-K count (8 for the toy
+// MLP), hence the partial-sum traffic of the reduce; the captured toy-MLP step measured
+// 0.371-0.374 ms vs 0.383-0.386 with 2,0 (profiles/r6/bench_modes_r6j.txt). The B prefetch
+// measured nothing (the K loop is not HBM-latency bound: TDP_PLANES_EXP experiments,
+// profiles/r6/planes_gemm_experiments.md)
 struct PlanesCfg {
   int stages, pf;
 };
 PlanesCfg& planes_cfg() {
   static PlanesCfg c = [] {
-    PlanesCfg v{2, 0};
+    PlanesCfg v{3, 0};
     if (const char* e = std::getenv("TDP_PLANES_CFG")) {
       int a = 0, b = 0;
       if (std::sscanf(e, "%d,%d", &a, &b) == 2 && (a == 2 || a == 3) && b >= 0 && b <= 4 &&
