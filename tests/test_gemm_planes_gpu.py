@@ -147,3 +147,25 @@ def test_mlp_linear_chain_planes_vs_split_path():
     for a, b, r in zip(res[True], res[False], ref):
         torch.testing.assert_close(a.double(), r, rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("O", [10, 3, 16])
+def test_head_bwd_one_launch(C, O):
+    """fc3-style head backward (csrc/gemm_skinny.hip head_bwd): dx = g W gated, its planes,
+    dW = g^T x and db = sum g, against fp64."""
+    torch.manual_seed(O)
+    B, I = 128, 1024
+    g = torch.randn(B, O, device="cuda")
+    x = torch.relu(torch.randn(B, I, device="cuda"))
+    w = torch.randn(O, I, device="cuda")
+    dx = torch.empty(B, I, device="cuda")
+    dw = torch.empty(O, I, device="cuda")
+    db = torch.empty(O, device="cuda")
+    ok, pl = C.head_bwd(g, x, w, dx, dw, db=db, gate=x, planes=True)
+    torch.cuda.synchronize()
+    assert ok
+    ref_dx = (g.double() @ w.double()) * (x > 0).double()
+    torch.testing.assert_close(dx.double(), ref_dx, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dw.double(), g.double().t() @ x.double(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db.double(), g.double().sum(0), rtol=1e-5, atol=1e-5)
+    assert torch.equal(pl, C.split_planes(dx))

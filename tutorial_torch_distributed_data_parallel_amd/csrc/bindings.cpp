@@ -213,6 +213,45 @@ Tensor split_planes_op(const Tensor& x) {
   return p;
 }
 
+// Head Linear backward in one launch (planes.h head_bwd): fills dx, dw, db (optional); returns
+// (launched, planes of dx or None). g [B, O] (O <= 16), x [B, I], w [O, I], dx [B, I], dw [O, I].
+py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor& dx, Tensor& dw,
+                      const c10::optional<Tensor>& db, const c10::optional<Tensor>& gate,
+                      bool planes) {
+  CHECK_GPU(g); CHECK_GPU(x); CHECK_GPU(w); CHECK_GPU(dx); CHECK_GPU(dw);
+  CHECK_F32(g); CHECK_F32(x); CHECK_F32(w); CHECK_F32(dx); CHECK_F32(dw);
+  CHECK_ROWMAJOR(g); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w); CHECK_ROWMAJOR(dx);
+  CHECK_ROWMAJOR(dw);
+  const int B = (int)g.size(0), O = (int)g.size(1), I = (int)x.size(1);
+  TORCH_CHECK(x.size(0) == B && w.size(0) == O && w.size(1) == I && dx.size(0) == B &&
+                  dx.size(1) == I && dw.size(0) == O && dw.size(1) == I,
+              "head_bwd: shape mismatch");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    CHECK_GPU(*db); CHECK_F32(*db); CHECK_CONTIG(*db);
+    TORCH_CHECK(db->numel() == O, "head_bwd: db must have O elements");
+    dbp = db->data_ptr<float>();
+  }
+  const float* gp = nullptr;
+  long ldgate = 0;
+  if (gate.has_value() && gate->defined()) {
+    CHECK_GPU(*gate); CHECK_F32(*gate); CHECK_ROWMAJOR(*gate);
+    TORCH_CHECK(gate->size(0) == B && gate->size(1) == I, "head_bwd: gate must have dx's shape");
+    gp = gate->data_ptr<float>();
+    ldgate = gate->stride(0);
+  }
+  Tensor pl;
+  if (planes) pl = at::empty({3, (long)B, (long)I}, dx.options().dtype(at::kBFloat16));
+  const bool ok = head_bwd(g.data_ptr<float>(), g.stride(0), x.data_ptr<float>(), x.stride(0),
+                           w.data_ptr<float>(), w.stride(0), dx.data_ptr<float>(), dx.stride(0),
+                           gp, ldgate,
+                           planes ? reinterpret_cast<uint16_t*>(pl.data_ptr()) : nullptr,
+                           planes ? pl.stride(0) : 0, dw.data_ptr<float>(), dw.stride(0), dbp, B,
+                           O, I, cur_stream());
+  if (ok && planes) return py::make_tuple(true, pl);
+  return py::make_tuple(ok, py::none());
+}
+
 std::vector<int64_t> gemm_planes_plan_op(int M, int N, int K, int cus) {
   GemmPlanesArgs a;
   a.M = M; a.N = N; a.K = K;
@@ -1262,6 +1301,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,
         py::arg("gate") = py::none(), py::arg("out_planes") = py::none());
   m.def("split_planes", &split_planes_op);
+  m.def("head_bwd", &head_bwd_op, py::arg("g"), py::arg("x"), py::arg("w"), py::arg("dx"),
+        py::arg("dw"), py::arg("db") = py::none(), py::arg("gate") = py::none(),
+        py::arg("planes") = false);
   m.def("gemm_planes_plan", &gemm_planes_plan_op);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);

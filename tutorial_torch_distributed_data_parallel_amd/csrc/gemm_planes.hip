@@ -149,7 +149,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // S pipeline stages; WN 32-column MFMA tiles per wave (block tile 128 x 128*WN: WN = 2 halves
 // the A (L2) traffic per MFMA at 112 KiB of LDS, one workgroup per CU)
 template <bool BKC, int S, int WN, int PF>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(WN == 1 ? 2 : 1))) void gemm_planes_kernel(
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 : 1))) void gemm_planes_kernel(
     PParams p) {
   constexpr int BN = kBN * WN;
   constexpr int BBYTES = BN * kBK * 4;
@@ -325,6 +325,69 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(WN == 1 ? 2 
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[f][0] = mfma6(a1[f][0], a1[f][1], a1[f][2], y0, y1, y2, acc[f][0]);
   };
+  if constexpr (S == 3) {
+    // Cross-tile pipeline (three stages, one workgroup = one wave per SIMD): a tile's B fragments
+    // and step-0 A fragments are read -- and its step-0 B split done -- while the PREVIOUS tile's
+    // step-1 MFMAs issue, so the matrix pipe never waits for a tile's first LDS reads or split.
+    // The wait + barrier sits between a tile's two MFMA steps: tile kt+1 has landed there (its
+    // DMA was issued two half-iterations earlier) and tile kt's stage is free for tile kt+3.
+    float b0[8], b1[8];
+    bf8 a0[4][3], a1[4][3], x0[3];
+    auto read_a = [&](const lds_char* st, int s, int f, bf8 (&a)[4][3]) {
+      const int row = f * 32 + l31;
+      const int off = row * 64 + (((2 * s + h) ^ aswz(row)) * 16);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[f][q] = *reinterpret_cast<const bf8*>(st + q * kAPlane + off);
+    };
+    if (nk > 0) {
+      issue(0);
+      issue(1);
+      issue(2);
+      wait_vmcnt<2 * G>();
+      __builtin_amdgcn_s_barrier();
+      read_b(smem, 0, b0);
+      read_b(smem, 1, b1);
+      read_a(smem, 0, 0, a0);
+      read_a(smem, 0, 1, a0);
+      __builtin_amdgcn_sched_barrier(0);
+      split_x8(b0, x0[0], x0[1], x0[2]);
+      read_a(smem, 0, 2, a0);
+      read_a(smem, 0, 3, a0);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      const lds_char* st = smem + (kt % 3) * STG;
+      unsigned h1[4], m1[4], l1[4];
+      __builtin_amdgcn_sched_barrier(0);
+      // step 0 of tile kt; step-1 A reads and the step-1 B split in between
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        acc[f][0] = mfma6(a0[f][0], a0[f][1], a0[f][2], x0[0], x0[1], x0[2], acc[f][0]);
+        read_a(st, 1, f, a1);
+        split_pair(b1[2 * f], b1[2 * f + 1], h1[f], m1[f], l1[f]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const bf8 y0 = __builtin_bit_cast(bf8, u32x4{h1[0], h1[1], h1[2], h1[3]});
+      const bf8 y1 = __builtin_bit_cast(bf8, u32x4{m1[0], m1[1], m1[2], m1[3]});
+      const bf8 y2 = __builtin_bit_cast(bf8, u32x4{l1[0], l1[1], l1[2], l1[3]});
+      // tile kt+1 landed (tile kt+2 may still be in flight); every wave's reads of tile kt done
+      wait_vmcnt<G>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(kt + 3);
+      const lds_char* sn = smem + ((kt + 1) % 3) * STG;
+      read_b(sn, 0, b0);
+      read_b(sn, 1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      // step 1 of tile kt; tile kt+1's step-0 A reads and B split in between
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        acc[f][0] = mfma6(a1[f][0], a1[f][1], a1[f][2], y0, y1, y2, acc[f][0]);
+        read_a(sn, 0, f, a0);
+        if (f == 1) split_x8(b0, x0[0], x0[1], x0[2]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
   float d0 = 0.f, d1 = 0.f;
   auto step = [&](int kt, float& d) {
     // tile kt has landed when at most the S - 2 younger tiles' loads (and the newest prefetch)
@@ -355,6 +418,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(WN == 1 ? 2 
   }
   if (kt < nk) step(kt, d0);
   asm volatile("" ::"v"(d0), "v"(d1));
+  }
 
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
   // Epilogue through LDS (the stages are free once every wave has left the K loop): the MFMA

@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "planes.h"
 
 namespace tdp {
 namespace {
@@ -164,6 +165,116 @@ __global__ __launch_bounds__(256) void skinny_m_kernel(SkinnyParams p) {
   }
 }
 
+// Backward of a classifier head Linear(I -> O <= 16) in ONE launch (the toy-MLP fc3): the input
+// gradient dx[B][I] = g . W (gated by the previous ReLU's output, optionally emitted as bf16 split
+// planes for the next skinny GEMM) from the first nb_dx workgroups, the weight gradient
+// dW[O][I] = g^T . x and the bias gradient db = sum_b g from the rest -- skinny_k + skinny_m
+// (+ a split pass) fused, so the head's backward is one node instead of three.
+struct HeadBwdParams {
+  const float* g;  // [B][O]
+  const float* x;  // [B][I]
+  const float* w;  // [O][I]
+  float* dx;       // [B][I], row stride lddx
+  const float* gate;
+  uint16_t* dxp;   // optional planes of dx [3][B][I] (row stride I, plane stride dxps)
+  float* dw;       // [O][I], row stride lddw
+  float* db;       // optional [O]
+  long ldg, ldx, ldw, lddx, ldgate, dxps, lddw;
+  int B, O, I, nb_dx;
+};
+
+__device__ __forceinline__ void split4_pair(float x0, float x1, unsigned& h, unsigned& m,
+                                            unsigned& l) {
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf2_ __attribute__((ext_vector_type(2)));
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{x0, x1}, bf2_));
+  const float r0 = x0 - __uint_as_float(hu << 16), r1 = x1 - __uint_as_float(hu & 0xffff0000u);
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{r0, r1}, bf2_));
+  const float s0 = r0 - __uint_as_float(mu << 16), s1 = r1 - __uint_as_float(mu & 0xffff0000u);
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{s0, s1}, bf2_));
+}
+
+template <int MMAX>
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
+  extern __shared__ float smem[];
+  if ((int)blockIdx.x < p.nb_dx) {
+    // input gradient: 4 adjacent outputs of a row per thread, the O <= 16 gradients of the row
+    // broadcast from wave-uniform loads
+    const long per_row = p.I / 4;
+    const long t = blockIdx.x * 256L + threadIdx.x;
+    if (t >= per_row * p.B) return;
+    const int row = (int)(t / per_row);
+    const int col = (int)(t % per_row) * 4;
+    const float* gr = p.g + (long)row * p.ldg;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < p.O; ++k) {
+      const float gv = gr[k];
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (long)k * p.ldw + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = fmaf(gv, wv[e], acc[e]);
+    }
+    if (p.gate) {
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(p.gate + (long)row * p.ldgate + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = gv[e] > 0.f ? acc[e] : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(p.dx + (long)row * p.lddx + col) = acc;
+    if (p.dxp) {
+      typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+      unsigned h0, m0, l0, h1, m1, l1;
+      split4_pair(acc[0], acc[1], h0, m0, l0);
+      split4_pair(acc[2], acc[3], h1, m1, l1);
+      uint16_t* o = p.dxp + (long)row * p.I + col;
+      *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
+      *reinterpret_cast<u32x2_*>(o + p.dxps) = u32x2_{m0, m1};
+      *reinterpret_cast<u32x2_*>(o + 2 * p.dxps) = u32x2_{l0, l1};
+    }
+    return;
+  }
+  // weight / bias gradient: skinny_m_kernel's algorithm (g staged in LDS, 64 columns and 4 batch
+  // quarters per workgroup, quarters combined through LDS; workgroup 0 sums g for the bias)
+  const int bid = blockIdx.x - p.nb_dx;
+  const int cl = threadIdx.x & 63;
+  const int q = threadIdx.x >> 6;
+  const int col = bid * 64 + cl;
+  for (int i = threadIdx.x; i < p.B * MMAX; i += 256) {
+    const int k = i / MMAX, m = i % MMAX;
+    smem[i] = m < p.O ? p.g[(long)k * p.ldg + m] : 0.f;
+  }
+  __syncthreads();
+  const int kq = (p.B + 3) / 4;
+  const int k0 = q * kq, k1 = min(p.B, k0 + kq);
+  float acc[MMAX];
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) acc[m] = 0.f;
+  const int cc = col < p.I ? col : p.I - 1;
+#pragma unroll 8
+  for (int k = k0; k < k1; ++k) {
+    const float bv = p.x[(long)k * p.ldx + cc];
+    const float* arow = smem + k * MMAX;
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) acc[m] = fmaf(arow[m], bv, acc[m]);
+  }
+  float rs = 0.f;
+  if (p.db && bid == 0 && threadIdx.x < p.O)
+    for (int k = 0; k < p.B; ++k) rs += smem[k * MMAX + threadIdx.x];
+  __syncthreads();
+  float* red = smem;  // [4][MMAX][64]
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) red[(q * MMAX + m) * 64 + cl] = acc[m];
+  __syncthreads();
+  for (int o = threadIdx.x; o < MMAX * 64; o += 256) {
+    const int m = o / 64, c = o % 64;
+    const int gc = bid * 64 + c;
+    if (m < p.O && gc < p.I)
+      p.dw[(long)m * p.lddw + gc] = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
+                                    red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
+  }
+  if (p.db && bid == 0 && threadIdx.x < p.O) p.db[threadIdx.x] = rs;
+}
+
 bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 SkinnyParams params_of(const GemmF32Args& a) {
@@ -192,6 +303,27 @@ int gemm_skinny_kind(const GemmF32Args& a) {
       (long)a.K * (a.M <= 8 ? 8 : kSkinnyMax) * 4 <= 65536)
     return 3;
   return 0;
+}
+
+bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w, long ldw,
+              float* dx, long lddx, const float* gate, long ldgate, uint16_t* dxp, long dxps,
+              float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s) {
+  if (O < 1 || O > kSkinnyMax || I % 4 || B < 1 || !al16(w) || !al16(dx) || ldw % 4 ||
+      lddx % 4 || (gate && (!al16(gate) || ldgate % 4)) || ((uintptr_t)dxp & 7) ||
+      (long)B * (O <= 8 ? 8 : kSkinnyMax) * 4 > 65536)
+    return false;
+  HeadBwdParams p{g, x, w, dx, gate, dxp, dw, db, ldg, ldx, ldw, lddx, ldgate, dxps, lddw,
+                  B, O, I, 0};
+  const long threads = (long)B * (I / 4);
+  p.nb_dx = (int)((threads + 255) / 256);
+  const int nb_dw = (I + 63) / 64;
+  const int mm = O <= 8 ? 8 : kSkinnyMax;
+  const size_t lds = sizeof(float) * (size_t)std::max(B * mm, 4 * mm * 64);
+  if (mm == 8)
+    hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(p.nb_dx + nb_dw), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<kSkinnyMax>, dim3(p.nb_dx + nb_dw), dim3(256), lds, s, p);
+  return true;
 }
 
 void gemm_skinny_run(int kind, const GemmF32Args& a, hipStream_t s) {

@@ -32,6 +32,10 @@ def planes_fit(M: int, N: int, K: int) -> bool:
     return _PLANES and M <= 256 and K % 32 == 0 and K >= 256 and N % 4 == 0 and N >= 512
 
 
+# one-launch head backward (TDP_HEAD_FUSED=0: the skinny_k + skinny_m pair, for A/B)
+_HEAD_FUSED = os.environ.get("TDP_HEAD_FUSED", "1") != "0"
+
+
 def planes_input_fit(M: int, K: int) -> bool:
     """A [M, K] activation may feed a planes GEMM (its producer should emit the planes)."""
     return _PLANES and M <= 256 and K % 32 == 0 and K >= 256
@@ -117,6 +121,22 @@ class _LinearFn(torch.autograd.Function):
         g = C.relu_bias_bwd(dy, y) if ctx.relu and not _pregated(dy, y) else dy
         fac = factor_target(w_param) if needs(ctx, 1) else None
         epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
+        if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16 and \
+                _HEAD_FUSED:
+            # classifier head (out <= 16): input gradient (gated, + its planes for the next skinny
+            # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd); a
+            # head's update stays in the reducer's flat pass (no GEMM epilogue on skinny plans)
+            dx = torch.empty_like(x2)
+            dw = grad_dest(w_param)
+            gate = x2 if ctx.gate_in else None
+            ok, pl = C.head_bwd(g, x2, weight, dx, dw, db=db, gate=gate,
+                                planes=planes_input_fit(dx.shape[0], dx.shape[1]))
+            if ok:
+                if gate is not None:
+                    _mark_gated(dx, x2)
+                if pl is not None:
+                    attach_planes(dx, pl)
+                return dx, dw, db, None, None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
