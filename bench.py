@@ -305,7 +305,8 @@ def main():
         from tutorial_torch_distributed_data_parallel_amd.data import (DeviceLoader,
                                                                         DistributedSampler,
                                                                         SyntheticDataset)
-        from tutorial_torch_distributed_data_parallel_amd.data.synthetic import gather_batch
+        from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
+            EpochCursor, gather_batch, gather_batch_cursor)
         from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
         from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
@@ -486,20 +487,33 @@ def main():
         # a captured graph reads them from a static index tensor, eager steps from a slice
         idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
         cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices(), "b": None}
+        idx_static.copy_(cur["idx"][:a.batch])
+        # captured toy-MLP step: the gather reads the epoch order through a device-side cursor
+        # it advances itself (no per-step index copy node in the graph)
+        ecur = None
+        if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch) and \
+                os.environ.get("TDP_NO_CURSOR", "0") != "1":
+            ecur = EpochCursor(len(cur["idx"]), a.batch, dev)
+            ecur.set_order(cur["idx"])
 
         def advance():
             if cur["pos"] + a.batch > len(cur["idx"]):
                 cur["epoch"] += 1
                 sampler.set_epoch(cur["epoch"])
                 cur["idx"], cur["pos"] = loader.epoch_indices(), 0
+                if ecur is not None:
+                    ecur.set_order(cur["idx"])
             b = cur["idx"][cur["pos"]: cur["pos"] + a.batch]
-            if graph:
+            if graph and ecur is None:
                 idx_static.copy_(b)
                 b = idx_static
             cur["b"] = b
             cur["pos"] += a.batch
 
         def tdp_step():
+            if ecur is not None:
+                x, y = gather_batch_cursor(data.x, data.y, ecur)
+                return body(x, y)
             b = idx_static if graph else cur["b"]
             x, y = gather_batch(data.x, data.y, b)
             return body(x, y)
@@ -522,6 +536,11 @@ def main():
 
             run = try_capture(tdp_step, warmup=3,
                               log=lambda m: print(m, file=sys.stderr, flush=True))
+            if ecur is not None:
+                # the warm-up / capture runs advanced the device cursor: restart the epoch's
+                # order so host and device positions agree from the first timed step on
+                ecur.set_order(cur["idx"])
+                cur["pos"] = 0
 
         def step():
             advance()

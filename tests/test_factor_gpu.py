@@ -143,8 +143,10 @@ def test_factored_skips_when_not_profitable(pg):
 def test_replicated_factored_update_matches_sharded(pg, opt_name):
     """FactorJob.replicate: every rank computes all rows of the averaged gradient and updates
     them itself (no parameter all-gather). Rehearsed at world size 1 (where the shard is the
-    whole weight) it must train bit-for-bit like the sharded job; the auto policy picks it for
-    W*B <= 768 only."""
+    whole weight) it must train like the sharded job: the weight rows are the same GEMM; the
+    replicated job takes the bias gradient from that GEMM's row sums (its optimizer epilogue
+    updates the bias) where the sharded job runs a column reduction, so the two agree to fp32
+    rounding, not bit for bit. The auto policy picks it for W*B <= 768 only."""
     tdp = pg
     m1, d1, o1 = _build(tdp, opt_name, True, seed=21)
     m2, d2, o2 = _build(tdp, opt_name, True, seed=21)
@@ -159,6 +161,6 @@ def test_replicated_factored_update_matches_sharded(pg, opt_name):
     torch.cuda.synchronize()
     assert set(d1._factor_last_B.values()) == {64}
     for a, b in zip(m1.parameters(), m2.parameters()):
-        torch.testing.assert_close(a, b, atol=0, rtol=0)
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
     assert d1._replicate_pays(2, 128) and d1._replicate_pays(4, 128)
     assert not d1._replicate_pays(8, 128) and d1._replicate_pays(1, 128)

@@ -169,3 +169,43 @@ def test_head_bwd_one_launch(C, O):
     torch.testing.assert_close(dw.double(), g.double().t() @ x.double(), rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(db.double(), g.double().sum(0), rtol=1e-5, atol=1e-5)
     assert torch.equal(pl, C.split_planes(dx))
+
+
+def test_cursor_gather_walks_the_epoch_order():
+    """EpochCursor: each gather reads the next batch of the installed order and advances the
+    device-side position itself (also inside a captured graph); set_order rewinds."""
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
+        EpochCursor, gather_batch_cursor)
+
+    torch.manual_seed(5)
+    x = torch.randn(512, 256, device="cuda")
+    y = torch.randint(0, 10, (512,), device="cuda")
+    order = torch.randperm(512, device="cuda")
+    assert EpochCursor.fits(x, y, 64)
+    cur = EpochCursor(512, 64, "cuda")
+    cur.set_order(order)
+    for k in range(3):
+        xb, yb = gather_batch_cursor(x, y, cur)
+        sl = order[64 * k: 64 * (k + 1)]
+        assert torch.equal(xb, x[sl]) and torch.equal(yb, y[sl])
+    assert int(cur.state[0]) == 192 and int(cur.state[1]) == 0
+    # captured: replays advance too
+    static = {}
+
+    def step():
+        static["xb"], static["yb"] = gather_batch_cursor(x, y, cur)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()  # warm-up (advances to 256)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    cur.set_order(order)
+    for k in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        sl = order[64 * k: 64 * (k + 1)]
+        assert torch.equal(static["xb"], x[sl]) and torch.equal(static["yb"], y[sl])

@@ -104,7 +104,7 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
 // they were: the gradient is never materialised).
 bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
                      SyncBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
-                     double rowsum_beta) {
+                     double rowsum_beta, int64_t bias_offset, int64_t bias_span) {
   CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
   CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
   CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_CONTIG(C);
@@ -144,6 +144,17 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
     a.opt.s2 = f.s2 ? f.s2 + offset : nullptr;
     a.opt.sgd = f.sgd;    // scalars: from the device hyper block (f.sgd.dev)
     a.opt.adam = f.adam;
+    if (bias_offset >= 0 && a.rowsum != nullptr && a.rowsum_beta == 0.f) {
+      // the layer's bias [bias_offset, + M) is updated from the row sums by the same kernel;
+      // its arena span (alignment padding included) is marked done for the reducer
+      TORCH_CHECK(bias_span >= M, "optimizer epilogue: bias span shorter than the bias");
+      backend.note_epilogue(bias_offset, bias_span);
+      a.bias_opt.kind = f.kind;
+      a.bias_opt.p = f.p + bias_offset;
+      a.bias_opt.s0 = f.s0 ? f.s0 + bias_offset : nullptr;
+      a.bias_opt.s1 = f.s1 ? f.s1 + bias_offset : nullptr;
+      a.bias_opt.s2 = f.s2 ? f.s2 + bias_offset : nullptr;
+    }
   }
   const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
   Tensor ws;
@@ -217,7 +228,8 @@ Tensor split_planes_op(const Tensor& x) {
 // (launched, planes of dx or None). g [B, O] (O <= 16), x [B, I], w [O, I], dx [B, I], dw [O, I].
 py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor& dx, Tensor& dw,
                       const c10::optional<Tensor>& db, const c10::optional<Tensor>& gate,
-                      bool planes) {
+                      bool planes, SyncBackend* backend, int64_t w_offset, int64_t b_offset,
+                      int64_t b_span) {
   CHECK_GPU(g); CHECK_GPU(x); CHECK_GPU(w); CHECK_GPU(dx); CHECK_GPU(dw);
   CHECK_F32(g); CHECK_F32(x); CHECK_F32(w); CHECK_F32(dx); CHECK_F32(dw);
   CHECK_ROWMAJOR(g); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w); CHECK_ROWMAJOR(dx);
@@ -242,12 +254,40 @@ py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor&
   }
   Tensor pl;
   if (planes) pl = at::empty({3, (long)B, (long)I}, dx.options().dtype(at::kBFloat16));
+  // world size 1 + fused optimizer (backend given): W and b are updated by the kernel instead of
+  // storing their gradients; their arena ranges are marked done for the reducer
+  OptEpilogue wo, bo;
+  if (backend != nullptr && w_offset >= 0) {
+    TORCH_CHECK(backend->epilogue_allowed(), "head_bwd: optimizer epilogue not allowed");
+    auto ops = std::dynamic_pointer_cast<RcclOps>(backend->ops());
+    TORCH_CHECK(ops != nullptr, "head_bwd: optimizer epilogue needs the device backend");
+    TORCH_CHECK(dw.is_contiguous(), "head_bwd: dw must be the contiguous arena slot");
+    const FusedOptimizer& f = ops->fused;
+    auto at_off = [&](int64_t off) {
+      OptEpilogue o;
+      o.kind = f.kind;
+      o.p = f.p + off;
+      o.s0 = f.s0 ? f.s0 + off : nullptr;
+      o.s1 = f.s1 ? f.s1 + off : nullptr;
+      o.s2 = f.s2 ? f.s2 + off : nullptr;
+      o.sgd = f.sgd;
+      o.adam = f.adam;
+      return o;
+    };
+    wo = at_off(w_offset);
+    if (dbp != nullptr && b_offset >= 0) {
+      TORCH_CHECK(b_span >= O, "head_bwd: bias span shorter than the bias");
+      bo = at_off(b_offset);
+    }
+  }
   const bool ok = head_bwd(g.data_ptr<float>(), g.stride(0), x.data_ptr<float>(), x.stride(0),
                            w.data_ptr<float>(), w.stride(0), dx.data_ptr<float>(), dx.stride(0),
                            gp, ldgate,
                            planes ? reinterpret_cast<uint16_t*>(pl.data_ptr()) : nullptr,
                            planes ? pl.stride(0) : 0, dw.data_ptr<float>(), dw.stride(0), dbp, B,
-                           O, I, cur_stream());
+                           O, I, cur_stream(), wo.kind ? &wo : nullptr, bo.kind ? &bo : nullptr);
+  if (ok && wo.kind) backend->note_epilogue(w_offset, (int64_t)O * I);
+  if (ok && bo.kind) backend->note_epilogue(b_offset, b_span);
   if (ok && planes) return py::make_tuple(true, pl);
   return py::make_tuple(ok, py::none());
 }
@@ -969,7 +1009,8 @@ Tensor relu_mask_op(const Tensor& dy, const Tensor& y) {
 
 // x [n, ...] fp32 contiguous, y [n] int64, idx [B] int64 (all on the GPU) -> (x[idx], y[idx])
 std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tensor& idx,
-                                    bool planes) {
+                                    bool planes, const c10::optional<Tensor>& cursor,
+                                    int64_t batch) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_GPU(y); CHECK_CONTIG(y); CHECK_GPU(idx);
   CHECK_CONTIG(idx);
   TORCH_CHECK(y.scalar_type() == at::kLong && idx.scalar_type() == at::kLong && idx.dim() == 1,
@@ -977,7 +1018,19 @@ std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tens
   TORCH_CHECK(x.dim() >= 1 && y.dim() == 1 && y.size(0) == x.size(0) && x.size(0) > 0,
               "gather_batch: x [n, ...] and y [n]");
   const long n = x.size(0), F = x.numel() / n;
-  const int B = (int)idx.numel();
+  int B = (int)idx.numel();
+  int64_t* cur = nullptr;
+  if (cursor.has_value() && cursor->defined()) {
+    // cursor form: idx is the epoch's whole order, the batch is `batch` entries from cursor[0]
+    CHECK_GPU(*cursor); CHECK_CONTIG(*cursor);
+    TORCH_CHECK(cursor->scalar_type() == at::kLong && cursor->numel() == 2,
+                "gather_batch: cursor must be an int64 [2] device tensor {position, 0}");
+    TORCH_CHECK(batch > 0 && batch <= idx.numel(), "gather_batch: bad batch for the cursor");
+    TORCH_CHECK(planes && F % 4 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0,
+                "gather_batch: the cursor form is the planes gather (F % 4 == 0)");
+    cur = cursor->data_ptr<int64_t>();
+    B = (int)batch;
+  }
   auto xs = x.sizes().vec();
   xs[0] = B;
   auto xb = at::empty(xs, x.options());
@@ -987,7 +1040,8 @@ std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tens
     auto p = at::empty({3, (long)B, F}, x.options().dtype(at::kBFloat16));
     gather_batch_planes(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F,
                         B, xb.data_ptr<float>(), yb.data_ptr<int64_t>(),
-                        reinterpret_cast<uint16_t*>(p.data_ptr()), cur_stream());
+                        reinterpret_cast<uint16_t*>(p.data_ptr()), cur_stream(), cur,
+                        (long)idx.numel());
     return {xb, yb, p};
   }
   gather_batch(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F, B,
@@ -1295,7 +1349,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowsum_beta") = 0.0, py::arg("relu") = false, py::arg("gate") = py::none());
   m.def("gemm_f32_opt", &gemm_f32_opt_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
-        py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0);
+        py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0,
+        py::arg("bias_offset") = -1, py::arg("bias_span") = 0);
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
   m.def("gemm_planes", &gemm_planes_op, py::arg("Ap"), py::arg("B"), py::arg("C"),
         py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,
@@ -1303,7 +1358,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_planes", &split_planes_op);
   m.def("head_bwd", &head_bwd_op, py::arg("g"), py::arg("x"), py::arg("w"), py::arg("dx"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("gate") = py::none(),
-        py::arg("planes") = false);
+        py::arg("planes") = false, py::arg("backend") = nullptr, py::arg("w_offset") = -1,
+        py::arg("b_offset") = -1, py::arg("b_span") = 0);
   m.def("gemm_planes_plan", &gemm_planes_plan_op);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);
@@ -1425,7 +1481,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("g"), py::arg("x"), py::arg("g_all"), py::arg("x_all"), py::arg("rank"),
      py::arg("alpha"), py::arg("slot_rows") = -1);
   m.def("gather_batch", &gather_batch_op, py::arg("x"), py::arg("y"), py::arg("idx"),
-        py::arg("planes") = false);
+        py::arg("planes") = false, py::arg("cursor") = py::none(), py::arg("batch") = 0);
   m.def("image_transform", &image_transform_op, py::arg("x"), py::arg("flip"), py::arg("Ho"),
         py::arg("Wo"), py::arg("mean"), py::arg("std"), py::arg("round_u8") = true,
         py::arg("channels_last") = true);

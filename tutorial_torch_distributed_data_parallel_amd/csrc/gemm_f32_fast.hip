@@ -85,6 +85,7 @@ struct FastParams {
   int cvec;  // C (or the split-K workspace) takes 16-B row stores: N % 4 == 0, aligned rows
   float* stats;  // optional [tiles_m][3][N]: per-tile column (count, mean, M2) of the stored C
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
+  OptEpilogue bopt;  // kind != 0 (with opt and rowsum): update the bias from the row sums
   int prio;         // EMU: static wave priority for every other hardware slot (A/B knob)
   // EMU timing experiment only (TDP_GEMM_EXP, numerically WRONG when set): bit 0 replaces the
   // A fragments' split by one conversion, bit 1 the B fragments' -- the bound a pre-split
@@ -717,8 +718,30 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   if (nk > 0) ktile(nk - 1, std::true_type{});
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
   if (do_rs && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
-    float* d = p.rowsum + m0 + threadIdx.x;
-    *d = (p.rowsum_beta != 0.f ? p.rowsum_beta * *d : 0.f) + rs;
+    const int m = m0 + threadIdx.x;
+    if (OPTK != 0 && p.bopt.kind != 0) {
+      // the bias gradient is complete here (K = the whole batch): update the bias in place
+      // (same optimizer and hyper block as the weight) instead of storing the gradient
+      OptEpilogue o = p.opt;
+      if constexpr ((OPTK & 3) == 1) {
+        load_hyper(o.sgd);
+        float pe = p.bopt.p[m];
+        float b = (o.sgd.momentum != 0.f && !o.sgd.first_step) ? p.bopt.s0[m] : 0.f;
+        sgd_elem(pe, rs, b, o.sgd);
+        p.bopt.p[m] = pe;
+        if (o.sgd.momentum != 0.f) p.bopt.s0[m] = b;
+      } else if constexpr ((OPTK & 3) == 2) {
+        load_hyper(o.adam);
+        float pe = p.bopt.p[m], mm = p.bopt.s0[m], vv = p.bopt.s1[m];
+        adam_elem(pe, rs, mm, vv, p.bopt.s2 ? p.bopt.s2 + m : nullptr, o.adam);
+        p.bopt.p[m] = pe;
+        p.bopt.s0[m] = mm;
+        p.bopt.s1[m] = vv;
+      }
+    } else {
+      float* d = p.rowsum + m;
+      *d = (p.rowsum_beta != 0.f ? p.rowsum_beta * *d : 0.f) + rs;
+    }
   }
 
   // epilogue
@@ -1379,6 +1402,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.relu = (plan.splits > 1 ? false : a.relu) ? 1 : 0;
   p.cvec = c_vec_ok(a.N, a.ldc, a.C, a.bias, plan.splits) && !o_no_cvec;
   p.opt = a.opt;
+  p.bopt = (a.opt.kind != 0 && a.rowsum != nullptr && a.rowsum_beta == 0.f) ? a.bias_opt
+                                                                             : OptEpilogue{};
   const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
   const bool ak = a.a_kcontig, bk = a.b_kcontig;
   const int fn = plan.tile, st = plan.stages;

@@ -492,9 +492,16 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
                                                            long F, float* __restrict__ xb,
                                                            int64_t* __restrict__ yb,
                                                            uint16_t* __restrict__ planes,
-                                                           long ps) {
+                                                           long ps, int64_t* cursor,
+                                                           long nidx) {
   const int b = blockIdx.x;
-  long i = idx[b];
+  // cursor form (a captured step): the batch is idx[cursor[0] + b] and the workgroup that
+  // finishes last advances cursor[0] by B (cursor[1] counts arrivals), so every replay of the
+  // same graph reads the next batch of the epoch's order with no per-step index copy
+  const int64_t base = cursor ? cursor[0] : 0;
+  long k = base + b;
+  k = k < 0 ? 0 : (k >= nidx ? nidx - 1 : k);  // a cursor past the order reads its last entry
+  long i = idx[k];
   i = i < 0 ? 0 : (i >= n ? n - 1 : i);  // indices checked on the host; clamped so none faults
   const f32x4* src = reinterpret_cast<const f32x4*>(x + i * F);
   f32x4* dst = reinterpret_cast<f32x4*>(xb + (long)b * F);
@@ -511,6 +518,17 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
     *reinterpret_cast<u32x2*>(o + 2 * ps + 4 * k) = u32x2{l0, l1};
   }
   if (threadIdx.x == 0 && blockIdx.y == 0) yb[b] = y[i];
+  if (cursor) {
+    __syncthreads();  // every lane of this workgroup has read cursor[0]
+    if (threadIdx.x == 0) {
+      unsigned long long* c = reinterpret_cast<unsigned long long*>(cursor);
+      const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
+      if (atomicAdd(c + 1, 1ull) == total - 1) {  // last arrival: all others have read it
+        atomicAdd(c, (unsigned long long)gridDim.x);
+        atomicExch(c + 1, 0ull);
+      }
+    }
+  }
 }
 
 inline bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -563,15 +581,18 @@ void launch_cfg(const PParams& p, const PlanesCfg& c, int nblocks, hipStream_t s
 }  // namespace
 
 void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
-                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s) {
+                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s,
+                         int64_t* cursor, long nidx) {
   if (F % 4 || !al16(x) || !al16(xb) || ((uintptr_t)planes & 7))
     throw std::runtime_error("gather_batch_planes: F % 4 == 0 and aligned buffers required");
   if (B <= 0) return;
   // row slices: B = 128 rows alone would leave half of the 256 CUs idle
   const long F4 = F / 4;
-  const int slices = (int)std::max<long>(1, std::min<long>(8, (F4 + kT - 1) / kT));
+  // cursor form: one workgroup per row -- every workgroup arrives on the cursor's counter, and
+  // 8 x B same-address atomics serialised (17.6 vs 7.3 us for 128 x 9216)
+  const int slices = cursor ? 1 : (int)std::max<long>(1, std::min<long>(8, (F4 + kT - 1) / kT));
   hipLaunchKernelGGL(gather_planes_kernel, dim3(B, slices), dim3(kT), 0, s, x, y, idx, n, F, xb,
-                     yb, planes, (long)B * F);
+                     yb, planes, (long)B * F, cursor, cursor ? nidx : (long)B);
 }
 
 bool gemm_planes_ok(const GemmPlanesArgs& a) {

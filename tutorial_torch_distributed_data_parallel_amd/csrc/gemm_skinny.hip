@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "optim_elem.h"
 #include "planes.h"
 
 namespace tdp {
@@ -181,7 +182,29 @@ struct HeadBwdParams {
   float* db;       // optional [O]
   long ldg, ldx, ldw, lddx, ldgate, dxps, lddw;
   int B, O, I, nb_dx;
+  // world size 1 + fused optimizer: update W / b in place of storing dW / db (kind != 0;
+  // p / state pointers at the parameters' arena offsets, rows of I elements for W)
+  OptEpilogue wopt, bopt;
 };
+
+__device__ __forceinline__ void opt_apply(const OptEpilogue& o, long i, float g) {
+  OptEpilogue h = o;
+  if (o.kind == 1) {
+    load_hyper(h.sgd);
+    float pe = o.p[i];
+    float b = (h.sgd.momentum != 0.f && !h.sgd.first_step) ? o.s0[i] : 0.f;
+    sgd_elem(pe, g, b, h.sgd);
+    o.p[i] = pe;
+    if (h.sgd.momentum != 0.f) o.s0[i] = b;
+  } else {
+    load_hyper(h.adam);
+    float pe = o.p[i], m = o.s0[i], v = o.s1[i];
+    adam_elem(pe, g, m, v, o.s2 ? o.s2 + i : nullptr, h.adam);
+    o.p[i] = pe;
+    o.s0[i] = m;
+    o.s1[i] = v;
+  }
+}
 
 __device__ __forceinline__ void split4_pair(float x0, float x1, unsigned& h, unsigned& m,
                                             unsigned& l) {
@@ -268,11 +291,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   for (int o = threadIdx.x; o < MMAX * 64; o += 256) {
     const int m = o / 64, c = o % 64;
     const int gc = bid * 64 + c;
-    if (m < p.O && gc < p.I)
-      p.dw[(long)m * p.lddw + gc] = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
-                                    red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
+    if (m < p.O && gc < p.I) {
+      const float v = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
+                      red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
+      if (p.wopt.kind) opt_apply(p.wopt, (long)m * p.I + gc, v);
+      else p.dw[(long)m * p.lddw + gc] = v;
+    }
   }
-  if (p.db && bid == 0 && threadIdx.x < p.O) p.db[threadIdx.x] = rs;
+  if (p.db && bid == 0 && threadIdx.x < p.O) {
+    if (p.bopt.kind) opt_apply(p.bopt, threadIdx.x, rs);
+    else p.db[threadIdx.x] = rs;
+  }
 }
 
 bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -307,13 +336,16 @@ int gemm_skinny_kind(const GemmF32Args& a) {
 
 bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w, long ldw,
               float* dx, long lddx, const float* gate, long ldgate, uint16_t* dxp, long dxps,
-              float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s) {
+              float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s,
+              const OptEpilogue* wopt, const OptEpilogue* bopt) {
   if (O < 1 || O > kSkinnyMax || I % 4 || B < 1 || !al16(w) || !al16(dx) || ldw % 4 ||
       lddx % 4 || (gate && (!al16(gate) || ldgate % 4)) || ((uintptr_t)dxp & 7) ||
       (long)B * (O <= 8 ? 8 : kSkinnyMax) * 4 > 65536)
     return false;
   HeadBwdParams p{g, x, w, dx, gate, dxp, dw, db, ldg, ldx, ldw, lddx, ldgate, dxps, lddw,
-                  B, O, I, 0};
+                  B, O, I, 0, OptEpilogue{}, OptEpilogue{}};
+  if (wopt) p.wopt = *wopt;
+  if (bopt && db) p.bopt = *bopt;
   const long threads = (long)B * (I / 4);
   p.nb_dx = (int)((threads + 255) / 256);
   const int nb_dw = (I + 63) / 64;

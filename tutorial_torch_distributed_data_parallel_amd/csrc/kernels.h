@@ -108,6 +108,10 @@ struct GemmF32Args {
   float beta = 0.f, rowsum_beta = 0.f;
   bool relu = false;
   OptEpilogue opt;  // kind != 0: apply the optimizer instead of storing C (needs splits == 1)
+  // with opt and rowsum (rowsum_beta == 0): also apply the optimizer to the bias elements at
+  // bias_opt's pointers with the row sums as their gradient, instead of storing rowsum (the
+  // layer's bias update rides on the weight-gradient GEMM; hyper-parameters are opt's)
+  OptEpilogue bias_opt;
   // optional C-shaped gate, applied last: C = epilogue(C) * (gate > 0). The input gradient of a
   // Linear whose input is a ReLU output leaves already masked, so the producer's backward
   // needs no separate mask pass (ops/linear.py)

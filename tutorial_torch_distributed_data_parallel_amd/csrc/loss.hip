@@ -83,6 +83,55 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
                                                      float* __restrict__ dpre) {
   __shared__ float red[4];
   float ls = 0.f, cr = 0.f, vd = 0.f;
+  if (C <= 32 && B <= 256) {
+    // one row per lane (a classifier head at batch <= 256): the three sums in ONE cross-wave
+    // reduction, the logits gradient written from the lane's own lse (no re-read of lse[],
+    // no second pass over the batch) -- ~half the latency of the general path
+    __shared__ float red3[4][3];
+    const int r = threadIdx.x;
+    RowOut o{0.f, 0.f, 0.f, 0.f};
+    int64_t y = ignore_index;
+    if (r < B) {
+      y = labels[r];
+      o = row_serial(logits + (long)r * ld, C, y, ignore_index, eps);
+      if (lse) lse[r] = o.lse;
+    }
+    ls = wave_sum(o.loss);
+    cr = wave_sum(o.correct);
+    vd = wave_sum(o.valid);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+      red3[wid][0] = ls;
+      red3[wid][1] = cr;
+      red3[wid][2] = vd;
+    }
+    __syncthreads();
+    ls = red3[0][0] + red3[1][0] + red3[2][0] + red3[3][0];
+    cr = red3[0][1] + red3[1][1] + red3[2][1] + red3[3][1];
+    vd = red3[0][2] + red3[1][2] + red3[2][2] + red3[3][2];
+    if (dpre && r < B) {
+      const float g = mean ? 1.f / vd : 1.f;
+      const bool valid = o.valid != 0.f;
+      const float* x = logits + (long)r * ld;
+      for (int c = 0; c < C; ++c) {
+        float v = 0.f;
+        if (valid) {
+          const float pr = __expf(x[c] - o.lse);
+          v = g * (pr - (c == (int)y ? (1.f - eps) : 0.f) - eps / C);
+        }
+        dpre[r * C + c] = v;
+      }
+    }
+    if (threadIdx.x == 0) {
+      if (!count_only) {
+        if (out_loss) out_loss[0] = mean ? (vd > 0.f ? ls / vd : NAN) : ls;
+        if (lse) lse[B] = vd;
+        if (acc) acc[0] += ls;
+      }
+      if (acc) { acc[1] += cr; acc[2] += vd; }
+    }
+    return;
+  }
   if (C <= 32) {
     for (int r = threadIdx.x; r < B; r += 256) {
       const RowOut o = row_serial(logits + (long)r * ld, C, labels[r], ignore_index, eps);

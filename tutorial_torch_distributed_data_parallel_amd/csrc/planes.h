@@ -35,16 +35,21 @@ void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes
                   hipStream_t s);
 
 // gather_batch (kernels.h) that also writes the planes of the gathered rows: planes [3][B][F]
-// (plane stride B*F), F % 4 == 0
+// (plane stride B*F), F % 4 == 0. cursor (optional, int64 [2] = {position, 0}): the batch is
+// idx[cursor[0] .. + B) and the kernel advances cursor[0] by B (a captured step reads the next
+// batch of the epoch's order at every replay)
 void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
-                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s);
+                         int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s,
+                         int64_t* cursor = nullptr, long nidx = 0);
 
 // Backward of a head Linear(I -> O <= 16) in one launch (csrc/gemm_skinny.hip): dx = g . W
 // (gated by gate > 0 when given, planes of dx when dxp != null), dW = g^T . x, db = sum_b g
 // (when db != null). g [B][O], x [B][I], W [O][I]; I % 4 == 0, 16-B aligned W / dx / gate rows.
+// wopt / bopt (kind != 0): apply that optimizer update to W / b instead of storing dW / db.
 // false = shape not supported (nothing launched).
 bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w, long ldw,
               float* dx, long lddx, const float* gate, long ldgate, uint16_t* dxp, long dxps,
-              float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s);
+              float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s,
+              const OptEpilogue* wopt = nullptr, const OptEpilogue* bopt = nullptr);
 
 }  // namespace tdp

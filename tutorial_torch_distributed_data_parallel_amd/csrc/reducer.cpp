@@ -156,16 +156,6 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     check_hip(hipMalloc(&buf, sizeof(float) * (size_t)want), "hipMalloc(factor)");
     have = want;
   };
-  if (j.bias_off >= 0) {
-    // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
-    // every rank: identical inputs, identical results, no collective
-    const int rows = W * j.B;
-    const int sl = relu_bias_slices(rows, j.out, cus);
-    grow(factor_part_, factor_part_floats_, (int64_t)sl * j.out, "bias workspace");
-    relu_bias_bwd_ws(j.g_all, nullptr, rows, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
-                     factor_part_, sl, s);
-    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
-  }
   const int64_t m0 = (own - begin) / j.in;
   GemmF32Args a;
   a.A = j.g_all + m0;  // stored [K = W*B][out]: MN-contiguous A, column offset m0
@@ -183,6 +173,20 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   probe.opt.kind = 1;
   const GemmPlan pp = gemm_f32_plan(probe, cus);
   const bool epi = fused.kind != 0 && pp.fast && !pp.skinny && pp.splits == 1;
+  // replicated job: this rank owns every row, so the GEMM's row sums of the gathered g ARE the
+  // whole averaged bias gradient -- the epilogue updates the bias from them (no separate column
+  // reduction + update launches); a sharded job would only see its own rows' bias entries
+  const bool bias_in_gemm = epi && j.bias_off >= 0 && j.replicate && a.M == j.out;
+  if (j.bias_off >= 0 && !bias_in_gemm) {
+    // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
+    // every rank: identical inputs, identical results, no collective
+    const int rows = W * j.B;
+    const int sl = relu_bias_slices(rows, j.out, cus);
+    grow(factor_part_, factor_part_floats_, (int64_t)sl * j.out, "bias workspace");
+    relu_bias_bwd_ws(j.g_all, nullptr, rows, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
+                     factor_part_, sl, s);
+    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
+  }
   if (epi) {
     // the epilogue updates p / state at C's element index: the arena offset `own`
     a.opt.kind = fused.kind;
@@ -192,6 +196,15 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     a.opt.s2 = fused.s2 ? fused.s2 + own : nullptr;
     a.opt.sgd = fused.sgd;
     a.opt.adam = fused.adam;
+    if (bias_in_gemm) {
+      a.rowsum = grad_ + j.bias_off;  // selects the row-sum tiles; never written (bias_opt)
+      a.rowsum_beta = 0.f;
+      a.bias_opt.kind = fused.kind;
+      a.bias_opt.p = fused.p + j.bias_off;
+      a.bias_opt.s0 = fused.s0 ? fused.s0 + j.bias_off : nullptr;
+      a.bias_opt.s1 = fused.s1 ? fused.s1 + j.bias_off : nullptr;
+      a.bias_opt.s2 = fused.s2 ? fused.s2 + j.bias_off : nullptr;
+    }
   }
   const GemmPlan plan = gemm_f32_plan(a, cus);
   grow(factor_ws_, factor_ws_floats_, plan.ws_floats, "split-K workspace");

@@ -91,6 +91,50 @@ def gather_batch(x: torch.Tensor, y: torch.Tensor, idx: torch.Tensor):
     return x.index_select(0, idx), y.index_select(0, idx)
 
 
+class EpochCursor:
+    """Device-side batch position over one epoch's sample order, for captured steps.
+
+    The planes gather (csrc/gemm_planes.hip ``gather_planes_kernel``, cursor form) reads its
+    batch from ``order[pos : pos + batch]`` and advances ``pos`` itself (the last workgroup to
+    finish), so every replay of a captured step gathers the next batch without a per-step index
+    copy. The host installs each epoch's order with ``set_order`` (one copy per epoch, stream
+    ordered before the next replay), which also rewinds the position."""
+
+    def __init__(self, capacity: int, batch: int, device):
+        self.order = torch.zeros(capacity, dtype=torch.long, device=device)
+        self.state = torch.zeros(2, dtype=torch.long, device=device)  # {position, arrivals}
+        self.batch = int(batch)
+
+    def set_order(self, idx: torch.Tensor) -> None:
+        n = len(idx)
+        if n > len(self.order):
+            raise ValueError(f"epoch order of {n} exceeds the cursor capacity {len(self.order)}")
+        self.order[:n].copy_(idx)
+        if n < len(self.order):
+            self.order[n:].fill_(int(idx[-1]) if idx.device.type == "cpu" else 0)
+        self.state.zero_()
+
+    @staticmethod
+    def fits(x: torch.Tensor, y: torch.Tensor, batch: int) -> bool:
+        """The dataset can use the cursor gather (a 2-D fp32 feature table for a skinny Linear)."""
+        from ..ops.linear import planes_input_fit
+
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and
+                y.dtype == torch.long and y.is_contiguous() and x.shape[1] % 4 == 0 and
+                planes_input_fit(batch, x.shape[1]))
+
+
+def gather_batch_cursor(x: torch.Tensor, y: torch.Tensor, cur: EpochCursor):
+    """``gather_batch`` of the cursor's next batch (advances the device-side position)."""
+    from .._native import native
+    from ..ops.linear import attach_planes
+
+    xb, yb, p = native().gather_batch(x, y, cur.order, planes=True, cursor=cur.state,
+                                      batch=cur.batch)
+    attach_planes(xb, p)
+    return xb, yb
+
+
 class DeviceLoader:
     """Iterates (inputs, labels) batches of a tensor dataset by sampler order, on device.
 

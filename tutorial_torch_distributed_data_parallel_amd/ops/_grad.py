@@ -63,6 +63,24 @@ def epilogue_target(p: torch.Tensor | None):
     return ddp.epilogue_slot(p) if ddp is not None else None
 
 
+def bias_epilogue(b: torch.Tensor | None):
+    """``(backend, arena_offset, span)`` when the kernel that reduces the bias gradient of ``b``
+    should also apply the fused optimizer to it (``DistributedDataParallel.bias_epilogue``)."""
+    ref = getattr(b, "_tdp_epi", None) if b is not None else None
+    if ref is None or b.grad is not None:
+        return None
+    ddp = ref()
+    return ddp.bias_epilogue(b) if ddp is not None else None
+
+
+def hand_off(p: torch.Tensor | None, t: torch.Tensor | None) -> None:
+    """``t`` (``p``'s gradient slot) goes to autograd unwritten: a kernel applied the update."""
+    ref = getattr(p, "_tdp_epi", None) if p is not None else None
+    ddp = ref() if ref is not None else None
+    if ddp is not None and t is not None:
+        ddp.note_handed(p, t)
+
+
 def factor_target(p: torch.Tensor | None):
     """The DDP whose factored synchronisation replaces the weight-gradient GEMM of ``p`` in
     this backward (``DistributedDataParallel.factor_slot``), else None."""

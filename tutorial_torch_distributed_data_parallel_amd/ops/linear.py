@@ -19,7 +19,8 @@ import torch.nn.functional as F
 import os
 
 from .._native import native
-from ._grad import epilogue_target, factor_target, grad_dest, needs, note_use
+from ._grad import (bias_epilogue, epilogue_target, factor_target, grad_dest, hand_off, needs,
+                    note_use)
 
 # Skinny GEMMs (batch rows against thousands of features) read their activation operand from
 # its exact bf16 split planes (csrc/gemm_planes.hip): split once by the producer instead of once
@@ -129,9 +130,20 @@ class _LinearFn(torch.autograd.Function):
             dx = torch.empty_like(x2)
             dw = grad_dest(w_param)
             gate = x2 if ctx.gate_in else None
+            kw = {}
+            if epi is not None and dw.is_contiguous():
+                # world size 1 + fused optimizer: the kernel updates W (and b) in place
+                kw = dict(backend=epi[0], w_offset=epi[1])
+                be = bias_epilogue(b_param) if db is not None else None
+                if be is not None:
+                    kw.update(b_offset=be[1], b_span=be[2])
             ok, pl = C.head_bwd(g, x2, weight, dx, dw, db=db, gate=gate,
-                                planes=planes_input_fit(dx.shape[0], dx.shape[1]))
+                                planes=planes_input_fit(dx.shape[0], dx.shape[1]), **kw)
             if ok:
+                if kw:
+                    hand_off(w_param, dw)
+                    if "b_offset" in kw:
+                        hand_off(b_param, db)
                 if gate is not None:
                     _mark_gated(dx, x2)
                 if pl is not None:
@@ -164,7 +176,14 @@ class _LinearFn(torch.autograd.Function):
             elif epi is not None:
                 # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
                 # from the accumulators; the gradient itself is never written to HBM
-                C.gemm_f32_opt(g, x2, dw, False, False, epi[0], epi[1], rowsum=db)
+                be = bias_epilogue(b_param) if db is not None else None
+                done = C.gemm_f32_opt(g, x2, dw, False, False, epi[0], epi[1], rowsum=db,
+                                      bias_offset=be[1] if be else -1,
+                                      bias_span=be[2] if be else 0)
+                if done:  # the epilogue ran: W (and b) were updated, their slots never written
+                    hand_off(w_param, dw)
+                    if be is not None:
+                        hand_off(b_param, db)
             else:
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:

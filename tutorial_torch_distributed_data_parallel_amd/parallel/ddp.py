@@ -277,11 +277,12 @@ class DistributedDataParallel(nn.Module):
                 ptr = self._factor_handed.pop(idx, None)
                 if ptr is not None and (p.grad is None or p.grad.data_ptr() != ptr):
                     raise RuntimeError(
-                        "DDP factored synchronisation: the gradient of a factored Linear weight "
-                        f"(arena index {idx}, shape {tuple(p.shape)}) received a contribution "
-                        "from an op other than its Linear layer (a weight penalty, tied weights, "
-                        "x @ w.t() ...); the factored job would drop it. Construct DDP with "
-                        "factor_sync=False for this model.")
+                        "DDP: the gradient of a Linear parameter updated in its own kernel "
+                        f"(factored synchronisation or optimizer epilogue; arena index {idx}, "
+                        f"shape {tuple(p.shape)}) received a contribution from an op other than "
+                        "its Linear layer (a weight penalty, tied weights, x @ w.t() ...), which "
+                        "would be dropped. Construct DDP with factor_sync=False, or register the "
+                        "optimizer without fusion, for this model.")
             if not arena.is_arena_grad(idx):
                 # a gradient produced outside the native ops: move it into its bucket slot
                 slot = arena.grad_view(idx)
@@ -648,6 +649,29 @@ class DistributedDataParallel(nn.Module):
         if i is None or not self.arena.numels[i]:
             return None
         return self._backend, self.arena.offsets[i]
+
+    def bias_epilogue(self, b):
+        """(backend, arena offset, span) when the bias ``b`` may be updated by the kernel that
+        reduces its gradient (the weight-gradient GEMM's row sums, the fused head backward) at
+        world size 1; span covers the alignment padding up to the next parameter so no flat
+        update pass remains for it. None otherwise."""
+        if not (self._epi_on and self.require_backward_grad_sync and self.reducer.expecting and
+                self._backend.epilogue_allowed):
+            return None
+        i = self._epi_index.get(id(b))
+        if i is None or not self.arena.numels[i]:
+            return None
+        off = self.arena.offsets[i]
+        later = [o for o in self.arena.offsets if o > off]
+        return self._backend, off, (min(later) if later else self.arena.numel) - off
+
+    def note_handed(self, p, t) -> None:
+        """``t`` is the gradient of ``p`` handed to autograd unwritten (a kernel applied the
+        update, or the factored job owns it): the post-accumulate hook raises if another op
+        added to it (the contribution would be lost)."""
+        i = self._epi_index.get(id(p))
+        if i is not None:
+            self._factor_handed[i] = t.data_ptr()
 
     def factor_slot(self, p):
         """This DDP when the weight-gradient GEMM of ``p`` should be replaced by the factored
