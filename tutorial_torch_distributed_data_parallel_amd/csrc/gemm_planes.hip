@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -208,11 +209,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
   auto issue = [&](int kt) {
     lds_char* st = smem + (kt % S) * STG;
     const int k0 = kb + min(kt, nk - 1) * kBK;
-    if (!(p.exp & 4)) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) glds16(abase[i] + k0, st + adst[i]);
-    }
-    if (p.exp & 2) return;
+    for (int i = 0; i < 6; ++i) glds16(abase[i] + k0, st + adst[i]);
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
       const float* src = BKC ? bbase[i] + k0 : bbase[i] + (long)k0 * p.ldb;
@@ -354,18 +352,43 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
       read_a(smem, 0, 2, a0);
       read_a(smem, 0, 3, a0);
     }
-    for (int kt = 0; kt < nk; ++kt) {
-      const lds_char* st = smem + (kt % 3) * STG;
+    // One tile, its stage index a compile-time constant (the loop is unrolled by the 3 stages:
+    // LDS offsets become immediates and no kt % 3 is computed). Each half-tile is ONE scheduling
+    // region whose MFMAs are interleaved with its LDS reads and split VALU by explicit
+    // sched_group_barrier patterns (left alone, the compiler issued the 36-VALU splits as blocks
+    // between MFMA runs, where no MFMA was in flight).
+    // every earlier LDS read into these registers has returned (they were issued a half-tile of
+    // MFMAs ago): one wait here instead of the compiler's lgkmcnt(0) in the middle of the region
+    auto settle = [&]() {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        asm volatile("" ::"v"(a0[f][0]), "v"(a0[f][1]), "v"(a0[f][2]));
+      asm volatile("" ::"v"(x0[0]), "v"(x0[1]), "v"(x0[2]));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(b1[j]));
+    };
+    auto tile = [&](int kt, auto stage_tag) {
+      constexpr int SG = decltype(stage_tag)::value;
+      const lds_char* st = smem + SG * STG;
+      const lds_char* sn = smem + ((SG + 1) % 3) * STG;
       unsigned h1[4], m1[4], l1[4];
+      settle();
       __builtin_amdgcn_sched_barrier(0);
-      // step 0 of tile kt; step-1 A reads and the step-1 B split in between
+      // step 0 of tile kt (24 MFMAs); step-1 A reads (12) and the step-1 B split (~36 VALU)
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         acc[f][0] = mfma6(a0[f][0], a0[f][1], a0[f][2], x0[0], x0[1], x0[2], acc[f][0]);
         read_a(st, 1, f, a1);
         split_pair(b1[2 * f], b1[2 * f + 1], h1[f], m1[f], l1[f]);
-        __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int u = 0; u < 12; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+      __builtin_amdgcn_sched_barrier(0);
       const bf8 y0 = __builtin_bit_cast(bf8, u32x4{h1[0], h1[1], h1[2], h1[3]});
       const bf8 y1 = __builtin_bit_cast(bf8, u32x4{m1[0], m1[1], m1[2], m1[3]});
       const bf8 y2 = __builtin_bit_cast(bf8, u32x4{l1[0], l1[1], l1[2], l1[3]});
@@ -373,19 +396,50 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
       wait_vmcnt<G>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      issue(kt + 3);
-      const lds_char* sn = smem + ((kt + 1) % 3) * STG;
+#pragma unroll
+      for (int f = 0; f < 4; ++f)  // drained above: keeps the compiler's own wait off the MFMAs
+        asm volatile("" ::"v"(a1[f][0]), "v"(a1[f][1]), "v"(a1[f][2]));
+      __builtin_amdgcn_sched_barrier(0);
+      // step 1 of tile kt (24 MFMAs) with: tile kt+1's B reads (4) first, the DMA of tile kt+3
+      // into stage SG (10, every wave has finished reading tile kt), tile kt+1's step-0 A reads
+      // (12), then its step-0 B split (~36 VALU) once the B reads have returned
       read_b(sn, 0, b0);
       read_b(sn, 1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      // step 1 of tile kt; tile kt+1's step-0 A reads and B split in between
+      acc[0][0] = mfma6(a1[0][0], a1[0][1], a1[0][2], y0, y1, y2, acc[0][0]);
+      read_a(sn, 0, 0, a0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int u = 0; u < 3; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(kt + 3);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int f = 1; f < 4; ++f) {
         acc[f][0] = mfma6(a1[f][0], a1[f][1], a1[f][2], y0, y1, y2, acc[f][0]);
         read_a(sn, 0, f, a0);
-        if (f == 1) split_x8(b0, x0[0], x0[1], x0[2]);
-        __builtin_amdgcn_sched_barrier(0);
       }
+      split_x8(b0, x0[0], x0[1], x0[2]);
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int kt = 0; kt < nk; kt += 3) {
+      tile(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nk) tile(kt + 1, std::integral_constant<int, 1>{});
+      if (kt + 2 < nk) tile(kt + 2, std::integral_constant<int, 2>{});
     }
   } else {
   float d0 = 0.f, d1 = 0.f;
