@@ -209,3 +209,46 @@ def test_cursor_gather_walks_the_epoch_order():
         torch.cuda.synchronize()
         sl = order[64 * k: 64 * (k + 1)]
         assert torch.equal(static["xb"], x[sl]) and torch.equal(static["yb"], y[sl])
+
+
+def test_batchnorm1d_planes_and_local_merge_match_torch():
+    """Linear -> BatchNorm1d(+ReLU) -> Linear (the toy MLP's SyncBN config at one rank): the BN
+    forward merges its own statistics (one launch) and emits bf16 planes for the next skinny GEMM,
+    its backward emits the input gradient's planes; forward, gradients and running statistics
+    match torch in fp64."""
+    import torch.nn.functional as F
+
+    from tutorial_torch_distributed_data_parallel_amd import ops
+
+    torch.manual_seed(11)
+    B, I, H, O = 128, 512, 1024, 1024
+    x = torch.randn(B, I, device="cuda")
+    w1 = (torch.randn(H, I, device="cuda") / 22).requires_grad_()
+    b1 = torch.randn(H, device="cuda").requires_grad_()
+    g = (torch.rand(H, device="cuda") + 0.5).requires_grad_()
+    bb = (torch.randn(H, device="cuda") * 0.1).requires_grad_()
+    w2 = (torch.randn(O, H, device="cuda") / 32).requires_grad_()
+    rm, rv = torch.zeros(H, device="cuda"), torch.ones(H, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    h = ops.linear(x, w1, b1)
+    a = ops.batch_norm(h, rm, rv, g, bb, training=True, momentum=0.1, eps=1e-5, relu=True,
+                       num_batches_tracked=nbt)
+    assert getattr(a, "_tdp_planes", None) is not None
+    out = ops.linear(a, w2)
+    seed = torch.linspace(-1, 1, out.numel(), device="cuda").view_as(out)
+    out.backward(seed)
+    torch.cuda.synchronize()
+    prm = [t.detach().double().requires_grad_() for t in (w1, b1, g, bb, w2)]
+    rm2, rv2 = torch.zeros(H, dtype=torch.float64, device="cuda"), \
+        torch.ones(H, dtype=torch.float64, device="cuda")
+    hr = x.double() @ prm[0].t() + prm[1]
+    ar = torch.relu(F.batch_norm(hr, rm2, rv2, prm[2], prm[3], training=True, momentum=0.1,
+                                 eps=1e-5))
+    outr = ar @ prm[4].t()
+    outr.backward(seed.double())
+    torch.testing.assert_close(out.double(), outr, rtol=1e-4, atol=1e-4)
+    for t, r in zip((w1, b1, g, bb, w2), prm):
+        torch.testing.assert_close(t.grad.double(), r.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rm.double(), rm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv.double(), rv2, rtol=1e-5, atol=1e-6)
+    assert int(nbt) == 1

@@ -575,10 +575,20 @@ static const uint8_t* mask_ptr(const c10::optional<Tensor>& m, const Tensor& x) 
   return m->data_ptr<uint8_t>();
 }
 
+static uint16_t* planes_ptr(const c10::optional<Tensor>& p, const Tensor& x) {
+  if (!p.has_value() || !p->defined()) return nullptr;
+  CHECK_GPU(*p);
+  TORCH_CHECK(p->scalar_type() == at::kBFloat16 && p->is_contiguous() && x.dim() == 2 &&
+                  p->numel() == 3 * x.numel() && x.size(1) % 4 == 0,
+              "planes_out: a contiguous [3, rows, C % 4 == 0] bf16 tensor");
+  return reinterpret_cast<uint16_t*>(p->data_ptr());
+}
+
 Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Tensor>& w,
                    const c10::optional<Tensor>& b, bool relu,
                    const c10::optional<Tensor>& residual,
-                   const c10::optional<Tensor>& mask_out) {
+                   const c10::optional<Tensor>& mask_out,
+                   const c10::optional<Tensor>& planes_out) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
@@ -591,8 +601,43 @@ Tensor bn_elemt_op(const Tensor& x, const Tensor& stats, const c10::optional<Ten
   const float* sp = stats.data_ptr<float>();
   bn_elemt(x.data_ptr<float>(), sp, sp + C, fptr(w), fptr(b), N, C, HW, relu,
            y.data_ptr<float>(), cur_stream(), fptr(residual),
-           const_cast<uint8_t*>(mask_ptr(mask_out, x)));
+           const_cast<uint8_t*>(mask_ptr(mask_out, x)), planes_ptr(planes_out, x));
   return y;
+}
+
+// one rank: (y, stats) from this rank's moments [mean | var | count] -- bn_merge fused in
+std::vector<Tensor> bn_elemt_local_op(const Tensor& x, const Tensor& moments,
+                                      const c10::optional<Tensor>& w,
+                                      const c10::optional<Tensor>& b, bool relu, double eps,
+                                      double momentum, const c10::optional<Tensor>& rmean,
+                                      const c10::optional<Tensor>& rvar,
+                                      const c10::optional<Tensor>& num_batches,
+                                      const c10::optional<Tensor>& mask_out,
+                                      const c10::optional<Tensor>& planes_out,
+                                      const c10::optional<Tensor>& residual) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2, "bn_elemt_local: [rows, C] input");
+  if (residual.has_value() && residual->defined()) {
+    CHECK_CONTIG(*residual);
+    TORCH_CHECK(residual->sizes() == x.sizes(), "bn_elemt_local: residual must have x's shape");
+  }
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  TORCH_CHECK(moments.numel() == 2 * C + 1, "bn_elemt_local: moments must be [2C+1]");
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+                "bn_elemt_local: num_batches_tracked must be one int64");
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  auto y = at::empty_like(x);
+  auto stats = at::empty({2 * C + 1}, x.options());
+  const bool ok = bn_elemt_local(x.data_ptr<float>(), moments.data_ptr<float>(), fptr(w),
+                                 fptr(b), N, C, relu, (float)eps, (float)momentum,
+                                 stats.data_ptr<float>(), fptr(rmean), fptr(rvar), nb,
+                                 y.data_ptr<float>(), const_cast<uint8_t*>(mask_ptr(mask_out, x)),
+                                 planes_ptr(planes_out, x), cur_stream(), fptr(residual));
+  if (!ok) return {};
+  return {y, stats};
 }
 
 Tensor bn_eval_op(const Tensor& x, const Tensor& rmean, const Tensor& rvar,
@@ -629,7 +674,8 @@ Tensor bn_bwd_reduce_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
 std::vector<Tensor> bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
                                     const c10::optional<Tensor>& w, const Tensor& sums,
                                     const c10::optional<Tensor>& y_relu, bool residual_grad,
-                                    const c10::optional<Tensor>& mask) {
+                                    const c10::optional<Tensor>& mask,
+                                    const c10::optional<Tensor>& planes_out) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   int N, C, HW;
   bn_dims(x, N, C, HW);
@@ -640,7 +686,7 @@ std::vector<Tensor> bn_bwd_elemt_op(const Tensor& dy, const Tensor& x, const Ten
   bn_bwd_elemt(dy.data_ptr<float>(), x.data_ptr<float>(), sp, sp + C, fptr(w),
                sums.data_ptr<float>(), fptr(y_relu), sp + 2 * C, N, C, HW, dx.data_ptr<float>(),
                cur_stream(), residual_grad ? dres.data_ptr<float>() : nullptr,
-               mask_ptr(mask, x));
+               mask_ptr(mask, x), planes_ptr(planes_out, x));
   if (residual_grad) return {dx, dres};
   return {dx};
 }
@@ -1500,14 +1546,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("momentum"), py::arg("rmean"), py::arg("rvar"),
         py::arg("num_batches") = py::none());
   m.def("bn_elemt", &bn_elemt_op, py::arg("x"), py::arg("stats"), py::arg("w"), py::arg("b"),
-        py::arg("relu"), py::arg("residual") = py::none(), py::arg("mask_out") = py::none());
+        py::arg("relu"), py::arg("residual") = py::none(), py::arg("mask_out") = py::none(),
+        py::arg("planes_out") = py::none());
+  m.def("bn_elemt_local", &bn_elemt_local_op, py::arg("x"), py::arg("moments"), py::arg("w"),
+        py::arg("b"), py::arg("relu"), py::arg("eps"), py::arg("momentum"),
+        py::arg("rmean") = py::none(), py::arg("rvar") = py::none(),
+        py::arg("num_batches") = py::none(), py::arg("mask_out") = py::none(),
+        py::arg("planes_out") = py::none(), py::arg("residual") = py::none());
   m.def("bn_eval", &bn_eval_op);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("y_relu"), py::arg("dw"), py::arg("db"), py::arg("grad_beta"),
         py::arg("mask") = py::none());
   m.def("bn_bwd_elemt", &bn_bwd_elemt_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("w"), py::arg("sums"), py::arg("y_relu"), py::arg("residual_grad") = false,
-        py::arg("mask") = py::none());
+        py::arg("mask") = py::none(), py::arg("planes_out") = py::none());
 
   m.def("rccl_unique_id", &unique_id_op);
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")

@@ -290,9 +290,18 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
 // residual (optional, [rows, C] form only): y = relu?(bn(x) + residual), the ResNet join
 // mask_out (optional, [rows, C] form with relu): the ReLU mask as one byte per 4 channels (bit j =
 // channel 4q+j > 0) -- what the backward reads instead of y (1/16 of the bytes)
+// planes_out (optional, [rows, C] form): the output's bf16 split planes [3][rows][C] too
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
-              const float* residual = nullptr, uint8_t* mask_out = nullptr);
+              const float* residual = nullptr, uint8_t* mask_out = nullptr,
+              uint16_t* planes_out = nullptr);
+// One rank (no gather): normalise [N][C] from this rank's moments [mean | var | count] and do
+// bn_merge's work in the same launch (stats [mean | invstd | count] out, running stats, the
+// batch counter). false = not the [rows, C % 4] form (nothing launched).
+bool bn_elemt_local(const float* x, const float* moments, const float* w, const float* b, int N,
+                    int C, bool relu, float eps, float momentum, float* stats, float* rmean,
+                    float* rvar, int64_t* nbt, float* y, uint8_t* mask_out, uint16_t* planes_out,
+                    hipStream_t s, const float* residual = nullptr);
 // part [T][3][C] per-row-tile (count, mean, M2) -> mean, var (biased), count (= cnt): the
 // moments of a convolution output whose forward GEMM epilogue produced them
 void bn_moments_partials(const float* part, int T, int C, float* ws, float* mean, float* var,
@@ -313,6 +322,6 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
                   int N, int C, int HW, float* dx, hipStream_t s, float* dres = nullptr,
-                  const uint8_t* mask = nullptr);
+                  const uint8_t* mask = nullptr, uint16_t* planes_out = nullptr);
 
 }  // namespace tdp

@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "split_bf16.h"
 
 namespace tdp {
 namespace {
@@ -511,6 +512,17 @@ __global__ __launch_bounds__(kRedT) void bwd_reduce_rows4(const float* __restric
 }
 
 // y = relu?(x * sc + sh) with per-channel sc/sh computed once per thread
+// LocalMerge (one rank: no gather): `invstd` holds this rank's biased variance; the kernel
+// derives invstd itself, and the workgroups of the first row split write the merged stats
+// [mean | invstd | count] and advance the running statistics -- bn_merge's work without its launch
+struct LocalMerge {
+  float* stats;  // [2C + 1] out; null = off
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float momentum;
+};
+
 __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
                                                    const float* __restrict__ mean,
                                                    const float* __restrict__ invstd,
@@ -519,7 +531,8 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
                                                    int splits, int relu, int eval, float eps,
                                                    const float* __restrict__ res,
                                                    float* __restrict__ y,
-                                                   uint8_t* __restrict__ mk) {
+                                                   uint8_t* __restrict__ mk,
+                                                   uint16_t* __restrict__ pl, LocalMerge lm) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
@@ -530,9 +543,24 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
   float sc[4], sf[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float is = eval ? rsqrtf(invstd[c + j] + eps) : invstd[c + j];
+    const float is = (eval || lm.stats) ? rsqrtf(invstd[c + j] + eps) : invstd[c + j];
     sc[j] = is * (w ? w[c + j] : 1.f);
     sf[j] = (bb ? bb[c + j] : 0.f) - mean[c + j] * sc[j];
+    if (lm.stats && blockIdx.y == 0 && rg == 0) {
+      const float n = invstd[C];  // the local count (moments layout [mean | var | count])
+      lm.stats[c + j] = mean[c + j];
+      lm.stats[C + c + j] = is;
+      if (lm.rmean) {
+        const float v = invstd[c + j];
+        const float unbiased = n > 1.f ? v * n / (n - 1.f) : v;
+        lm.rmean[c + j] = fmaf(lm.momentum, mean[c + j] - lm.rmean[c + j], lm.rmean[c + j]);
+        lm.rvar[c + j] = fmaf(lm.momentum, unbiased - lm.rvar[c + j], lm.rvar[c + j]);
+      }
+      if (c + j == 0) {
+        lm.stats[2 * C] = n;
+        if (lm.nbt) *lm.nbt += 1;
+      }
+    }
   }
 #pragma unroll 4
   for (long r = b + rg; r < e; r += RPW) {
@@ -547,6 +575,8 @@ __global__ __launch_bounds__(256) void elemt_rows4(const float* __restrict__ x,
       o[j] = relu ? fmaxf(q, 0.f) : q;
     }
     *reinterpret_cast<f32x4*>(y + r * C + c) = o;
+    // bf16 split planes of the output for a consuming skinny Linear (planes GEMM)
+    if (pl) store_planes4(pl + r * C + c, (long)N * C, o[0], o[1], o[2], o[3]);
     // ReLU mask for the backward: one byte per 4 channels (64 lanes: 64 consecutive bytes)
     if (mk)
       mk[(r * C + c) >> 2] = (uint8_t)((o[0] > 0.f ? 1 : 0) | (o[1] > 0.f ? 2 : 0) |
@@ -560,7 +590,7 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
     const float* __restrict__ invstd, const float* __restrict__ w,
     const float* __restrict__ sums, const float* __restrict__ yr, const float* __restrict__ cnt,
     int N, int C, int splits, float* __restrict__ dx, float* __restrict__ dres,
-    const uint8_t* __restrict__ mk) {
+    const uint8_t* __restrict__ mk, uint16_t* __restrict__ pl) {
   int CB, LPR, RPW;
   rows4_layout(C, CB, LPR, RPW);
   const int t = threadIdx.x, cq = t % LPR, rg = t / LPR;
@@ -599,6 +629,7 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = fmaf(d[j], k1[j], fmaf(xv[j], k2[j], k3[j]));
     *reinterpret_cast<f32x4*>(dx + off) = o;
+    if (pl) store_planes4(pl + off, (long)N * C, o[0], o[1], o[2], o[3]);
     // gradient of the fused residual input: the ReLU-masked dy itself
     if (dres) *reinterpret_cast<f32x4*>(dres + off) = d;
   }
@@ -697,17 +728,32 @@ void bn_merge(const float* gathered, int R, int C, float eps, float momentum, fl
                      momentum, mean, invstd, running_mean, running_var, num_batches);
 }
 
+bool bn_elemt_local(const float* x, const float* moments, const float* w, const float* b, int N,
+                    int C, bool relu, float eps, float momentum, float* stats, float* rmean,
+                    float* rvar, int64_t* nbt, float* y, uint8_t* mask_out, uint16_t* planes_out,
+                    hipStream_t s, const float* residual) {
+  if (!rows4_ok(C, 1, {x, y, moments, w, b, stats, residual})) return false;
+  const int sp = rows4_ew_splits(N, C);
+  hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, moments,
+                     moments + C, w, b, N, C, sp, relu ? 1 : 0, 0, eps, residual, y,
+                     relu ? mask_out : nullptr, planes_out,
+                     LocalMerge{stats, rmean, rvar, nbt, momentum});
+  return true;
+}
+
 void bn_elemt(const float* x, const float* mean, const float* invstd, const float* w,
               const float* b, int N, int C, int HW, bool relu, float* y, hipStream_t s,
-              const float* residual, uint8_t* mask_out) {
+              const float* residual, uint8_t* mask_out, uint16_t* planes_out) {
   if (rows4_ok(C, HW, {x, y, mean, invstd, w, b, residual})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, mean, invstd, w,
-                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, residual, y, relu ? mask_out : nullptr);
+                       b, N, C, sp, relu ? 1 : 0, 0, 0.f, residual, y, relu ? mask_out : nullptr,
+                       planes_out, LocalMerge{});
     return;
   }
   if (residual) throw std::runtime_error("bn_elemt: a fused residual needs the [rows, C%4] form");
   if (mask_out) throw std::runtime_error("bn_elemt: a ReLU mask needs the [rows, C%4] form");
+  if (planes_out) throw std::runtime_error("bn_elemt: planes need the [rows, C%4] form");
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, x, mean, invstd, w, b,
                      total, C, HW, relu ? 1 : 0, 0, 0.f, y);
@@ -719,7 +765,7 @@ void bn_eval(const float* x, const float* rmean, const float* rvar, const float*
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, x, rmean, rvar, w,
                        b, N, C, sp, relu ? 1 : 0, 1, eps, (const float*)nullptr, y,
-                       (uint8_t*)nullptr);
+                       (uint8_t*)nullptr, (uint16_t*)nullptr, LocalMerge{});
     return;
   }
   const long total = (long)N * C * HW;
@@ -749,13 +795,14 @@ void bn_bwd_reduce(const float* dy, const float* x, const float* mean, const flo
 void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const float* invstd,
                   const float* w, const float* sums, const float* y_relu, const float* count,
                   int N, int C, int HW, float* dx, hipStream_t s, float* dres,
-                  const uint8_t* mask) {
+                  const uint8_t* mask, uint16_t* planes_out) {
   if (rows4_ok(C, HW, {dy, x, y_relu, dx, dres})) {
     const int sp = rows4_ew_splits(N, C);
     hipLaunchKernelGGL(bwd_elemt_rows4, dim3(rows4_nblk(C), sp), dim3(256), 0, s, dy, x, mean,
-                       invstd, w, sums, y_relu, count, N, C, sp, dx, dres, mask);
+                       invstd, w, sums, y_relu, count, N, C, sp, dx, dres, mask, planes_out);
     return;
   }
+  if (planes_out) throw std::runtime_error("bn_bwd_elemt: planes need the [rows, C%4] form");
   if (dres) throw std::runtime_error("bn_bwd_elemt: a fused residual needs the [rows, C%4] form");
   if (mask) throw std::runtime_error("bn_bwd_elemt: a ReLU mask needs the [rows, C%4] form");
   const long total = (long)N * C * HW;

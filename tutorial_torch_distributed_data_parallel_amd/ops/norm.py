@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from .._native import native
 from ._grad import grad_dest, needs
+from .linear import attach_planes, planes_input_fit
 
 
 class _TorchKernels:
@@ -135,16 +136,35 @@ class _BatchNormFn(torch.autograd.Function):
             st = native().bn_moments_partials(part, float(x.shape[0]))
         else:
             st = K.bn_moments(x)[0]
-        gathered = group.all_gather_flat(st) if group is not None else st
-        stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var, num_batches)
         # [rows, C % 4] form on the GPU: the backward reads a 1-byte-per-4-channels ReLU mask
         # instead of the float output (1/16 of the bytes, twice per backward)
         mask = None
-        if relu and x.is_cuda and x.dim() == 2 and C % 4 == 0 and _MASK:
+        rows4 = x.is_cuda and x.dim() == 2 and C % 4 == 0
+        if relu and rows4 and _MASK:
             mask = torch.empty((x.shape[0], C // 4), dtype=torch.uint8, device=x.device)
-            y = K.bn_elemt(x, stats, weight, bias, relu, residual, mask_out=mask)
-        else:
-            y = K.bn_elemt(x, stats, weight, bias, relu, residual)
+        # a BatchNorm1d output feeding a skinny Linear: its bf16 split planes from the same pass
+        pl = None
+        if rows4 and not ctx.nhwc and planes_input_fit(x.shape[0], C):
+            pl = torch.empty((3, x.shape[0], C), dtype=torch.bfloat16, device=x.device)
+        y = None
+        if group is None and rows4:
+            # one rank: bn_merge's work runs inside the normalisation pass (one launch fewer)
+            r = native().bn_elemt_local(x, st, weight, bias, relu, float(eps), float(momentum),
+                                        rmean=running_mean, rvar=running_var,
+                                        num_batches=num_batches, mask_out=mask, planes_out=pl,
+                                        residual=residual)
+            if r:
+                y, stats = r
+        if y is None:
+            gathered = group.all_gather_flat(st) if group is not None else st
+            stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var,
+                               num_batches)
+            kw = {} if mask is None else {"mask_out": mask}
+            if pl is not None:
+                kw["planes_out"] = pl
+            y = K.bn_elemt(x, stats, weight, bias, relu, residual, **kw)
+        if pl is not None:
+            attach_planes(y, pl)
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.group = group
@@ -169,8 +189,16 @@ class _BatchNormFn(torch.autograd.Function):
         if needs(ctx, 0) or want_res:
             if ctx.group is not None:
                 ctx.group.all_reduce_sum_(sums)
-            # one pass: dx, and the residual input's gradient (the ReLU-masked dy) when fused
+            # one pass: dx, and the residual input's gradient (the ReLU-masked dy) when fused;
+            # a BatchNorm1d input gradient feeding a skinny Linear's backward also leaves as planes
+            pl = None
+            if needs(ctx, 0) and x.is_cuda and not ctx.nhwc and x.dim() == 2 and \
+                    x.shape[1] % 4 == 0 and planes_input_fit(x.shape[0], x.shape[1]):
+                pl = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+                mk = dict(mk, planes_out=pl)
             out = K.bn_bwd_elemt(dy, x, stats, weight, sums, y, want_res, **mk)
+            if pl is not None:
+                attach_planes(out[0], pl)
             dx = out[0] if needs(ctx, 0) else None
             dres = out[1] if want_res else None
             if ctx.nhwc:
