@@ -211,6 +211,54 @@ def test_cursor_gather_walks_the_epoch_order():
         assert torch.equal(static["xb"], x[sl]) and torch.equal(static["yb"], y[sl])
 
 
+def test_cursor_gather_sliced_rows_and_legacy_state(C):
+    """Wide rows: several workgroups per row count on per-row counters (state [2 + batch]), one
+    arrival per row on the shared counter; all counters re-armed. A [2] state (no per-row
+    counters) still works with one workgroup per row. Captured replays advance both ways."""
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
+        EpochCursor, gather_batch_cursor)
+
+    torch.manual_seed(6)
+    x = torch.randn(300, 4096, device="cuda")
+    y = torch.randint(0, 10, (300,), device="cuda")
+    order = torch.randperm(300, device="cuda")
+    cur = EpochCursor(300, 32, "cuda")
+    assert cur.state.numel() == 34
+    cur.set_order(order)
+    for k in range(4):
+        xb, yb = gather_batch_cursor(x, y, cur)
+        sl = order[32 * k: 32 * (k + 1)]
+        assert torch.equal(xb, x[sl]) and torch.equal(yb, y[sl])
+    assert int(cur.state[0]) == 128 and int(cur.state[1:].abs().sum()) == 0
+    legacy = torch.zeros(2, dtype=torch.long, device="cuda")
+    for k in range(2):
+        xb, yb, p = C.gather_batch(x, y, order, planes=True, cursor=legacy, batch=32)
+        sl = order[32 * k: 32 * (k + 1)]
+        assert torch.equal(xb, x[sl]) and torch.equal(yb, y[sl])
+        assert torch.equal(p[0].double() + p[1].double() + p[2].double(), xb.double())
+    assert int(legacy[0]) == 64 and int(legacy[1]) == 0
+    static = {}
+
+    def step():
+        static["xb"], static["yb"] = gather_batch_cursor(x, y, cur)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    cur.set_order(order)
+    for k in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        sl = order[32 * k: 32 * (k + 1)]
+        assert torch.equal(static["xb"], x[sl]) and torch.equal(static["yb"], y[sl])
+    assert int(cur.state[0]) == 96 and int(cur.state[1:].abs().sum()) == 0
+
+
 def test_batchnorm1d_planes_and_local_merge_match_torch():
     """Linear -> BatchNorm1d(+ReLU) -> Linear (the toy MLP's SyncBN config at one rank): the BN
     forward merges its own statistics (one launch) and emits bf16 planes for the next skinny GEMM,
@@ -252,3 +300,46 @@ def test_batchnorm1d_planes_and_local_merge_match_torch():
     torch.testing.assert_close(rm.double(), rm2, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rv.double(), rv2, rtol=1e-5, atol=1e-6)
     assert int(nbt) == 1
+
+
+_FIXUP_PROBE = r"""
+import sys, torch
+from tutorial_torch_distributed_data_parallel_amd._native import native
+C = native()
+torch.manual_seed(5)
+outs = []
+for (M, N, K, bk) in [(128, 4096, 9216, True), (128, 4096, 4096, False), (300, 256, 512, True)]:
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn((N, K) if bk else (K, N), device="cuda")
+    bias = torch.randn(N, device="cuda")
+    for rep in range(3):  # replays of the same launch re-use re-armed counters
+        out = torch.empty(M, N, device="cuda")
+        op = torch.empty((3, M, N), dtype=torch.bfloat16, device="cuda")
+        C.gemm_planes(C.split_planes(A), B, out, bk, bias=bias, relu=True, out_planes=op)
+        outs += [out.cpu(), op.cpu()]
+torch.save(outs, sys.argv[1])
+"""
+
+
+def test_split_k_fixup_matches_reduce_kernel_bitwise(tmp_path):
+    """The last-arriving workgroup's split-K fix-up (default) sums the partials in split order,
+    like planes_reduce_kernel (TDP_PLANES_FIXUP=0): outputs and planes bitwise equal, and equal
+    across repeated launches whichever workgroup arrives last."""
+    import os
+    import subprocess
+    import sys
+
+    script = tmp_path / "probe.py"
+    script.write_text(_FIXUP_PROBE)
+    res = {}
+    for mode in ("1", "0"):
+        env = dict(os.environ, TDP_PLANES_FIXUP=mode)
+        out = tmp_path / f"o{mode}.pt"
+        subprocess.run([sys.executable, str(script), str(out)], check=True, env=env, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        res[mode] = torch.load(out, weights_only=True)
+    assert len(res["1"]) == len(res["0"])
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
+    for i in range(0, len(res["1"]), 6):  # three launches per shape
+        assert torch.equal(res["1"][i], res["1"][i + 2]) and torch.equal(res["1"][i], res["1"][i + 4])

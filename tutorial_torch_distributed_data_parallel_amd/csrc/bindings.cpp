@@ -1069,8 +1069,10 @@ std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tens
   if (cursor.has_value() && cursor->defined()) {
     // cursor form: idx is the epoch's whole order, the batch is `batch` entries from cursor[0]
     CHECK_GPU(*cursor); CHECK_CONTIG(*cursor);
-    TORCH_CHECK(cursor->scalar_type() == at::kLong && cursor->numel() == 2,
-                "gather_batch: cursor must be an int64 [2] device tensor {position, 0}");
+    TORCH_CHECK(cursor->scalar_type() == at::kLong &&
+                    (cursor->numel() == 2 || cursor->numel() == 2 + batch),
+                "gather_batch: cursor must be an int64 [2] or [2 + batch] device tensor "
+                "{position, 0, per-row arrivals (zero)}");
     TORCH_CHECK(batch > 0 && batch <= idx.numel(), "gather_batch: bad batch for the cursor");
     TORCH_CHECK(planes && F % 4 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0,
                 "gather_batch: the cursor form is the planes gather (F % 4 == 0)");
@@ -1087,7 +1089,7 @@ std::vector<Tensor> gather_batch_op(const Tensor& x, const Tensor& y, const Tens
     gather_batch_planes(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F,
                         B, xb.data_ptr<float>(), yb.data_ptr<int64_t>(),
                         reinterpret_cast<uint16_t*>(p.data_ptr()), cur_stream(), cur,
-                        (long)idx.numel());
+                        (long)idx.numel(), cur != nullptr && cursor->numel() == 2 + batch);
     return {xb, yb, p};
   }
   gather_batch(x.data_ptr<float>(), y.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), n, F, B,

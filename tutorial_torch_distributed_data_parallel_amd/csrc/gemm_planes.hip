@@ -69,6 +69,7 @@ struct PParams {
   int relu;
   int M, N, K, kps, splits, tiles_n, tiles_mn;
   int prio;
+  unsigned* cnt;  // split-K arrival counters, one per output tile (nullptr: planes_reduce_kernel)
   int exp;  // timing experiments only (TDP_PLANES_EXP, numerically WRONG when set): bit 0 skips
             // the MFMA step, bit 1 the B DMA, bit 2 the A DMA, bit 3 the epilogue stores
 };
@@ -503,7 +504,59 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
     if (p.splits > 1) *reinterpret_cast<f32x4*>(ws + (long)row * p.N + col) = v;
     else finish4(p, row, col, v);
   }
+  if (p.splits == 1 || !p.cnt) return;
+  // Split-K fix-up in the last-arriving workgroup of the tile (no planes_reduce_kernel launch:
+  // 3 launches and their inter-kernel gaps per toy-MLP step). Nobody waits on anybody: every
+  // workgroup publishes its partial (agent-scope release: the partials of the other splits were
+  // written on other XCDs' L2s) and counts itself in; the one that sees splits - 1 earlier
+  // arrivals acquires, sums all partials in split order (its own from LDS: the same fp32 sum as
+  // the reduce kernel, bitwise) and runs the epilogue. It also re-arms the counter for the next
+  // launch of this slot (graph replays included).
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(p.cnt + t, 1u);
+    last = prev == (unsigned)(p.splits - 1);
+    if (last) atomicExch(p.cnt + t, 0u);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  f32x4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = i * kT + threadIdx.x;
+    const int lr = e / C4, lc = (e % C4) * 4;
+    const int row = min(m0 + lr, p.M - 1), col = min(n0 + lc, p.N - 4);
+    v[i] = z == 0 ? *reinterpret_cast<const f32x4*>(T + lr * TS + lc)
+                  : *reinterpret_cast<const f32x4*>(p.ws + (long)row * p.N + col);
+  }
+  for (int zz = 1; zz < p.splits; ++zz) {
+    const float* src = p.ws + (long)zz * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = i * kT + threadIdx.x;
+      const int lr = e / C4, lc = (e % C4) * 4;
+      const int row = min(m0 + lr, p.M - 1), col = min(n0 + lc, p.N - 4);
+      v[i] += zz == z ? *reinterpret_cast<const f32x4*>(T + lr * TS + lc)
+                      : *reinterpret_cast<const f32x4*>(src + (long)row * p.N + col);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = i * kT + threadIdx.x;
+    const int lr = e / C4, lc = (e % C4) * 4;
+    const int row = m0 + lr, col = n0 + lc;
+    if (row < p.M && col < p.N) finish4(p, row, col, v[i]);
+  }
 }
+
+// split-K arrival counters (zero at load, re-armed by each tile's last arrival): kCntSlots
+// regions used round-robin, so back-to-back launches -- possibly on different streams -- never
+// share a region while one of them can still be running
+constexpr int kCntSlots = 64, kCntTiles = 512;
+__device__ unsigned g_planes_cnt[kCntSlots * kCntTiles];
 
 // C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread
 __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
@@ -576,8 +629,16 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
     __syncthreads();  // every lane of this workgroup has read cursor[0]
     if (threadIdx.x == 0) {
       unsigned long long* c = reinterpret_cast<unsigned long long*>(cursor);
-      const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
-      if (atomicAdd(c + 1, 1ull) == total - 1) {  // last arrival: all others have read it
+      // two-level arrivals: a row's slices count on the row's own counter (distinct addresses),
+      // the row's last slice on the shared one -- B same-address atomics per launch, not B x
+      // slices (serialised: 17.6 vs 7.3 us for 8 x 128 arrivals on one counter)
+      bool row_done = true;
+      if (gridDim.y > 1) {
+        row_done = atomicAdd(c + 2 + b, 1ull) == (unsigned long long)gridDim.y - 1;
+        if (row_done) atomicExch(c + 2 + b, 0ull);
+      }
+      // last arrival: every workgroup of the launch has read the position
+      if (row_done && atomicAdd(c + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
         atomicAdd(c, (unsigned long long)gridDim.x);
         atomicExch(c + 1, 0ull);
       }
@@ -636,15 +697,16 @@ void launch_cfg(const PParams& p, const PlanesCfg& c, int nblocks, hipStream_t s
 
 void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
                          int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s,
-                         int64_t* cursor, long nidx) {
+                         int64_t* cursor, long nidx, bool row_counters) {
   if (F % 4 || !al16(x) || !al16(xb) || ((uintptr_t)planes & 7))
     throw std::runtime_error("gather_batch_planes: F % 4 == 0 and aligned buffers required");
   if (B <= 0) return;
   // row slices: B = 128 rows alone would leave half of the 256 CUs idle
   const long F4 = F / 4;
-  // cursor form: one workgroup per row -- every workgroup arrives on the cursor's counter, and
-  // 8 x B same-address atomics serialised (17.6 vs 7.3 us for 128 x 9216)
-  const int slices = cursor ? 1 : (int)std::max<long>(1, std::min<long>(8, (F4 + kT - 1) / kT));
+  // cursor form: several slices per row only with per-row arrival counters (see the kernel)
+  const int slices = (cursor && !row_counters)
+                         ? 1
+                         : (int)std::max<long>(1, std::min<long>(8, (F4 + kT - 1) / kT));
   hipLaunchKernelGGL(gather_planes_kernel, dim3(B, slices), dim3(kT), 0, s, x, y, idx, n, F, xb,
                      yb, planes, (long)B * F, cursor, cursor ? nidx : (long)B);
 }
@@ -715,10 +777,28 @@ void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.tiles_mn = ceil_div(a.M, kBM) * p.tiles_n;
   if (plan.splits > 1 && ws == nullptr) throw std::runtime_error("gemm_planes: workspace missing");
+  // split-K fix-up in the GEMM's last-arriving workgroups (TDP_PLANES_FIXUP=0: the reduce kernel)
+  static const bool fixup = [] {
+    const char* e = std::getenv("TDP_PLANES_FIXUP");
+    return !(e && e[0] == '0');
+  }();
+  p.cnt = nullptr;
+  if (plan.splits > 1 && fixup && p.tiles_mn <= kCntTiles) {
+    static unsigned* base[64] = {};
+    static int slot = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+      throw std::runtime_error("gemm_planes: hipGetDevice");
+    if (!base[dev] && hipGetSymbolAddress(reinterpret_cast<void**>(&base[dev]),
+                                          HIP_SYMBOL(g_planes_cnt)) != hipSuccess)
+      throw std::runtime_error("gemm_planes: counter symbol");
+    p.cnt = base[dev] + (long)slot * kCntTiles;
+    slot = (slot + 1) % kCntSlots;
+  }
   const int nblocks = p.tiles_mn * plan.splits;
   if (a.b_kcontig) launch_cfg<true>(p, planes_cfg(), nblocks, s);
   else launch_cfg<false>(p, planes_cfg(), nblocks, s);
-  if (plan.splits > 1) {
+  if (plan.splits > 1 && !p.cnt) {
     const long ng = (long)a.M * a.N / 4;
     hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
                        p);

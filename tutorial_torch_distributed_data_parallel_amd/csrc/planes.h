@@ -37,10 +37,11 @@ void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes
 // gather_batch (kernels.h) that also writes the planes of the gathered rows: planes [3][B][F]
 // (plane stride B*F), F % 4 == 0. cursor (optional, int64 [2] = {position, 0}): the batch is
 // idx[cursor[0] .. + B) and the kernel advances cursor[0] by B (a captured step reads the next
-// batch of the epoch's order at every replay)
+// batch of the epoch's order at every replay). row_counters: the cursor is int64 [2 + B] (zeros
+// after the first two), per-row arrival counters that let several workgroups share a row
 void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, long n, long F,
                          int B, float* xb, int64_t* yb, uint16_t* planes, hipStream_t s,
-                         int64_t* cursor = nullptr, long nidx = 0);
+                         int64_t* cursor = nullptr, long nidx = 0, bool row_counters = false);
 
 // Backward of a head Linear(I -> O <= 16) in one launch (csrc/gemm_skinny.hip): dx = g . W
 // (gated by gate > 0 when given, planes of dx when dxp != null), dW = g^T . x, db = sum_b g

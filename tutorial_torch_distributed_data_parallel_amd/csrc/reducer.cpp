@@ -135,11 +135,14 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   const int W = comm_->world(), r = comm_->rank();
   if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
   if (!skip_collectives) {
-    // in place: this rank's factor rows already sit at slot r (written on the compute stream)
+    // in place: this rank's factor rows already sit at slot r (written on the compute stream);
+    // one RCCL group, so g and x share one launch and the links carry both back to back
+    comm_->group_start();
     comm_->all_gather(j.g_all + (int64_t)r * j.B * j.out, j.g_all, (size_t)j.B * j.out,
                       ncclFloat32, s);
     comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in, ncclFloat32,
                       s);
+    comm_->group_end();
   }
   // this rank's rows of the averaged gradient: dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all
   int dev = 0;

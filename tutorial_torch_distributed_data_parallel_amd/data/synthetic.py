@@ -10,6 +10,8 @@ model can actually learn (loss curves are meaningful in tests).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -102,7 +104,10 @@ class EpochCursor:
 
     def __init__(self, capacity: int, batch: int, device):
         self.order = torch.zeros(capacity, dtype=torch.long, device=device)
-        self.state = torch.zeros(2, dtype=torch.long, device=device)  # {position, arrivals}
+        # {position, arrivals, per-row slice arrivals [batch]} (all re-armed by the kernel); the
+        # per-row counters let several workgroups share a row (TDP_CURSOR_ROWS=0: one per row)
+        rows = 0 if os.environ.get("TDP_CURSOR_ROWS") == "0" else int(batch)
+        self.state = torch.zeros(2 + rows, dtype=torch.long, device=device)
         self.batch = int(batch)
 
     def set_order(self, idx: torch.Tensor) -> None:
