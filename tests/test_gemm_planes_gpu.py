@@ -322,8 +322,8 @@ torch.save(outs, sys.argv[1])
 
 
 def test_split_k_fixup_matches_reduce_kernel_bitwise(tmp_path):
-    """The last-arriving workgroup's split-K fix-up (default) sums the partials in split order,
-    like planes_reduce_kernel (TDP_PLANES_FIXUP=0): outputs and planes bitwise equal, and equal
+    """The last-arriving workgroup's split-K fix-up (opt-in TDP_PLANES_FIXUP=1) sums the partials
+    in split order, like planes_reduce_kernel (the default): outputs and planes bitwise equal, and equal
     across repeated launches whichever workgroup arrives last."""
     import os
     import subprocess
@@ -332,11 +332,13 @@ def test_split_k_fixup_matches_reduce_kernel_bitwise(tmp_path):
     script = tmp_path / "probe.py"
     script.write_text(_FIXUP_PROBE)
     res = {}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for mode in ("1", "0"):
-        env = dict(os.environ, TDP_PLANES_FIXUP=mode)
+        env = dict(os.environ, TDP_PLANES_FIXUP=mode,
+                   PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]))
         out = tmp_path / f"o{mode}.pt"
         subprocess.run([sys.executable, str(script), str(out)], check=True, env=env, timeout=240,
-                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+                       cwd=root)
         res[mode] = torch.load(out, weights_only=True)
     assert len(res["1"]) == len(res["0"])
     for a, b in zip(res["1"], res["0"]):

@@ -505,8 +505,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
     else finish4(p, row, col, v);
   }
   if (p.splits == 1 || !p.cnt) return;
-  // Split-K fix-up in the last-arriving workgroup of the tile (no planes_reduce_kernel launch:
-  // 3 launches and their inter-kernel gaps per toy-MLP step). Nobody waits on anybody: every
+  // Split-K fix-up in the last-arriving workgroup of the tile (opt-in, measured slower than the
+  // reduce launch: see gemm_planes_run). Nobody waits on anybody: every
   // workgroup publishes its partial (agent-scope release: the partials of the other splits were
   // written on other XCDs' L2s) and counts itself in; the one that sees splits - 1 earlier
   // arrivals acquires, sums all partials in split order (its own from LDS: the same fp32 sum as
@@ -777,10 +777,15 @@ void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.tiles_mn = ceil_div(a.M, kBM) * p.tiles_n;
   if (plan.splits > 1 && ws == nullptr) throw std::runtime_error("gemm_planes: workspace missing");
-  // split-K fix-up in the GEMM's last-arriving workgroups (TDP_PLANES_FIXUP=0: the reduce kernel)
+  // split-K fix-up in the GEMM's last-arriving workgroups: OFF by default (TDP_PLANES_FIXUP=1
+  // turns it on). Measured (profiles/r7/planes_fixup_negative_r7b.md): bitwise equal to the
+  // reduce kernel but the toy-MLP step went 0.357 -> 0.474 ms -- the agent-scope release every
+  // workgroup needs before counting in (its partial must leave its XCD's L2) writes back the
+  // whole L2, and 32 of them per XCD serialise: +40 us per GEMM against a 5-6 us reduce launch
+  // (inside a hipGraph the launch itself leaves no gap).
   static const bool fixup = [] {
     const char* e = std::getenv("TDP_PLANES_FIXUP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   p.cnt = nullptr;
   if (plan.splits > 1 && fixup && p.tiles_mn <= kCntTiles) {
