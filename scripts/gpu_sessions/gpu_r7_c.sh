@@ -16,4 +16,9 @@ for m in resnet50 alexnet; do
 timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 --no-diag > gpurun_out/r7c/$m.json 2>/dev/null; fatal $? $m; echo "$m eager $(ms gpurun_out/r7c/$m.json)"
 timeout -k 10 300 python bench.py --model $m --graph --steps 20 --warmup 5 --no-diag > gpurun_out/r7c/${m}_g.json 2>gpurun_out/r7c/${m}_g.err; fatal $? ${m}_g; echo "$m graph $(ms gpurun_out/r7c/${m}_g.json)"
 done
+
+timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r7c/prof -o kt -- python3 bench.py --steps 60 --warmup 10 --no-diag > gpurun_out/r7c/prof.log 2>&1; fatal $? prof
+python3 scripts/step_kernels.py $(find gpurun_out/r7c/prof -name '*kernel_trace.csv' | head -1) ce_fwd 40 > gpurun_out/r7c/mlp_kernels.md
+python3 scripts/step_timeline.py $(find gpurun_out/r7c/prof -name '*kernel_trace.csv' | head -1) ce_fwd 40 > gpurun_out/r7c/mlp_timeline.md
+cat gpurun_out/r7c/mlp_timeline.md
 echo done

@@ -149,12 +149,12 @@ def test_mlp_linear_chain_planes_vs_split_path():
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("O", [10, 3, 16])
-def test_head_bwd_one_launch(C, O):
+@pytest.mark.parametrize("O,I,B", [(10, 1024, 128), (3, 1024, 128), (16, 1024, 128),
+                                   (10, 4100, 128), (10, 4096, 100), (9, 68, 37)])
+def test_head_bwd_one_launch(C, O, I, B):
     """fc3-style head backward (csrc/gemm_skinny.hip head_bwd): dx = g W gated, its planes,
-    dW = g^T x and db = sum g, against fp64."""
-    torch.manual_seed(O)
-    B, I = 128, 1024
+    dW = g^T x and db = sum g, against fp64 (ragged column / batch-slice edges included)."""
+    torch.manual_seed(O + I + B)
     g = torch.randn(B, O, device="cuda")
     x = torch.relu(torch.randn(B, I, device="cuda"))
     w = torch.randn(O, I, device="cuda")
@@ -345,3 +345,54 @@ def test_split_k_fixup_matches_reduce_kernel_bitwise(tmp_path):
         assert torch.equal(a, b)
     for i in range(0, len(res["1"]), 6):  # three launches per shape
         assert torch.equal(res["1"][i], res["1"][i + 2]) and torch.equal(res["1"][i], res["1"][i + 4])
+
+
+def test_planes_reduce_computes_head_logits(C):
+    """The split-K reduce of a planes GEMM also computes the classifier head fed by its finished
+    rows (head_w [O, N]): C and the head output against fp64; deterministic across launches."""
+    torch.manual_seed(11)
+    M, N, K, O = 128, 4096, 4096, 10
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.randn(N, device="cuda")
+    hw = torch.randn(O, N, device="cuda") / N ** 0.5
+    hb = torch.randn(O, device="cuda")
+    outs = []
+    for _ in range(2):
+        y = torch.empty(M, N, device="cuda")
+        ho = torch.empty(M, O, device="cuda")
+        took = C.gemm_planes(C.split_planes(A), B, y, True, bias=bias, relu=True, head_w=hw,
+                             head_b=hb, head_out=ho)
+        assert took
+        outs.append((y, ho))
+    torch.cuda.synchronize()
+    yref = torch.relu(A.double() @ B.double().t() + bias.double())
+    torch.testing.assert_close(outs[0][0].double(), yref, rtol=1e-5, atol=1e-5)
+    href = outs[0][0].double() @ hw.double().t() + hb.double()
+    torch.testing.assert_close(outs[0][1].double(), href, rtol=1e-5, atol=1e-5)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_toy_mlp_head_in_reduce_matches_separate_head():
+    """ToyMLP: fc2's reduce computes fc3's logits (fc3 launches nothing in forward); logits and
+    every gradient match the model with the fused head disabled, and no record outlives fc3."""
+    import tutorial_torch_distributed_data_parallel_amd.ops.linear as L
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.ops import cross_entropy
+
+    torch.manual_seed(3)
+    m = ToyMLP(in_features=1024, hidden=(1024, 1024), device="cuda")
+    x = torch.randn(128, 1024, device="cuda")
+    y = torch.randint(0, 10, (128,), device="cuda")
+    res = {}
+    for on in (True, False):
+        prev, L._HEAD_IN_REDUCE = L._HEAD_IN_REDUCE, on
+        try:
+            m.zero_grad(set_to_none=True)
+            out = m(x)
+            cross_entropy(out, y).backward()
+            res[on] = [out.detach().clone()] + [p.grad.clone() for p in m.parameters()]
+        finally:
+            L._HEAD_IN_REDUCE = prev
+    for a, b in zip(res[True], res[False]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)

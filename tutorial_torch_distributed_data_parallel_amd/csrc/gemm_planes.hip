@@ -70,6 +70,10 @@ struct PParams {
   int M, N, K, kps, splits, tiles_n, tiles_mn;
   int prio;
   unsigned* cnt;  // split-K arrival counters, one per output tile (nullptr: planes_reduce_kernel)
+  const float* hw;  // head (planes_reduce_head_kernel): hw [hn][N], hb [hn], ho [M][hn]
+  const float* hb;
+  float* ho;
+  int hn;
   int exp;  // timing experiments only (TDP_PLANES_EXP, numerically WRONG when set): bit 0 skips
             // the MFMA step, bit 1 the B DMA, bit 2 the A DMA, bit 3 the epilogue stores
 };
@@ -572,6 +576,54 @@ __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
   finish4(p, row, col, a);
 }
 
+// planes_reduce_kernel for one whole row per workgroup, plus the classifier head fed by the
+// finished row: ho[row][m] = sum_n C[row][n] hw[m][n] + hb[m] (m < hn <= 16). Per-thread partial
+// dot products in a fixed order, then a fixed reduction tree: deterministic.
+__global__ __launch_bounds__(kT) void planes_reduce_head_kernel(PParams p) {
+  constexpr int HM = 16;
+  const int row = blockIdx.x;
+  const long ng = (long)p.M * p.N / 4;
+  const int n4 = p.N / 4;
+  float part[HM];
+#pragma unroll
+  for (int m = 0; m < HM; ++m) part[m] = 0.f;
+  for (int c4 = threadIdx.x; c4 < n4; c4 += kT) {
+    const long idx = (long)row * n4 + c4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(p.ws) + idx;
+    f32x4 a = src[0];
+#pragma unroll 4
+    for (int z = 1; z < p.splits; ++z) a += src[z * ng];
+    const int col = c4 * 4;
+    finish4(p, row, col, a);
+    // the stored value, as finish4 computed it (bias, ReLU, gate)
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p.C + (long)row * p.ldc + col);
+#pragma unroll
+    for (int m = 0; m < HM; ++m) {
+      if (m < p.hn) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(p.hw + (long)m * p.N + col);
+        part[m] = fmaf(v[0], w[0], fmaf(v[1], w[1], fmaf(v[2], w[2], fmaf(v[3], w[3], part[m]))));
+      }
+    }
+  }
+  __shared__ float red[kT / 64][HM];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 0; m < HM; ++m) {
+    float x = part[m];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) red[wv][m] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < p.hn) {
+    const int m = threadIdx.x;
+    float x = red[0][m];
+#pragma unroll
+    for (int w = 1; w < kT / 64; ++w) x += red[w][m];
+    p.ho[(long)row * p.hn + m] = x + (p.hb ? p.hb[m] : 0.f);
+  }
+}
+
 // x [rows][cols] (row stride ldx) -> planes [3][rows][cols] (plane stride ps), cols % 4 == 0
 __global__ __launch_bounds__(kT) void split_planes_kernel(const float* __restrict__ x, long ldx,
                                                           int rows, int cols, uint16_t* planes,
@@ -751,7 +803,7 @@ GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus) {
   return plan;
 }
 
-void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   if (!gemm_planes_ok(a)) throw std::runtime_error("gemm_planes: unsupported operands");
   PParams p{};
   p.Ap = a.Ap; p.ps = a.ps; p.lda = a.lda;
@@ -803,11 +855,18 @@ void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   const int nblocks = p.tiles_mn * plan.splits;
   if (a.b_kcontig) launch_cfg<true>(p, planes_cfg(), nblocks, s);
   else launch_cfg<false>(p, planes_cfg(), nblocks, s);
-  if (plan.splits > 1 && !p.cnt) {
+  const bool head = a.head_w && a.head_out && a.head_n >= 1 && a.head_n <= 16 &&
+                    plan.splits > 1 && !p.cnt && a.N <= 8192 && al16(a.head_w) &&
+                    a.ldc % 4 == 0;
+  if (head) {
+    p.hw = a.head_w; p.hb = a.head_b; p.ho = a.head_out; p.hn = a.head_n;
+    hipLaunchKernelGGL(planes_reduce_head_kernel, dim3((unsigned)a.M), dim3(kT), 0, s, p);
+  } else if (plan.splits > 1 && !p.cnt) {
     const long ng = (long)a.M * a.N / 4;
     hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
                        p);
   }
+  return head;
 }
 
 void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,

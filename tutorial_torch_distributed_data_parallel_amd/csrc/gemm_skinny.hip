@@ -219,6 +219,8 @@ __device__ __forceinline__ void split4_pair(float x0, float x1, unsigned& h, uns
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{s0, s1}, bf2_));
 }
 
+constexpr int kHeadCols = 32;  // weight-gradient columns per head_bwd workgroup
+
 template <int MMAX>
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   extern __shared__ float smem[];
@@ -256,18 +258,21 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
     }
     return;
   }
-  // weight / bias gradient: skinny_m_kernel's algorithm (g staged in LDS, 64 columns and 4 batch
-  // quarters per workgroup, quarters combined through LDS; workgroup 0 sums g for the bias)
+  // weight / bias gradient: g staged in LDS, kHeadCols columns and 256 / kHeadCols batch slices
+  // per workgroup, slices combined through LDS; workgroup 0 sums g for the bias. 32 columns x 8
+  // slices (not skinny_m's 64 x 4): twice the workgroups and half of each thread's dependent
+  // chain of x loads -- this part was the launch's long pole (64 workgroups for I = 4096)
+  constexpr int CW = kHeadCols, NQ = 256 / kHeadCols;
   const int bid = blockIdx.x - p.nb_dx;
-  const int cl = threadIdx.x & 63;
-  const int q = threadIdx.x >> 6;
-  const int col = bid * 64 + cl;
+  const int cl = threadIdx.x % CW;
+  const int q = threadIdx.x / CW;
+  const int col = bid * CW + cl;
   for (int i = threadIdx.x; i < p.B * MMAX; i += 256) {
     const int k = i / MMAX, m = i % MMAX;
     smem[i] = m < p.O ? p.g[(long)k * p.ldg + m] : 0.f;
   }
   __syncthreads();
-  const int kq = (p.B + 3) / 4;
+  const int kq = (p.B + NQ - 1) / NQ;
   const int k0 = q * kq, k1 = min(p.B, k0 + kq);
   float acc[MMAX];
 #pragma unroll
@@ -284,16 +289,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   if (p.db && bid == 0 && threadIdx.x < p.O)
     for (int k = 0; k < p.B; ++k) rs += smem[k * MMAX + threadIdx.x];
   __syncthreads();
-  float* red = smem;  // [4][MMAX][64]
+  float* red = smem;  // [NQ][MMAX][CW]
 #pragma unroll
-  for (int m = 0; m < MMAX; ++m) red[(q * MMAX + m) * 64 + cl] = acc[m];
+  for (int m = 0; m < MMAX; ++m) red[(q * MMAX + m) * CW + cl] = acc[m];
   __syncthreads();
-  for (int o = threadIdx.x; o < MMAX * 64; o += 256) {
-    const int m = o / 64, c = o % 64;
-    const int gc = bid * 64 + c;
+  for (int o = threadIdx.x; o < MMAX * CW; o += 256) {
+    const int m = o / CW, c = o % CW;
+    const int gc = bid * CW + c;
     if (m < p.O && gc < p.I) {
-      const float v = red[(0 * MMAX + m) * 64 + c] + red[(1 * MMAX + m) * 64 + c] +
-                      red[(2 * MMAX + m) * 64 + c] + red[(3 * MMAX + m) * 64 + c];
+      float v = red[m * CW + c];
+#pragma unroll
+      for (int qq = 1; qq < NQ; ++qq) v += red[(qq * MMAX + m) * CW + c];
       if (p.wopt.kind) opt_apply(p.wopt, (long)m * p.I + gc, v);
       else p.dw[(long)m * p.lddw + gc] = v;
     }
@@ -348,13 +354,14 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
   if (bopt && db) p.bopt = *bopt;
   const long threads = (long)B * (I / 4);
   p.nb_dx = (int)((threads + 255) / 256);
-  const int nb_dw = (I + 63) / 64;
-  const int mm = O <= 8 ? 8 : kSkinnyMax;
-  const size_t lds = sizeof(float) * (size_t)std::max(B * mm, 4 * mm * 64);
-  if (mm == 8)
-    hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(p.nb_dx + nb_dw), dim3(256), lds, s, p);
-  else
-    hipLaunchKernelGGL(head_bwd_kernel<kSkinnyMax>, dim3(p.nb_dx + nb_dw), dim3(256), lds, s, p);
+  const int nb_dw = (I + kHeadCols - 1) / kHeadCols;
+  // the 10-class heads get their own width (no FMAs on 6 padding classes)
+  const int mm = O <= 8 ? 8 : O <= 10 ? 10 : kSkinnyMax;
+  const size_t lds = sizeof(float) * (size_t)std::max(B * mm, mm * 256);
+  const dim3 grid(p.nb_dx + nb_dw);
+  if (mm == 8) hipLaunchKernelGGL(head_bwd_kernel<8>, grid, dim3(256), lds, s, p);
+  else if (mm == 10) hipLaunchKernelGGL(head_bwd_kernel<10>, grid, dim3(256), lds, s, p);
+  else hipLaunchKernelGGL(head_bwd_kernel<kSkinnyMax>, grid, dim3(256), lds, s, p);
   return true;
 }
 

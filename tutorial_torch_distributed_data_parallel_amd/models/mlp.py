@@ -33,6 +33,10 @@ class ToyMLP(nn.Module):
         for name, m in layers:
             self.add_module(name, m)
         self._order = [n for n, _ in layers]
+        if not batchnorm and hidden:
+            # the last hidden Linear's split-K reduce also computes the 10 logits (no launch of
+            # its own for the head's forward; ops/linear.py ``head``)
+            layers[-2][1].feeds_head(layers[-1][1])
 
     def forward(self, x):
         x = x.reshape(x.shape[0], -1)

@@ -85,20 +85,50 @@ def _mark_gated(dx: torch.Tensor, gate: torch.Tensor) -> None:
     dx._tdp_gated_by = (gate.data_ptr(), tuple(gate.shape))
 
 
+def _head_key(weight, bias):
+    return (weight.data_ptr(), weight._version,
+            None if bias is None else (bias.data_ptr(), bias._version))
+
+
+def _head_precomputed(x2, weight, bias):
+    """The head output its producer's split-K reduce already computed for ``x2`` (see
+    _LinearFn.forward ``head``), if it still matches x2 and this head's weight / bias."""
+    rec = getattr(x2, "_tdp_head_out", None)
+    if rec is None or rec[1] != x2._version or rec[2] != _head_key(weight, bias):
+        return None
+    return rec[0]
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, head=None, pre=None):
         C = native()
         M, K = x2.shape
         N = weight.shape[0]
-        y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
-        if planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
+        if pre is not None:
+            # computed by the producer's split-K reduce (head of the previous fused Linear)
+            y = pre
+        else:
+            y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
+        if pre is not None:
+            pass
+        elif planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
             # a hidden layer's output also leaves as planes: the next skinny GEMM's A operand
             op = torch.empty((3, M, N), device=x2.device, dtype=torch.bfloat16) \
                 if relu and N % 32 == 0 else None
-            C.gemm_planes(planes_of(x2), weight, y, True, bias=bias, relu=relu, out_planes=op)
+            kw = {}
+            if head is not None:
+                # the classifier head fed by this output: its logits from the split-K reduce
+                hw, hb = head
+                kw = dict(head_w=hw, head_b=hb,
+                          head_out=torch.empty((M, hw.shape[0]), device=x2.device,
+                                               dtype=torch.float32))
+            took = C.gemm_planes(planes_of(x2), weight, y, True, bias=bias, relu=relu,
+                                 out_planes=op, **kw)
             if op is not None:
                 attach_planes(y, op)
+            if took and kw:
+                y._tdp_head_out = (kw["head_out"], y._version, _head_key(hw, hb))
         else:
             C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
         ctx.relu = relu
@@ -148,7 +178,7 @@ class _LinearFn(torch.autograd.Function):
                     _mark_gated(dx, x2)
                 if pl is not None:
                     attach_planes(dx, pl)
-                return dx, dw, db, None, None
+                return dx, dw, db, None, None, None, None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
@@ -188,7 +218,7 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None, None
 
 
 class _LinearCpuFn(torch.autograd.Function):
@@ -234,9 +264,17 @@ class _LinearCpuFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+# TDP_HEAD_IN_REDUCE=0: the head Linear runs its own forward (A/B of the fused head logits)
+_HEAD_IN_REDUCE = os.environ.get("TDP_HEAD_IN_REDUCE", "1") != "0"
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
-           relu: bool = False) -> torch.Tensor:
-    """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
+           relu: bool = False, head=None) -> torch.Tensor:
+    """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features].
+
+    ``head`` (weight, bias) of a small classifier Linear (out <= 16) that consumes this output:
+    the split-K reduce of this layer's GEMM also computes the head's output, and the head's own
+    ``linear`` call returns it without a launch (models/mlp.py: fc2 -> fc3)."""
     # the input is the ReLU output of a previous fused Linear(+ReLU): this layer's input-gradient
     # epilogue applies that ReLU's mask (see _LinearFn.backward)
     gate_in = bool(getattr(x, "_tdp_relu_out", False)) and x.dim() == 2
@@ -261,7 +299,16 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         gate_in = False
     if torch.is_grad_enabled():
         note_use(weight)
-    y = _LinearFn.apply(x2, weight, bias, relu, gate_in)
+    pre = _head_precomputed(x2, weight, bias) if x.dim() == 2 else None
+    if pre is not None:
+        # consumed: the record must not outlive this call (x2 -> logits -> their grad_fn ->
+        # saved x2 would be a cycle through a C++ node that Python's collector cannot see)
+        del x2._tdp_head_out
+    if head is not None and not (_HEAD_IN_REDUCE and x.dim() == 2 and head[0].dim() == 2 and
+                                 head[0].shape[0] <= 16 and head[0].shape[1] == weight.shape[0]
+                                 and head[0].is_cuda and head[0].is_contiguous()):
+        head = None
+    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, head, pre)
     if x.dim() == 2:
         if relu:
             y._tdp_relu_out = True

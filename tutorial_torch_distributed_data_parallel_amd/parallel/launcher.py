@@ -36,6 +36,26 @@ def free_port(addr: str = "127.0.0.1") -> int:
         return s.getsockname()[1]
 
 
+def _launcher_store(addr: str, nprocs: int):
+    """The rendezvous store, hosted by the launcher itself on a port the OS picks at bind time
+    (torchrun's agent store): no window between choosing a free port and rank 0 binding it, in
+    which another socket can take it (seen as EADDRINUSE on a shared GPU box). Ranks connect as
+    clients (TORCHELASTIC_USE_AGENT_STORE, torch/distributed/rendezvous.py). Returns
+    (store or None, port, extra env)."""
+    if nprocs <= 1:
+        return None, free_port(addr), {}
+    try:
+        import datetime
+
+        from torch.distributed import TCPStore
+
+        store = TCPStore(addr, 0, nprocs, True, timeout=datetime.timedelta(minutes=30),
+                         wait_for_workers=False)
+        return store, int(store.port), {"TORCHELASTIC_USE_AGENT_STORE": "True"}
+    except Exception:  # noqa: BLE001 - no torch store here: fall back to a probed free port
+        return None, free_port(addr), {}
+
+
 class ProcessRaisedException(RuntimeError):
     def __init__(self, msg, rank, pid):
         super().__init__(msg)
@@ -82,13 +102,14 @@ def spawn(fn, nprocs: int, args=(), master_addr: str = "127.0.0.1",
     """Run ``fn(rank, *args)`` on ``nprocs`` spawned ranks; re-raise the first failure."""
     if not 1 <= nprocs:
         raise ValueError("nprocs must be >= 1")
-    port = master_port or free_port(master_addr)
+    store, port, extra = (None, master_port, {}) if master_port else \
+        _launcher_store(master_addr, nprocs)
     ctx = mp.get_context("spawn")
     err_q = ctx.SimpleQueue()
     procs = []
     for r in range(nprocs):
-        p = ctx.Process(target=_child, args=(fn, r, args, _rank_env(r, nprocs, master_addr, port),
-                                             err_q), daemon=False)
+        env = dict(_rank_env(r, nprocs, master_addr, port), **extra)
+        p = ctx.Process(target=_child, args=(fn, r, args, env, err_q), daemon=False)
         p.start()
         procs.append(p)
     try:
@@ -122,11 +143,12 @@ def spawn(fn, nprocs: int, args=(), master_addr: str = "127.0.0.1",
 def run_script(nproc: int, argv, master_addr: str = "127.0.0.1", master_port: int | None = None,
                grace: float = 30.0) -> int:
     """torchrun-style: run ``python argv...`` nproc times with rank env; fail-fast."""
-    port = master_port or free_port(master_addr)
+    store, port, extra = (None, master_port, {}) if master_port else \
+        _launcher_store(master_addr, nproc)
     procs = []
     for r in range(nproc):
         env = dict(os.environ)
-        env.update(_rank_env(r, nproc, master_addr, port))
+        env.update(_rank_env(r, nproc, master_addr, port), **extra)
         procs.append(subprocess.Popen([sys.executable, *argv], env=env, start_new_session=True))
     rc = 0
     try:
