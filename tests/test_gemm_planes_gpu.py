@@ -375,11 +375,14 @@ def test_planes_reduce_computes_head_logits(C):
 
 def test_toy_mlp_head_in_reduce_matches_separate_head():
     """ToyMLP: fc2's reduce computes fc3's logits (fc3 launches nothing in forward); logits and
-    every gradient match the model with the fused head disabled, and no record outlives fc3."""
-    import tutorial_torch_distributed_data_parallel_amd.ops.linear as L
+    every gradient match the model with the fused head disabled."""
+    import importlib
+
     from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
     from tutorial_torch_distributed_data_parallel_amd.ops import cross_entropy
 
+    # the module (ops/__init__ re-exports the function under the same name)
+    L = importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear")
     torch.manual_seed(3)
     m = ToyMLP(in_features=1024, hidden=(1024, 1024), device="cuda")
     x = torch.randn(128, 1024, device="cuda")
