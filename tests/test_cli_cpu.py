@@ -95,3 +95,21 @@ def test_train_ddp_host_pipeline_two_ranks(tmp_path):
     r = _run([os.path.join(ROOT, "scripts", "train_ddp.py"), "--settings_file", str(p)])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Epoch 1/1, Train Loss:" in r.stdout
+
+
+def test_launcher_hosts_the_rendezvous_store():
+    """The launcher binds the rendezvous store itself (OS-picked port, held for the job): no
+    window between probing a free port and rank 0 binding it; ranks connect as clients."""
+    import socket
+
+    from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import _launcher_store
+
+    store, port, env = _launcher_store("127.0.0.1", 2)
+    assert store is not None and port > 0
+    assert env == {"TORCHELASTIC_USE_AGENT_STORE": "True"}
+    with socket.socket() as s, pytest.raises(OSError):
+        s.bind(("127.0.0.1", port))  # held by the store for the job's lifetime
+    store.set("k", "v")
+    assert store.get("k") == b"v"
+    one, _, env1 = _launcher_store("127.0.0.1", 1)
+    assert one is None and env1 == {}
