@@ -122,8 +122,8 @@ __device__ __forceinline__ int aswz(int row) { return (row >> 2) & 3; }
 __device__ __forceinline__ int bswz(int row) { return (row ^ (row >> 3)) & 7; }
 
 // bias, ReLU, gate of four adjacent finished outputs, then C (16-B store) and, when requested,
-// the three bf16 planes of the result (8-B stores)
-__device__ __forceinline__ void finish4(const PParams& p, int row, int col, f32x4 v) {
+// the three bf16 planes of the result (8-B stores); returns the stored value
+__device__ __forceinline__ f32x4 finish4(const PParams& p, int row, int col, f32x4 v) {
   if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
   if (p.relu) {
 #pragma unroll
@@ -144,6 +144,7 @@ __device__ __forceinline__ void finish4(const PParams& p, int row, int col, f32x
     *reinterpret_cast<u32x2*>(o + p.ops) = u32x2{m0, m1};
     *reinterpret_cast<u32x2*>(o + 2 * p.ops) = u32x2{l0, l1};
   }
+  return v;
 }
 
 template <int N>
@@ -576,10 +577,12 @@ __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
   finish4(p, row, col, a);
 }
 
-// planes_reduce_kernel for one whole row per workgroup, plus the classifier head fed by the
-// finished row: ho[row][m] = sum_n C[row][n] hw[m][n] + hb[m] (m < hn <= 16). Per-thread partial
-// dot products in a fixed order, then a fixed reduction tree: deterministic.
-__global__ __launch_bounds__(kT) void planes_reduce_head_kernel(PParams p) {
+// planes_reduce_kernel for one whole row per workgroup (1024 threads: a 4096-wide row is one
+// float4 per thread, the same parallelism as the flat reduce's 512 x 256), plus the classifier
+// head fed by the finished row: ho[row][m] = sum_n C[row][n] hw[m][n] + hb[m] (m < hn <= 16).
+// Per-thread partial dot products in a fixed order, then a fixed reduction tree: deterministic.
+constexpr int kHT = 1024;
+__global__ __launch_bounds__(kHT) void planes_reduce_head_kernel(PParams p) {
   constexpr int HM = 16;
   const int row = blockIdx.x;
   const long ng = (long)p.M * p.N / 4;
@@ -587,16 +590,14 @@ __global__ __launch_bounds__(kT) void planes_reduce_head_kernel(PParams p) {
   float part[HM];
 #pragma unroll
   for (int m = 0; m < HM; ++m) part[m] = 0.f;
-  for (int c4 = threadIdx.x; c4 < n4; c4 += kT) {
+  for (int c4 = threadIdx.x; c4 < n4; c4 += kHT) {
     const long idx = (long)row * n4 + c4;
     const f32x4* src = reinterpret_cast<const f32x4*>(p.ws) + idx;
     f32x4 a = src[0];
-#pragma unroll 4
+#pragma unroll 8
     for (int z = 1; z < p.splits; ++z) a += src[z * ng];
     const int col = c4 * 4;
-    finish4(p, row, col, a);
-    // the stored value, as finish4 computed it (bias, ReLU, gate)
-    const f32x4 v = *reinterpret_cast<const f32x4*>(p.C + (long)row * p.ldc + col);
+    const f32x4 v = finish4(p, row, col, a);  // bias, ReLU, gate applied: the stored value
 #pragma unroll
     for (int m = 0; m < HM; ++m) {
       if (m < p.hn) {
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(kT) void planes_reduce_head_kernel(PParams p) {
       }
     }
   }
-  __shared__ float red[kT / 64][HM];
+  __shared__ float red[kHT / 64][HM];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int m = 0; m < HM; ++m) {
@@ -619,7 +620,7 @@ __global__ __launch_bounds__(kT) void planes_reduce_head_kernel(PParams p) {
     const int m = threadIdx.x;
     float x = red[0][m];
 #pragma unroll
-    for (int w = 1; w < kT / 64; ++w) x += red[w][m];
+    for (int w = 1; w < kHT / 64; ++w) x += red[w][m];
     p.ho[(long)row * p.hn + m] = x + (p.hb ? p.hb[m] : 0.f);
   }
 }
@@ -860,7 +861,7 @@ bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
                     a.ldc % 4 == 0;
   if (head) {
     p.hw = a.head_w; p.hb = a.head_b; p.ho = a.head_out; p.hn = a.head_n;
-    hipLaunchKernelGGL(planes_reduce_head_kernel, dim3((unsigned)a.M), dim3(kT), 0, s, p);
+    hipLaunchKernelGGL(planes_reduce_head_kernel, dim3((unsigned)a.M), dim3(kHT), 0, s, p);
   } else if (plan.splits > 1 && !p.cnt) {
     const long ng = (long)a.M * a.N / 4;
     hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
