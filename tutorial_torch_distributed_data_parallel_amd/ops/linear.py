@@ -264,8 +264,11 @@ class _LinearCpuFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-# TDP_HEAD_IN_REDUCE=0: the head Linear runs its own forward (A/B of the fused head logits)
-_HEAD_IN_REDUCE = os.environ.get("TDP_HEAD_IN_REDUCE", "1") != "0"
+# TDP_HEAD_IN_REDUCE=1: the previous Linear's split-K reduce computes the head's forward. Off by
+# default: measured neutral (toy MLP 0.3506-0.3517 vs 0.3509-0.3516 ms/step interleaved; the
+# one-row-per-workgroup reduce + head takes 13.4 us vs 5.3 + 6.0 us for reduce + head launch,
+# 128 workgroups on 256 CUs -- profiles/r7/head_in_reduce_r7d.md)
+_HEAD_IN_REDUCE = os.environ.get("TDP_HEAD_IN_REDUCE", "0") == "1"
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
