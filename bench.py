@@ -9,6 +9,7 @@ one full DDP step per iteration: sampler-ordered batch gather -> forward -> loss
 bucketed RCCL gradient reduction -> optimizer step. Weak scaling: per-GPU work is fixed.
 
   python bench.py                                   # 1 GPU
+  python bench.py --gpus N                          # N ranks, spawned by bench.py itself
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
   python bench.py --impl torch                      # stock torch DDP + torch.optim (comparison)
   python bench.py --api accelerate                  # the same step through Accelerator.prepare()
@@ -280,8 +281,80 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
     return out
 
 
+def _launcher_env() -> bool:
+    """True when a launcher (torchrun, parallel/launcher.py, this script's own parent) already
+    made this process one rank of a job."""
+    return "RANK" in os.environ or "LOCAL_RANK" in os.environ
+
+
+def _multi_rank_vehicle() -> str | None:
+    """Several ranks may share one GPU only through an explicit vehicle (parallel/relay.py,
+    parallel/peer.py); RCCL refuses duplicate devices."""
+    if os.environ.get("TDP_GPU_PEER", "0") == "1":
+        return "peer"
+    if os.environ.get("TDP_GPU_RELAY", "0") == "1":
+        return "relay"
+    return None
+
+
+def launched_by() -> str:
+    if os.environ.get("TDP_BENCH_LAUNCHED_BY"):
+        return os.environ["TDP_BENCH_LAUNCHED_BY"]
+    if "TORCHELASTIC_RUN_ID" in os.environ:
+        return "torch.distributed.run"
+    return "external launcher" if _launcher_env() else "direct (one process)"
+
+
+def self_launch(a) -> int:
+    """``python bench.py --gpus N`` (N > 1) with no launcher environment: this process becomes
+    the launcher (the reference spawns its ranks from the configured world size itself,
+    REF/multi-GPU-training-torch.py:269-279,306). It never touches the GPU -- counting devices
+    does not initialise HIP on this image -- and never re-executes itself: the N ranks are child
+    processes (parallel/launcher.run_script, fail-fast), rank 0's stdout comes back through a
+    file, and its single JSON line is checked (n_gpus / parallelism = N) and relayed. Exit code:
+    the first failing rank's, 3 for a malformed record, 2 when fewer than N GPUs are visible and
+    no one-GPU vehicle was asked for."""
+    import tempfile
+
+    from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import run_script
+
+    n = a.gpus
+    if not a.cpu:
+        have = torch.cuda.device_count()
+        if have < n and _multi_rank_vehicle() is None:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) are visible; refusing to report "
+                  f"a {n}-rank number (TDP_GPU_PEER=1 / TDP_GPU_RELAY=1 run several ranks on one "
+                  f"GPU for testing)", file=sys.stderr, flush=True)
+            return 2
+    how = f"bench.py (self-launched {n} ranks, parallel/launcher.run_script)"
+    with tempfile.TemporaryFile(mode="w+") as f0:
+        rc = run_script(n, [str(Path(__file__).resolve()), *sys.argv[1:]],
+                        env_extra={"TDP_BENCH_LAUNCHED_BY": how}, rank0_stdout=f0)
+        f0.seek(0)
+        lines = [ln for ln in f0.read().splitlines() if ln.strip()]
+    if rc != 0:
+        print(f"bench.py: a rank failed with exit code {rc}", file=sys.stderr, flush=True)
+        for ln in lines:
+            print(ln, file=sys.stderr)
+        return rc if rc > 0 else 1
+    try:
+        rec = json.loads(lines[-1])
+        want_n = n if not a.cpu else 0
+        ok = rec["n_gpus"] == want_n and rec["config"]["parallelism"] == f"dp{n}"
+    except Exception:  # noqa: BLE001 - anything unparsable is a malformed record
+        ok, rec = False, None
+    if not ok:
+        print(f"bench.py: rank 0 printed no valid {n}-rank record: {lines[-3:]}",
+              file=sys.stderr, flush=True)
+        return 3
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and not _launcher_env():
+        sys.exit(self_launch(a))
     out = _private_stdout()
     if a.dataset is None:
         a.dataset = 8192 if a.model == "toy_mlp" else 512
@@ -598,6 +671,10 @@ def main():
                 "backend": rt.get_backend(), "modes": ddp.sync_plan(),
                 "factor_tuning": ddp.factor_tuning}
 
+    comm_nranks = None
+    if a.impl == "tdp" and rt.comm() is not None:
+        comm_nranks = int(rt.comm().nranks)
+
     def record(diag):
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
                                           bn=", +SyncBatchNorm" if a.syncbn else "")
@@ -637,6 +714,8 @@ def main():
                 if a.impl == "tdp" and ddp is not None else None,
                 "gemm_products": _gemm_products(a.impl, use_gpu),
                 "sync": sync,
+                "launched_by": launched_by(),
+                "comm_nranks": comm_nranks,
             },
         }
         if diag is not None:

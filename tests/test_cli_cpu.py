@@ -26,6 +26,7 @@ def _settings(tmp_path, **train):
 def _run(args, env_extra=None, timeout=300):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     env.update(env_extra or {})
+    env = {k: v for k, v in env.items() if v is not None}  # None: drop the variable
     return subprocess.run([sys.executable, *args], capture_output=True, text=True, env=env,
                           timeout=timeout, cwd=ROOT)
 
@@ -82,6 +83,33 @@ def test_bench_two_ranks_one_json_line(api):
     assert rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 32
     assert rec["value"] > 0 and rec["steps"] == 3 and rec["warmup"] == 1
     assert ("Accelerator.prepare" in rec["config"]["impl"]) == (api == "accelerate")
+
+
+def test_bench_self_launches_n_ranks():
+    """``python bench.py --gpus 3`` with no launcher environment spawns its own 3 ranks (no
+    torchrun), relays rank 0's single JSON line, and reports dp3 / 3x the per-rank batch."""
+    env = {k: None for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    r = _run(["bench.py", "--cpu", "--gpus", "3", "--steps", "2", "--warmup", "1",
+              "--dataset", "192", "--batch", "16", "--mlp-dims", "64,32,32"],
+             env_extra=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["config"]["parallelism"] == "dp3" and rec["config"]["global_batch"] == 48
+    assert rec["config"]["launched_by"].startswith("bench.py (self-launched 3 ranks")
+    assert rec["steps"] == 2 and rec["warmup"] == 1
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """Without a one-GPU vehicle, --gpus N on a box with fewer GPUs exits non-zero instead of
+    reporting a one-rank number as an N-GPU one."""
+    env = {k: None for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "TDP_GPU_RELAY", "TDP_GPU_PEER")}
+    r = _run(["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0"], env_extra=env,
+             timeout=120)
+    assert r.returncode == 2, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.stdout.strip() == ""
+    assert "only 0 GPU(s) are visible" in r.stderr
 
 
 def test_train_ddp_host_pipeline_two_ranks(tmp_path):

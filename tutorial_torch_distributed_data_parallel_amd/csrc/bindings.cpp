@@ -1595,6 +1595,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("world", &Communicator::world)
       .def_property_readonly("device", &Communicator::device)
       .def_property_readonly("native_rccl", &Communicator::native_rccl)
+      .def_property_readonly("nranks", &Communicator::nranks)
       // collectives enqueued on the CURRENT stream (ordered with surrounding PyTorch work)
       .def("all_reduce",
            [](Communicator& c, Tensor& t, const std::string& op) {

@@ -157,6 +157,13 @@ void Communicator::watchdog_loop() {
   }
 }
 
+int Communicator::nranks() const {
+  if (!comm_) return world_;
+  int n = 0;
+  check_nccl(ncclCommCount(comm_, &n), "ncclCommCount");
+  return n;
+}
+
 void Communicator::abort() {
   if (comm_) {
     ncclCommAbort(comm_);

@@ -70,8 +70,12 @@ class Communicator {
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   double timeout() const { return timeout_s_; }
   int pending_watches();
-  // true when collectives really run on RCCL (false: the host relay of bindings.cpp)
+  // true when collectives really run on RCCL (false: the host relay of bindings.cpp, the peer
+  // vehicle of peer.hip)
   virtual bool native_rccl() const { return true; }
+  // ranks the transport itself reports (ncclCommCount for RCCL): the bench's self-check that a
+  // world-size-N job really built an N-rank communicator
+  virtual int nranks() const;
 
  protected:
   // for subclasses that move the bytes themselves: creates the comm stream, no RCCL communicator

@@ -141,15 +141,21 @@ def spawn(fn, nprocs: int, args=(), master_addr: str = "127.0.0.1",
 
 
 def run_script(nproc: int, argv, master_addr: str = "127.0.0.1", master_port: int | None = None,
-               grace: float = 30.0) -> int:
-    """torchrun-style: run ``python argv...`` nproc times with rank env; fail-fast."""
+               grace: float = 30.0, env_extra: dict | None = None, rank0_stdout=None) -> int:
+    """torchrun-style: run ``python argv...`` nproc times with rank env; fail-fast.
+    ``env_extra`` is added to every rank's environment; ``rank0_stdout`` (a file object)
+    receives rank 0's stdout instead of the launcher's (bench.py relays it)."""
     store, port, extra = (None, master_port, {}) if master_port else \
         _launcher_store(master_addr, nproc)
     procs = []
     for r in range(nproc):
         env = dict(os.environ)
         env.update(_rank_env(r, nproc, master_addr, port), **extra)
-        procs.append(subprocess.Popen([sys.executable, *argv], env=env, start_new_session=True))
+        if env_extra:
+            env.update({k: str(v) for k, v in env_extra.items()})
+        out = rank0_stdout if r == 0 and rank0_stdout is not None else None
+        procs.append(subprocess.Popen([sys.executable, *argv], env=env, start_new_session=True,
+                                      stdout=out))
     rc = 0
     try:
         while procs:
