@@ -143,6 +143,55 @@ def test_captured_step_matches_eager(pg):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
 
 
+def test_captured_step_keeps_ddp_host_bookkeeping(pg):
+    """Replays advance DDP's iteration counter like eager steps (the capture itself does not
+    count), check_replicas_every fires after replays, and find_unused_parameters=True refuses
+    capture (the per-iteration unused set is host logic) so try_capture runs eagerly."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.train import graph as G
+
+    torch.manual_seed(5)
+    m = ToyMLP(in_features=128, hidden=(64,), num_classes=10, device="cuda")
+    d = tdp.DDP(m, device_ids=[0], check_replicas_every=2)
+    o = tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+    x = torch.randn(32, 128, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    calls = []
+    d.check_replicas = lambda: calls.append(d._iter)
+
+    def step():
+        o.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d(x), y))
+        o.step()
+
+    g = G.CapturedStep(step, warmup=3)
+    assert d._iter == 3  # three real warm-up steps; recording the graph is not a step
+    calls.clear()
+    for _ in range(5):
+        g.replay()
+    assert d._iter == 8
+    assert calls == [4, 6, 8]
+    del g
+
+    m2 = ToyMLP(in_features=128, hidden=(64,), num_classes=10, device="cuda")
+    d2 = tdp.DDP(m2, device_ids=[0], find_unused_parameters=True)
+    o2 = tdp.optim.SGD(d2.parameters(), lr=0.05)
+
+    def step2():
+        o2.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d2(x), y))
+        o2.step()
+
+    logs = []
+    got = G.try_capture(step2, warmup=1, log=logs.append)
+    assert got is step2 and "find_unused_parameters" in logs[0]
+    it = d2._iter
+    got()
+    assert d2._iter == it + 1
+    del d2, d
+
+
 @pytest.mark.parametrize("opt_name", ["sgd", "adam"])
 def test_fused_optimizer_matches_unfused(pg, opt_name):
     """Optimizer applied per bucket inside the reduction == optimizer.step() after backward."""

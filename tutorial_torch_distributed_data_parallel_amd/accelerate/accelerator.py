@@ -98,20 +98,35 @@ class ShardedLoader:
                 self.acc.end_of_dataloader = i == n - 1
                 yield batch
             return
-        W, r = self.acc.num_processes, self.acc.process_index
+        # host datasets: the same one-batch look-ahead, so the last batch this rank yields --
+        # the even_batches completion round included -- is flagged end_of_dataloader
         dev = self.acc.device
+        it = self._host_batches()
+        cur = next(it, None)
+        while cur is not None:
+            nxt = next(it, None)
+            self.acc.end_of_dataloader = nxt is None
+            yield _to_device(cur, dev)
+            cur = nxt
+
+    def _host_batches(self):
+        """This rank's batches of a host loader: round-robin over whole batches
+        (BatchSamplerShard with split_batches=False, ACC/data_loader.py:213-271)."""
+        W, r = self.acc.num_processes, self.acc.process_index
         batches = []
-        for i, batch in enumerate(self.base):
+        for batch in self.base:
             batches.append(batch)
             if len(batches) == W:
-                yield _to_device(batches[r], dev)
+                yield batches[r]
                 batches = []
         if batches and self.even:
             # complete the last round with batches from the start, like even_batches=True
             head = iter(self.base)
             while len(batches) < W:
                 batches.append(next(head))
-            yield _to_device(batches[r], dev)
+            yield batches[r]
+        elif len(batches) > r:
+            yield batches[r]
 
     def __len__(self):
         n = len(self.base)
@@ -226,9 +241,14 @@ class Accelerator:
         ``zero_grad`` are skipped. With a fused optimizer registered, its in-reduction update
         happens on the synchronising micro-step only (the accumulated gradient goes through the
         bucket path)."""
-        self._step += 1
-        self.sync_gradients = (self._step % self.gradient_accumulation_steps == 0 or
-                               self.end_of_dataloader)
+        # Accelerate's _do_sync: the epoch's last batch forces a sync AND restarts the window
+        # (step = 0), so every epoch's windows start at its first batch
+        if self.end_of_dataloader:
+            self._step = 0
+            self.sync_gradients = True
+        else:
+            self._step += 1
+            self.sync_gradients = self._step % self.gradient_accumulation_steps == 0
         with contextlib.ExitStack() as stack:
             if not self.sync_gradients:
                 for m in models or self._models:

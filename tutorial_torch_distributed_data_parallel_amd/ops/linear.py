@@ -108,11 +108,8 @@ class _LinearFn(torch.autograd.Function):
         if pre is not None:
             # computed by the producer's split-K reduce (head of the previous fused Linear)
             y = pre
-        else:
-            y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
-        if pre is not None:
-            pass
         elif planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
+            y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
             # a hidden layer's output also leaves as planes: the next skinny GEMM's A operand
             op = torch.empty((3, M, N), device=x2.device, dtype=torch.bfloat16) \
                 if relu and N % 32 == 0 else None
@@ -130,6 +127,7 @@ class _LinearFn(torch.autograd.Function):
             if took and kw:
                 y._tdp_head_out = (kw["head_out"], y._version, _head_key(hw, hb))
         else:
+            y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
             C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
         ctx.relu = relu
         ctx.gate_in = gate_in
@@ -155,8 +153,11 @@ class _LinearFn(torch.autograd.Function):
         if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16 and \
                 _HEAD_FUSED:
             # classifier head (out <= 16): input gradient (gated, + its planes for the next skinny
-            # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd); a
-            # head's update stays in the reducer's flat pass (no GEMM epilogue on skinny plans)
+            # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd). At
+            # world size 1 with the fused optimizer the same kernel also applies the SGD / Adam
+            # update to W (and b) in place and marks them done through note_epilogue (hand_off):
+            # the reducer's bucket pass then skips them; otherwise it writes dw / db and the
+            # update happens in the reducer's pass
             dx = torch.empty_like(x2)
             dw = grad_dest(w_param)
             gate = x2 if ctx.gate_in else None

@@ -372,8 +372,9 @@ class DistributedDataParallel(nn.Module):
     # --------------------------------------------------------------------------- nn.Module
     def forward(self, *inputs, **kwargs):
         if self.check_replicas_every and self._iter and \
-                self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled():
-            self.check_replicas()
+                self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled() and \
+                not (self._gpu and torch.cuda.is_current_stream_capturing()):
+            self.check_replicas()  # (a captured step checks after its replays: CapturedStep)
         sample = (self._sample_every and torch.is_grad_enabled() and
                   self._iter % self._sample_every == 0 and
                   not (self._gpu and torch.cuda.is_current_stream_capturing()))
@@ -695,7 +696,7 @@ class DistributedDataParallel(nn.Module):
         agrees the slot size (max per-rank batch, one all-reduce; it must run eagerly); later
         steps zero-pad smaller batches into it (a ragged last batch on one rank contributes only
         its rows), so the decision depends on agreed values only. A batch larger than the slot
-        raises (the launcher's fail-fast then ends every rank)."""
+        re-agrees a larger one in eager execution and raises inside a capture."""
         i = self._epi_index[id(p)]
         o, n, bi = self._factor[i]
         B = int(g.shape[0])
@@ -714,9 +715,20 @@ class DistributedDataParallel(nn.Module):
             cap = int(t.item())
             self._factor_cap[i] = cap
         if B > cap:
-            raise RuntimeError(
-                f"DDP factored synchronisation: per-rank batch {B} exceeds the {cap} rows agreed "
-                "at the first step (keep later batches <= the first one, or factor_sync=False)")
+            if self._gpu and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(
+                    f"DDP factored synchronisation: per-rank batch {B} exceeds the {cap} rows "
+                    "agreed before this hipGraph capture (the slots are baked into the graph)")
+            # eager: re-agree a larger slot (max over ranks) and reallocate. Under
+            # DistributedSampler / even_batches every rank sees the same batch size at the same
+            # step, so every rank enters this collective together (a first step smaller than
+            # later ones: a resumed ragged batch, a small warm-up batch)
+            t = torch.tensor([B], dtype=torch.int64, device=self.device)
+            rt.all_reduce(t, "max")
+            cap = int(t.item())
+            self._factor_cap[i] = cap
+            for k in [k for k in self._factor_bufs if k[0] == i]:
+                del self._factor_bufs[k]
         if 2 * W * cap * (o + n) > o * n:
             self._factor_mode[i] = "bucket"
             return False

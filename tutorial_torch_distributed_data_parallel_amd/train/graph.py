@@ -28,6 +28,7 @@ construction the model has taken exactly ``warmup`` steps.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -61,18 +62,37 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         # a bucket rebuild planned by the warm-up must happen now, eagerly: recorded into the
         # graph, its relayout would restore the pre-capture buffers at every replay
-        for d in list(_LIVE):
+        live = list(_LIVE)
+        for d in live:
             d.settle()
         torch.cuda.synchronize()
         if _capture_fault_injected():
             raise CaptureFailed("injected capture fault (TDP_FAULT_CAPTURE)")
+        # DDP's host-side per-iteration logic (its iteration counter, which drives
+        # check_replicas_every) runs while the step is recorded but not on replays: note the
+        # counters, restore them after the capture -- on success AND failure, so ranks that
+        # captured and ranks that did not agree on the count -- and advance them per replay
+        before = {id(d): (d, d._iter) for d in live}
         self.graph = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(self.graph, pool=pool):
                 self.output = step_fn()
         except Exception as e:
             raise CaptureFailed(repr(e)) from e
+        finally:
+            self._ddps = []
+            for d, it in before.values():
+                if d._iter != it:
+                    self._ddps.append(weakref.ref(d))
+                    d._iter = it
         torch.cuda.synchronize()
+        if any(r().find_unused_parameters for r in self._ddps if r() is not None):
+            # which parameters went unused is decided on the host every iteration (the reducer
+            # zeroes their slots): a graph would freeze the capture-time answer. The flag is a
+            # constructor argument, identical on every rank, so every rank refuses alike.
+            self.graph = None
+            raise CaptureFailed("DDP(find_unused_parameters=True): the unused-parameter set is "
+                                "host bookkeeping per iteration; the step runs eagerly")
 
     def replay(self):
         from ..optim.fused import sync_all_hyper
@@ -84,6 +104,15 @@ class CapturedStep:
         comm = rt.comm()
         if comm is not None and comm.world > 1:
             comm.watch_current("captured training step")  # RCCL watchdog covers the replay
+        for ref in self._ddps:
+            d = ref()
+            if d is None:
+                continue
+            d._iter += 1
+            # the eager forward checks before the step whose count is a multiple: same cadence,
+            # run outside the graph (it is a collective: every rank replays in lock-step)
+            if d.check_replicas_every and d._iter % d.check_replicas_every == 0:
+                d.check_replicas()
         return self.output
 
     __call__ = replay
