@@ -80,11 +80,12 @@ def _close(model, ref, tag, atol=5e-5, rtol=2e-4):
         torch.testing.assert_close(a, b, atol=atol, rtol=rtol, msg=lambda m: f"{tag} param {i}: {m}")
 
 
-def collectives(rank, out_dir):
-    """The relay's collectives have RCCL's semantics, in place included."""
-    tdp.init_process_group("relay")
+def collectives(rank, out_dir, backend="relay"):
+    """The relay's (and the peer vehicle's) collectives have RCCL's semantics, in place
+    included."""
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
-    assert rt.get_backend() == "relay" and not rt.comm().native_rccl
+    assert rt.get_backend() == backend and not rt.comm().native_rccl
     t = torch.full((5,), float(r + 1), device="cuda")
     rt.all_reduce(t, "sum")
     assert torch.equal(t, torch.full_like(t, W * (W + 1) / 2))
@@ -113,11 +114,11 @@ def collectives(rank, out_dir):
 
 
 def ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, fused=True, steps=5,
-               ragged=True):
+               ragged=True, backend="relay"):
     """The production world>1 step on the device path vs the fp32 torch oracle: fused (sharded
     or factored) optimizer, an LR change at step 3, a ragged batch on the last rank at step 4,
     replicas bit-identical (checksum all-gather) and the reported sync plan."""
-    tdp.init_process_group("relay")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
     torch.manual_seed(0)
     model = ToyMLP(**DIMS, device="cuda")
@@ -156,10 +157,10 @@ def ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, fused=Tru
     tdp.destroy_process_group()
 
 
-def syncbn_parity(rank, out_dir, steps=3):
+def syncbn_parity(rank, out_dir, steps=3, backend="relay"):
     """SyncBatchNorm on the device path at W ranks == BatchNorm over the concatenated global
     batch (forward statistics all-gathered, backward sums all-reduced), running stats included."""
-    tdp.init_process_group("relay")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
     torch.manual_seed(0)
     model = tdp.nn.convert_sync_batchnorm(ToyMLP(**DIMS, batchnorm=True, device="cuda"))

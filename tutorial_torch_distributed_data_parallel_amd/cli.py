@@ -144,8 +144,10 @@ def train_ddp(argv=None):
                                 s["out_dir"], optional_args, s["train"])
         return 0
     world = world_size_from(s)
-    if torch.cuda.is_available() and os.environ.get("TDP_GPU_RELAY", "0") != "1":
-        world = min(world, torch.cuda.device_count())  # the relay shares one GPU among ranks
+    if torch.cuda.is_available() and os.environ.get("TDP_GPU_RELAY", "0") != "1" and \
+            os.environ.get("TDP_GPU_PEER", "0") != "1":
+        # (the relay and peer vehicles share one GPU among ranks)
+        world = min(world, torch.cuda.device_count())
     spawn(basic_ddp_training_loop, world, args=(world, s["out_dir"], optional_args, s["train"]))
     return 0
 

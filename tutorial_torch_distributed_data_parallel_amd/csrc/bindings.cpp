@@ -17,6 +17,7 @@
 #include "kernels.h"
 #include "planes.h"
 #include "loader.h"
+#include "peer.h"
 #include "pool.h"
 #include "reducer.h"
 
@@ -1261,6 +1262,11 @@ class RelayCommunicator : public Communicator {
   py::object relay_;
 };
 
+std::shared_ptr<PeerCommunicator> make_peer_comm(int rank, int world, int device,
+                                                 int64_t slot_bytes) {
+  return std::make_shared<PeerCommunicator>(rank, world, device, slot_bytes);
+}
+
 std::shared_ptr<RelayCommunicator> make_relay_comm(int rank, int world, int device,
                                                    py::object relay) {
   return std::make_shared<RelayCommunicator>(rank, world, device, std::move(relay));
@@ -1647,6 +1653,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       m, "RelayCommunicator")
       .def(py::init(&make_relay_comm), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("relay"));
+
+  py::class_<PeerCommunicator, Communicator, std::shared_ptr<PeerCommunicator>>(
+      m, "PeerCommunicator")
+      .def(py::init(&make_peer_comm), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("slot_bytes") = (int64_t)64 << 20)
+      .def("local_handle", [](const PeerCommunicator& c) {
+        auto v = c.local_handle();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("connect", [](PeerCommunicator& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::vector<uint8_t>> v;
+        for (const auto& h : hs) {
+          std::string s = h;
+          v.emplace_back(s.begin(), s.end());
+        }
+        c.connect(v);
+      })
+      .def_property_readonly("slot_bytes", &PeerCommunicator::slot_bytes)
+      .def("inject_stall_ms", &PeerCommunicator::inject_stall_ms)
+      .def("device_error", [](PeerCommunicator& c) {
+        std::string w;
+        return c.device_error(&w) ? py::object(py::str(w)) : py::object(py::none());
+      });
 
   py::class_<ReducerBackend, std::shared_ptr<ReducerBackend>>(m, "ReducerBackend")
       .def("last_comm_ms", &ReducerBackend::last_comm_ms);

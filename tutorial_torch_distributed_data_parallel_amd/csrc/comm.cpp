@@ -94,12 +94,16 @@ void Communicator::make_stream() {
   else if (const char* m = std::getenv("TDP_TIMEOUT_MIN")) timeout_s_ = 60.0 * std::atof(m);
 }
 
-Communicator::~Communicator() {
+void Communicator::stop_watchdog() {
   if (thread_.joinable()) {
     stop_ = true;
     cv_.notify_all();
     thread_.join();
   }
+}
+
+Communicator::~Communicator() {
+  stop_watchdog();
   for (auto& w : watches_) (void)hipEventDestroy(w.ev);
   for (auto e : free_events_) (void)hipEventDestroy(e);
   if (comm_) ncclCommDestroy(comm_);
@@ -109,6 +113,11 @@ Communicator::~Communicator() {
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
+}
+
+void Communicator::start_watchdog() {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!thread_.joinable()) thread_ = std::thread([this] { watchdog_loop(); });
 }
 
 void Communicator::watch(hipStream_t s, const char* what) {
@@ -142,6 +151,13 @@ void Communicator::watchdog_loop() {
     while (!watches_.empty() && hipEventQuery(watches_.front().ev) == hipSuccess) {
       free_events_.push_back(watches_.front().ev);
       watches_.pop_front();
+    }
+    std::string err;
+    if (device_error(&err)) {
+      std::fprintf(stderr, "[tdp] %s; aborting the communicator and exiting\n", err.c_str());
+      std::fflush(stderr);
+      if (comm_) ncclCommAbort(comm_);
+      std::_Exit(86);
     }
     if (!watches_.empty() && now_s() > watches_.front().deadline) {
       const Watch w = watches_.front();

@@ -76,11 +76,17 @@ class Communicator {
   // ranks the transport itself reports (ncclCommCount for RCCL): the bench's self-check that a
   // world-size-N job really built an N-rank communicator
   virtual int nranks() const;
+  // an error the transport detected on the device (the peer vehicle's bounded spins); polled by
+  // the watchdog thread, which then reports it and exits 86 like a watchdog timeout
+  virtual bool device_error(std::string* what) { (void)what; return false; }
 
  protected:
   // for subclasses that move the bytes themselves: creates the comm stream, no RCCL communicator
   Communicator(int rank, int world, int device);
   void make_stream();
+  void start_watchdog();
+  // a subclass whose device_error() the watchdog calls stops the thread in ITS destructor
+  void stop_watchdog();
 
  private:
   struct Watch {

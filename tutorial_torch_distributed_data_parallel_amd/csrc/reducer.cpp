@@ -1,6 +1,7 @@
 #include "reducer.h"
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
@@ -237,8 +238,9 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
   }
   const char* mode = std::getenv("TDP_COMM_STREAM");
   const std::string m = mode ? mode : "auto";
-  const char* fm = std::getenv("TDP_GRAPH_FORK_MARKER");
-  fork_marker_ = !(fm && fm[0] == '0');
+  const char* fm = std::getenv("TDP_GRAPH_FORK");
+  const std::string f = fm ? fm : "defer";
+  fork_mode_ = f == "marker" ? kForkMarker : f == "inline" ? kForkInline : kForkDefer;
   stream_mode_ = m == "side" ? kStreamSide
                  : m == "compute" ? kStreamCompute
                  : m == "hostsync" ? kStreamHostSync
@@ -290,6 +292,7 @@ void SyncBackend::begin_iteration(hipStream_t compute) {
   // an iteration that never reached wait_all (an exception, an aborted capture) must not leak
   // its stream choice into this one
   launched_side_ = launched_any_ = false;
+  forks_.clear();
   for (auto& f : factor_) f.B = 0;
   std::fill(factor_skip_.begin(), factor_skip_.end(), 0);
   epi_done_.clear();
@@ -300,7 +303,17 @@ void SyncBackend::begin_iteration(hipStream_t compute) {
   if (clip == ClipMode::LOCAL) ops_->clip_begin(1, compute);
 }
 
-hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute) {
+static std::vector<hipGraphNode_t> capture_frontier(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const hipGraphNode_t* deps = nullptr;
+  size_t n = 0;
+  check_hip(hipStreamGetCaptureInfo_v2(s, &st, nullptr, nullptr, &deps, &n),
+            "hipStreamGetCaptureInfo_v2");
+  return std::vector<hipGraphNode_t>(deps, deps + n);
+}
+
+hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute, bool* deferred) {
+  *deferred = false;
   if (!ops_->on_device()) return nullptr;
   // Stream choice (measured on MI355X, profiles/side_stream_eager.md): in EAGER execution a
   // side stream costs 1.5-3x step time -- a hipStreamWaitEvent left pending on one hardware
@@ -321,17 +334,55 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute) {
     // HIP's replay puts the chain on a different stream at every fork and, after a few buckets,
     // on the collectives' hardware queue -- backward serialised behind an all-reduce (measured:
     // profiles/graph_fork_order_r3.md; consistent with the first child edge of a node inheriting
-    // its stream). An empty node on the compute stream, captured before the collective, keeps
-    // compute and collectives on separate queues: the probe replays fully concurrent.
-    if (capturing && fork_marker_) graph_fork_marker(compute);
-    if (stream_mode_ == kStreamHostSync)
-      check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
-    else
-      check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+    // its stream). Default: defer the side branch until the compute chain has its next node
+    // (issue / flush_forks); "marker" captures an empty kernel first instead (15 us per fork
+    // on the replay, profiles/r7/mlp_rehearsal_kernels_r7a.md).
+    if (capturing && fork_mode_ == kForkDefer) {
+      if (forks_.empty()) fork_deps_ = capture_frontier(compute);
+      *deferred = true;
+      return cs;
+    }
+    if (capturing && fork_mode_ == kForkMarker) graph_fork_marker(compute);
+    enter_side(bucket, cs);
+    return cs;
   }
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
   return cs;
+}
+
+void SyncBackend::enter_side(int bucket, hipStream_t cs) {
+  if (stream_mode_ == kStreamHostSync)
+    check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
+  else
+    check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+  if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
+  launched_any_ = true;
+}
+
+void SyncBackend::issue(int bucket, hipStream_t compute, std::function<void(hipStream_t)> fn) {
+  bool deferred = false;
+  hipStream_t cs = pick_stream(bucket, compute, &deferred);
+  if (deferred) {
+    launched_any_ = true;
+    forks_.push_back({bucket, std::move(fn)});
+    return;
+  }
+  fn(cs);
+}
+
+void SyncBackend::flush_forks(hipStream_t compute, bool force) {
+  if (forks_.empty()) return;
+  // the compute stream captured a node since the first deferred fork: its chain owns the
+  // producer's first child edge now, so the side branches can be captured
+  if (!force && capture_frontier(compute) == fork_deps_) return;
+  auto forks = std::move(forks_);
+  forks_.clear();
+  hipStream_t cs = ops_->comm_stream();
+  for (auto& f : forks) {
+    enter_side(f.bucket, cs);
+    f.fn(cs);
+  }
 }
 
 static bool is_sharded(const SyncBackend& b, int W) {
@@ -392,6 +443,7 @@ void SyncBackend::finish_bucket(int64_t begin, int64_t end, hipStream_t cs) {
 
 void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t compute) {
   if (end <= begin) return;
+  flush_forks(compute, false);
   if (clip == ClipMode::LOCAL) {
     // the local norm needs the whole local gradient: nothing goes on the wire before backward ends
     pending_.push_back({begin, end});
@@ -422,18 +474,19 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
         (int64_t)j.out * j.in != end - begin)
       throw std::runtime_error("factored bucket: needs the fused optimizer, no clipping / "
                                "compression, and one whole-row-sharded weight per bucket");
-    hipStream_t cs = pick_stream(bucket, compute);
-    ops_->factor_sync(begin, own.first, cnt, j, cs);
+    const int64_t own0 = own.first;
+    issue(bucket, compute, [this, begin, own0, cnt, j](hipStream_t cs) {
+      ops_->factor_sync(begin, own0, cnt, j, cs);
+    });
     return;
   }
-  hipStream_t cs = pick_stream(bucket, compute);
-  reduce_bucket(begin, end, cs);
-  if (fused_kind == 0) return;
-  if (clip == ClipMode::GLOBAL) {
+  if (clip == ClipMode::GLOBAL && fused_kind != 0)
     pending_.push_back({begin, end});  // the update needs the norm of every bucket
-    return;
-  }
-  finish_bucket(begin, end, cs);
+  const bool finish = fused_kind != 0 && clip != ClipMode::GLOBAL;
+  issue(bucket, compute, [this, begin, end, finish](hipStream_t cs) {
+    reduce_bucket(begin, end, cs);
+    if (finish) finish_bucket(begin, end, cs);
+  });
 }
 
 void SyncBackend::run_clip_local(hipStream_t s) {
@@ -480,6 +533,7 @@ void SyncBackend::run_clip_global(hipStream_t s) {
 }
 
 void SyncBackend::wait_all(hipStream_t compute) {
+  flush_forks(compute, true);  // end of backward: nothing left for the compute chain to own
   // 1. join the comm stream: the compute stream waits for every bucket launched on it
   if (launched_side_) {
     launched_side_ = false;

@@ -218,7 +218,16 @@ class SyncBackend : public ReducerBackend {
   void finish_bucket(int64_t begin, int64_t end, hipStream_t cs);   // update + all-gather
   Ranges update_ranges(int64_t begin, int64_t end) const;           // own ranges minus epilogue
   Ranges minus_epilogue(const Ranges& in) const;
-  hipStream_t pick_stream(int bucket, hipStream_t compute);
+  // Run `fn` (a bucket's collectives + update) on the stream pick_stream chooses. While a graph
+  // is captured with the comm stream as a side branch, the fork is DEFERRED: the ready event is
+  // recorded now, but the side-stream wait and `fn` are captured only once the compute stream
+  // has captured its next node (flush_forks), so the compute chain is the producer's first child
+  // -- what keeps the two branches on separate hardware queues at replay
+  // (profiles/graph_fork_order_r3.md: "compute_first") without an empty marker kernel.
+  void issue(int bucket, hipStream_t compute, std::function<void(hipStream_t)> fn);
+  void flush_forks(hipStream_t compute, bool force);
+  hipStream_t pick_stream(int bucket, hipStream_t compute, bool* deferred);
+  void enter_side(int bucket, hipStream_t cs);
   void run_clip_local(hipStream_t cs);
   void run_clip_global(hipStream_t cs);
 
@@ -230,6 +239,12 @@ class SyncBackend : public ReducerBackend {
   Ranges deferred_;              // world size 1: bucket updates deferred to the end of backward
   std::vector<FactorJob> factor_;  // per bucket, armed for this iteration when B > 0
   std::vector<char> factor_skip_;  // per bucket: a factored bias, handled by its weight's job
+  struct Fork {
+    int bucket;
+    std::function<void(hipStream_t)> fn;
+  };
+  std::vector<Fork> forks_;               // deferred side-stream launches (capture only)
+  std::vector<hipGraphNode_t> fork_deps_; // compute stream's capture frontier at the first one
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;
@@ -240,7 +255,10 @@ class SyncBackend : public ReducerBackend {
     kStreamHostJoin = 4, kStreamNoJoin = 5
   };
   int stream_mode_ = kStreamAuto;
-  bool fork_marker_ = true;  // TDP_GRAPH_FORK_MARKER=0 disables (A/B)
+  // captured fork form (TDP_GRAPH_FORK, A/B only): defer (default) | marker (an empty kernel on
+  // the compute stream before each fork, the round-3 form) | inline (fork captured first)
+  enum { kForkDefer = 0, kForkMarker = 1, kForkInline = 2 };
+  int fork_mode_ = kForkDefer;
 };
 
 class Reducer {

@@ -87,7 +87,9 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
                        timeout: _dt.timedelta | None = None) -> None:
     """Join the job. ``backend``: "nccl"/"rccl" (GPU), "gloo" (CPU), "relay" (GPU tensors and
     kernels, collectives relayed through the host over gloo: several ranks sharing one GPU,
-    parallel/relay.py) or None (auto). ``TDP_GPU_RELAY=1`` turns a GPU backend into "relay".
+    parallel/relay.py), "peer" (several ranks sharing one GPU with device-side, capturable
+    collectives through IPC-mapped windows, parallel/peer.py) or None (auto).
+    ``TDP_GPU_RELAY=1`` / ``TDP_GPU_PEER=1`` turn a GPU backend into "relay" / "peer".
 
     Auto picks RCCL when a GPU is visible, else gloo (the reference's NCCL-else-gloo rule,
     REF/multi-GPU-training-torch.py:34-42, decided on what can actually run).
@@ -104,11 +106,13 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
         os.environ["MASTER_PORT"] = str(master_port)
     os.environ.setdefault("MASTER_PORT", "29500")
     want = (backend or "auto").lower()
-    relay = want == "relay" or (os.environ.get("TDP_GPU_RELAY", "0") == "1" and
-                                want in ("nccl", "rccl", "auto") and torch.cuda.is_available())
-    if relay:
+    gpu_kind = want in ("nccl", "rccl", "auto") and torch.cuda.is_available()
+    peer = want == "peer" or (os.environ.get("TDP_GPU_PEER", "0") == "1" and gpu_kind)
+    relay = not peer and (want == "relay" or (os.environ.get("TDP_GPU_RELAY", "0") == "1" and
+                                              gpu_kind))
+    if relay or peer:
         if not torch.cuda.is_available():
-            raise RuntimeError("backend 'relay' needs a GPU")
+            raise RuntimeError(f"backend '{'peer' if peer else 'relay'}' needs a GPU")
         use_gpu = True
     elif want in ("nccl", "rccl"):
         if not torch.cuda.is_available():
@@ -136,14 +140,18 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
     owns = False
     # a single-rank job needs no rendezvous at all (and must not grab MASTER_PORT)
     if world > 1 and not dist.is_initialized():
-        pg_backend = "cpu:gloo,cuda:nccl" if use_gpu and not relay else "gloo"
+        pg_backend = "cpu:gloo,cuda:nccl" if use_gpu and not (relay or peer) else "gloo"
         dist.init_process_group(backend=pg_backend, rank=rank, world_size=world, timeout=timeout)
         owns = True
     _S.initialized = True
-    _S.backend = ("relay" if relay else "rccl") if use_gpu else "gloo"
+    _S.backend = ("peer" if peer else "relay" if relay else "rccl") if use_gpu else "gloo"
     _S.rank, _S.world, _S.local_rank, _S.device = rank, world, local_rank, dev
     _S.owns_torch_pg = owns
-    if use_gpu and relay:
+    if use_gpu and peer:
+        from .peer import make_peer_communicator
+
+        _S.comm = make_peer_communicator(rank, world, dev.index)
+    elif use_gpu and relay:
         from .relay import HostRelay
 
         _S.comm = native().RelayCommunicator(rank, world, dev.index, HostRelay(world))
@@ -165,6 +173,8 @@ def destroy_process_group() -> None:
         return
     if _S.comm is not None and torch.cuda.is_available():
         torch.cuda.synchronize()
+        if _S.backend == "peer" and _S.world > 1 and dist.is_initialized():
+            dist.barrier()  # every rank's kernels are done before any window is freed
     _S.comm = None
     if _S.owns_torch_pg and dist.is_initialized():
         dist.destroy_process_group()
