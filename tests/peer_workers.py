@@ -1,0 +1,177 @@
+"""Multi-rank workers for the peer-memory vehicle (parallel/peer.py, csrc/peer.hip): W rank
+processes on ONE GPU whose collectives are device kernels over IPC-mapped windows -- so, unlike
+the host relay, the multi-rank training step can be CAPTURED into a hipGraph and replayed with
+real peers. Oracles: closed-form collective results, the eager run of the same step (bitwise)
+and the fp32 torch DDP-semantics oracle of relay_workers."""
+import os
+import time
+
+import torch
+
+import tutorial_torch_distributed_data_parallel_amd as tdp
+from tutorial_torch_distributed_data_parallel_amd._native import native
+from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+
+from relay_workers import DIMS, B, _batch, _close, _oracle_step, _torch_mlp
+
+
+def chunked_collectives(rank, out_dir):
+    """Collectives larger than the staging slot (chunked launches), every dtype / op the
+    framework issues, in place and out of place, and a CAPTURED all-reduce / all-gather pair
+    replayed with new inputs (epochs live on the device)."""
+    os.environ["TDP_PEER_SLOT_MB"] = "0.0625"  # 64 KiB slots: every case below is chunked
+    tdp.init_process_group("peer")
+    r, W = rt.get_rank(), rt.get_world_size()
+    comm = rt.comm()
+    assert rt.get_backend() == "peer" and not comm.native_rccl and comm.nranks == W
+    assert comm.slot_bytes == 65536
+    n = 50_001  # odd: vector body + scalar tail in every chunk
+    base = torch.arange(n, device="cuda", dtype=torch.float64)
+    for dt in (torch.float32, torch.float64, torch.int64, torch.int32):
+        t = (base * (r + 1)).to(dt)
+        comm.all_reduce(t, "sum")
+        assert torch.equal(t, (base * (W * (W + 1) // 2)).to(dt)), dt
+        t = (base + r).to(dt)
+        comm.all_reduce(t, "max")
+        assert torch.equal(t, (base + W - 1).to(dt)), dt
+        t = (base + r).to(dt)
+        comm.all_reduce(t, "min")
+        assert torch.equal(t, base.to(dt)), dt
+    t = torch.full((n,), float(r), device="cuda")
+    comm.all_reduce(t, "avg")
+    assert torch.equal(t, torch.full_like(t, sum(range(W)) / W))
+    hb = torch.full((n,), float(r + 1), device="cuda", dtype=torch.bfloat16)
+    comm.all_reduce(hb, "sum")
+    assert torch.equal(hb.float(), torch.full((n,), float(W * (W + 1) // 2), device="cuda"))
+    # all-gather, in place (send = own slice of recv)
+    flat = torch.full((W * n,), -1.0, device="cuda")
+    flat[r * n: (r + 1) * n] = torch.arange(n, device="cuda", dtype=torch.float32) + 1000 * r
+    comm.all_gather(flat, flat[r * n: (r + 1) * n])
+    want = torch.cat([torch.arange(n, device="cuda", dtype=torch.float32) + 1000 * k
+                      for k in range(W)])
+    assert torch.equal(flat, want)
+    # reduce-scatter, in place (recv = own slice of send)
+    full = torch.arange(W * n, dtype=torch.float32, device="cuda") * (r + 1)
+    comm.reduce_scatter(full[r * n: (r + 1) * n], full, "sum")
+    want = torch.arange(r * n, (r + 1) * n, dtype=torch.float32, device="cuda") * W * (W + 1) / 2
+    assert torch.equal(full[r * n: (r + 1) * n], want)
+    b = torch.full((n,), float(r), device="cuda")
+    comm.broadcast(b, W - 1)
+    assert torch.equal(b, torch.full_like(b, W - 1))
+    # captured: the kernels' epoch comes from device memory, so replays stay in step
+    x = torch.zeros(n, device="cuda")
+    out = torch.zeros(W * n, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            comm.all_reduce(x, "sum")
+            comm.all_gather(out, x)
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(3):
+        x.fill_(float(r + it))
+        g.replay()
+        tot = float(sum(k + it for k in range(W)))
+        assert torch.equal(x, torch.full_like(x, tot)), (it, float(x[0]))
+        assert torch.equal(out, torch.full_like(out, tot)), it
+    rt.barrier()
+    tdp.destroy_process_group()
+
+
+def captured_ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, steps=6):
+    """The multi-rank DDP step captured into a hipGraph and replayed with real peers (bucket
+    collectives / factored gathers on the side stream, deferred forks, join) == the same step
+    run eagerly, BITWISE, on every rank; both match the fp32 torch oracle; replicas identical."""
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    tdp.init_process_group("peer")
+    r, W = rt.get_rank(), rt.get_world_size()
+    lr = 0.05 if kind == "sgd" else 2e-3
+
+    def build():
+        torch.manual_seed(0)
+        m = ToyMLP(**DIMS, device="cuda")
+        d = tdp.DDP(m, device_ids=[rt.device().index], factor_sync=factor)
+        d.factor_replicate = replicate
+        o = (tdp.optim.SGD(d.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+             if kind == "sgd" else tdp.optim.Adam(d.parameters(), lr=lr, weight_decay=1e-4))
+        assert d.register_fused_optimizer(o)
+        return m, d, o
+
+    m1, d1, o1 = build()
+    m2, d2, o2 = build()
+    ref = _torch_mlp(m1)
+    ropt = (torch.optim.SGD(ref.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+            if kind == "sgd" else torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-4))
+    sx = torch.empty(B, DIMS["in_features"], device="cuda")
+    sy = torch.empty(B, dtype=torch.long, device="cuda")
+
+    def step2():
+        o2.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d2(sx), sy))
+        o2.step()
+
+    g = None
+    for step in range(steps):
+        if step == 3:
+            for o in (o1, o2, ropt):
+                o.param_groups[0]["lr"] *= 0.5
+        x, y = _batch(r, step)
+        o1.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d1(x), y))
+        o1.step()
+        sx.copy_(x)
+        sy.copy_(y)
+        if g is None:
+            g = CapturedStep(step2, warmup=1)  # one real (eager) step on this batch, then record
+        else:
+            g.replay()
+        _oracle_step(ref, ropt, W, step, -1, -1)
+    torch.cuda.synchronize()
+    plan = d2.sync_plan()
+    if factor:
+        assert plan["fc1.weight"].startswith("factored"), plan
+    for i, (a, b) in enumerate(zip(m1.parameters(), m2.parameters())):
+        assert torch.equal(a, b), f"rank {r}: captured != eager for param {i} " \
+                                  f"(max diff {float((a - b).abs().max())})"
+    _close(m2, ref, f"captured W={W} {kind} factor={factor} replicate={replicate}")
+    d1.check_replicas()
+    d2.check_replicas()
+    rt.barrier()
+    tdp.destroy_process_group()
+
+
+def stalled_peer_times_out(rank, out_dir):
+    """Rank 1 stalls its next collective 6 s (device-side, bounded) while every wait is bounded
+    by TDP_PEER_TIMEOUT_S=1: rank 0's wait expires, its watchdog reports and exits 86."""
+    os.environ["TDP_PEER_TIMEOUT_S"] = "1"
+    tdp.init_process_group("peer")
+    comm = rt.comm()
+    if rt.get_rank() == 1:
+        comm.inject_stall_ms(6000)
+    t = torch.ones(1024, device="cuda")
+    comm.all_reduce(t, "sum")
+    time.sleep(30)  # the watchdog ends this process first (exit 86); never reached in time
+    raise SystemExit(0)
+
+
+def rccl_watchdog_child():
+    """One rank on RCCL: a bounded 8 s stall ahead of a watched collective, 2 s timeout -> the
+    watchdog aborts the communicator and exits 86 (run in a child process by the test)."""
+    os.environ["TDP_TIMEOUT_S"] = "2"
+    tdp.init_process_group("nccl", rank=0, world_size=1, local_rank=0)
+    comm = rt.comm()
+    assert comm.native_rccl and comm.timeout == 2.0
+    comm.set_watch_single_rank(True)
+    native().debug_spin_ms(8000)
+    t = torch.ones(16, device="cuda")
+    comm.all_reduce(t, "sum")
+    comm.watch_current("stalled collective")
+    time.sleep(30)
+    raise SystemExit(0)
+
+
+if __name__ == "__main__":
+    rccl_watchdog_child()

@@ -1,0 +1,90 @@
+"""MI355X: W ranks on ONE GPU through the peer-memory vehicle (csrc/peer.hip): collectives as
+device kernels, the captured multi-rank DDP step replayed with real peers,
+bounded device-side waits, and the RCCL watchdog firing on a stalled collective (item 7)."""
+import functools
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import (
+    ProcessExitedException, spawn)
+
+import peer_workers as PW  # noqa: E402  (tests/ is on sys.path via conftest)
+import relay_workers as RW  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(fn, tmp_path, n=2, **kw):
+    spawn(functools.partial(fn, **kw) if kw else fn, n, args=(str(tmp_path),), grace=5.0)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_peer_collectives_chunked_and_captured(tmp_path, n):
+    run(PW.chunked_collectives, tmp_path, n=n)
+
+
+def test_peer_relay_semantics(tmp_path):
+    """The relay's collective checks, unchanged, on the peer vehicle."""
+    run(RW.collectives, tmp_path, n=3, backend="peer")
+
+
+@pytest.mark.parametrize("world,kind,factor,replicate", [
+    (2, "sgd", True, None), (2, "adam", True, False), (3, "sgd", True, False),
+    (3, "adam", True, True), (2, "sgd", False, None), (3, "adam", False, None)])
+def test_captured_step_with_real_peers(tmp_path, world, kind, factor, replicate):
+    run(PW.captured_ddp_parity, tmp_path, n=world, kind=kind, factor=factor, replicate=replicate)
+
+
+@pytest.mark.parametrize("world,kind,replicate", [(2, "adam", False), (4, "sgd", True)])
+def test_peer_eager_device_path_matches_oracle(tmp_path, world, kind, replicate):
+    run(RW.ddp_parity, tmp_path, n=world, kind=kind, factor=True, replicate=replicate,
+        backend="peer")
+
+
+def test_peer_syncbn_matches_global_batch(tmp_path):
+    run(RW.syncbn_parity, tmp_path, n=2, backend="peer")
+
+
+def test_stalled_peer_exits_86(tmp_path):
+    with pytest.raises(ProcessExitedException) as ei:
+        run(PW.stalled_peer_times_out, tmp_path, n=2)
+    assert ei.value.exit_code == 86
+
+
+def test_rccl_watchdog_fires_on_stalled_collective():
+    """the collective watchdog (TORCH/distributed/constants.py:21 in the
+    reference's stack) aborts a stuck RCCL collective and ends the rank with exit code 86;
+    the parent process is unaffected."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "peer_workers.py")],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env=dict(os.environ, PYTHONPATH=os.path.join(ROOT, "tests") + os.pathsep +
+                                ROOT))
+    assert r.returncode == 86, (r.returncode, r.stderr[-2000:])
+    assert "RCCL watchdog" in r.stderr and "stalled collective" in r.stderr, r.stderr[-2000:]
+
+
+def test_bench_self_launch_peer_captured():
+    """``TDP_GPU_PEER=1 python bench.py --gpus 2``: bench.py spawns its two ranks itself, the
+    multi-rank step is CAPTURED with real peers, replicas end bit-identical."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    env.update(TDP_GPU_PEER="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
+           "--warmup", "3", "--mlp-dims", "1024,512,512", "--dataset", "1024", "--batch", "32",
+           "--no-diag", "--device-warmup-ms", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["launched_by"].startswith("bench.py (self-launched 2 ranks")
+    assert rec["config"]["comm_nranks"] == 2
+    sync = rec["config"]["sync"]
+    assert sync["backend"] == "peer" and sync["captured"] is True, sync
+    assert sync["replicas_identical"] is True, sync
+    assert sync["modes"]["fc1.weight"].startswith("factored"), sync

@@ -1534,14 +1534,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // g [B][out] * alpha and x [B][in]; each slot holds `slot_rows` >= B rows (the batch size the
   // ranks agreed on) and rows B.. are zeroed, so a smaller (ragged last) batch on some rank
   // still issues the same collectives and contributes exactly its own rows to g_all^T x_all
-  m.def("factor_stage", [](const Tensor& g, const Tensor& x, Tensor& g_all, Tensor& x_all,
-                          int64_t rank, double alpha, int64_t slot_rows) {
+  m.def("factor_stage", [](const Tensor& g, const c10::optional<Tensor>& xo, Tensor& g_all,
+                          Tensor& x_all, int64_t rank, double alpha, int64_t slot_rows) {
+    // x = None: x was staged (and gathered) at forward time; only g goes into its slot
     CHECK_GPU(g); CHECK_F32(g); CHECK_CONTIG(g);
-    CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
     CHECK_GPU(g_all); CHECK_F32(g_all); CHECK_CONTIG(g_all);
     CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
+    const bool has_x = xo.has_value();
+    const Tensor x = has_x ? *xo : g;
+    if (has_x) { CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); }
     TORCH_CHECK(g.dim() == 2 && x.dim() == 2 && g.size(0) == x.size(0), "factor_stage: [B][*]");
-    const int64_t B = g.size(0), out = g.size(1), in = x.size(1);
+    const int64_t B = g.size(0), out = g.size(1), in = has_x ? x.size(1) : 0;
     const int64_t rows = slot_rows < 0 ? B : slot_rows;
     TORCH_CHECK(B <= rows, "factor_stage: batch larger than the agreed slot");
     const int64_t ng = B * out, nx = B * in, sg = rows * out, sx = rows * in;
@@ -1552,10 +1555,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     float* gd = g_all.data_ptr<float>() + rank * sg;
     float* xd = x_all.data_ptr<float>() + rank * sx;
     hipStream_t s = cur_stream();
-    if (B > 0) factor_stage(g.data_ptr<float>(), x.data_ptr<float>(), gd, xd, ng, nx, (float)alpha, s);
+    if (B > 0)
+      factor_stage(g.data_ptr<float>(), has_x ? x.data_ptr<float>() : nullptr, gd,
+                   has_x ? xd : nullptr, ng, nx, (float)alpha, s);
     if (rows > B) {
       check_hip(hipMemsetAsync(gd + ng, 0, sizeof(float) * (size_t)(sg - ng), s), "memset(pad)");
-      check_hip(hipMemsetAsync(xd + nx, 0, sizeof(float) * (size_t)(sx - nx), s), "memset(pad)");
+      if (has_x)
+        check_hip(hipMemsetAsync(xd + nx, 0, sizeof(float) * (size_t)(sx - nx), s), "memset(pad)");
     }
   }, py::arg("g"), py::arg("x"), py::arg("g_all"), py::arg("x_all"), py::arg("rank"),
      py::arg("alpha"), py::arg("slot_rows") = -1);
@@ -1595,6 +1601,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask") = py::none(), py::arg("planes_out") = py::none());
 
   m.def("rccl_unique_id", &unique_id_op);
+  m.def("debug_spin_ms", [](int ms) { debug_spin_ms(ms, cur_stream()); });
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
       .def(py::init(&make_comm))
       .def_property_readonly("rank", &Communicator::rank)
@@ -1642,6 +1649,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("watch_current",
            [](Communicator& c, const std::string& what) { c.watch(cur_stream(), what.c_str()); })
       .def_property("timeout", &Communicator::timeout, &Communicator::set_timeout)
+      .def("set_watch_single_rank", &Communicator::set_watch_single_rank)
       .def("pending_watches", &Communicator::pending_watches)
       // block the host until everything enqueued on the current stream (incl. comms) finished
       .def("synchronize_current", [](Communicator&) {
@@ -1748,7 +1756,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("owned_shard", &SyncBackend::owned_shard)
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
-              int64_t bias_off, int bias_bucket, bool replicate) {
+              int64_t bias_off, int bias_bucket, bool replicate, bool x_ready) {
              // device buffers for RcclOps; host buffers for PyOps (the CPU twin looks them up by
              // address in parallel/ddp.py _CpuSyncOps.factor_sync)
              TORCH_CHECK(g_all.is_cuda() == b.ops()->on_device() &&
@@ -1765,11 +1773,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.B = B; j.out = out; j.in = in;
              j.bias_off = bias_off;
              j.replicate = replicate;
+             j.x_ready = x_ready;
              b.arm_factor(bucket, j, bias_bucket);
            },
            py::arg("bucket"), py::arg("g_all"), py::arg("x_all"), py::arg("B"), py::arg("out"),
            py::arg("in"), py::arg("bias_off"), py::arg("bias_bucket"),
-           py::arg("replicate") = false)
+           py::arg("replicate") = false, py::arg("x_ready") = false)
+      .def("prefetch_factor_x",
+           [](SyncBackend& b, int bucket, Tensor& x_all, int B, int in) {
+             CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
+             TORCH_CHECK(x_all.numel() == (int64_t)b.ops()->world() * B * in,
+                         "prefetch_factor_x: x_all must hold W*B rows of in floats");
+             b.prefetch_factor_x(bucket, x_all.data_ptr<float>(), B, in, cur_stream());
+           })
+      .def("flush", [](SyncBackend& b) { b.flush(cur_stream()); })
+      .def("reserve_factor",
+           [](SyncBackend& b, int64_t begin, int64_t end, Tensor& g_all, Tensor& x_all, int B,
+              int out, int in, int64_t bias_off, bool replicate) {
+             FactorJob j;
+             j.g_all = g_all.data_ptr<float>();
+             j.x_all = x_all.data_ptr<float>();
+             j.B = B; j.out = out; j.in = in;
+             j.bias_off = bias_off;
+             j.replicate = replicate;
+             b.reserve_factor(begin, end, j);
+           })
       .def("begin_iteration", [](SyncBackend& b, bool gpu) {
         b.begin_iteration(gpu ? cur_stream() : nullptr);
       });

@@ -121,7 +121,7 @@ void Communicator::start_watchdog() {
 }
 
 void Communicator::watch(hipStream_t s, const char* what) {
-  if (timeout_s_ <= 0.0 || world_ <= 1) return;
+  if (timeout_s_ <= 0.0 || (world_ <= 1 && !watch_single_)) return;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
   std::unique_lock<std::mutex> lk(mu_);

@@ -68,6 +68,8 @@ class Communicator {
   // watched by the caller) or when the timeout is 0.
   void watch(hipStream_t s, const char* what);
   void set_timeout(double seconds) { timeout_s_ = seconds; }
+  // watch at world size 1 too (tests: the watchdog path on a one-GPU box)
+  void set_watch_single_rank(bool on) { watch_single_ = on; }
   double timeout() const { return timeout_s_; }
   int pending_watches();
   // true when collectives really run on RCCL (false: the host relay of bindings.cpp, the peer
@@ -99,6 +101,7 @@ class Communicator {
   hipStream_t stream_ = nullptr;
   int rank_ = 0, world_ = 1, device_ = 0;
   double timeout_s_ = 600.0;
+  bool watch_single_ = false;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Watch> watches_;

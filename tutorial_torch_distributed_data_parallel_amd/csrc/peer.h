@@ -36,6 +36,10 @@ namespace tdp {
 
 constexpr int kPeerMaxWorld = 16;
 
+// test hook: one workgroup that waits `ms` of wall-clock time on `s`, then exits (a bounded stall
+// in front of a watched collective: the watchdog tests)
+void debug_spin_ms(int ms, hipStream_t s);
+
 class PeerCommunicator : public Communicator {
  public:
   PeerCommunicator(int rank, int world, int device, int64_t slot_bytes);
@@ -70,6 +74,16 @@ class PeerCommunicator : public Communicator {
   void launch(int kind, const void* send, void* recv, int64_t n_elems, int64_t seg_stride,
               int esize, ncclDataType_t dt, ncclRedOp_t op, int root, hipStream_t s);
   void check_connected() const;
+  // Collectives of one communicator must run one at a time, in issue order, on every rank: the
+  // epoch counters (and the slots) are per communicator. A collective issued on another stream
+  // than the previous one first waits for it (an event; a graph edge while capturing), as RCCL
+  // orders a communicator's operations across streams.
+  void order_after_previous(hipStream_t s);
+  void note_issued(hipStream_t s);
+  hipEvent_t last_ev_ = nullptr;
+  hipStream_t last_stream_ = nullptr;
+  unsigned long long last_capture_ = 0;  // capture id of the last issue (0 = eager)
+  bool have_last_ = false;
   char* win_ = nullptr;                      // own window (control + slot)
   std::vector<char*> peers_;                 // every rank's window as mapped here
   std::vector<bool> opened_;                 // peers_[p] came from hipIpcOpenMemHandle

@@ -258,7 +258,24 @@ void* kernel_for(ncclDataType_t dt, bool reduces) {
   }
 }
 
+__global__ void debug_spin_kernel(uint64_t ticks) {
+  if (threadIdx.x == 0) {
+    const long long t0 = wall_clock64();
+    while ((uint64_t)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
+  }
+}
+
 }  // namespace
+
+void debug_spin_ms(int ms, hipStream_t s) {
+  int dev = 0, khz = 0;
+  check_hip(hipGetDevice(&dev), "hipGetDevice");
+  check_hip(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev),
+            "hipDeviceGetAttribute(wall clock)");
+  const uint64_t ticks = (uint64_t)std::max(0, ms) * (uint64_t)(khz > 0 ? khz : 100000);
+  hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, s, ticks);
+  check_hip(hipGetLastError(), "debug_spin_kernel");
+}
 
 PeerCommunicator::PeerCommunicator(int rank, int world, int device, int64_t slot_bytes)
     : Communicator(rank, world, device), slot_bytes_(slot_bytes) {
@@ -285,6 +302,28 @@ PeerCommunicator::PeerCommunicator(int rank, int world, int device, int64_t slot
   peers_.assign(world, nullptr);
   opened_.assign(world, false);
   peers_[rank] = win_;
+  check_hip(hipEventCreateWithFlags(&last_ev_, hipEventDisableTiming), "hipEventCreate");
+}
+
+static unsigned long long capture_id(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  check_hip(hipStreamGetCaptureInfo(s, &st, &id), "hipStreamGetCaptureInfo");
+  return st == hipStreamCaptureStatusActive ? id : 0ull;
+}
+
+void PeerCommunicator::order_after_previous(hipStream_t s) {
+  // an eager issue cannot wait on a node of a finished capture, nor a capture on eager work
+  // (that work is complete before any replay: the callers synchronise around captures)
+  if (have_last_ && last_stream_ != s && last_capture_ == capture_id(s))
+    check_hip(hipStreamWaitEvent(s, last_ev_, 0), "hipStreamWaitEvent(peer order)");
+}
+
+void PeerCommunicator::note_issued(hipStream_t s) {
+  check_hip(hipEventRecord(last_ev_, s), "hipEventRecord(peer order)");
+  last_stream_ = s;
+  last_capture_ = capture_id(s);
+  have_last_ = true;
 }
 
 PeerCommunicator::~PeerCommunicator() {
@@ -294,6 +333,7 @@ PeerCommunicator::~PeerCommunicator() {
   for (int p = 0; p < (int)peers_.size(); ++p)
     if (opened_[p]) (void)hipIpcCloseMemHandle(peers_[p]);
   if (win_) (void)hipFree(win_);
+  if (last_ev_) (void)hipEventDestroy(last_ev_);
   if (err_host_) (void)hipHostFree(err_host_);
 }
 
@@ -368,8 +408,10 @@ void PeerCommunicator::launch(int kind, const void* send, void* recv, int64_t n_
     stall_ms_ = 0;
   }
   void* args[] = {&a};
+  order_after_previous(s);
   check_hip(hipLaunchKernel(kernel_for(dt, reduces), dim3(kG), dim3(kT), args, 0, s),
             "hipLaunchKernel(peer collective)");
+  note_issued(s);
 }
 
 void PeerCommunicator::all_gather(const void* send, void* recv, size_t send_count,

@@ -131,37 +131,37 @@ void SyncOps::factor_sync(int64_t, int64_t, int64_t, const FactorJob&, hipStream
   throw std::runtime_error("factored gradient synchronisation needs the device backend");
 }
 
-void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
-                          hipStream_t s) {
-  const int W = comm_->world(), r = comm_->rank();
+void SyncOps::factor_reserve(int64_t, int64_t, int64_t, const FactorJob&) {}
+
+void SyncOps::factor_gather_x(float*, int, int, hipStream_t) {
+  throw std::runtime_error("forward-time factor gathers need the device backend");
+}
+
+void RcclOps::factor_gather_x(float* x_all, int B, int in, hipStream_t s) {
+  if (skip_collectives) return;
+  const int r = comm_->rank();
+  comm_->all_gather(x_all + (int64_t)r * B * in, x_all, (size_t)B * in, ncclFloat32, s);
+}
+
+// The shard GEMM of a factored job, planned once for factor_sync and factor_reserve: this
+// rank's rows of the averaged gradient, dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all.
+struct RcclOps::FactorPlan {
+  GemmF32Args a;
+  GemmPlan plan;
+  bool epi = false, bias_in_gemm = false;
+  int bias_slices = 0;  // > 0: the bias column sums run as their own launch with this workspace
+};
+
+RcclOps::FactorPlan RcclOps::plan_factor(int64_t begin, int64_t own, int64_t cnt,
+                                         const FactorJob& j) const {
+  const int W = comm_->world();
   if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
-  if (!skip_collectives) {
-    // in place: this rank's factor rows already sit at slot r (written on the compute stream);
-    // one RCCL group, so g and x share one launch and the links carry both back to back
-    comm_->group_start();
-    comm_->all_gather(j.g_all + (int64_t)r * j.B * j.out, j.g_all, (size_t)j.B * j.out,
-                      ncclFloat32, s);
-    comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in, ncclFloat32,
-                      s);
-    comm_->group_end();
-  }
-  // this rank's rows of the averaged gradient: dW[m0:m0+rows][:] = g_all[:, m0:m0+rows]^T x_all
   int dev = 0;
   check_hip(hipGetDevice(&dev), "hipGetDevice");
   const int cus = compute_cus(dev);
-  auto grow = [&](float*& buf, int64_t& have, int64_t want, const char* what) {
-    if (want <= have) return;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
-    if (cap != hipStreamCaptureStatusNone)
-      throw std::runtime_error(std::string("factor_sync: ") + what +
-                               " must be sized by an eager step before capture");
-    if (buf) check_hip(hipFree(buf), "hipFree");
-    check_hip(hipMalloc(&buf, sizeof(float) * (size_t)want), "hipMalloc(factor)");
-    have = want;
-  };
+  FactorPlan f;
   const int64_t m0 = (own - begin) / j.in;
-  GemmF32Args a;
+  GemmF32Args& a = f.a;
   a.A = j.g_all + m0;  // stored [K = W*B][out]: MN-contiguous A, column offset m0
   a.lda = j.out;
   a.a_kcontig = false;
@@ -176,22 +176,13 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   GemmF32Args probe = a;
   probe.opt.kind = 1;
   const GemmPlan pp = gemm_f32_plan(probe, cus);
-  const bool epi = fused.kind != 0 && pp.fast && !pp.skinny && pp.splits == 1;
+  f.epi = fused.kind != 0 && pp.fast && !pp.skinny && pp.splits == 1;
   // replicated job: this rank owns every row, so the GEMM's row sums of the gathered g ARE the
   // whole averaged bias gradient -- the epilogue updates the bias from them (no separate column
   // reduction + update launches); a sharded job would only see its own rows' bias entries
-  const bool bias_in_gemm = epi && j.bias_off >= 0 && j.replicate && a.M == j.out;
-  if (j.bias_off >= 0 && !bias_in_gemm) {
-    // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
-    // every rank: identical inputs, identical results, no collective
-    const int rows = W * j.B;
-    const int sl = relu_bias_slices(rows, j.out, cus);
-    grow(factor_part_, factor_part_floats_, (int64_t)sl * j.out, "bias workspace");
-    relu_bias_bwd_ws(j.g_all, nullptr, rows, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
-                     factor_part_, sl, s);
-    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
-  }
-  if (epi) {
+  f.bias_in_gemm = f.epi && j.bias_off >= 0 && j.replicate && a.M == j.out;
+  if (j.bias_off >= 0 && !f.bias_in_gemm) f.bias_slices = relu_bias_slices(W * j.B, j.out, cus);
+  if (f.epi) {
     // the epilogue updates p / state at C's element index: the arena offset `own`
     a.opt.kind = fused.kind;
     a.opt.p = fused.p + own;
@@ -200,7 +191,7 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     a.opt.s2 = fused.s2 ? fused.s2 + own : nullptr;
     a.opt.sgd = fused.sgd;
     a.opt.adam = fused.adam;
-    if (bias_in_gemm) {
+    if (f.bias_in_gemm) {
       a.rowsum = grad_ + j.bias_off;  // selects the row-sum tiles; never written (bias_opt)
       a.rowsum_beta = 0.f;
       a.bias_opt.kind = fused.kind;
@@ -210,10 +201,60 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
       a.bias_opt.s2 = fused.s2 ? fused.s2 + j.bias_off : nullptr;
     }
   }
-  const GemmPlan plan = gemm_f32_plan(a, cus);
-  grow(factor_ws_, factor_ws_floats_, plan.ws_floats, "split-K workspace");
-  gemm_f32_run(a, plan, factor_ws_, s);
-  if (!epi) opt_update({{own, own + cnt}}, s);
+  f.plan = gemm_f32_plan(a, cus);
+  return f;
+}
+
+void RcclOps::grow_factor_ws(const FactorPlan& f, int out, hipStream_t s) {
+  auto grow = [&](float*& buf, int64_t& have, int64_t want, const char* what) {
+    if (want <= have) return;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (s) check_hip(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+    if (cap != hipStreamCaptureStatusNone)
+      throw std::runtime_error(std::string("factor_sync: ") + what +
+                               " must be sized before capture (DDP.settle reserves it)");
+    if (buf) check_hip(hipFree(buf), "hipFree");
+    check_hip(hipMalloc(&buf, sizeof(float) * (size_t)want), "hipMalloc(factor)");
+    have = want;
+  };
+  if (f.bias_slices > 0)
+    grow(factor_part_, factor_part_floats_, (int64_t)f.bias_slices * out, "bias workspace");
+  grow(factor_ws_, factor_ws_floats_, f.plan.ws_floats, "split-K workspace");
+}
+
+void RcclOps::factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j) {
+  // eager, outside any capture: size the job's workspaces for the current bucket layout (a
+  // rebuild between the first factored step and a capture changes the plans)
+  grow_factor_ws(plan_factor(begin, own, cnt, j), j.out, nullptr);
+}
+
+void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+                          hipStream_t s) {
+  const int W = comm_->world(), r = comm_->rank();
+  if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
+  if (!skip_collectives) {
+    // in place: this rank's factor rows already sit at slot r (written on the compute stream);
+    // one RCCL group, so g and x share one launch and the links carry both back to back -- x
+    // only when it was not gathered at forward time already (prefetch_factor_x)
+    comm_->group_start();
+    comm_->all_gather(j.g_all + (int64_t)r * j.B * j.out, j.g_all, (size_t)j.B * j.out,
+                      ncclFloat32, s);
+    if (!j.x_ready)
+      comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in,
+                        ncclFloat32, s);
+    comm_->group_end();
+  }
+  const FactorPlan f = plan_factor(begin, own, cnt, j);
+  grow_factor_ws(f, j.out, s);
+  if (f.bias_slices > 0) {
+    // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
+    // every rank: identical inputs, identical results, no collective
+    relu_bias_bwd_ws(j.g_all, nullptr, W * j.B, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
+                     factor_part_, f.bias_slices, s);
+    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
+  }
+  gemm_f32_run(f.a, f.plan, factor_ws_, s);
+  if (!f.epi) opt_update({{own, own + cnt}}, s);
   if (!j.replicate) all_gather_params(begin, cnt, s);
 }
 
@@ -286,6 +327,21 @@ void SyncBackend::arm_factor(int bucket, const FactorJob& j, int bias_bucket) {
   if ((j.bias_off >= 0) != (bias_bucket >= 0)) throw std::runtime_error("arm_factor: bias");
   factor_[bucket] = j;
   if (bias_bucket >= 0) factor_skip_[bias_bucket] = 1;
+}
+
+void SyncBackend::reserve_factor(int64_t begin, int64_t end, const FactorJob& j) {
+  if (!ops_->on_device()) return;
+  const Range own = j.replicate ? Range{begin, end} : owned_shard(begin, end);
+  if (own.second > own.first) ops_->factor_reserve(begin, own.first, own.second - own.first, j);
+}
+
+void SyncBackend::prefetch_factor_x(int bucket, float* x_all, int B, int in,
+                                    hipStream_t compute) {
+  if (!collective() || !ops_->on_device()) return;
+  if (bucket < 0 || bucket >= (int)factor_.size()) throw std::runtime_error("prefetch: bucket");
+  issue(bucket, compute, [this, x_all, B, in](hipStream_t cs) {
+    ops_->factor_gather_x(x_all, B, in, cs);
+  });
 }
 
 void SyncBackend::begin_iteration(hipStream_t compute) {

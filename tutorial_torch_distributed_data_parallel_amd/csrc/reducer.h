@@ -85,6 +85,9 @@ struct FactorJob {
   // so no parameter all-gather follows. Chosen when W*B is small enough that the extra GEMM rows
   // cost less than the out*in*(W-1)/W all-gather on xGMI (parallel/ddp.py factor_replicate).
   bool replicate = false;
+  // x_all was already all-gathered at forward time (SyncBackend::prefetch_factor_x): the job
+  // gathers only g
+  bool x_ready = false;
 };
 
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
@@ -115,6 +118,10 @@ struct SyncOps {
   // factored weight bucket [begin, begin + W*cnt): this rank owns [own, own + cnt) (FactorJob)
   virtual void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
                            hipStream_t s);
+  // forward-time all-gather of a factored weight's x_all ([W*B][in], this rank's rows at slot r)
+  virtual void factor_gather_x(float* x_all, int B, int in, hipStream_t s);
+  // size the workspaces factor_sync(begin, own, cnt, j) will need (eagerly, before a capture)
+  virtual void factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j);
 };
 
 // Device implementation: RCCL communicator + gfx950 kernels over the device arenas.
@@ -152,6 +159,8 @@ class RcclOps : public SyncOps {
   void watch(hipStream_t s, const char* what) override { comm_->watch(s, what); }
   void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
                    hipStream_t s) override;
+  void factor_gather_x(float* x_all, int B, int in, hipStream_t s) override;
+  void factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j) override;
 
   FusedOptimizer fused;
   float* clip_block = nullptr;  // DDP-owned hyper block for LOCAL clipping
@@ -161,6 +170,9 @@ class RcclOps : public SyncOps {
   std::shared_ptr<Communicator> comm() const { return comm_; }
 
  private:
+  struct FactorPlan;
+  FactorPlan plan_factor(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j) const;
+  void grow_factor_ws(const FactorPlan& f, int out, hipStream_t s);
   float* block(int b) const { return b == 0 ? fused.hyper : clip_block; }
   std::shared_ptr<Communicator> comm_;
   float* grad_;
@@ -207,6 +219,17 @@ class SyncBackend : public ReducerBackend {
   // iteration: its launch runs ops.factor_sync instead of reduce-scatter / update / all-gather.
   // `bias_bucket` (>= 0): the bucket holding exactly the layer's bias, updated by the job.
   void arm_factor(int bucket, const FactorJob& j, int bias_bucket);
+  // Forward-time gather of a factored weight's input factor: x exists as
+  // soon as the layer's forward runs, so its all-gather is issued then -- on the comm stream,
+  // as a deferred fork while capturing -- and overlaps the rest of forward and backward; the
+  // bucket's job at backward time then gathers only g (FactorJob::x_ready).
+  void prefetch_factor_x(int bucket, float* x_all, int B, int in, hipStream_t compute);
+  // eagerly size the workspaces of the factored job of bucket [begin, end) (DDP.settle, before
+  // a capture: the first factored step may have run under another bucket layout)
+  void reserve_factor(int64_t begin, int64_t end, const FactorJob& j);
+  // capture the deferred side branches once the compute stream has a node behind them (a
+  // caller that just launched compute work: ops/linear.py after a factored layer's forward GEMM)
+  void flush(hipStream_t compute) { flush_forks(compute, false); }
   std::shared_ptr<SyncOps> ops() const { return ops_; }
   bool collective() const { return !(skip_single_rank_ && ops_->world() == 1); }
 

@@ -101,10 +101,14 @@ def _head_precomputed(x2, weight, bias):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, head=None, pre=None):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, head=None, pre=None,
+                fac=None):
         C = native()
         M, K = x2.shape
         N = weight.shape[0]
+        # a factored DDP weight (world size > 1): this rank's x rows are staged now and their
+        # all-gather issued on the comm stream, after the GEMM below is launched
+        fwd_gather = fac is not None and fac.factor_forward(weight, x2)
         if pre is not None:
             # computed by the producer's split-K reduce (head of the previous fused Linear)
             y = pre
@@ -129,6 +133,8 @@ class _LinearFn(torch.autograd.Function):
         else:
             y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
             C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
+        if fwd_gather:
+            fac.factor_flush()  # the compute chain now owns the staging copy's first child
         ctx.relu = relu
         ctx.gate_in = gate_in
         ctx.params = (weight, bias)
@@ -179,7 +185,7 @@ class _LinearFn(torch.autograd.Function):
                     _mark_gated(dx, x2)
                 if pl is not None:
                     attach_planes(dx, pl)
-                return dx, dw, db, None, None, None, None
+                return dx, dw, db, None, None, None, None, None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
@@ -219,7 +225,7 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 class _LinearCpuFn(torch.autograd.Function):
@@ -272,6 +278,13 @@ class _LinearCpuFn(torch.autograd.Function):
 _HEAD_IN_REDUCE = os.environ.get("TDP_HEAD_IN_REDUCE", "0") == "1"
 
 
+def _factor_owner(weight):
+    """The DDP that factors ``weight``'s gradient synchronisation (it may gather the layer's
+    input at forward time: DDP.factor_forward), else None."""
+    ref = getattr(weight, "_tdp_factor", None)
+    return ref() if ref is not None else None
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            relu: bool = False, head=None) -> torch.Tensor:
     """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features].
@@ -312,7 +325,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
                                  head[0].shape[0] <= 16 and head[0].shape[1] == weight.shape[0]
                                  and head[0].is_cuda and head[0].is_contiguous()):
         head = None
-    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, head, pre)
+    fac = _factor_owner(weight) if torch.is_grad_enabled() else None
+    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, head, pre, fac)
     if x.dim() == 2:
         if relu:
             y._tdp_relu_out = True
