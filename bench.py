@@ -238,6 +238,30 @@ def _time_steps(step, n):
     return (time.perf_counter() - t0) * 1000.0 / n
 
 
+def predicted_comm(a, ddp, world, sweep) -> dict:
+    """The step model (parallel/commmodel.py, docs/COMM_MODEL.md) fed with this job's measured
+    bus bandwidths (largest swept size per collective) and its sync plan: the exposed
+    communication it predicts, reported next to the measured overlap."""
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commmodel as cm
+
+    big = {}
+    for r in sweep:
+        if r["bytes"] >= big.get(r["op"], (0, 0))[0]:
+            big[r["op"]] = (r["bytes"], r["busbw_GBps"])
+    hw = cm.Hardware(busbw_GBps={op: bw for op, (_, bw) in big.items()})
+    dims = tuple(int(v) for v in a.mlp_dims.split(",")) if a.mlp_dims else (9216, 4096, 4096)
+    layers = cm.toy_mlp_layers(a.batch, dims)
+    plan = ddp.sync_plan()
+    modes = {}
+    for name in ("fc1", "fc2"):
+        m = plan.get(f"{name}.weight", "allreduce")
+        modes[name] = m if m in cm.MODES else "allreduce"
+    r = cm.simulate(layers, modes, world, a.batch, hw)
+    return {"predicted_comm_exposed_ms": round(r["exposed_us"] / 1000.0, 4),
+            "predicted_step_ms": round(r["step_us"] / 1000.0, 4),
+            "predicted_modes": modes}
+
+
 def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
     """Post-measurement evidence for the scaling curve (module doc). Every rank runs the same
     collectives in the same order; rank 0 reports."""
@@ -270,6 +294,8 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
         sweep = commbench.collective_busbw([m * 2 ** 20 for m in DIAG_SWEEP_MB], iters=5,
                                            warmup=2)
         out["busbw_GBps"] = {f"{r['op']}@{r['bytes'] >> 20}MiB": r["busbw_GBps"] for r in sweep}
+        if a.model == "toy_mlp":
+            out.update(predicted_comm(a, ddp, world, sweep))
     elif build_rehearsal is not None:
         from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
 
@@ -594,8 +620,9 @@ def main():
         advance()
         run = tdp_step
         if a.impl == "tdp" and ddp is not None and world > 1 and use_gpu:
-            # measured replicated-vs-sharded choice for the factored Linear weights (untimed
-            # training steps, agreed over ranks) before the step is captured
+            # measured replicated-vs-sharded choice per factored Linear weight (untimed training
+            # steps, agreed over ranks) before the step is captured -- timed the way the step
+            # will run: captured and replayed when the bench captures it
             def eager_step():
                 advance()
                 tdp_step_eager()
@@ -603,7 +630,10 @@ def main():
             def tdp_step_eager():
                 x, y = gather_batch(data.x, data.y, cur["b"])
                 return body(x, y)
-            ddp.tune_factor_replicate(eager_step, iters=3)
+            if graph:
+                ddp.tune_factor_replicate(tdp_step, iters=5, capture=True)
+            else:
+                ddp.tune_factor_replicate(eager_step, iters=3)
         if graph:
             from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
 

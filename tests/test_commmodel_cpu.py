@@ -1,0 +1,54 @@
+"""The step model of the gradient synchronisation modes (parallel/commmodel.py,
+docs/COMM_MODEL.md): wire bytes per mode, the forward-time x gather, the per-weight best plan."""
+from tutorial_torch_distributed_data_parallel_amd.parallel import commmodel as cm
+
+
+def _wire(W, mode):
+    layers = cm.toy_mlp_layers(128)
+    r = cm.simulate(layers, {"fc1": mode, "fc2": mode}, W, 128, cm.Hardware())
+    return sum(j["wire_MB"] for j in r["jobs"]), r
+
+
+def test_wire_bytes_per_mode():
+    # all-reduce of the 218 MB gradient moves 2 (W-1)/W of it per rank
+    ar, _ = _wire(8, "allreduce")
+    assert abs(ar - 2 * 7 / 8 * 4 * (9216 * 4096 + 4096 * 4096) / 1e6) < 1.0
+    rep, _ = _wire(8, "factored-replicated")
+    shd, _ = _wire(8, "factored-sharded")
+    # factors only (W*B rows of g and x) < factors + parameter all-gather < gradient all-reduce
+    assert rep < shd < ar
+    assert abs(rep - 7 / 8 * 4 * 1024 * (9216 + 4096 + 4096 + 4096) / 1e6) < 1.0
+
+
+def test_forward_x_gather_shortens_the_tail():
+    layers = cm.toy_mlp_layers(128)
+    modes = {"fc1": "factored-sharded", "fc2": "factored-sharded"}
+    hw = cm.Hardware()
+    early = cm.simulate(layers, modes, 8, 128, hw, prefetch_x=True)
+    late = cm.simulate(layers, modes, 8, 128, hw, prefetch_x=False)
+    assert early["exposed_us"] < late["exposed_us"]
+
+
+def test_best_plan_beats_uniform_plans_and_follows_bandwidth():
+    layers = cm.toy_mlp_layers(128)
+    for W in (2, 4, 8):
+        best = cm.best_plan(layers, W, 128, cm.Hardware())
+        for mode in cm.MODES:
+            r = cm.simulate(layers, {"fc1": mode, "fc2": mode}, W, 128, cm.Hardware())
+            assert best["step_us"] <= r["step_us"] + 1e-6
+    # a slow link makes the parameter all-gather expensive: replication wins
+    slow = cm.Hardware(busbw_GBps={"all_gather": 20.0, "all_reduce": 20.0, "reduce_scatter": 20.0})
+    b = cm.best_plan(layers, 8, 128, slow)
+    assert set(b["modes"].values()) == {"factored-replicated"}
+
+
+def test_one_rank_has_no_communication():
+    layers = cm.toy_mlp_layers(128)
+    r = cm.simulate(layers, {"fc1": "allreduce", "fc2": "allreduce"}, 1, 128, cm.Hardware())
+    assert all(j["wire_MB"] == 0 for j in r["jobs"])
+
+
+def test_table_rows():
+    rows = cm.table((2, 8))
+    assert len(rows) == 2 * (len(cm.MODES) + 1)
+    assert all(r["step_us"] >= r["exposed_us"] >= 0 for r in rows)

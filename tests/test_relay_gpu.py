@@ -63,7 +63,10 @@ def test_bench_world2_record(tmp_path):
     assert sync["replicas_identical"] is True, sync
     assert sync["captured"] is False  # relayed collectives cannot be captured: agreed eager
     assert sync["modes"]["fc1.weight"].startswith("factored"), sync
-    assert sync["factor_tuning"]["chosen"] in ("replicated", "sharded"), sync
+    chosen = sync["factor_tuning"]["chosen"]
+    assert set(chosen) == {"fc1.weight", "fc2.weight"}, sync  # a choice per factored weight
+    assert set(chosen.values()) <= {"replicated", "sharded"}, sync
+    assert len(sync["factor_tuning"]["timings_ms"]) == 4, sync  # 2 weights: 4 combinations
 
 
 def _port():
