@@ -167,11 +167,9 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
 // Skinny GEMM from the bf16 split planes of A (csrc/gemm_planes.hip):
 //   Ap [3][M][K] bf16 (contiguous), B [N][K] (b_kcontig) or [K][N] fp32, C [M][N] fp32;
 //   out_planes (optional) [3][M][N] bf16 receives the planes of the finished C.
-bool gemm_planes_op(const Tensor& Ap, const Tensor& B, Tensor& C, bool b_kcontig,
+void gemm_planes_op(const Tensor& Ap, const Tensor& B, Tensor& C, bool b_kcontig,
                     const c10::optional<Tensor>& bias, bool relu,
-                    const c10::optional<Tensor>& gate, const c10::optional<Tensor>& out_planes,
-                    const c10::optional<Tensor>& head_w, const c10::optional<Tensor>& head_b,
-                    const c10::optional<Tensor>& head_out) {
+                    const c10::optional<Tensor>& gate, const c10::optional<Tensor>& out_planes) {
   CHECK_GPU(Ap); CHECK_GPU(B); CHECK_GPU(C);
   TORCH_CHECK(Ap.scalar_type() == at::kBFloat16 && Ap.dim() == 3 && Ap.size(0) == 3 &&
                   Ap.is_contiguous(), "gemm_planes: Ap must be a contiguous [3, M, K] bf16 tensor");
@@ -207,33 +205,12 @@ bool gemm_planes_op(const Tensor& Ap, const Tensor& B, Tensor& C, bool b_kcontig
     a.out_planes = reinterpret_cast<uint16_t*>(o.data_ptr());
     a.out_ps = o.stride(0);
   }
-  if (head_w.has_value() && head_w->defined()) {
-    // the classifier head fed by C (returns false when the reduce could not take it: the caller
-    // then runs the head Linear itself)
-    const Tensor& hw = *head_w;
-    TORCH_CHECK(head_out.has_value() && head_out->defined(), "gemm_planes: head_out missing");
-    const Tensor& ho = *head_out;
-    CHECK_GPU(hw); CHECK_F32(hw); CHECK_CONTIG(hw); CHECK_GPU(ho); CHECK_F32(ho); CHECK_CONTIG(ho);
-    TORCH_CHECK(hw.dim() == 2 && hw.size(1) == N && hw.size(0) >= 1 && hw.size(0) <= 16,
-                "gemm_planes: head_w must be [O <= 16, N]");
-    TORCH_CHECK(ho.dim() == 2 && ho.size(0) == M && ho.size(1) == hw.size(0),
-                "gemm_planes: head_out must be [M, O]");
-    a.head_w = hw.data_ptr<float>();
-    a.head_out = ho.data_ptr<float>();
-    a.head_n = (int)hw.size(0);
-    if (head_b.has_value() && head_b->defined()) {
-      CHECK_GPU(*head_b); CHECK_F32(*head_b); CHECK_CONTIG(*head_b);
-      TORCH_CHECK(head_b->numel() == hw.size(0), "gemm_planes: head_b must have O elements");
-      a.head_b = head_b->data_ptr<float>();
-    }
-  }
   TORCH_CHECK(gemm_planes_ok(a), "gemm_planes: unsupported shape / alignment (K % 32, N % 4, "
               "16-B aligned rows)");
   const GemmPlan plan = gemm_planes_plan(a, num_cus(C.get_device()));
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
-  return gemm_planes_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr,
-                         cur_stream());
+  gemm_planes_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
 }
 
 // x [rows, cols] fp32 (unit inner stride) -> its exact bf16 split planes [3, rows, cols]
@@ -1431,9 +1408,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
   m.def("gemm_planes", &gemm_planes_op, py::arg("Ap"), py::arg("B"), py::arg("C"),
         py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,
-        py::arg("gate") = py::none(), py::arg("out_planes") = py::none(),
-        py::arg("head_w") = py::none(), py::arg("head_b") = py::none(),
-        py::arg("head_out") = py::none());
+        py::arg("gate") = py::none(), py::arg("out_planes") = py::none());
   m.def("split_planes", &split_planes_op);
   m.def("head_bwd", &head_bwd_op, py::arg("g"), py::arg("x"), py::arg("w"), py::arg("dx"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("gate") = py::none(),
@@ -1445,7 +1420,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_set_cvec", &gemm_f32_set_cvec);
   m.def("gemm_f32_set_bm", &gemm_f32_set_bm);
   m.def("gemm_f32_set_emu", &gemm_f32_set_emu);
-  m.def("gemm_f32_set_exp", &gemm_f32_set_exp);
   m.def("gemm_f32_emu", &gemm_f32_emu);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);

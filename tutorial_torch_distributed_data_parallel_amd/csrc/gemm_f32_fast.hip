@@ -87,10 +87,6 @@ struct FastParams {
   OptEpilogue opt;  // kind != 0 (splits == 1 only): update p/state instead of storing C
   OptEpilogue bopt;  // kind != 0 (with opt and rowsum): update the bias from the row sums
   int prio;         // EMU: static wave priority for every other hardware slot (A/B knob)
-  // EMU timing experiment only (TDP_GEMM_EXP, numerically WRONG when set): bit 0 replaces the
-  // A fragments' split by one conversion, bit 1 the B fragments' -- the bound a pre-split
-  // operand would reach (scripts/bench_gemm_emu.py --exp)
-  int exp;
   const float* gate;  // optional C-shaped gate (GemmF32Args::gate), non-split epilogues
   long ldg;
 };
@@ -601,18 +597,6 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
         float a4[4][FM][4], b4[4][FN][4];
         bf8 xh[2][NF], xm[2][NF], xl[2][NF];  // fragment i: A tile i (< FM) or B tile i - FM
         auto split_frag = [&](int j, int i) {
-          if (p.exp & (i < FM ? 1 : 2)) {
-            const float (&u)[4] = i < FM ? a4[2 * j][i] : b4[2 * j][i - FM];
-            const float (&v)[4] = i < FM ? a4[2 * j + 1][i] : b4[2 * j + 1][i - FM];
-            const bf2 c0 = __builtin_convertvector(f32x2{u[0], u[1]}, bf2);
-            const bf2 c1 = __builtin_convertvector(f32x2{u[2], u[3]}, bf2);
-            const bf2 c2 = __builtin_convertvector(f32x2{v[0], v[1]}, bf2);
-            const bf2 c3 = __builtin_convertvector(f32x2{v[2], v[3]}, bf2);
-            const u32x4 hv = {__builtin_bit_cast(unsigned, c0), __builtin_bit_cast(unsigned, c1),
-                              __builtin_bit_cast(unsigned, c2), __builtin_bit_cast(unsigned, c3)};
-            xh[j][i] = xm[j][i] = xl[j][i] = __builtin_bit_cast(bf8, hv);
-            return;
-          }
           if (i < FM) split3_x8(a4[2 * j][i], a4[2 * j + 1][i], xh[j][i], xm[j][i], xl[j][i]);
           else split3_x8(b4[2 * j][i - FM], b4[2 * j + 1][i - FM], xh[j][i], xm[j][i], xl[j][i]);
         };
@@ -1243,10 +1227,6 @@ bool o_emu = [] {
   const char* e = std::getenv("TDP_GEMM_EMU");
   return !(e && e[0] == '0');
 }();
-int o_emu_exp = [] {
-  const char* e = std::getenv("TDP_GEMM_EXP");
-  return e ? std::atoi(e) : 0;
-}();
 
 // bm = 256: the FM 4 kernel (64-wide tile, 2 stages = 80 KiB of LDS, two workgroups per CU);
 // instantiated for K-contiguous A operands only
@@ -1336,7 +1316,6 @@ static int o_bm = [] {  // 0 auto, 128 / 256 forced (sweeps; TDP_GEMM_BM=256 fro
   return e ? ((std::atoi(e) == 256 || std::atoi(e) == 128) ? std::atoi(e) : 0) : 0;
 }();
 void gemm_f32_set_emu(bool on) { o_emu = on; }
-void gemm_f32_set_exp(int bits) { o_emu_exp = bits; }
 bool gemm_f32_emu() { return o_emu; }
 void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
 void gemm_f32_set_cvec(bool on) { o_no_cvec = !on; }
@@ -1388,7 +1367,6 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   FastParams p{};  // zero: every optional pointer (stats, wt, ...) unset unless assigned below
   p.prio = o_emu_prio;
-  p.exp = o_emu_exp;
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
   p.gate = a.gate; p.ldg = a.ldgate;
   p.rowsum = a.rowsum; p.rowsum_beta = a.rowsum_beta;
@@ -1618,7 +1596,6 @@ bool conv_nhwc_run(const ConvPlan& pl, const ConvGeom& g, const float* A, const 
                    hipStream_t s, const WeightTaps* wtap, float* stats) {
   FastParams p{};
   p.prio = o_emu_prio;
-  p.exp = o_emu_exp;
   if (wtap) {
     if (pl.mode != kConvDgrad) throw std::runtime_error("weight taps are for the input gradient");
     p.wt.Cout = g.Cout; p.wt.Sp = g.S;

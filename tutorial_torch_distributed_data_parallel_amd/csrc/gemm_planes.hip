@@ -69,13 +69,6 @@ struct PParams {
   int relu;
   int M, N, K, kps, splits, tiles_n, tiles_mn;
   int prio;
-  unsigned* cnt;  // split-K arrival counters, one per output tile (nullptr: planes_reduce_kernel)
-  const float* hw;  // head (planes_reduce_head_kernel): hw [hn][N], hb [hn], ho [M][hn]
-  const float* hb;
-  float* ho;
-  int hn;
-  int exp;  // timing experiments only (TDP_PLANES_EXP, numerically WRONG when set): bit 0 skips
-            // the MFMA step, bit 1 the B DMA, bit 2 the A DMA, bit 3 the epilogue stores
 };
 
 // exact 3-way bf16 split of a pair (identical instruction sequence to gemm_f32_fast.hip
@@ -464,7 +457,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
     __builtin_amdgcn_s_barrier();
     issue(kt + S - 1);
     if constexpr (PF > 0) prefetch(kt + S - 1 + PF, d);
-    if (!(p.exp & 1)) compute(kt);
+    compute(kt);
   };
   if (nk > 0) {
 #pragma unroll
@@ -504,64 +497,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
     const int e = i * kT + threadIdx.x;
     const int lr = e / C4, lc = (e % C4) * 4;
     const int row = m0 + lr, col = n0 + lc;
-    if (row >= p.M || col >= p.N || (p.exp & 8)) continue;
+    if (row >= p.M || col >= p.N) continue;
     const f32x4 v = *reinterpret_cast<const f32x4*>(T + lr * TS + lc);
     if (p.splits > 1) *reinterpret_cast<f32x4*>(ws + (long)row * p.N + col) = v;
     else finish4(p, row, col, v);
   }
-  if (p.splits == 1 || !p.cnt) return;
-  // Split-K fix-up in the last-arriving workgroup of the tile (opt-in, measured slower than the
-  // reduce launch: see gemm_planes_run). Nobody waits on anybody: every
-  // workgroup publishes its partial (agent-scope release: the partials of the other splits were
-  // written on other XCDs' L2s) and counts itself in; the one that sees splits - 1 earlier
-  // arrivals acquires, sums all partials in split order (its own from LDS: the same fp32 sum as
-  // the reduce kernel, bitwise) and runs the epilogue. It also re-arms the counter for the next
-  // launch of this slot (graph replays included).
-  __shared__ int last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(p.cnt + t, 1u);
-    last = prev == (unsigned)(p.splits - 1);
-    if (last) atomicExch(p.cnt + t, 0u);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  f32x4 v[IT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = i * kT + threadIdx.x;
-    const int lr = e / C4, lc = (e % C4) * 4;
-    const int row = min(m0 + lr, p.M - 1), col = min(n0 + lc, p.N - 4);
-    v[i] = z == 0 ? *reinterpret_cast<const f32x4*>(T + lr * TS + lc)
-                  : *reinterpret_cast<const f32x4*>(p.ws + (long)row * p.N + col);
-  }
-  for (int zz = 1; zz < p.splits; ++zz) {
-    const float* src = p.ws + (long)zz * p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int e = i * kT + threadIdx.x;
-      const int lr = e / C4, lc = (e % C4) * 4;
-      const int row = min(m0 + lr, p.M - 1), col = min(n0 + lc, p.N - 4);
-      v[i] += zz == z ? *reinterpret_cast<const f32x4*>(T + lr * TS + lc)
-                      : *reinterpret_cast<const f32x4*>(src + (long)row * p.N + col);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = i * kT + threadIdx.x;
-    const int lr = e / C4, lc = (e % C4) * 4;
-    const int row = m0 + lr, col = n0 + lc;
-    if (row < p.M && col < p.N) finish4(p, row, col, v[i]);
-  }
 }
-
-// split-K arrival counters (zero at load, re-armed by each tile's last arrival): kCntSlots
-// regions used round-robin, so back-to-back launches -- possibly on different streams -- never
-// share a region while one of them can still be running
-constexpr int kCntSlots = 64, kCntTiles = 512;
-__device__ unsigned g_planes_cnt[kCntSlots * kCntTiles];
 
 // C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread
 __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
@@ -577,53 +518,6 @@ __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
   finish4(p, row, col, a);
 }
 
-// planes_reduce_kernel for one whole row per workgroup (1024 threads: a 4096-wide row is one
-// float4 per thread, the same parallelism as the flat reduce's 512 x 256), plus the classifier
-// head fed by the finished row: ho[row][m] = sum_n C[row][n] hw[m][n] + hb[m] (m < hn <= 16).
-// Per-thread partial dot products in a fixed order, then a fixed reduction tree: deterministic.
-constexpr int kHT = 1024;
-__global__ __launch_bounds__(kHT) void planes_reduce_head_kernel(PParams p) {
-  constexpr int HM = 16;
-  const int row = blockIdx.x;
-  const long ng = (long)p.M * p.N / 4;
-  const int n4 = p.N / 4;
-  float part[HM];
-#pragma unroll
-  for (int m = 0; m < HM; ++m) part[m] = 0.f;
-  for (int c4 = threadIdx.x; c4 < n4; c4 += kHT) {
-    const long idx = (long)row * n4 + c4;
-    const f32x4* src = reinterpret_cast<const f32x4*>(p.ws) + idx;
-    f32x4 a = src[0];
-#pragma unroll 8
-    for (int z = 1; z < p.splits; ++z) a += src[z * ng];
-    const int col = c4 * 4;
-    const f32x4 v = finish4(p, row, col, a);  // bias, ReLU, gate applied: the stored value
-#pragma unroll
-    for (int m = 0; m < HM; ++m) {
-      if (m < p.hn) {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(p.hw + (long)m * p.N + col);
-        part[m] = fmaf(v[0], w[0], fmaf(v[1], w[1], fmaf(v[2], w[2], fmaf(v[3], w[3], part[m]))));
-      }
-    }
-  }
-  __shared__ float red[kHT / 64][HM];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-  for (int m = 0; m < HM; ++m) {
-    float x = part[m];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    if (lane == 0) red[wv][m] = x;
-  }
-  __syncthreads();
-  if (threadIdx.x < p.hn) {
-    const int m = threadIdx.x;
-    float x = red[0][m];
-#pragma unroll
-    for (int w = 1; w < kHT / 64; ++w) x += red[w][m];
-    p.ho[(long)row * p.hn + m] = x + (p.hb ? p.hb[m] : 0.f);
-  }
-}
 
 // x [rows][cols] (row stride ldx) -> planes [3][rows][cols] (plane stride ps), cols % 4 == 0
 __global__ __launch_bounds__(kT) void split_planes_kernel(const float* __restrict__ x, long ldx,
@@ -804,7 +698,7 @@ GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus) {
   return plan;
 }
 
-bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s) {
   if (!gemm_planes_ok(a)) throw std::runtime_error("gemm_planes: unsupported operands");
   PParams p{};
   p.Ap = a.Ap; p.ps = a.ps; p.lda = a.lda;
@@ -815,11 +709,6 @@ bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   p.op = a.out_planes; p.ops = a.out_ps;
   p.relu = a.relu ? 1 : 0;
   p.M = a.M; p.N = a.N; p.K = a.K;
-  static const int exp = [] {
-    const char* e = std::getenv("TDP_PLANES_EXP");
-    return e ? std::atoi(e) : 0;
-  }();
-  p.exp = exp;
   static const int prio = [] {
     const char* e = std::getenv("TDP_PLANES_PRIO");
     return (e && e[0] == '0') ? 0 : 1;
@@ -830,44 +719,14 @@ bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   p.tiles_n = ceil_div(a.N, plan.bn);
   p.tiles_mn = ceil_div(a.M, kBM) * p.tiles_n;
   if (plan.splits > 1 && ws == nullptr) throw std::runtime_error("gemm_planes: workspace missing");
-  // split-K fix-up in the GEMM's last-arriving workgroups: OFF by default (TDP_PLANES_FIXUP=1
-  // turns it on). Measured (profiles/r7/planes_fixup_negative_r7b.md): bitwise equal to the
-  // reduce kernel but the toy-MLP step went 0.357 -> 0.474 ms -- the agent-scope release every
-  // workgroup needs before counting in (its partial must leave its XCD's L2) writes back the
-  // whole L2, and 32 of them per XCD serialise: +40 us per GEMM against a 5-6 us reduce launch
-  // (inside a hipGraph the launch itself leaves no gap).
-  static const bool fixup = [] {
-    const char* e = std::getenv("TDP_PLANES_FIXUP");
-    return e && e[0] == '1';
-  }();
-  p.cnt = nullptr;
-  if (plan.splits > 1 && fixup && p.tiles_mn <= kCntTiles) {
-    static unsigned* base[64] = {};
-    static int slot = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-      throw std::runtime_error("gemm_planes: hipGetDevice");
-    if (!base[dev] && hipGetSymbolAddress(reinterpret_cast<void**>(&base[dev]),
-                                          HIP_SYMBOL(g_planes_cnt)) != hipSuccess)
-      throw std::runtime_error("gemm_planes: counter symbol");
-    p.cnt = base[dev] + (long)slot * kCntTiles;
-    slot = (slot + 1) % kCntSlots;
-  }
   const int nblocks = p.tiles_mn * plan.splits;
   if (a.b_kcontig) launch_cfg<true>(p, planes_cfg(), nblocks, s);
   else launch_cfg<false>(p, planes_cfg(), nblocks, s);
-  const bool head = a.head_w && a.head_out && a.head_n >= 1 && a.head_n <= 16 &&
-                    plan.splits > 1 && !p.cnt && a.N <= 8192 && al16(a.head_w) &&
-                    a.ldc % 4 == 0;
-  if (head) {
-    p.hw = a.head_w; p.hb = a.head_b; p.ho = a.head_out; p.hn = a.head_n;
-    hipLaunchKernelGGL(planes_reduce_head_kernel, dim3((unsigned)a.M), dim3(kHT), 0, s, p);
-  } else if (plan.splits > 1 && !p.cnt) {
+  if (plan.splits > 1) {
     const long ng = (long)a.M * a.N / 4;
     hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
                        p);
   }
-  return head;
 }
 
 void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,

@@ -151,7 +151,6 @@ void gemm_f32_set_override(int fn, int splits, int stages);
 void gemm_f32_set_cvec(bool on);
 // fast GEMM products: split-bf16 emulation on the bf16 matrix core (default) or native f32 MFMA
 void gemm_f32_set_emu(bool on);
-void gemm_f32_set_exp(int bits);  // timing experiment only (numerically wrong when != 0)
 bool gemm_f32_emu();
 // fast-GEMM block rows: 0 auto, 128 or 256 forced (measurements, tests)
 void gemm_f32_set_bm(int bm);

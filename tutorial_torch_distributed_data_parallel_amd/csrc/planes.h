@@ -26,18 +26,10 @@ struct GemmPlanesArgs {
   uint16_t* out_planes = nullptr;
   long out_ps = 0;
   int M = 0, N = 0, K = 0;
-  // optional classifier head fed by this output: head_out[M][head_n] = C . head_w^T + head_b
-  // (head_w [head_n][N], head_n <= 16), computed by the split-K reduce from the finished rows --
-  // the head Linear's forward then launches nothing. Taken only when the reduce runs (split-K)
-  // and N <= 8192; gemm_planes_run returns whether it was.
-  const float* head_w = nullptr;
-  const float* head_b = nullptr;
-  float* head_out = nullptr;
-  int head_n = 0;
 };
 bool gemm_planes_ok(const GemmPlanesArgs& a);
 GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus);
-bool gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s);
+void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s);
 // x [rows][cols] (row stride ldx, cols % 4 == 0) -> planes [3][rows][cols] (plane stride ps)
 void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,
                   hipStream_t s);

@@ -33,10 +33,6 @@ class ToyMLP(nn.Module):
         for name, m in layers:
             self.add_module(name, m)
         self._order = [n for n, _ in layers]
-        if not batchnorm and hidden:
-            # the last hidden Linear's split-K reduce may also compute the 10 logits (no launch of
-            # its own for the head's forward; ops/linear.py ``head``, opt-in TDP_HEAD_IN_REDUCE=1)
-            layers[-2][1].feeds_head(layers[-1][1])
 
     def forward(self, x):
         x = x.reshape(x.shape[0], -1)

@@ -19,19 +19,9 @@ class Linear(nn.Linear):
                  relu: bool = False, device=None, dtype=None):
         super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
         self.relu = relu
-        # a small classifier Linear that consumes this layer's output (set by the model with
-        # feeds_head): this layer's GEMM reduce computes the head's output too (ops.linear head)
-        self.__dict__["_head"] = None
-
-    def feeds_head(self, head: "Linear | None") -> None:
-        """Declare ``head`` as the consumer of this layer's output (not a submodule: no state
-        dict keys; only its weight / bias are read at forward time)."""
-        self.__dict__["_head"] = head
 
     def forward(self, x):
-        h = self.__dict__.get("_head")
-        hd = (h.weight, h.bias) if h is not None and x.is_cuda else None
-        return ops.linear(x, self.weight, self.bias, relu=self.relu, head=hd)
+        return ops.linear(x, self.weight, self.bias, relu=self.relu)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")

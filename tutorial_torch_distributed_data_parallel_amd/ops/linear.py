@@ -85,51 +85,23 @@ def _mark_gated(dx: torch.Tensor, gate: torch.Tensor) -> None:
     dx._tdp_gated_by = (gate.data_ptr(), tuple(gate.shape))
 
 
-def _head_key(weight, bias):
-    return (weight.data_ptr(), weight._version,
-            None if bias is None else (bias.data_ptr(), bias._version))
-
-
-def _head_precomputed(x2, weight, bias):
-    """The head output its producer's split-K reduce already computed for ``x2`` (see
-    _LinearFn.forward ``head``), if it still matches x2 and this head's weight / bias."""
-    rec = getattr(x2, "_tdp_head_out", None)
-    if rec is None or rec[1] != x2._version or rec[2] != _head_key(weight, bias):
-        return None
-    return rec[0]
-
-
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, head=None, pre=None,
-                fac=None):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None):
         C = native()
         M, K = x2.shape
         N = weight.shape[0]
         # a factored DDP weight (world size > 1): this rank's x rows are staged now and their
         # all-gather issued on the comm stream, after the GEMM below is launched
         fwd_gather = fac is not None and fac.factor_forward(weight, x2)
-        if pre is not None:
-            # computed by the producer's split-K reduce (head of the previous fused Linear)
-            y = pre
-        elif planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
+        if planes_fit(M, N, K) and weight.stride(1) == 1 and _al16(weight, bias):
             y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
             # a hidden layer's output also leaves as planes: the next skinny GEMM's A operand
             op = torch.empty((3, M, N), device=x2.device, dtype=torch.bfloat16) \
                 if relu and N % 32 == 0 else None
-            kw = {}
-            if head is not None:
-                # the classifier head fed by this output: its logits from the split-K reduce
-                hw, hb = head
-                kw = dict(head_w=hw, head_b=hb,
-                          head_out=torch.empty((M, hw.shape[0]), device=x2.device,
-                                               dtype=torch.float32))
-            took = C.gemm_planes(planes_of(x2), weight, y, True, bias=bias, relu=relu,
-                                 out_planes=op, **kw)
+            C.gemm_planes(planes_of(x2), weight, y, True, bias=bias, relu=relu, out_planes=op)
             if op is not None:
                 attach_planes(y, op)
-            if took and kw:
-                y._tdp_head_out = (kw["head_out"], y._version, _head_key(hw, hb))
         else:
             y = torch.empty((M, N), device=x2.device, dtype=torch.float32)
             C.gemm_f32(x2, weight, y, True, True, bias=bias, relu=relu)
@@ -185,7 +157,7 @@ class _LinearFn(torch.autograd.Function):
                     _mark_gated(dx, x2)
                 if pl is not None:
                     attach_planes(dx, pl)
-                return dx, dw, db, None, None, None, None, None
+                return dx, dw, db, None, None, None
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
@@ -225,7 +197,7 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None
 
 
 class _LinearCpuFn(torch.autograd.Function):
@@ -271,13 +243,6 @@ class _LinearCpuFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-# TDP_HEAD_IN_REDUCE=1: the previous Linear's split-K reduce computes the head's forward. Off by
-# default: measured neutral (toy MLP 0.3506-0.3517 vs 0.3509-0.3516 ms/step interleaved; the
-# one-row-per-workgroup reduce + head takes 13.4 us vs 5.3 + 6.0 us for reduce + head launch,
-# 128 workgroups on 256 CUs -- profiles/r7/head_in_reduce_r7d.md)
-_HEAD_IN_REDUCE = os.environ.get("TDP_HEAD_IN_REDUCE", "0") == "1"
-
-
 def _factor_owner(weight):
     """The DDP that factors ``weight``'s gradient synchronisation (it may gather the layer's
     input at forward time: DDP.factor_forward), else None."""
@@ -286,12 +251,8 @@ def _factor_owner(weight):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
-           relu: bool = False, head=None) -> torch.Tensor:
-    """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features].
-
-    ``head`` (weight, bias) of a small classifier Linear (out <= 16) that consumes this output:
-    the split-K reduce of this layer's GEMM also computes the head's output, and the head's own
-    ``linear`` call returns it without a launch (models/mlp.py: fc2 -> fc3)."""
+           relu: bool = False) -> torch.Tensor:
+    """``relu?(x @ weight.T + bias)`` for x of shape [..., in_features]."""
     # the input is the ReLU output of a previous fused Linear(+ReLU): this layer's input-gradient
     # epilogue applies that ReLU's mask (see _LinearFn.backward)
     gate_in = bool(getattr(x, "_tdp_relu_out", False)) and x.dim() == 2
@@ -316,17 +277,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         gate_in = False
     if torch.is_grad_enabled():
         note_use(weight)
-    pre = _head_precomputed(x2, weight, bias) if x.dim() == 2 else None
-    if pre is not None:
-        # consumed: the record must not outlive this call (x2 -> logits -> their grad_fn ->
-        # saved x2 would be a cycle through a C++ node that Python's collector cannot see)
-        del x2._tdp_head_out
-    if head is not None and not (_HEAD_IN_REDUCE and x.dim() == 2 and head[0].dim() == 2 and
-                                 head[0].shape[0] <= 16 and head[0].shape[1] == weight.shape[0]
-                                 and head[0].is_cuda and head[0].is_contiguous()):
-        head = None
     fac = _factor_owner(weight) if torch.is_grad_enabled() else None
-    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, head, pre, fac)
+    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, fac)
     if x.dim() == 2:
         if relu:
             y._tdp_relu_out = True
