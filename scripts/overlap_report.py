@@ -75,6 +75,10 @@ def main():
     ap.add_argument("--step-marker", default=None)
     ap.add_argument("--last-steps", type=int, default=0)
     ap.add_argument("--title", default="collective / compute overlap")
+    ap.add_argument("--by-queue", action="store_true",
+                    help="side-stream work = EVERY kernel on the hardware queue(s) that run the "
+                         "collectives (the factored jobs' GEMMs and updates too), compute = the "
+                         "kernels of every other queue")
     a = ap.parse_args()
     ks = load(a.trace)
     if a.step_marker and a.last_steps:
@@ -82,8 +86,13 @@ def main():
         if len(starts) >= a.last_steps:
             t_lo = starts[-a.last_steps]
             ks = [k for k in ks if k[0] >= t_lo]
-    coll = [k for k in ks if is_coll(k[2])]
-    comp = union([(k[0], k[1]) for k in ks if not is_coll(k[2])])
+    if a.by_queue:
+        side_q = {k[3] for k in ks if is_coll(k[2])}
+        side = lambda k: k[3] in side_q  # noqa: E731
+    else:
+        side = lambda k: is_coll(k[2])  # noqa: E731
+    coll = [k for k in ks if side(k)]
+    comp = union([(k[0], k[1]) for k in ks if not side(k)])
     span = (ks[-1][1] - ks[0][0]) if ks else 0
     print(f"# {a.title}\n")
     print(f"Source: `{a.trace}`; window {span / 1e6:.3f} ms, {len(ks)} kernels, "
@@ -106,7 +115,7 @@ def main():
         d = k[1] - k[0]
         c = covered(k[0], k[1], comp)
         names = sorted({short(x[2], 40) for x in ks
-                        if not is_coll(x[2]) and x[0] < k[1] and x[1] > k[0]})
+                        if not side(x) and x[0] < k[1] and x[1] > k[0]})
         print(f"| `{short(k[2])}` | {(k[0] - base) / 1e3:.1f} | {d / 1e3:.1f} | "
               f"{100.0 * c / max(d, 1):.1f} | {', '.join('`%s`' % n for n in names[:4])} |")
 

@@ -133,6 +133,8 @@ def captured_ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, 
     plan = d2.sync_plan()
     if factor:
         assert plan["fc1.weight"].startswith("factored"), plan
+        if isinstance(replicate, float):
+            assert plan["fc1.weight"] == plan["fc2.weight"] == "factored-split", plan
     for i, (a, b) in enumerate(zip(m1.parameters(), m2.parameters())):
         assert torch.equal(a, b), f"rank {r}: captured != eager for param {i} " \
                                   f"(max diff {float((a - b).abs().max())})"

@@ -141,10 +141,16 @@ def ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, fused=Tru
     torch.cuda.synchronize()
     plan = ddp.sync_plan()
     if fused and factor:
-        want = {True: "factored-replicated", False: "factored-sharded",
-                None: "factored-replicated" if W * B <= ddp._REPLICATE_MAX_WB else
-                "factored-sharded"}[replicate]
-        assert plan["fc1.weight"] == want and plan["fc2.weight"] == want, plan
+        if isinstance(replicate, float):  # a split job: part of the rows replicated
+            want = "factored-split"
+        elif replicate is None:  # auto: measured bandwidth + step model (ddp._rep_rows_for)
+            want = None
+        else:
+            want = {True: "factored-replicated", False: "factored-sharded"}[replicate]
+        if want is None:
+            assert plan["fc1.weight"].startswith("factored"), plan
+        else:
+            assert plan["fc1.weight"] == want and plan["fc2.weight"] == want, plan
         assert plan["fc1.bias"] == "factored-bias", plan
         assert set(ddp._factor_cap.values()) == {B}, ddp._factor_cap
     elif fused:

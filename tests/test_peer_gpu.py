@@ -35,12 +35,14 @@ def test_peer_relay_semantics(tmp_path):
 
 @pytest.mark.parametrize("world,kind,factor,replicate", [
     (2, "sgd", True, None), (2, "adam", True, False), (3, "sgd", True, False),
-    (3, "adam", True, True), (2, "sgd", False, None), (3, "adam", False, None)])
+    (3, "adam", True, True), (2, "sgd", False, None), (3, "adam", False, None),
+    (2, "sgd", True, 0.5), (3, "adam", True, 0.5)])
 def test_captured_step_with_real_peers(tmp_path, world, kind, factor, replicate):
     run(PW.captured_ddp_parity, tmp_path, n=world, kind=kind, factor=factor, replicate=replicate)
 
 
-@pytest.mark.parametrize("world,kind,replicate", [(2, "adam", False), (4, "sgd", True)])
+@pytest.mark.parametrize("world,kind,replicate", [(2, "adam", False), (4, "sgd", True),
+                                                  (4, "adam", 0.5)])
 def test_peer_eager_device_path_matches_oracle(tmp_path, world, kind, replicate):
     run(RW.ddp_parity, tmp_path, n=world, kind=kind, factor=True, replicate=replicate,
         backend="peer")

@@ -28,7 +28,7 @@ def test_relay_collectives(tmp_path):
 
 @pytest.mark.parametrize("world,kind,replicate", [
     (2, "sgd", None), (2, "adam", False), (3, "sgd", False), (3, "adam", True),
-    (4, "sgd", True), (4, "adam", False)])
+    (4, "sgd", True), (4, "adam", False), (3, "sgd", 0.5)])
 def test_factored_device_path_matches_oracle(tmp_path, world, kind, replicate):
     run(RW.ddp_parity, tmp_path, n=world, kind=kind, factor=True, replicate=replicate)
 
@@ -65,8 +65,8 @@ def test_bench_world2_record(tmp_path):
     assert sync["modes"]["fc1.weight"].startswith("factored"), sync
     chosen = sync["factor_tuning"]["chosen"]
     assert set(chosen) == {"fc1.weight", "fc2.weight"}, sync  # a choice per factored weight
-    assert set(chosen.values()) <= {"replicated", "sharded"}, sync
-    assert len(sync["factor_tuning"]["timings_ms"]) == 4, sync  # 2 weights: 4 combinations
+    assert set(chosen.values()) <= {"replicated", "sharded", "split"}, sync
+    assert len(sync["factor_tuning"]["timings_ms"]) == 9, sync  # 2 weights x 3 modes
 
 
 def _port():

@@ -1286,7 +1286,7 @@ struct PyOps : SyncOps {
   void scale_grads(int b, const Ranges& r, hipStream_t) override {
     fns.attr("scale_grads")(b, pylist(r));
   }
-  void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
+  void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j, hipStream_t,
                    hipStream_t) override {
     fns.attr("factor_sync")(begin, own, cnt, j.B, j.out, j.in, j.bias_off, j.replicate,
                             reinterpret_cast<intptr_t>(j.g_all),
@@ -1730,7 +1730,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("owned_shard", &SyncBackend::owned_shard)
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
-              int64_t bias_off, int bias_bucket, bool replicate, bool x_ready) {
+              int64_t bias_off, int bias_bucket, bool replicate, bool x_ready, int rep_rows) {
              // device buffers for RcclOps; host buffers for PyOps (the CPU twin looks them up by
              // address in parallel/ddp.py _CpuSyncOps.factor_sync)
              TORCH_CHECK(g_all.is_cuda() == b.ops()->on_device() &&
@@ -1748,11 +1748,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.bias_off = bias_off;
              j.replicate = replicate;
              j.x_ready = x_ready;
+             j.rep_rows = replicate ? out : rep_rows;
              b.arm_factor(bucket, j, bias_bucket);
            },
            py::arg("bucket"), py::arg("g_all"), py::arg("x_all"), py::arg("B"), py::arg("out"),
            py::arg("in"), py::arg("bias_off"), py::arg("bias_bucket"),
-           py::arg("replicate") = false, py::arg("x_ready") = false)
+           py::arg("replicate") = false, py::arg("x_ready") = false, py::arg("rep_rows") = 0)
       .def("prefetch_factor_x",
            [](SyncBackend& b, int bucket, Tensor& x_all, int B, int in) {
              CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
@@ -1763,8 +1764,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("flush", [](SyncBackend& b) { b.flush(cur_stream()); })
       .def("reserve_factor",
            [](SyncBackend& b, int64_t begin, int64_t end, Tensor& g_all, Tensor& x_all, int B,
-              int out, int in, int64_t bias_off, bool replicate) {
+              int out, int in, int64_t bias_off, bool replicate, int rep_rows) {
              FactorJob j;
+             j.rep_rows = replicate ? out : rep_rows;
              j.g_all = g_all.data_ptr<float>();
              j.x_all = x_all.data_ptr<float>();
              j.B = B; j.out = out; j.in = in;

@@ -23,6 +23,8 @@ RcclOps::RcclOps(std::shared_ptr<Communicator> comm, float* grad, float* param, 
 }
 
 RcclOps::~RcclOps() {
+  for (auto e : fac_ev_)
+    if (e) (void)hipEventDestroy(e);
   if (wire_) (void)hipFree(wire_);
   if (factor_ws_) (void)hipFree(factor_ws_);
   if (factor_part_) (void)hipFree(factor_part_);
@@ -127,7 +129,8 @@ void RcclOps::scale_grads(int b, const Ranges& r, hipStream_t s) {
   for_range_sets(r, [&](const RangeSet& rs) { scale_ranges_by(grad_, rs, blk, s); });
 }
 
-void SyncOps::factor_sync(int64_t, int64_t, int64_t, const FactorJob&, hipStream_t) {
+void SyncOps::factor_sync(int64_t, int64_t, int64_t, const FactorJob&, hipStream_t,
+                          hipStream_t) {
   throw std::runtime_error("factored gradient synchronisation needs the device backend");
 }
 
@@ -229,7 +232,7 @@ void RcclOps::factor_reserve(int64_t begin, int64_t own, int64_t cnt, const Fact
 }
 
 void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
-                          hipStream_t s) {
+                          hipStream_t s, hipStream_t compute) {
   const int W = comm_->world(), r = comm_->rank();
   if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
   if (!skip_collectives) {
@@ -244,18 +247,50 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
                         ncclFloat32, s);
     comm_->group_end();
   }
+  // The job's arithmetic (bias column sums, shard GEMM with the update in its epilogue) runs on
+  // the COMPUTE stream when the collectives ride a side stream: the comm stream then carries
+  // only collectives, so the next job's gathers and this job's parameter all-gather are not
+  // queued behind GEMMs (toy MLP at W > 1: fc1's g gather overlaps fc2's GEMM, fc2's parameter
+  // all-gather overlaps fc1's GEMM; profiles/r8). Cross-stream edges are events (graph edges
+  // under capture).
+  hipStream_t gs = s;
+  if (compute && compute != s) {
+    for (auto& e : fac_ev_)
+      if (!e) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventRecord(fac_ev_[0], s), "hipEventRecord(factor)");
+    check_hip(hipStreamWaitEvent(compute, fac_ev_[0], 0), "hipStreamWaitEvent(factor)");
+    gs = compute;
+  }
   const FactorPlan f = plan_factor(begin, own, cnt, j);
-  grow_factor_ws(f, j.out, s);
+  grow_factor_ws(f, j.out, gs);
+  const bool split = !j.replicate && j.rep_rows > 0;
+  const int64_t rep = split ? (int64_t)j.rep_rows * j.in : 0;  // replicated [begin, begin + rep)
+  FactorPlan fr;
+  if (split) {
+    fr = plan_factor(begin, begin, rep, j);
+    grow_factor_ws(fr, j.out, gs);
+  }
   if (f.bias_slices > 0) {
     // the whole averaged bias gradient (column sums of the gathered g / W) and its update, on
     // every rank: identical inputs, identical results, no collective
     relu_bias_bwd_ws(j.g_all, nullptr, W * j.B, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
-                     factor_part_, f.bias_slices, s);
-    opt_update({{j.bias_off, j.bias_off + j.out}}, s);
+                     factor_part_, f.bias_slices, gs);
+    opt_update({{j.bias_off, j.bias_off + j.out}}, gs);
   }
-  gemm_f32_run(f.a, f.plan, factor_ws_, s);
-  if (!f.epi) opt_update({{own, own + cnt}}, s);
-  if (!j.replicate) all_gather_params(begin, cnt, s);
+  gemm_f32_run(f.a, f.plan, factor_ws_, gs);
+  if (!f.epi) opt_update({{own, own + cnt}}, gs);
+  if (!j.replicate) {
+    if (gs != s) {
+      check_hip(hipEventRecord(fac_ev_[1], gs), "hipEventRecord(factor)");
+      check_hip(hipStreamWaitEvent(s, fac_ev_[1], 0), "hipStreamWaitEvent(factor)");
+    }
+    all_gather_params(begin + rep, cnt, s);  // the sharded rows only
+  }
+  if (split) {
+    // the replicated rows, computed by every rank while the sharded rows travel
+    gemm_f32_run(fr.a, fr.plan, factor_ws_, gs);
+    if (!fr.epi) opt_update({{begin, begin + rep}}, gs);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -329,10 +364,18 @@ void SyncBackend::arm_factor(int bucket, const FactorJob& j, int bias_bucket) {
   if (bias_bucket >= 0) factor_skip_[bias_bucket] = 1;
 }
 
+Range SyncBackend::factor_own(int64_t begin, int64_t end, const FactorJob& j) const {
+  // replicated: every row; sharded / split: this rank's share of the rows past the replicated
+  if (j.replicate) return {begin, end};
+  return owned_shard(begin + (int64_t)j.rep_rows * j.in, end);
+}
+
 void SyncBackend::reserve_factor(int64_t begin, int64_t end, const FactorJob& j) {
   if (!ops_->on_device()) return;
-  const Range own = j.replicate ? Range{begin, end} : owned_shard(begin, end);
+  const Range own = factor_own(begin, end, j);
   if (own.second > own.first) ops_->factor_reserve(begin, own.first, own.second - own.first, j);
+  if (!j.replicate && j.rep_rows > 0)
+    ops_->factor_reserve(begin, begin, (int64_t)j.rep_rows * j.in, j);
 }
 
 void SyncBackend::prefetch_factor_x(int bucket, float* x_all, int B, int in,
@@ -522,17 +565,20 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
   if (bucket < (int)factor_.size() && factor_[bucket].B > 0) {
     const FactorJob j = factor_[bucket];
     factor_[bucket].B = 0;
-    // replicated jobs own the whole weight; sharded ones this rank's 1/W of its rows
-    const Range own = j.replicate ? Range{begin, end} : owned_shard(begin, end);
+    // replicated jobs own the whole weight; sharded ones this rank's 1/W of its rows; split
+    // ones this rank's 1/W of the rows past the replicated ones
+    const Range own = factor_own(begin, end, j);
     const int64_t cnt = own.second - own.first;
+    const int64_t shared = end - begin - (j.replicate ? 0 : (int64_t)j.rep_rows * j.in);
     if (fused_kind == 0 || clip != ClipMode::NONE || compressed ||
-        (!j.replicate && cnt * ops_->world() != end - begin) ||
+        (!j.replicate && (j.rep_rows < 0 || j.rep_rows >= j.out ||
+                          cnt * ops_->world() != shared || cnt % j.in != 0)) ||
         (int64_t)j.out * j.in != end - begin)
       throw std::runtime_error("factored bucket: needs the fused optimizer, no clipping / "
                                "compression, and one whole-row-sharded weight per bucket");
     const int64_t own0 = own.first;
-    issue(bucket, compute, [this, begin, own0, cnt, j](hipStream_t cs) {
-      ops_->factor_sync(begin, own0, cnt, j, cs);
+    issue(bucket, compute, [this, begin, own0, cnt, j, compute](hipStream_t cs) {
+      ops_->factor_sync(begin, own0, cnt, j, cs, compute);
     });
     return;
   }

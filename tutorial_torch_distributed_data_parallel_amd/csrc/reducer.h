@@ -85,6 +85,11 @@ struct FactorJob {
   // so no parameter all-gather follows. Chosen when W*B is small enough that the extra GEMM rows
   // cost less than the out*in*(W-1)/W all-gather on xGMI (parallel/ddp.py factor_replicate).
   bool replicate = false;
+  // split job (0 < rep_rows < out, replicate false): rows [0, rep_rows) replicated -- every rank
+  // computes and updates them, overlapped with the all-gather of the rest -- and rows
+  // [rep_rows, out) sharded over the ranks as in a sharded job (parallel/commmodel.py
+  // "factored-split": at W = 8 it hides most of the parameter all-gather of the last bucket)
+  int rep_rows = 0;
   // x_all was already all-gathered at forward time (SyncBackend::prefetch_factor_x): the job
   // gathers only g
   bool x_ready = false;
@@ -116,8 +121,10 @@ struct SyncOps {
   // collective watchdog: the work enqueued on `s` so far must finish within the timeout
   virtual void watch(hipStream_t s, const char* what) { (void)s; (void)what; }
   // factored weight bucket [begin, begin + W*cnt): this rank owns [own, own + cnt) (FactorJob)
+  // `s` carries the collectives; `compute` (when a different stream) runs the job's GEMM and
+  // updates, so the comm stream stays free for the next job's gathers (see RcclOps)
   virtual void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
-                           hipStream_t s);
+                           hipStream_t s, hipStream_t compute);
   // forward-time all-gather of a factored weight's x_all ([W*B][in], this rank's rows at slot r)
   virtual void factor_gather_x(float* x_all, int B, int in, hipStream_t s);
   // size the workspaces factor_sync(begin, own, cnt, j) will need (eagerly, before a capture)
@@ -158,7 +165,7 @@ class RcclOps : public SyncOps {
   void scale_grads(int block, const Ranges& r, hipStream_t s) override;
   void watch(hipStream_t s, const char* what) override { comm_->watch(s, what); }
   void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
-                   hipStream_t s) override;
+                   hipStream_t s, hipStream_t compute) override;
   void factor_gather_x(float* x_all, int B, int in, hipStream_t s) override;
   void factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j) override;
 
@@ -184,6 +191,7 @@ class RcclOps : public SyncOps {
   int64_t factor_ws_floats_ = 0;
   float* factor_part_ = nullptr;  // column-sum partials of the factored biases
   int64_t factor_part_floats_ = 0;
+  hipEvent_t fac_ev_[2] = {nullptr, nullptr};  // comm <-> compute edges of a factored job
 };
 
 // The bucket algorithm (one instance per DDP model).
@@ -227,6 +235,8 @@ class SyncBackend : public ReducerBackend {
   // eagerly size the workspaces of the factored job of bucket [begin, end) (DDP.settle, before
   // a capture: the first factored step may have run under another bucket layout)
   void reserve_factor(int64_t begin, int64_t end, const FactorJob& j);
+  // the rows of bucket [begin, end) this rank computes under job j (elements)
+  Range factor_own(int64_t begin, int64_t end, const FactorJob& j) const;
   // capture the deferred side branches once the compute stream has a node behind them (a
   // caller that just launched compute work: ops/linear.py after a factored layer's forward GEMM)
   void flush(hipStream_t compute) { flush_forks(compute, false); }

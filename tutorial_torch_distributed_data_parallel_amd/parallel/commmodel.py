@@ -2,7 +2,8 @@
 VERDICT r3 item 3: "publish the model ... per-rank bytes and predicted exposed us at W=2/4/8").
 
 Two timelines of one captured step are simulated: the compute stream (forward, then backward
-layer by layer) and the communicator's side stream, which runs the sync jobs in issue order.
+layer by layer, plus the sync jobs' arithmetic) and the communicator's side stream, which runs
+the collectives in issue order.
 Each Linear weight W[out][in] (per-rank batch B) is synchronised in one of four modes:
 
   allreduce           ring all-reduce of the out*in gradient, update on every rank
@@ -13,14 +14,18 @@ Each Linear weight W[out][in] (per-rank batch B) is synchronised in one of four 
                       out/W rows with the update in its epilogue, all-gather of the rows
   factored-replicated the same gathers, the GEMM over ALL rows on every rank, no parameter
                       all-gather
+  factored-split      a fraction f of the rows replicated, the rest sharded: this rank's shard
+                      GEMM first, then the all-gather of the sharded rows on the side stream
+                      WHILE the compute stream computes the replicated rows (f balances the two)
 
-A job can start when its gradient factor exists (backward of the layer above) and when the
-side stream is free; the step ends when both streams are done, so the exposed communication is
-``max(0, side_end - compute_end)``. Wire times use bus bandwidth (nccl-tests convention):
+A job's collectives start when its gradient factor exists (backward of the layer above) and
+the side stream is free; its arithmetic runs on the compute stream once they are in; the step
+ends when both streams are done, so the exposed communication is the step minus the compute a
+single rank would do. Wire times use bus bandwidth (nccl-tests convention):
 ``t = bytes * factor / busbw`` with factor 2(W-1)/W (all-reduce) or (W-1)/W (all-gather,
 reduce-scatter), plus a fixed latency per collective. Compute on the side stream (the factored
-GEMM, updates) is costed at the given rates and assumed not to slow the compute stream -- an
-optimistic bound, stated as such in docs/COMM_MODEL.md.
+GEMM, updates) is costed at the given rates; collectives are assumed not to slow the compute
+kernels they overlap -- an optimistic bound, stated as such in docs/COMM_MODEL.md.
 
 Inputs are either assumed (``Hardware``: per-link xGMI bandwidth x links used, the split-bf16
 fp32 GEMM rate, HBM bandwidth) or measured (bench.py passes the RCCL busbw of its diagnostic
@@ -31,7 +36,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-MODES = ("allreduce", "sharded", "factored-sharded", "factored-replicated")
+MODES = ("allreduce", "sharded", "factored-sharded", "factored-replicated", "factored-split")
 
 
 @dataclass
@@ -80,75 +85,93 @@ def _coll_us(hw: Hardware, op: str, W: int, nbytes: float) -> float:
 
 
 def job_cost(layer: Layer, mode: str, W: int, B: int, hw: Hardware) -> dict:
-    """Per-rank wire bytes and side-stream time (us) of one weight's sync job. ``x_us`` is the
-    part issued at forward time (factored x gather), the rest runs when g is ready."""
+    """Per-rank wire bytes and the parts of one weight's sync job, in us: ``x_us`` the factored
+    x gather (issued at forward time), ``pre_us`` side-stream collectives before the update
+    arithmetic, ``compute_us`` the arithmetic (wgrad GEMM / factored GEMM + update; on the
+    compute stream), ``post_us`` side-stream collectives after it. ``g_us`` = pre + compute +
+    post: the job alone, serialised."""
     o, n = layer.out, layer.inp
     P = 4.0 * o * n
-    upd_full = 16.0 * o * n / (hw.hbm_TBps * 1e6)     # p + momentum read + write (SGD)
+    # bucket modes: the weight-gradient GEMM and one update pass (layer.wgrad_us: the dp1
+    # epilogue GEMM, which does both) on the compute stream, the collectives on the side stream
     if mode == "allreduce":
-        t = _coll_us(hw, "all_reduce", W, P) + upd_full
-        return {"mode": mode, "wire_MB": 2 * (W - 1) / W * P / 1e6, "x_us": 0.0, "g_us": t,
-                "compute_wgrad_us": layer.wgrad_us - 0.0}
-    if mode == "sharded":
-        t = _coll_us(hw, "reduce_scatter", W, P) + upd_full / W + _coll_us(hw, "all_gather", W, P)
-        return {"mode": mode, "wire_MB": 2 * (W - 1) / W * P / 1e6, "x_us": 0.0, "g_us": t,
-                "compute_wgrad_us": layer.wgrad_us}
-    gx = 4.0 * B * n * W               # gathered x bytes (W slots)
-    gg = 4.0 * B * o * W
-    x_us = _coll_us(hw, "all_gather", W, gx)
-    g_us = _coll_us(hw, "all_gather", W, gg)
-    rows = o if mode == "factored-replicated" else o / W
-    gemm = 2.0 * W * B * rows * n / (hw.gemm_TFps * 1e6)
-    upd = 16.0 * rows * n / (hw.hbm_TBps * 1e6)
-    t = g_us + max(gemm, upd)
-    wire = (gx + gg) * (W - 1) / W
-    if mode == "factored-sharded":
-        t += _coll_us(hw, "all_gather", W, P)
-        wire += P * (W - 1) / W
-    return {"mode": mode, "wire_MB": wire / 1e6, "x_us": x_us, "g_us": t,
-            "compute_wgrad_us": 0.0}
+        pre, comp, post = 0.0, layer.wgrad_us, _coll_us(hw, "all_reduce", W, P)
+        wire = 2 * (W - 1) / W * P
+        x_us = 0.0
+    elif mode == "sharded":
+        pre, comp = 0.0, layer.wgrad_us
+        post = _coll_us(hw, "reduce_scatter", W, P) + _coll_us(hw, "all_gather", W, P)
+        wire = 2 * (W - 1) / W * P
+        x_us = 0.0
+    else:
+        gx = 4.0 * B * n * W               # gathered x bytes (W slots)
+        gg = 4.0 * B * o * W
+        x_us = _coll_us(hw, "all_gather", W, gx)
+        pre = _coll_us(hw, "all_gather", W, gg)
+
+        def arith(rows):
+            gemm = 2.0 * W * B * rows * n / (hw.gemm_TFps * 1e6)
+            return max(gemm, 16.0 * rows * n / (hw.hbm_TBps * 1e6))
+        f = 1.0 if mode == "factored-replicated" else 0.0
+        if mode == "factored-split" and W > 1:
+            # balance the replicated rows' arithmetic against the all-gather of the others
+            ag = _coll_us(hw, "all_gather", W, P)
+            f = max(0.0, min(1.0, ag / (ag + arith(o))))
+        comp = arith(o * f) if mode == "factored-replicated" else arith((1.0 - f) * o / W)
+        after = arith(o * f) if mode == "factored-split" else 0.0
+        post = 0.0 if mode == "factored-replicated" else \
+            _coll_us(hw, "all_gather", W, (1.0 - f) * P)
+        wire = (gx + gg) * (W - 1) / W + (1.0 - f) * P * (W - 1) / W * (mode != "factored-replicated")
+        return {"mode": mode, "wire_MB": wire / 1e6, "x_us": x_us, "pre_us": pre,
+                "compute_us": comp, "after_us": after, "post_us": post, "rep_fraction": f,
+                "g_us": pre + comp + max(post, after)}
+    return {"mode": mode, "wire_MB": wire / 1e6, "x_us": x_us, "pre_us": pre,
+            "compute_us": comp, "after_us": 0.0, "post_us": post, "rep_fraction": 0.0,
+            "g_us": pre + comp + post}
 
 
 def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
              prefetch_x: bool = True) -> dict:
-    """Predicted step of a captured W-rank step: compute-stream time, side-stream end, exposed
-    communication and the per-job table. ``modes``: layer name -> mode (layers absent, e.g. the
-    small head, ride in the first bucket: all-reduced with the job of the layer below them)."""
-    t = 0.0
-    side = 0.0
-    jobs = []
+    """Predicted captured W-rank step (reducer.cpp / ops/linear.py schedule): forward issues the
+    factored x gathers on the side stream; backward runs, per weight from the last layer down,
+    the layer's input gradient and then its job -- side-stream collectives (gathers, all-reduce,
+    parameter all-gather) in FIFO order, the job's arithmetic on the compute stream once its
+    gathers are in. The step ends when both streams are done: ``exposed_us`` = step - compute
+    alone. ``modes``: layer name -> mode; layers absent (the small head) cost their compute time
+    and ride, as an all-reduce, with the first job."""
+    tc = ts = 0.0
     costs = {L.name: job_cost(L, modes[L.name], W, B, hw) for L in layers if L.name in modes}
-    # forward: the factored layers' x gathers start as soon as the layer runs
-    for L in layers:
-        t += L.fwd_us
-        c = costs.get(L.name)
-        if c and c["x_us"] > 0 and prefetch_x:
-            start = max(side, t - L.fwd_us)
-            side = start + c["x_us"]
-    fwd_end = t
-    # backward, last layer first: a layer's job starts once its g exists (after the layer
-    # above's input gradient); its own dgrad / wgrad run on the compute stream
+    for L in layers:  # forward
+        if L.name in costs and costs[L.name]["x_us"] > 0 and prefetch_x:
+            ts = max(ts, tc) + costs[L.name]["x_us"]
+        tc += L.fwd_us
+    fwd_end = tc
+    alone = fwd_end + sum(L.dgrad_us + L.wgrad_us for L in layers)  # dp1-like compute
     small = [L for L in layers if L.name not in modes]
-    t += sum(L.dgrad_us + L.wgrad_us for L in small)
-    # small layers' gradients ride with the next job: an all-reduce of their bytes
+    tc += sum(L.dgrad_us + L.wgrad_us for L in small)
     small_bytes = sum(4.0 * L.out * L.inp for L in small)
+    jobs = []
     for L in reversed([L for L in layers if L.name in modes]):
         c = costs[L.name]
-        ready = t
-        start = max(side, ready)
-        dur = c["g_us"] + (0.0 if prefetch_x else c["x_us"])
+        ready = tc                       # this layer's g exists
+        tc += L.dgrad_us                 # its input gradient (captured before the job's fork)
+        pre = c["pre_us"] + (0.0 if prefetch_x else c["x_us"])
         if small_bytes:
-            dur += _coll_us(hw, "all_reduce", W, small_bytes)
+            pre += _coll_us(hw, "all_reduce", W, small_bytes)
             small_bytes = 0.0
-        side = start + dur
+        start = max(ts, ready)
+        ts = start + pre
+        tc = max(tc, ts if c["mode"].startswith("factored") else tc) + c["compute_us"]
+        if c["post_us"] > 0:
+            ts = max(ts, tc) + c["post_us"]
+        tc += c["after_us"]  # replicated rows of a split job, while its all-gather runs
         jobs.append({"layer": L.name, **{k: round(v, 2) if isinstance(v, float) else v
                                          for k, v in c.items()},
-                     "start_us": round(start, 1), "end_us": round(side, 1)})
-        t += L.dgrad_us + c["compute_wgrad_us"]
-    exposed = max(0.0, side - t)
-    return {"W": W, "B": B, "compute_us": round(t, 1), "forward_us": round(fwd_end, 1),
-            "side_end_us": round(side, 1), "exposed_us": round(exposed, 1),
-            "step_us": round(max(t, side), 1), "jobs": jobs}
+                     "start_us": round(start, 1), "end_us": round(max(ts, tc), 1)})
+    step = max(tc, ts)
+    return {"W": W, "B": B, "compute_us": round(alone, 1), "forward_us": round(fwd_end, 1),
+            "side_end_us": round(ts, 1), "exposed_us": round(max(0.0, step - alone), 1),
+            "step_us": round(step, 1), "jobs": jobs}
 
 
 def best_plan(layers: list[Layer], W: int, B: int, hw: Hardware,

@@ -131,6 +131,7 @@ class DistributedDataParallel(nn.Module):
         self.factor_replicate = None if env_rep in (None, "", "auto") else env_rep != "0"
         self.factor_tuning = None  # measured replicate-vs-shard timings (tune_factor_replicate)
         self._busbw = None  # measured all-gather bus bandwidth (_probe_bandwidth)
+        self._factor_rep = {}  # arena index -> replicated rows of its last factored job
         self._factor = {}          # arena index -> (out, in) of factor-eligible Linear weights
         self._factor_bucket = {}   # arena index -> its (dedicated) bucket
         self._factor_bias_bucket = {}  # arena index -> the (dedicated) bucket of its bias
@@ -254,6 +255,7 @@ class DistributedDataParallel(nn.Module):
         new_of = {old: new for new, old in enumerate(order)}
         self._factor_cap = {new_of[i]: v for i, v in self._factor_cap.items()}
         self._factor_mode = {new_of[i]: v for i, v in self._factor_mode.items()}
+        self._factor_rep = {new_of[i]: v for i, v in self._factor_rep.items()}
         self._factor_last_B = {new_of[i]: v for i, v in self._factor_last_B.items()}
         self._factor_bufs = {(new_of[i], b): v for (i, b), v in self._factor_bufs.items()}
         self._factor = {new_of[i]: (o, n, None if bi is None else new_of[bi])
@@ -286,9 +288,10 @@ class DistributedDataParallel(nn.Module):
                 continue
             g_all, x_all = self._factor_buffers(i, cap)
             b = self._factor_bucket[i]
+            rows = self._rep_rows_for(i, cap)
             self._backend.reserve_factor(self._bounds[b], self._bounds[b + 1], g_all, x_all, cap,
                                          o, n, -1 if bi is None else self.arena.offsets[bi],
-                                         bool(self._replicate_for(i, cap)))
+                                         rows == o, rows)
 
     def _make_hook(self, idx):
         arena = self.arena
@@ -821,13 +824,16 @@ class DistributedDataParallel(nn.Module):
                 gs[B:].zero_()
                 xs[:B].copy_(x)
                 xs[B:].zero_()
-        rep = self._replicate_for(i, cap)
+        rows = self._rep_rows_for(i, cap)
         self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], cap, o, n,
                                  -1 if bi is None else self.arena.offsets[bi],
-                                 self._factor_bias_bucket.get(i, -1), replicate=bool(rep),
+                                 self._factor_bias_bucket.get(i, -1), replicate=rows == o,
+                                 rep_rows=rows,
                                  x_ready=bool(x_ready))
         self._factor_last_B[i] = B
-        self._factor_mode[i] = "factored-replicated" if rep else "factored-sharded"
+        self._factor_rep[i] = rows
+        self._factor_mode[i] = ("factored-replicated" if rows == o else
+                                "factored-split" if rows > 0 else "factored-sharded")
         if dw is not None:
             self._factor_handed[i] = dw.data_ptr()
         return True
@@ -882,27 +888,60 @@ class DistributedDataParallel(nn.Module):
         rt.all_reduce(t, "min")
         self._busbw = {"all_gather": float(t.item()), "bytes": size}
 
-    def _replicate_for(self, i, cap) -> bool:
-        """Replicated (True) or sharded factored job for weight ``i``: an explicit choice
-        (``factor_replicate`` bool or {arena index: bool}, tune_factor_replicate's result),
-        else the step model with the measured all-gather bandwidth, else the fallback rule.
-        Identical on every rank (agreed inputs only)."""
+    @staticmethod
+    def _split_rows(o: int, n: int, W: int, f: float) -> int:
+        """Replicated rows of a split job replicating ~``f`` of the ``o`` rows: the sharded rest
+        is W equal whole-row shards of a multiple of 64 elements (SyncBackend.owned_shard)."""
+        import math
+
+        # rows per rank: a shard of 64-element multiples, and 16 rows at least (16-B aligned
+        # A columns for the fast GEMM's loads, fewer partial tiles)
+        u64 = 64 // math.gcd(n, 64)
+        unit = u64 * 16 // math.gcd(u64, 16)
+        q = int(round((1.0 - f) * o / W / unit)) * unit
+        q = max(0, min(q, o // W // unit * unit))
+        rows = o - W * q
+        return o if q == 0 else rows
+
+    def _rep_rows_for(self, i, cap) -> int:
+        """How many rows of factored weight ``i`` every rank computes itself: all of them
+        (replicated), none (sharded) or a share (split: parallel/commmodel.py
+        "factored-split"). An explicit ``factor_replicate`` (True / False / "split" / a fraction,
+        or {arena index: one of these}: tune_factor_replicate's result) decides, else the step
+        model with the measured all-gather bandwidth, else the fallback rule. Identical on every
+        rank (agreed inputs only). The CPU twin knows replicated and sharded only."""
+        o, n, _ = self._factor[i]
+        W = self.world_size
+        if W == 1:
+            return o
         rep = self.factor_replicate
         if isinstance(rep, dict):
             rep = rep.get(i)
-        if rep is not None:
-            return bool(rep)
-        W = self.world_size
-        if W == 1 or self._busbw is None:
-            return self._replicate_pays(W, cap)
+        if rep is True or rep is False:
+            return o if rep else 0
         from . import commmodel as cm
 
-        o, n, _ = self._factor[i]
-        hw = cm.Hardware(busbw_GBps={"all_gather": self._busbw["all_gather"]})
+        hw = cm.Hardware(busbw_GBps={"all_gather": self._busbw["all_gather"]}) \
+            if self._busbw is not None else cm.Hardware()
         lay = cm.Layer(f"w{i}", o, n, 0.0, 0.0, 0.0)
-        rep_us = cm.job_cost(lay, "factored-replicated", W, cap, hw)["g_us"]
-        shd_us = cm.job_cost(lay, "factored-sharded", W, cap, hw)["g_us"]
-        return rep_us <= shd_us
+        if isinstance(rep, float) and 0.0 < rep < 1.0:
+            f = rep
+        elif rep == "split":
+            f = cm.job_cost(lay, "factored-split", W, cap, hw)["rep_fraction"]
+        else:  # auto
+            if self._busbw is None:
+                return o if self._replicate_pays(W, cap) else 0
+            costs = {m: cm.job_cost(lay, m, W, cap, hw)
+                     for m in ("factored-replicated", "factored-sharded", "factored-split")}
+            best = min(costs, key=lambda m: costs[m]["g_us"])
+            if best == "factored-replicated":
+                return o
+            if best == "factored-sharded":
+                return 0
+            f = costs[best]["rep_fraction"]
+        if not self._gpu:
+            return o if f >= 0.5 else 0
+        return self._split_rows(o, n, W, f)
 
     def tune_factor_replicate(self, step_fn, iters: int = 3, capture: bool = False):
         """Measure, don't guess: time ``step_fn`` (one full training step) under every
@@ -924,8 +963,9 @@ class DistributedDataParallel(nn.Module):
         from ..train.graph import CapturedStep, try_capture
 
         idx = sorted(self._factor)
-        combos = list(itertools.product((True, False), repeat=len(idx))) if len(idx) <= 3 \
-            else [(True,) * len(idx), (False,) * len(idx)]
+        choices = (True, False, "split")
+        combos = list(itertools.product(choices, repeat=len(idx))) if len(idx) <= 2 \
+            else [(c,) * len(idx) for c in choices]
         ms = []
         for combo in combos:
             self.consolidate_optimizer_state()
@@ -952,13 +992,15 @@ class DistributedDataParallel(nn.Module):
 
         def label(combo):
             return {names.get(id(self.arena.params[i]), f"param{i}"):
-                    ("replicated" if c else "sharded") for i, c in zip(idx, combo)}
+                    ("replicated" if c is True else "sharded" if c is False else "split")
+                    for i, c in zip(idx, combo)}
         self.factor_tuning = {
             "captured": bool(capture),
             "timings_ms": [{"modes": label(c), "ms": round(m, 4)} for c, m in zip(combos, ms)],
             "chosen": label(combos[best]),
             # the round-3 record's keys: all-replicated / all-sharded times
-            "replicated_ms": round(ms[0], 4), "sharded_ms": round(ms[-1], 4),
+            "replicated_ms": round(ms[combos.index((True,) * len(idx))], 4),
+            "sharded_ms": round(ms[combos.index((False,) * len(idx))], 4),
         }
         return self.factor_replicate
 
@@ -973,8 +1015,17 @@ class DistributedDataParallel(nn.Module):
         for name, buf in bufs.items():
             if not torch.is_tensor(buf) or buf.numel() != self.arena.numel:
                 continue
-            for i in range(len(self._bounds) - 1):
-                begin, end = self._bounds[i], self._bounds[i + 1]
+            fac_of = {b: i for i, b in self._factor_bucket.items()}
+            for k in range(len(self._bounds) - 1):
+                begin, end = self._bounds[k], self._bounds[k + 1]
+                i = fac_of.get(k)
+                if i is not None and self._factor_mode.get(i, "").startswith("factored"):
+                    # a factored weight's last job: replicated rows are current everywhere,
+                    # the sharded ones (past the replicated) on their owners
+                    rows = self._factor_rep.get(i, 0)
+                    if rows == self._factor[i][0]:
+                        continue
+                    begin += rows * self._factor[i][1]
                 lo, hi = self._backend.owned_shard(begin, end)
                 cnt = (hi - lo)
                 if cnt > 0:
