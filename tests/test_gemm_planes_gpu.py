@@ -320,4 +320,5 @@ def test_split_k_reduce_is_deterministic(C):
         for out, op in outs[1:]:
             assert torch.equal(out, outs[0][0]) and torch.equal(op, outs[0][1])
         ref = torch.relu((A.double() @ (B.double().t() if bk else B.double())) + bias.double())
-        torch.testing.assert_close(outs[0][0].double(), ref, rtol=1e-5, atol=1e-4)
+        # |C| ~ sqrt(K): fp32 accumulation over K terms, scaled like the other planes tests
+        torch.testing.assert_close(outs[0][0].double(), ref, rtol=1e-4, atol=2e-5 * K ** 0.5)

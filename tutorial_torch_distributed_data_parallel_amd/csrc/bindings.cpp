@@ -1730,7 +1730,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("owned_shard", &SyncBackend::owned_shard)
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
-              int64_t bias_off, int bias_bucket, bool replicate, bool x_ready, int rep_rows) {
+              int64_t bias_off, int bias_bucket, bool replicate, bool x_ready, int rep_rows,
+              const c10::optional<Tensor>& g_src, double g_scale) {
              // device buffers for RcclOps; host buffers for PyOps (the CPU twin looks them up by
              // address in parallel/ddp.py _CpuSyncOps.factor_sync)
              TORCH_CHECK(g_all.is_cuda() == b.ops()->on_device() &&
@@ -1749,18 +1750,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.replicate = replicate;
              j.x_ready = x_ready;
              j.rep_rows = replicate ? out : rep_rows;
+             if (g_src.has_value()) {  // out-of-place g gather (unscaled g, scaled update)
+               CHECK_GPU(*g_src); CHECK_F32(*g_src); CHECK_CONTIG(*g_src);
+               TORCH_CHECK(g_src->numel() == (int64_t)B * out, "arm_factor: g must be [B][out]");
+               j.g_src = g_src->data_ptr<float>();
+               j.g_scale = (float)g_scale;
+             }
              b.arm_factor(bucket, j, bias_bucket);
            },
            py::arg("bucket"), py::arg("g_all"), py::arg("x_all"), py::arg("B"), py::arg("out"),
            py::arg("in"), py::arg("bias_off"), py::arg("bias_bucket"),
-           py::arg("replicate") = false, py::arg("x_ready") = false, py::arg("rep_rows") = 0)
+           py::arg("replicate") = false, py::arg("x_ready") = false, py::arg("rep_rows") = 0,
+           py::arg("g_src") = py::none(), py::arg("g_scale") = 1.0)
       .def("prefetch_factor_x",
-           [](SyncBackend& b, int bucket, Tensor& x_all, int B, int in) {
+           [](SyncBackend& b, int bucket, Tensor& x_all, int B, int in,
+              const c10::optional<Tensor>& x) {
              CHECK_GPU(x_all); CHECK_F32(x_all); CHECK_CONTIG(x_all);
              TORCH_CHECK(x_all.numel() == (int64_t)b.ops()->world() * B * in,
                          "prefetch_factor_x: x_all must hold W*B rows of in floats");
-             b.prefetch_factor_x(bucket, x_all.data_ptr<float>(), B, in, cur_stream());
-           })
+             const float* src = nullptr;
+             if (x.has_value()) {  // out of place: this rank's rows straight from the input
+               CHECK_GPU(*x); CHECK_F32(*x); CHECK_CONTIG(*x);
+               TORCH_CHECK(x->numel() == (int64_t)B * in, "prefetch_factor_x: x must be [B][in]");
+               src = x->data_ptr<float>();
+             }
+             b.prefetch_factor_x(bucket, x_all.data_ptr<float>(), src, B, in, cur_stream());
+           }, py::arg("bucket"), py::arg("x_all"), py::arg("B"), py::arg("in"),
+           py::arg("x") = py::none())
       .def("flush", [](SyncBackend& b) { b.flush(cur_stream()); })
       .def("reserve_factor",
            [](SyncBackend& b, int64_t begin, int64_t end, Tensor& g_all, Tensor& x_all, int B,

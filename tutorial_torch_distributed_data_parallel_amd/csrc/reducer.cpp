@@ -84,8 +84,14 @@ static void for_range_sets(const Ranges& r, F&& f) {
   if (rs.n > 0) f(rs);
 }
 
-void RcclOps::opt_update(const Ranges& r, hipStream_t s) {
+void RcclOps::opt_update(const Ranges& r, hipStream_t s) { opt_update_scaled(r, 1.f, s); }
+
+void RcclOps::opt_update_scaled(const Ranges& r, float scale, hipStream_t s) {
   if (fused.kind == 0) return;
+  SgdHyper sgd = fused.sgd;
+  AdamHyper adam = fused.adam;
+  sgd.grad_scale *= scale;
+  adam.grad_scale *= scale;
   Ranges small;
   for (const auto& x : r) {
     const int64_t n = x.second - x.first, o = x.first;
@@ -95,14 +101,14 @@ void RcclOps::opt_update(const Ranges& r, hipStream_t s) {
       continue;
     }
     if (fused.kind == 1)
-      sgd_flat(fused.p + o, grad_ + o, fused.s0 ? fused.s0 + o : nullptr, n, fused.sgd, s);
+      sgd_flat(fused.p + o, grad_ + o, fused.s0 ? fused.s0 + o : nullptr, n, sgd, s);
     else
       adam_flat(fused.p + o, grad_ + o, fused.s0 + o, fused.s1 + o,
-                fused.s2 ? fused.s2 + o : nullptr, n, fused.adam, s);
+                fused.s2 ? fused.s2 + o : nullptr, n, adam, s);
   }
   for_range_sets(small, [&](const RangeSet& rs) {
-    if (fused.kind == 1) sgd_ranges(fused.p, grad_, fused.s0, rs, fused.sgd, s);
-    else adam_ranges(fused.p, grad_, fused.s0, fused.s1, fused.s2, rs, fused.adam, s);
+    if (fused.kind == 1) sgd_ranges(fused.p, grad_, fused.s0, rs, sgd, s);
+    else adam_ranges(fused.p, grad_, fused.s0, fused.s1, fused.s2, rs, adam, s);
   });
 }
 
@@ -136,14 +142,15 @@ void SyncOps::factor_sync(int64_t, int64_t, int64_t, const FactorJob&, hipStream
 
 void SyncOps::factor_reserve(int64_t, int64_t, int64_t, const FactorJob&) {}
 
-void SyncOps::factor_gather_x(float*, int, int, hipStream_t) {
+void SyncOps::factor_gather_x(float*, const float*, int, int, hipStream_t) {
   throw std::runtime_error("forward-time factor gathers need the device backend");
 }
 
-void RcclOps::factor_gather_x(float* x_all, int B, int in, hipStream_t s) {
+void RcclOps::factor_gather_x(float* x_all, const float* x_src, int B, int in, hipStream_t s) {
   if (skip_collectives) return;
   const int r = comm_->rank();
-  comm_->all_gather(x_all + (int64_t)r * B * in, x_all, (size_t)B * in, ncclFloat32, s);
+  comm_->all_gather(x_src ? x_src : x_all + (int64_t)r * B * in, x_all, (size_t)B * in,
+                    ncclFloat32, s);
 }
 
 // The shard GEMM of a factored job, planned once for factor_sync and factor_reserve: this
@@ -194,6 +201,8 @@ RcclOps::FactorPlan RcclOps::plan_factor(int64_t begin, int64_t own, int64_t cnt
     a.opt.s2 = fused.s2 ? fused.s2 + own : nullptr;
     a.opt.sgd = fused.sgd;
     a.opt.adam = fused.adam;
+    a.opt.sgd.grad_scale *= j.g_scale;  // unscaled gathered g: the 1/W of the average here
+    a.opt.adam.grad_scale *= j.g_scale;
     if (f.bias_in_gemm) {
       a.rowsum = grad_ + j.bias_off;  // selects the row-sum tiles; never written (bias_opt)
       a.rowsum_beta = 0.f;
@@ -240,8 +249,8 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     // one RCCL group, so g and x share one launch and the links carry both back to back -- x
     // only when it was not gathered at forward time already (prefetch_factor_x)
     comm_->group_start();
-    comm_->all_gather(j.g_all + (int64_t)r * j.B * j.out, j.g_all, (size_t)j.B * j.out,
-                      ncclFloat32, s);
+    comm_->all_gather(j.g_src ? j.g_src : j.g_all + (int64_t)r * j.B * j.out, j.g_all,
+                      (size_t)j.B * j.out, ncclFloat32, s);
     if (!j.x_ready)
       comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in,
                         ncclFloat32, s);
@@ -275,10 +284,10 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
     // every rank: identical inputs, identical results, no collective
     relu_bias_bwd_ws(j.g_all, nullptr, W * j.B, j.out, j.out, nullptr, grad_ + j.bias_off, 0.f,
                      factor_part_, f.bias_slices, gs);
-    opt_update({{j.bias_off, j.bias_off + j.out}}, gs);
+    opt_update_scaled({{j.bias_off, j.bias_off + j.out}}, j.g_scale, gs);
   }
   gemm_f32_run(f.a, f.plan, factor_ws_, gs);
-  if (!f.epi) opt_update({{own, own + cnt}}, gs);
+  if (!f.epi) opt_update_scaled({{own, own + cnt}}, j.g_scale, gs);
   if (!j.replicate) {
     if (gs != s) {
       check_hip(hipEventRecord(fac_ev_[1], gs), "hipEventRecord(factor)");
@@ -289,7 +298,7 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   if (split) {
     // the replicated rows, computed by every rank while the sharded rows travel
     gemm_f32_run(fr.a, fr.plan, factor_ws_, gs);
-    if (!fr.epi) opt_update({{begin, begin + rep}}, gs);
+    if (!fr.epi) opt_update_scaled({{begin, begin + rep}}, j.g_scale, gs);
   }
 }
 
@@ -378,12 +387,12 @@ void SyncBackend::reserve_factor(int64_t begin, int64_t end, const FactorJob& j)
     ops_->factor_reserve(begin, begin, (int64_t)j.rep_rows * j.in, j);
 }
 
-void SyncBackend::prefetch_factor_x(int bucket, float* x_all, int B, int in,
+void SyncBackend::prefetch_factor_x(int bucket, float* x_all, const float* x_src, int B, int in,
                                     hipStream_t compute) {
   if (!collective() || !ops_->on_device()) return;
   if (bucket < 0 || bucket >= (int)factor_.size()) throw std::runtime_error("prefetch: bucket");
-  issue(bucket, compute, [this, x_all, B, in](hipStream_t cs) {
-    ops_->factor_gather_x(x_all, B, in, cs);
+  issue(bucket, compute, [this, x_all, x_src, B, in](hipStream_t cs) {
+    ops_->factor_gather_x(x_all, x_src, B, in, cs);
   });
 }
 

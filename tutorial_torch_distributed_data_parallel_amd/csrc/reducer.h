@@ -93,6 +93,10 @@ struct FactorJob {
   // x_all was already all-gathered at forward time (SyncBackend::prefetch_factor_x): the job
   // gathers only g
   bool x_ready = false;
+  // out-of-place g gather: this rank's UNSCALED g [B][out] straight from the layer's gradient
+  // buffer (no staging copy into slot r); the update then scales by g_scale (= 1/W) instead
+  const float* g_src = nullptr;
+  float g_scale = 1.f;
 };
 
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
@@ -125,8 +129,9 @@ struct SyncOps {
   // updates, so the comm stream stays free for the next job's gathers (see RcclOps)
   virtual void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
                            hipStream_t s, hipStream_t compute);
-  // forward-time all-gather of a factored weight's x_all ([W*B][in], this rank's rows at slot r)
-  virtual void factor_gather_x(float* x_all, int B, int in, hipStream_t s);
+  // forward-time all-gather of a factored weight's x_all ([W*B][in]): from this rank's rows at
+  // slot r (x_src null) or straight from the layer's input x_src [B][in] (out of place)
+  virtual void factor_gather_x(float* x_all, const float* x_src, int B, int in, hipStream_t s);
   // size the workspaces factor_sync(begin, own, cnt, j) will need (eagerly, before a capture)
   virtual void factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j);
 };
@@ -166,7 +171,9 @@ class RcclOps : public SyncOps {
   void watch(hipStream_t s, const char* what) override { comm_->watch(s, what); }
   void factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j,
                    hipStream_t s, hipStream_t compute) override;
-  void factor_gather_x(float* x_all, int B, int in, hipStream_t s) override;
+  void factor_gather_x(float* x_all, const float* x_src, int B, int in, hipStream_t s) override;
+  // opt_update with the gradient multiplied by `scale` first (factored jobs over unscaled g)
+  void opt_update_scaled(const Ranges& r, float scale, hipStream_t s);
   void factor_reserve(int64_t begin, int64_t own, int64_t cnt, const FactorJob& j) override;
 
   FusedOptimizer fused;
@@ -231,7 +238,8 @@ class SyncBackend : public ReducerBackend {
   // soon as the layer's forward runs, so its all-gather is issued then -- on the comm stream,
   // as a deferred fork while capturing -- and overlaps the rest of forward and backward; the
   // bucket's job at backward time then gathers only g (FactorJob::x_ready).
-  void prefetch_factor_x(int bucket, float* x_all, int B, int in, hipStream_t compute);
+  void prefetch_factor_x(int bucket, float* x_all, const float* x_src, int B, int in,
+                         hipStream_t compute);
   // eagerly size the workspaces of the factored job of bucket [begin, end) (DDP.settle, before
   // a capture: the first factored step may have run under another bucket layout)
   void reserve_factor(int64_t begin, int64_t end, const FactorJob& j);

@@ -146,6 +146,8 @@ class DistributedDataParallel(nn.Module):
         self._factor_handed = {}
         # arena index -> per-rank batch whose x this iteration's forward staged and gathered
         self._factor_x_ready = {}
+        # factor sources gathered out of place (x, g): alive until the next iteration
+        self._factor_keep = []
         self._epi_on = False
         self._epi_index = {}
         self._opt_begin_countdown = 0
@@ -414,6 +416,7 @@ class DistributedDataParallel(nn.Module):
             self._rebuild_buckets()
         self._factor_handed.clear()
         self._factor_x_ready.clear()
+        self._factor_keep.clear()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             if self._fused_opt is not None:
                 # hyper-parameters as they are NOW (after any LR-scheduler step) drive this
@@ -744,11 +747,17 @@ class DistributedDataParallel(nn.Module):
         if x.stride(1) != 1 or x.stride(0) != n:
             x = x.contiguous()
         bufs = self._factor_buffers(i, cap)
-        xs = bufs[1].view(W, cap, n)[self.rank]
-        xs[:B].copy_(x)
-        if B < cap:
+        if B == cap:
+            # out of place: the all-gather reads this rank's rows straight from x (no staging
+            # copy); x is kept alive until the next iteration -- the collective runs on the side
+            # stream, and the end-of-backward join orders it before anything that reuses x's memory
+            self._factor_keep.append(x)
+            self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[1], cap, n, x)
+        else:  # a ragged batch: staged into slot r, zero-padded to the agreed rows
+            xs = bufs[1].view(W, cap, n)[self.rank]
+            xs[:B].copy_(x)
             xs[B:].zero_()
-        self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[1], cap, n)
+            self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[1], cap, n)
         self._factor_x_ready[i] = B
         return True
 
@@ -813,7 +822,13 @@ class DistributedDataParallel(nn.Module):
                 self._cpu_ops.factor_bufs[t.data_ptr()] = t
         # the forward of this iteration staged and gathered x already (factor_forward)
         x_ready = self._gpu and self._factor_x_ready.pop(i, None) == B
-        if self._gpu:
+        g_src = None
+        if self._gpu and x_ready and B == cap:
+            # out of place: the all-gather reads this rank's (unscaled) g where the layer's
+            # backward wrote it, and the update applies the 1/W (no staging kernel at all)
+            g_src = g
+            self._factor_keep.append(g)
+        elif self._gpu:
             native().factor_stage(g, None if x_ready else x, bufs[0], bufs[1], self.rank,
                                   1.0 / W, cap)
         else:
@@ -828,7 +843,7 @@ class DistributedDataParallel(nn.Module):
         self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], cap, o, n,
                                  -1 if bi is None else self.arena.offsets[bi],
                                  self._factor_bias_bucket.get(i, -1), replicate=rows == o,
-                                 rep_rows=rows,
+                                 rep_rows=rows, g_src=g_src, g_scale=1.0 / W,
                                  x_ready=bool(x_ready))
         self._factor_last_B[i] = B
         self._factor_rep[i] = rows
