@@ -1750,11 +1750,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.replicate = replicate;
              j.x_ready = x_ready;
              j.rep_rows = replicate ? out : rep_rows;
-             if (g_src.has_value()) {  // out-of-place g gather (unscaled g, scaled update)
+             // g_scale: the factor of the update applied to the gathered g (1/W when the slots
+             // hold unscaled g). Every rank must gather the same convention whichever way its own
+             // slot was filled (out of place at a full batch, staged at a ragged one).
+             j.g_scale = (float)g_scale;
+             if (g_src.has_value()) {  // out-of-place g gather straight from the layer's buffer
                CHECK_GPU(*g_src); CHECK_F32(*g_src); CHECK_CONTIG(*g_src);
                TORCH_CHECK(g_src->numel() == (int64_t)B * out, "arm_factor: g must be [B][out]");
                j.g_src = g_src->data_ptr<float>();
-               j.g_scale = (float)g_scale;
              }
              b.arm_factor(bucket, j, bias_bucket);
            },

@@ -93,9 +93,11 @@ struct FactorJob {
   // x_all was already all-gathered at forward time (SyncBackend::prefetch_factor_x): the job
   // gathers only g
   bool x_ready = false;
-  // out-of-place g gather: this rank's UNSCALED g [B][out] straight from the layer's gradient
-  // buffer (no staging copy into slot r); the update then scales by g_scale (= 1/W) instead
+  // out-of-place g gather: this rank's g [B][out] straight from the layer's gradient buffer
+  // (no staging copy into slot r)
   const float* g_src = nullptr;
+  // factor applied to the gathered g by the update (1/W on the device path, where every rank's
+  // slot holds unscaled g whether it was read in place or staged; 1 on the CPU twin)
   float g_scale = 1.f;
 };
 

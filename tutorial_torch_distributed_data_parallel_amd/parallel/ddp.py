@@ -822,15 +822,18 @@ class DistributedDataParallel(nn.Module):
                 self._cpu_ops.factor_bufs[t.data_ptr()] = t
         # the forward of this iteration staged and gathered x already (factor_forward)
         x_ready = self._gpu and self._factor_x_ready.pop(i, None) == B
+        # device path: the slots hold UNSCALED g on every rank and the update applies the 1/W
+        # (g_scale) -- one convention whether a rank's slot is read in place (full batch) or
+        # staged (ragged batch), since ranks may take different branches in the same step
         g_src = None
         if self._gpu and x_ready and B == cap:
-            # out of place: the all-gather reads this rank's (unscaled) g where the layer's
-            # backward wrote it, and the update applies the 1/W (no staging kernel at all)
+            # out of place: the all-gather reads this rank's g where the layer's backward wrote
+            # it (no staging kernel at all)
             g_src = g
             self._factor_keep.append(g)
         elif self._gpu:
             native().factor_stage(g, None if x_ready else x, bufs[0], bufs[1], self.rank,
-                                  1.0 / W, cap)
+                                  1.0, cap)
         else:
             with torch.no_grad():
                 gs = bufs[0].view(W, cap, o)[self.rank]
@@ -843,7 +846,8 @@ class DistributedDataParallel(nn.Module):
         self._backend.arm_factor(self._factor_bucket[i], bufs[0], bufs[1], cap, o, n,
                                  -1 if bi is None else self.arena.offsets[bi],
                                  self._factor_bias_bucket.get(i, -1), replicate=rows == o,
-                                 rep_rows=rows, g_src=g_src, g_scale=1.0 / W,
+                                 rep_rows=rows, g_src=g_src,
+                                 g_scale=1.0 / W if self._gpu else 1.0,
                                  x_ready=bool(x_ready))
         self._factor_last_B[i] = B
         self._factor_rep[i] = rows
