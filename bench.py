@@ -541,11 +541,6 @@ def main():
             opt.step()
             return loss
 
-    if use_gpu and os.environ.get("TDP_BENCH_STREAM") == "1":
-        # measurement knob: run the loop on a non-default stream
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(s)
     sync = (torch.cuda.synchronize if use_gpu else (lambda: None))
     epoch = [0]
     it = [iter(loader)]
@@ -590,8 +585,7 @@ def main():
         # captured toy-MLP step: the gather reads the epoch order through a device-side cursor
         # it advances itself (no per-step index copy node in the graph)
         ecur = None
-        if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch) and \
-                os.environ.get("TDP_NO_CURSOR", "0") != "1":
+        if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch):
             ecur = EpochCursor(len(cur["idx"]), a.batch, dev)
             ecur.set_order(cur["idx"])
 

@@ -63,7 +63,7 @@ def main():
         flops = 2.0 * M * N * 128
         for fn, st, wgs in ((0, 0, 2), (1, 2, 2), (1, 2, 3), (1, 3, 2), (2, 2, 2)):
             C.gemm_f32_set_override(fn, 0, st)
-            os.environ["TDP_OPT_WGS"] = str(wgs)  # persistent epilogue grid: workgroups per CU
+            C.gemm_f32_set_opt_variant(wgs=wgs)  # persistent epilogue grid: workgroups per CU
             t_gemm = timed(lambda: C.gemm_f32(g, a, dw, False, False))
             t_sgd = timed(lambda: C.sgd_flat(p, dw.view(-1), b, 1e-6, 0.9, 0.0, 0.0, False, False,
                                              False, 1.0))
@@ -76,7 +76,7 @@ def main():
             out.append(rec)
             print(json.dumps(rec), flush=True)
     C.gemm_f32_set_override(0, 0, 0)
-    os.environ.pop("TDP_OPT_WGS", None)
+    C.gemm_f32_set_opt_variant(wgs=2)
     tdp.destroy_process_group()
 
 

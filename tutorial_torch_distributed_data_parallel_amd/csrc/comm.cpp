@@ -80,14 +80,9 @@ void Communicator::make_stream() {
   check_hip(hipSetDevice(device_), "hipSetDevice");
   // Highest priority for the comm stream: bucket all-reduces should not queue behind backward
   // GEMMs on the hardware queues (GPU_MAX_HW_QUEUES=4 per process on this pool).
-  // TDP_COMM_PRIORITY=normal selects a default-priority stream instead (measurement knob).
   int lo = 0, hi = 0;
   check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-  const char* pr = std::getenv("TDP_COMM_PRIORITY");
-  const bool normal = pr && std::string(pr) == "normal";
-  const bool blocking = pr && std::string(pr) == "blocking";
-  check_hip(hipStreamCreateWithPriority(&stream_, blocking ? hipStreamDefault : hipStreamNonBlocking,
-                                        (normal || blocking) ? lo : hi),
+  check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi),
             "hipStreamCreateWithPriority");
   // TDP_TIMEOUT_S (seconds) or TDP_TIMEOUT_MIN (minutes); torch's NCCL default is 10 minutes
   if (const char* t = std::getenv("TDP_TIMEOUT_S")) timeout_s_ = std::atof(t);

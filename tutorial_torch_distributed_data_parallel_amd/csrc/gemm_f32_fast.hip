@@ -1218,11 +1218,8 @@ void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
 // fp32 products on the bf16 matrix core (split3 emulation, see split3_pair) unless
 // TDP_GEMM_EMU=0 (or gemm_f32_set_emu(false)) selects the native v_mfma_f32_32x32x2_f32 path
 // same-box A/B (profiles/micro/gemm_emu_prio_ab_r4l.txt): toy MLP 0.4069 -> 0.3975 ms/step,
-// ResNet-50 35.57 -> 35.43; the isolated GEMMs do not move. TDP_GEMM_EMU_PRIO=0 turns it off.
-static const int o_emu_prio = [] {
-  const char* e = std::getenv("TDP_GEMM_EMU_PRIO");
-  return (e && e[0] == '0') ? 0 : 1;
-}();
+// ResNet-50 35.57 -> 35.43; the isolated GEMMs do not move.
+static constexpr int o_emu_prio = 1;
 bool o_emu = [] {
   const char* e = std::getenv("TDP_GEMM_EMU");
   return !(e && e[0] == '0');
@@ -1275,26 +1272,15 @@ bool gemm_f32_fast_ok(const GemmF32Args& a) {
 // FN=2 (32 KiB/stage) 2 stages.
 static int o_fn = 0, o_splits = 0, o_stages = 0;
 
-// Optimizer-epilogue variant knobs: TDP_OPT_VARIANT / TDP_OPT_ADAM_VARIANT / TDP_OPT_PERSIST /
-// TDP_OPT_WGS at first use, overridable at run time (gemm_f32_set_opt_variant) so one test
-// process can cover every variant.
+// Optimizer-epilogue variant (defaults: LDS-staged non-temporal epilogue on a persistent grid of
+// two workgroups per CU, profiles/opt_epilogue_variants.md), overridable at run time
+// (gemm_f32_set_opt_variant) so one test process can cover every variant.
 struct OptVariant {
   int sgd, adam, wgs;
   bool persist;
 };
 static OptVariant& opt_variant() {
-  static OptVariant v = [] {
-    OptVariant o;
-    const char* e = std::getenv("TDP_OPT_VARIANT");
-    o.sgd = e ? (std::atoi(e) & (kOptWide | kOptNT | kOptLds)) : (kOptLds | kOptNT);
-    e = std::getenv("TDP_OPT_ADAM_VARIANT");
-    o.adam = e ? (std::atoi(e) & (kOptNT | kOptLds)) : (kOptLds | kOptNT);
-    e = std::getenv("TDP_OPT_PERSIST");
-    o.persist = !(e && e[0] == '0');
-    e = std::getenv("TDP_OPT_WGS");
-    o.wgs = e ? std::atoi(e) : 2;
-    return o;
-  }();
+  static OptVariant v{kOptLds | kOptNT, kOptLds | kOptNT, 2, true};
   return v;
 }
 
@@ -1310,11 +1296,8 @@ void gemm_f32_set_override(int fn, int splits, int stages) {
   o_fn = fn; o_splits = splits; o_stages = stages;
 }
 // Row-vector (LDS-staged) output stores: 16-B aligned rows of C, bias and the workspace
-static bool o_no_cvec = std::getenv("TDP_GEMM_NO_CVEC") != nullptr;  // A/B measurements
-static int o_bm = [] {  // 0 auto, 128 / 256 forced (sweeps; TDP_GEMM_BM=256 from the environment)
-  const char* e = std::getenv("TDP_GEMM_BM");
-  return e ? ((std::atoi(e) == 256 || std::atoi(e) == 128) ? std::atoi(e) : 0) : 0;
-}();
+static bool o_no_cvec = false;  // gemm_f32_set_cvec(false): A/B measurements
+static int o_bm = 0;            // 0 auto, 128 / 256 forced (gemm_f32_set_bm: sweeps)
 void gemm_f32_set_emu(bool on) { o_emu = on; }
 bool gemm_f32_emu() { return o_emu; }
 void gemm_f32_set_bm(int bm) { o_bm = (bm == 128 || bm == 256) ? bm : 0; }
@@ -1330,8 +1313,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   // 128-wide tiles split the fewest fragments per MFMA; with split-bf16 products (VALU-heavy
   // per fragment) they win on the skinny-M GEMMs too (toy-MLP fc1 forward 84.5 -> 68.4 us,
   // fc2 forward 40.7 -> 38.4, fc2 input gradient 45.0 -> 39.6: profiles/micro/gemm_plan_sweep_emu_r4f.log)
-  static const bool skinny_fn1 = std::getenv("TDP_GEMM_SKINNY_FN1") != nullptr;  // A/B
-  int fn = (a.N >= 512 && (a.M >= 512 || (o_emu && !skinny_fn1))) ? 2 : 1;
+  int fn = (a.N >= 512 && (a.M >= 512 || o_emu)) ? 2 : 1;
   if (o_fn == 1 || o_fn == 2) fn = o_fn;
   const int bn = 64 * fn;
   const long tiles = (long)ceil_div(a.M, 128) * ceil_div(a.N, bn);
@@ -1347,7 +1329,8 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   plan.grid = 0;
   if (a.opt.kind != 0) {
-    // persistent: 2 workgroups per CU (TDP_OPT_WGS overrides, for measurements: 3 fit with FN=1)
+    // persistent: 2 workgroups per CU (gemm_f32_set_opt_variant overrides, for measurements:
+    // 3 fit with FN=1)
     const OptVariant& v = opt_variant();
     if (v.persist) plan.grid = (v.wgs >= 1 && v.wgs <= 4 ? v.wgs : 2) * num_cus;
   }

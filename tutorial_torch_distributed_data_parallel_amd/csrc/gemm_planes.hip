@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, l31 = lane & 31;
   // two workgroups share each SIMD running the same read / split / MFMA sequence; a static
-  // priority for every other hardware slot keeps them out of lockstep (TDP_PLANES_PRIO=0: off)
+  // priority for every other hardware slot keeps them out of lockstep
   if (p.prio && ((blockIdx.x >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
   // XCD-aware order (bijective): hardware ids b and b + 8 share an XCD; each XCD takes a
   // contiguous range of logical tiles, split-major, so an XCD's workgroups share A's K slices
@@ -596,28 +596,30 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
 inline bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 // variant: pipeline depth (2 stages: 80 KiB, two workgroups per CU; 3: 120 KiB, one) and the
-// B prefetch distance in tiles (0 = off; two stages only). TDP_PLANES_CFG = "S,PF"
-// (measurements). Default 3,0: one workgroup per CU halves the split-K count (8 for the toy
+// B prefetch distance in tiles (0 = off; two stages only), set by gemm_planes_set_cfg
+// (measurements; with a split-K override). Default 3,0: one workgroup per CU halves the split-K count (8 for the toy
 // MLP), hence the partial-sum traffic of the reduce; the captured toy-MLP step measured
 // 0.371-0.374 ms vs 0.383-0.386 with 2,0 (profiles/r6/bench_modes_r6j.txt). The B prefetch
 // measured nothing (the K loop is not HBM-latency bound: TDP_PLANES_EXP experiments,
 // profiles/r6/planes_gemm_experiments.md)
 struct PlanesCfg {
-  int stages, pf;
+  int stages, pf, splits;  // splits > 0: split-K override
 };
 PlanesCfg& planes_cfg() {
-  static PlanesCfg c = [] {
-    PlanesCfg v{3, 0};
-    if (const char* e = std::getenv("TDP_PLANES_CFG")) {
-      int a = 0, b = 0;
-      if (std::sscanf(e, "%d,%d", &a, &b) == 2 && (a == 2 || a == 3) && b >= 0 && b <= 4 &&
-          (a == 2 || b == 0))
-        v = {a, b};
-    }
-    return v;
-  }();
+  static PlanesCfg c{3, 0, 0};
   return c;
 }
+}  // namespace
+
+bool gemm_planes_set_cfg(int stages, int pf, int splits) {
+  if (!((stages == 2 || stages == 3) && pf >= 0 && pf <= 4 && (stages == 2 || pf == 0) &&
+        splits >= 0))
+    return false;
+  planes_cfg() = {stages, pf, splits};
+  return true;
+}
+
+namespace {
 
 template <bool BKC, int S, int PF>
 void launch_planes(const PParams& p, int nblocks, hipStream_t s) {
@@ -679,12 +681,8 @@ GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus) {
   // two workgroups per CU when both fit (2 stages), else one
   const long target = (cfg.stages == 2 ? 2L : 1L) * num_cus;
   int splits = 1;
-  static const int force = [] {  // TDP_PLANES_SPLITS: split-K override (measurements)
-    const char* e = std::getenv("TDP_PLANES_SPLITS");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (force > 0) {
-    splits = force;
+  if (cfg.splits > 0) {
+    splits = cfg.splits;
   } else if (tiles < target) {
     const int want = (int)((target + tiles - 1) / tiles);
     const int kmax = a.K / (kBK * 4);  // >= 4 K tiles per split
@@ -709,11 +707,7 @@ void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   p.op = a.out_planes; p.ops = a.out_ps;
   p.relu = a.relu ? 1 : 0;
   p.M = a.M; p.N = a.N; p.K = a.K;
-  static const int prio = [] {
-    const char* e = std::getenv("TDP_PLANES_PRIO");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  p.prio = prio;
+  p.prio = 1;
   p.kps = plan.k_per_split;
   p.splits = plan.splits;
   p.tiles_n = ceil_div(a.N, plan.bn);

@@ -62,7 +62,6 @@ struct AdamHyper {
 // the new step (kind 2), first-step flag from the host request, clip accumulators reset.
 void opt_step_begin(float* dev, int kind, hipStream_t s);
 // one-lane empty kernel on s (a graph node; see reducer.cpp pick_stream)
-void graph_fork_marker(hipStream_t s);
 // Global-norm clipping on the device: kHNorm = sqrt(kHSumsq) and
 // kHScale = min(1, kHMaxNorm / (kHNorm + 1e-6)) (torch.nn.utils.clip_grad_norm_ semantics).
 void clip_coef_from_sumsq(float* dev, hipStream_t s);

@@ -665,12 +665,8 @@ inline int ew_grid(long total) {
 int bn_splits(int N, int C, int HW, int num_cus) {
   if (HW == 1 && C % 4 == 0) {
     // rows4 reductions (1024-thread workgroups): one workgroup per CU, >= 8 row iterations per
-    // thread; TDP_BN_WG_PER_CU overrides the per-CU count (sweeps)
-    static const int per_cu = [] {
-      const char* e = std::getenv("TDP_BN_WG_PER_CU");
-      const int v = e ? std::atoi(e) : 1;
-      return v >= 1 && v <= 16 ? v : 1;
-    }();
+    // thread
+    constexpr int per_cu = 1;
     const int CB = C < 1024 ? C : 1024, RPW = kRedT / (CB / 4);
     const int nblk = rows4_nblk(C);
     long s = ((long)per_cu * num_cus + nblk - 1) / nblk;

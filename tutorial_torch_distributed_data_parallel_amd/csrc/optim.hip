@@ -193,9 +193,6 @@ __global__ void bf2f_kernel(const unsigned short* __restrict__ x, float* __restr
     y[i] = bf16_to_f32(x[i]);
 }
 
-// Empty kernel: a graph node the compute chain continues from (reducer.cpp pick_stream)
-__global__ void graph_fork_marker_kernel() {}
-
 // ---------------------------------------------------------------- device hyper block (kernels.h)
 __global__ void opt_step_begin_kernel(float* d, int kind) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -394,10 +391,6 @@ void bf16_to_f32_copy(const uint16_t* x, float* y, long n, hipStream_t s) {
   if (n > 0)
     hipLaunchKernelGGL(bf2f_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const unsigned short*)x,
                        y, n);
-}
-
-void graph_fork_marker(hipStream_t s) {
-  hipLaunchKernelGGL(graph_fork_marker_kernel, dim3(1), dim3(64), 0, s);
 }
 
 void opt_step_begin(float* dev, int kind, hipStream_t s) {

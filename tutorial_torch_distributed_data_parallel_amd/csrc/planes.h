@@ -29,6 +29,9 @@ struct GemmPlanesArgs {
 };
 bool gemm_planes_ok(const GemmPlanesArgs& a);
 GemmPlan gemm_planes_plan(const GemmPlanesArgs& a, int num_cus);
+// measurements: pipeline stages (2 | 3), B prefetch distance (2 stages only), split-K override
+// (0 = planned); returns false (and changes nothing) for an invalid combination
+bool gemm_planes_set_cfg(int stages, int pf, int splits);
 void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, hipStream_t s);
 // x [rows][cols] (row stride ldx, cols % 4 == 0) -> planes [3][rows][cols] (plane stride ps)
 void split_planes(const float* x, long ldx, int rows, int cols, uint16_t* planes, long ps,

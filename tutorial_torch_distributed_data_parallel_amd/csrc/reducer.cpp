@@ -321,17 +321,6 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
   } else {
     timing_ = false;
   }
-  const char* mode = std::getenv("TDP_COMM_STREAM");
-  const std::string m = mode ? mode : "auto";
-  const char* fm = std::getenv("TDP_GRAPH_FORK");
-  const std::string f = fm ? fm : "defer";
-  fork_mode_ = f == "marker" ? kForkMarker : f == "inline" ? kForkInline : kForkDefer;
-  stream_mode_ = m == "side" ? kStreamSide
-                 : m == "compute" ? kStreamCompute
-                 : m == "hostsync" ? kStreamHostSync
-                 : m == "hostjoin" ? kStreamHostJoin
-                 : m == "nojoin" ? kStreamNoJoin
-                                   : kStreamAuto;
 }
 
 SyncBackend::~SyncBackend() {
@@ -427,12 +416,11 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute, bool* defe
   // side stream costs 1.5-3x step time -- a hipStreamWaitEvent left pending on one hardware
   // queue while the host runs ahead slows every launch on the other queue. Inside a hipGraph the
   // same dependency is a graph edge and the collectives overlap backward. So: side stream while
-  // capturing, the compute stream itself otherwise (TDP_COMM_STREAM overrides for measurements).
+  // capturing, the compute stream itself otherwise.
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   check_hip(hipStreamIsCapturing(compute, &cap), "hipStreamIsCapturing");
   const bool capturing = cap == hipStreamCaptureStatusActive;
-  const bool side_wanted = stream_mode_ == kStreamAuto ? capturing : stream_mode_ != kStreamCompute;
-  bool side = side_wanted;
+  bool side = capturing;
   if (!side && launched_side_) side = true;  // never switch streams within one iteration
   hipStream_t cs = side ? ops_->comm_stream() : compute;
   if (side) {
@@ -442,15 +430,15 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute, bool* defe
     // HIP's replay puts the chain on a different stream at every fork and, after a few buckets,
     // on the collectives' hardware queue -- backward serialised behind an all-reduce (measured:
     // profiles/graph_fork_order_r3.md; consistent with the first child edge of a node inheriting
-    // its stream). Default: defer the side branch until the compute chain has its next node
-    // (issue / flush_forks); "marker" captures an empty kernel first instead (15 us per fork
-    // on the replay, profiles/r7/mlp_rehearsal_kernels_r7a.md).
-    if (capturing && fork_mode_ == kForkDefer) {
+    // its stream). So the side branch is deferred until the compute chain has its next node
+    // (issue / flush_forks). The round-3 form captured an empty marker kernel first instead
+    // (15 us per fork on the replay, profiles/r7/mlp_rehearsal_kernels_r7a.md; A/B against the
+    // deferred fork: profiles/r8/fork_form_ab_r8a.md).
+    if (capturing) {
       if (forks_.empty()) fork_deps_ = capture_frontier(compute);
       *deferred = true;
       return cs;
     }
-    if (capturing && fork_mode_ == kForkMarker) graph_fork_marker(compute);
     enter_side(bucket, cs);
     return cs;
   }
@@ -460,10 +448,7 @@ hipStream_t SyncBackend::pick_stream(int bucket, hipStream_t compute, bool* defe
 }
 
 void SyncBackend::enter_side(int bucket, hipStream_t cs) {
-  if (stream_mode_ == kStreamHostSync)
-    check_hip(hipEventSynchronize(ready_[bucket]), "hipEventSynchronize");
-  else
-    check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
+  check_hip(hipStreamWaitEvent(cs, ready_[bucket], 0), "hipStreamWaitEvent");
   if (!launched_any_ && timing_) check_hip(hipEventRecord(t0_, cs), "hipEventRecord");
   launched_any_ = true;
 }
@@ -653,13 +638,8 @@ void SyncBackend::wait_all(hipStream_t compute) {
       check_hip(hipEventRecord(t1_, cs), "hipEventRecord");
       timed_pending_ = true;
     }
-    if (stream_mode_ == kStreamHostJoin) {
-      check_hip(hipEventRecord(done_, cs), "hipEventRecord");
-      check_hip(hipEventSynchronize(done_), "hipEventSynchronize");
-    } else if (stream_mode_ != kStreamNoJoin) {
-      check_hip(hipEventRecord(done_, cs), "hipEventRecord");
-      check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
-    }
+    check_hip(hipEventRecord(done_, cs), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(compute, done_, 0), "hipStreamWaitEvent");
   }
   launched_any_ = false;
   // 2. work that needed the whole backward, on the compute stream

@@ -291,17 +291,6 @@ class SyncBackend : public ReducerBackend {
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;
-  // where bucket collectives run: auto = side stream only while capturing a hipGraph;
-  // hostjoin: side stream, end-of-backward join by a host wait; nojoin: no join (measurement)
-  enum {
-    kStreamAuto = 0, kStreamSide = 1, kStreamCompute = 2, kStreamHostSync = 3,
-    kStreamHostJoin = 4, kStreamNoJoin = 5
-  };
-  int stream_mode_ = kStreamAuto;
-  // captured fork form (TDP_GRAPH_FORK, A/B only): defer (default) | marker (an empty kernel on
-  // the compute stream before each fork, the round-3 form) | inline (fork captured first)
-  enum { kForkDefer = 0, kForkMarker = 1, kForkInline = 2 };
-  int fork_mode_ = kForkDefer;
 };
 
 class Reducer {

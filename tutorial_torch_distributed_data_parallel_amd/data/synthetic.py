@@ -10,7 +10,6 @@ model can actually learn (loss curves are meaningful in tests).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -105,8 +104,8 @@ class EpochCursor:
     def __init__(self, capacity: int, batch: int, device):
         self.order = torch.zeros(capacity, dtype=torch.long, device=device)
         # {position, arrivals, per-row slice arrivals [batch]} (all re-armed by the kernel); the
-        # per-row counters let several workgroups share a row (TDP_CURSOR_ROWS=0: one per row)
-        rows = 0 if os.environ.get("TDP_CURSOR_ROWS") == "0" else int(batch)
+        # per-row counters let several workgroups share a row
+        rows = int(batch)
         self.state = torch.zeros(2 + rows, dtype=torch.long, device=device)
         self.batch = int(batch)
 

@@ -16,7 +16,6 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-import os
 
 from .._native import native
 from ._grad import (bias_epilogue, epilogue_target, factor_target, grad_dest, hand_off, needs,
@@ -24,8 +23,8 @@ from ._grad import (bias_epilogue, epilogue_target, factor_target, grad_dest, ha
 
 # Skinny GEMMs (batch rows against thousands of features) read their activation operand from
 # its exact bf16 split planes (csrc/gemm_planes.hip): split once by the producer instead of once
-# per column tile inside the GEMM. TDP_PLANES=0 keeps the in-kernel split (A/B measurements).
-_PLANES = os.environ.get("TDP_PLANES", "1") != "0"
+# per column tile inside the GEMM (set_planes(False) keeps the in-kernel split: A/B measurements).
+_PLANES = True
 
 
 def planes_fit(M: int, N: int, K: int) -> bool:
@@ -33,8 +32,6 @@ def planes_fit(M: int, N: int, K: int) -> bool:
     return _PLANES and M <= 256 and K % 32 == 0 and K >= 256 and N % 4 == 0 and N >= 512
 
 
-# one-launch head backward (TDP_HEAD_FUSED=0: the skinny_k + skinny_m pair, for A/B)
-_HEAD_FUSED = os.environ.get("TDP_HEAD_FUSED", "1") != "0"
 
 
 def planes_input_fit(M: int, K: int) -> bool:
@@ -128,8 +125,7 @@ class _LinearFn(torch.autograd.Function):
         g = C.relu_bias_bwd(dy, y) if ctx.relu and not _pregated(dy, y) else dy
         fac = factor_target(w_param) if needs(ctx, 1) else None
         epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
-        if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16 and \
-                _HEAD_FUSED:
+        if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16:
             # classifier head (out <= 16): input gradient (gated, + its planes for the next skinny
             # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd). At
             # world size 1 with the fused optimizer the same kernel also applies the SGD / Adam

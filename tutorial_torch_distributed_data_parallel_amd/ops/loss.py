@@ -6,7 +6,6 @@ forward kernel, which is how the training/eval loops keep the reference's per-ep
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -17,7 +16,7 @@ from .._native import native
 # small heads (the toy MLP's / AlexNet's 128 x 10): the forward kernel also writes the gradient
 # for an upstream gradient of 1, so a backward seeded with the cached unit seed (seed_grad /
 # backward below; autograd hands the seed tensor itself to this node) launches nothing
-_FUSED_GRAD_MAX = 0 if os.environ.get("TDP_CE_FUSED_GRAD") == "0" else 1 << 16  # 0: A/B off
+_FUSED_GRAD_MAX = 1 << 16
 
 
 class _CrossEntropyFn(torch.autograd.Function):

@@ -11,7 +11,6 @@ multi-process tests exercise.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -96,7 +95,6 @@ class _TorchKernels:
 _TORCH_K = _TorchKernels()
 
 
-_MASK = os.environ.get("TDP_BN_MASK", "1") != "0"  # A/B: 0 = the backward reads the float output
 
 
 def _is_nhwc(x) -> bool:
@@ -140,7 +138,7 @@ class _BatchNormFn(torch.autograd.Function):
         # instead of the float output (1/16 of the bytes, twice per backward)
         mask = None
         rows4 = x.is_cuda and x.dim() == 2 and C % 4 == 0
-        if relu and rows4 and _MASK:
+        if relu and rows4:
             mask = torch.empty((x.shape[0], C // 4), dtype=torch.uint8, device=x.device)
         # a BatchNorm1d output feeding a skinny Linear: its bf16 split planes from the same pass
         pl = None
