@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 4: same-box stock comparisons for the BASELINE.md table at 1 GPU (the multi-GPU rows are
+# the driver's): toy MLP + SyncBatchNorm, toy MLP via Accelerator.prepare, Adam, ResNet-50,
+# AlexNet -- tdp and stock torch DDP + torch.optim interleaved.
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r8d; export TMPDIR=/tmp
+fatal() { case "$1" in 0) ;; *) echo "fatal rc=$1 in $2"; exit "$1";; esac; }
+ms() { python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["ms_per_step"], d["value"], d["config"].get("final_loss"))' $1; }
+run() {  # name, timeout, args...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t python bench.py --no-diag "$@" > gpurun_out/r8d/$n.json 2> gpurun_out/r8d/$n.err; fatal $? $n
+  echo "$n $(ms gpurun_out/r8d/$n.json)"
+}
+run mlp_syncbn_tdp 300 --syncbn
+run mlp_syncbn_torch 300 --syncbn --impl torch
+run mlp_accel_tdp 300 --api accelerate
+run mlp_accel_torch 300 --api accelerate --impl torch
+run mlp_adam_tdp 300 --optim adam
+run mlp_adam_torch 300 --optim adam --impl torch
+run r50_tdp 400 --model resnet50 --steps 20 --warmup 5
+run r50_torch 400 --model resnet50 --steps 20 --warmup 5 --impl torch
+run alexnet_tdp 300 --model alexnet --steps 20 --warmup 5
+run alexnet_torch 300 --model alexnet --steps 20 --warmup 5 --impl torch
+echo done
