@@ -20,4 +20,6 @@ run r50_tdp 400 --model resnet50 --steps 20 --warmup 5
 run r50_torch 400 --model resnet50 --steps 20 --warmup 5 --impl torch
 run alexnet_tdp 300 --model alexnet --steps 20 --warmup 5
 run alexnet_torch 300 --model alexnet --steps 20 --warmup 5 --impl torch
+timeout -k 10 240 python scripts/diag_adam_capture.py --runs 6 > gpurun_out/r8d/diag_adam_capture.jsonl 2>gpurun_out/r8d/diag_adam_capture.err; fatal $? diag_adam
+python3 -c "import json; [print(r['seed'], r['fused'], r['loss_max_diff'], {k: (v['max'], v['n_over_1e-5']) for k, v in r['params'].items() if v['max'] > 0}) for r in map(json.loads, open('gpurun_out/r8d/diag_adam_capture.jsonl'))]"
 echo done
