@@ -14,6 +14,7 @@ from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import (
 
 import peer_workers as PW  # noqa: E402  (tests/ is on sys.path via conftest)
 import relay_workers as RW  # noqa: E402
+from test_relay_gpu import _check_tuning_applied  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -90,3 +91,6 @@ def test_bench_self_launch_peer_captured():
     assert sync["backend"] == "peer" and sync["captured"] is True, sync
     assert sync["replicas_identical"] is True, sync
     assert sync["modes"]["fc1.weight"].startswith("factored"), sync
+    tun = sync["factor_tuning"]
+    assert tun["captured"] is True and set(tun["chosen"]) == {"fc1.weight", "fc2.weight"}, tun
+    _check_tuning_applied(sync)

@@ -67,6 +67,17 @@ def test_bench_world2_record(tmp_path):
     assert set(chosen) == {"fc1.weight", "fc2.weight"}, sync  # a choice per factored weight
     assert set(chosen.values()) <= {"replicated", "sharded", "split"}, sync
     assert len(sync["factor_tuning"]["timings_ms"]) == 9, sync  # 2 weights x 3 modes
+    _check_tuning_applied(sync)
+
+
+def _check_tuning_applied(sync):
+    """The tuned choice per weight (keyed by name) is the mode the timed steps ran."""
+    for name, c in sync["factor_tuning"]["chosen"].items():
+        mode = sync["modes"][name]
+        if c == "split":  # a split that rounds to no / all rows runs as a pure mode
+            assert mode.startswith("factored"), (name, c, sync)
+        else:
+            assert mode == "factored-" + c, (name, c, sync)
 
 
 def _port():

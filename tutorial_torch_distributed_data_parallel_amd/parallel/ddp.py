@@ -922,20 +922,30 @@ class DistributedDataParallel(nn.Module):
         rows = o - W * q
         return o if q == 0 else rows
 
+    def _param_name(self, p) -> str:
+        """Module name of parameter ``p`` (the arena keeps the Parameter objects across a
+        rebuild, so the map by identity stays valid)."""
+        names = getattr(self, "_names_by_id", None)
+        if names is None or id(p) not in names:
+            names = {id(q): n for n, q in self.module.named_parameters()}
+            self._names_by_id = names
+        return names.get(id(p), f"param{self.arena.params.index(p)}")
+
     def _rep_rows_for(self, i, cap) -> int:
         """How many rows of factored weight ``i`` every rank computes itself: all of them
         (replicated), none (sharded) or a share (split: parallel/commmodel.py
         "factored-split"). An explicit ``factor_replicate`` (True / False / "split" / a fraction,
-        or {arena index: one of these}: tune_factor_replicate's result) decides, else the step
-        model with the measured all-gather bandwidth, else the fallback rule. Identical on every
-        rank (agreed inputs only). The CPU twin knows replicated and sharded only."""
+        or {parameter name: one of these}: tune_factor_replicate's result; names, not arena
+        indices, because a bucket rebuild re-orders the arena) decides, else the step model with
+        the measured all-gather bandwidth, else the fallback rule. Identical on every rank
+        (agreed inputs only). The CPU twin knows replicated and sharded only."""
         o, n, _ = self._factor[i]
         W = self.world_size
         if W == 1:
             return o
         rep = self.factor_replicate
         if isinstance(rep, dict):
-            rep = rep.get(i)
+            rep = rep.get(self._param_name(self.arena.params[i]))
         if rep is True or rep is False:
             return o if rep else 0
         from . import commmodel as cm
@@ -964,9 +974,10 @@ class DistributedDataParallel(nn.Module):
 
     def tune_factor_replicate(self, step_fn, iters: int = 3, capture: bool = False):
         """Measure, don't guess: time ``step_fn`` (one full training step) under every
-        replicated / sharded combination of the factored weights (each weight on its own: up to
-        three weights, 2^k combinations; more: all-replicated vs all-sharded), take the max over
-        ranks, keep the fastest, record the timings in ``factor_tuning``. ``capture=True`` times
+        replicated / sharded / split combination of the factored weights (each weight on its
+        own: up to two weights, 3^k combinations; more: the three uniform plans), take the max
+        over ranks, keep the fastest (``factor_replicate`` = {parameter name: choice}), record
+        the timings in ``factor_tuning``. ``capture=True`` times
         the step as it will run -- captured into a hipGraph and replayed, collectives on the side
         stream overlapping backward -- instead of eagerly (collectives then serialise on the
         compute stream and the comparison is skewed: VERDICT r3 weak 2). Every rank must call it
@@ -981,18 +992,25 @@ class DistributedDataParallel(nn.Module):
             return None
         from ..train.graph import CapturedStep, try_capture
 
-        idx = sorted(self._factor)
+        # one eager step first, then any pending bucket rebuild: every combination is then timed
+        # in the final arena layout (a rebuild inside the first one would skew its time)
+        step_fn()
+        self.settle()
+        # by NAME: arena indices move with a rebuild
+        names = [self._param_name(self.arena.params[i]) for i in sorted(self._factor)]
         choices = (True, False, "split")
-        combos = list(itertools.product(choices, repeat=len(idx))) if len(idx) <= 2 \
-            else [(c,) * len(idx) for c in choices]
+        combos = list(itertools.product(choices, repeat=len(names))) if len(names) <= 2 \
+            else [(c,) * len(names) for c in choices]
         ms = []
+        captured = bool(capture)
         for combo in combos:
             self.consolidate_optimizer_state()
-            self.factor_replicate = dict(zip(idx, combo))
+            self.factor_replicate = dict(zip(names, combo))
             run = step_fn
             step_fn()  # one eager step in this mode (sizes its buffers)
             if capture:
                 run = try_capture(step_fn, warmup=1, log=lambda m: None)
+                captured = captured and isinstance(run, CapturedStep)
             rt.barrier()
             t0 = time.perf_counter()
             for _ in range(iters):
@@ -1006,20 +1024,18 @@ class DistributedDataParallel(nn.Module):
         ms = [float(v) for v in t.tolist()]
         best = min(range(len(combos)), key=lambda k: ms[k])
         self.consolidate_optimizer_state()
-        self.factor_replicate = dict(zip(idx, combos[best]))
-        names = {id(p): n for n, p in self.module.named_parameters()}
+        self.factor_replicate = dict(zip(names, combos[best]))
 
         def label(combo):
-            return {names.get(id(self.arena.params[i]), f"param{i}"):
-                    ("replicated" if c is True else "sharded" if c is False else "split")
-                    for i, c in zip(idx, combo)}
+            return {n: ("replicated" if c is True else "sharded" if c is False else "split")
+                    for n, c in zip(names, combo)}
         self.factor_tuning = {
-            "captured": bool(capture),
+            "captured": captured,  # every combination timed as a replayed hipGraph
             "timings_ms": [{"modes": label(c), "ms": round(m, 4)} for c, m in zip(combos, ms)],
             "chosen": label(combos[best]),
             # the round-3 record's keys: all-replicated / all-sharded times
-            "replicated_ms": round(ms[combos.index((True,) * len(idx))], 4),
-            "sharded_ms": round(ms[combos.index((False,) * len(idx))], 4),
+            "replicated_ms": round(ms[combos.index((True,) * len(names))], 4),
+            "sharded_ms": round(ms[combos.index((False,) * len(names))], 4),
         }
         return self.factor_replicate
 
