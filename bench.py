@@ -635,7 +635,7 @@ def main():
                 x, y = gather_batch(data.x, data.y, cur["b"])
                 return body(x, y)
             if graph:
-                ddp.tune_factor_replicate(tdp_step, iters=5, capture=True)
+                ddp.tune_factor_replicate(tdp_step, iters=10, capture=True)
             else:
                 ddp.tune_factor_replicate(eager_step, iters=3)
         if graph:
