@@ -64,3 +64,20 @@ def test_table_rows():
     rows = cm.table((2, 8))
     assert len(rows) == 2 * (len(cm.MODES) + 1)
     assert all(r["step_us"] >= r["exposed_us"] >= 0 for r in rows)
+
+
+def test_cnn_bucket_model_resnet50():
+    """BASELINE config 5: ResNet-50's bucketed gradient sync hides behind its 22 ms backward
+    except the last bucket (the stem / layer1 gradients arrive last); a smaller bucket cap
+    shrinks that tail on xGMI (docs/COMM_MODEL.md)."""
+    fwd, grads = cm.cnn_grads("resnet50")
+    assert len(grads) == 161 and sum(g.numel for g in grads) == 23_528_522
+    t = cm.CNN_DP1_MS["resnet50"]
+    assert abs(sum(g.bwd_us for g in grads) - 1e3 * (2 * t["gemm"] / 3 + t["bn_bwd"])) < 1.0
+    assert grads[0].name.startswith("fc.") and grads[-1].name in ("conv1.weight", "bn1.weight")
+    hw = cm.Hardware()
+    exp = {cap: cm.simulate_buckets(fwd, grads, 2, hw, cap_mb=cap)["exposed_us"]
+           for cap in (4, 25, 64, 1024)}
+    assert exp[4] <= exp[25] <= exp[64] <= exp[1024] and exp[1024] > 1000.0, exp
+    r8 = cm.simulate_buckets(fwd, grads, 8, hw)  # the default plan: 1 MiB first, 25 MiB
+    assert r8["exposed_us"] < 0.01 * r8["compute_us"], r8

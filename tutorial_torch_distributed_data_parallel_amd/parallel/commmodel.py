@@ -194,6 +194,111 @@ def best_plan(layers: list[Layer], W: int, B: int, hw: Hardware,
     return best
 
 
+# ----------------------------------------------------------------------------- CNN buckets
+# BASELINE config 5 ("ResNet-50-sized CNN DDP 8x: stresses grad-bucket all-reduce overlap"): the
+# convolution weights are not factored (their gradient is not low-rank in a useful way), so they
+# go through the bucket path -- per bucket a reduce-scatter, the 1/W optimizer update and the
+# parameter all-gather on the side stream while backward continues (reducer.cpp SyncBackend).
+
+# dp1 kernel times (ms per step, B = 128, 224 x 224) the per-layer backward times are scaled to:
+# GEMM / convolution forward and backward, BatchNorm backward passes
+# (profiles/resnet50_dp1_b128_r4e.md, profiles/alexnet_dp1_b128_r4e.md)
+CNN_DP1_MS = {"resnet50": {"gemm": 23.5, "bn_bwd": 6.1, "fwd_other": 5.0},
+              "alexnet": {"gemm": 4.0, "bn_bwd": 0.0, "fwd_other": 0.3}}
+
+
+@dataclass
+class Grad:
+    name: str
+    numel: int
+    bwd_us: float      # backward compute that ends with this gradient ready (its layer's share)
+
+
+def cnn_grads(model: str = "resnet50", image: int = 224, times: dict | None = None):
+    """(forward us, [Grad] in backward order) for a tdp CNN (models/registry.py): the module
+    order of one forward (hooks), per-layer backward time in proportion to 2 x its forward FLOPs
+    (convolutions / Linear: input + weight gradient) or to its output size (BatchNorm), scaled to
+    the model's measured dp1 kernel times (CNN_DP1_MS). Runs a B = 1 forward on the CPU."""
+    import torch
+
+    from .. import nn as tnn
+    from ..models.registry import build_model
+
+    t = dict(CNN_DP1_MS[model], **(times or {}))
+    m = build_model(model, device="cpu")
+    rec = []
+
+    def hook(mod, inp, out):
+        w = getattr(mod, "weight", None)
+        if isinstance(mod, (tnn.Conv2d, tnn.Linear)):
+            flops = 2.0 * out.numel() * (w.numel() // w.shape[0])
+            rec.append((mod, "gemm", flops))
+        else:
+            rec.append((mod, "bn", float(out.numel())))
+    for mod in m.modules():
+        if isinstance(mod, (tnn.Conv2d, tnn.Linear)) or "BatchNorm" in type(mod).__name__:
+            mod.register_forward_hook(hook)
+            if hasattr(mod, "relu_join"):  # bn3's fused residual join bypasses forward()
+                def joined(*args, _f=mod.relu_join, _m=mod, **kw):
+                    y = _f(*args, **kw)
+                    hook(_m, args, y)
+                    return y
+                mod.relu_join = joined
+    with torch.no_grad():
+        m(torch.randn(1, 3, image, image))
+    gemm_tot = sum(c for _, k, c in rec if k == "gemm") or 1.0
+    bn_tot = sum(c for _, k, c in rec if k == "bn") or 1.0
+    # forward = a third of the GEMM time + the rest of the forward passes; backward = the other
+    # two thirds + the BN backward passes
+    fwd_us = 1e3 * (t["gemm"] / 3.0 + t["fwd_other"])
+    names = {id(p): n for n, p in m.named_parameters()}
+    out = []
+    for mod, kind, c in reversed(rec):
+        us = 1e3 * (2.0 * t["gemm"] / 3.0 * c / gemm_tot if kind == "gemm"
+                    else t["bn_bwd"] * c / bn_tot)
+        ps = [p for p in (getattr(mod, "bias", None), getattr(mod, "weight", None))
+              if isinstance(p, torch.nn.Parameter)]
+        for j, p in enumerate(ps):  # the layer's time ends with its last gradient
+            out.append(Grad(names[id(p)], p.numel(), us if j == len(ps) - 1 else 0.0))
+    return fwd_us, out
+
+
+def simulate_buckets(fwd_us: float, grads: list, W: int, hw: Hardware, first_mb: float = 1.0,
+                     cap_mb: float = 25.0, mode: str = "sharded") -> dict:
+    """Predicted captured CNN step at W ranks with the bucket plan (first bucket ``first_mb``,
+    then ``cap_mb``; reducer.cpp compute_bucket_bounds): each bucket's collectives (``sharded``:
+    reduce-scatter + all-gather around the 1/W update; ``allreduce``: one all-reduce + the full
+    update) start on the side stream once its last gradient is ready and the side stream is
+    free. ``exposed_us`` = step - (forward + backward + the one-rank update)."""
+    buckets, cur, cur_b, lim = [], [], 0.0, first_mb
+    for g in grads:
+        cur.append(g)
+        cur_b += 4.0 * g.numel
+        if cur_b >= lim * 2 ** 20:
+            buckets.append(cur)
+            cur, cur_b, lim = [], 0.0, cap_mb
+    if cur:
+        buckets.append(cur)
+    tc, ts = fwd_us, 0.0
+    upd_alone = 16.0 * sum(g.numel for g in grads) / (hw.hbm_TBps * 1e6)
+    for bk in buckets:
+        tc += sum(g.bwd_us for g in bk)
+        nbytes = 4.0 * sum(g.numel for g in bk)
+        if mode == "allreduce":
+            comm = _coll_us(hw, "all_reduce", W, nbytes)
+            upd = 16.0 * nbytes / 4.0 / (hw.hbm_TBps * 1e6)
+        else:
+            comm = _coll_us(hw, "reduce_scatter", W, nbytes) + _coll_us(hw, "all_gather", W, nbytes)
+            upd = 16.0 * nbytes / 4.0 / W / (hw.hbm_TBps * 1e6)
+        ts = max(ts, tc) + comm + upd
+    step = max(tc, ts)
+    alone = tc + upd_alone
+    return {"W": W, "buckets": len(buckets), "first_mb": first_mb, "cap_mb": cap_mb,
+            "mode": mode, "compute_us": round(alone, 1), "step_us": round(step, 1),
+            "exposed_us": round(max(0.0, step - alone), 1),
+            "last_bucket_mb": round(4.0 * sum(g.numel for g in buckets[-1]) / 2 ** 20, 2)}
+
+
 def table(W_list=(2, 4, 8), B: int = 128, hw: Hardware | None = None) -> list[dict]:
     """Rows for docs/COMM_MODEL.md: every uniform mode and the best per-weight plan per W."""
     hw = hw or Hardware()
