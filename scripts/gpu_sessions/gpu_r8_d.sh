@@ -10,6 +10,12 @@ run() {  # name, timeout, args...
   timeout -k 10 $t python bench.py --no-diag "$@" > gpurun_out/r8d/$n.json 2> gpurun_out/r8d/$n.err; fatal $? $n
   echo "$n $(ms gpurun_out/r8d/$n.json)"
 }
+# SGD epilogue: default (24 = LDS + non-temporal) vs 28 (+ one batch per tile), interleaved
+timeout -k 10 200 python -u -m pytest tests/test_sync_gpu.py -x -q --timeout 120 --timeout-method thread -k "epilogue_variants and 28" > gpurun_out/r8d/variant28_test.log 2>&1; fatal $? variant28_test; tail -1 gpurun_out/r8d/variant28_test.log
+for r in 1 2 3; do
+for v in 24 28; do
+timeout -k 10 300 python scripts/run_with_variant.py --sgd $v -- bench.py --no-diag > gpurun_out/r8d/epi_v${v}_r$r.json 2>gpurun_out/r8d/epi_v${v}_r$r.err; fatal $? epi_$v; echo "epilogue variant $v r$r $(ms gpurun_out/r8d/epi_v${v}_r$r.json)"
+done; done
 run mlp_syncbn_tdp 300 --syncbn
 run mlp_syncbn_torch 300 --syncbn --impl torch
 run mlp_accel_tdp 300 --api accelerate

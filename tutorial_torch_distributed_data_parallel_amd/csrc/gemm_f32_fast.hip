@@ -772,7 +772,9 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
       __syncthreads();
       constexpr int C4 = BN / 4;                  // float4 per tile row
       constexpr int IT = BM * C4 / kT;            // float4 per thread (16)
-      constexpr int HB = 8;                       // float4 per batch (one HBM round trip)
+      // float4 per batch (one HBM round trip); kOptWide: the whole tile's p / momentum loads in
+      // flight at once (128 VGPRs: the K loop's fragments are dead here)
+      constexpr int HB = (OPTK & kOptWide) != 0 ? IT : 8;
 #pragma unroll
       for (int i0 = 0; i0 < IT; i0 += HB) {
         int gi[HB];
@@ -1373,19 +1375,23 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
   if (opt) {
     const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
-    // TDP_OPT_VARIANT: SGD epilogue variant flags (kOptWide | kOptNT | kOptLds). Default
-    // kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four 0.498), kOptLds alone 0.468,
-    // kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure; profiles/opt_epilogue_variants.md).
+    // SGD epilogue variant flags (kOptWide | kOptNT | kOptLds, gemm_f32_set_opt_variant).
+    // Default kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four 0.498), kOptLds
+    // alone 0.468, kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure;
+    // profiles/opt_epilogue_variants.md). With kOptLds, kOptWide = one batch per tile.
     // Non-128-wide tiles ignore kOptLds.
     const int variant = opt_variant().sgd;
-    // TDP_OPT_ADAM_VARIANT: Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam
-    // 0.555 ms/step vs 0.566 LDS only, 0.594 register epilogue (profiles/opt_epilogue_variants.md)
+    // Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam 0.555 ms/step vs 0.566
+    // LDS only, 0.594 register epilogue (profiles/opt_epilogue_variants.md)
     const int adam_variant = opt_variant().adam;
     if (a.opt.kind == 1) {
       switch (variant) {
         case kOptLds: launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds>(p, fn, st, nb, s); break;
         case kOptLds | kOptNT:
           launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT>(p, fn, st, nb, s);
+          break;
+        case kOptLds | kOptNT | kOptWide:
+          launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT | kOptWide>(p, fn, st, nb, s);
           break;
         case kOptWide: launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide>(p, fn, st, nb, s); break;
         case kOptNT: launch_kinds<kDenseMN, kDenseMN, 1 | kOptNT>(p, fn, st, nb, s); break;
