@@ -16,6 +16,10 @@ for r in 1 2 3; do
 for v in 24 28; do
 timeout -k 10 300 python scripts/run_with_variant.py --sgd $v -- bench.py --no-diag > gpurun_out/r8d/epi_v${v}_r$r.json 2>gpurun_out/r8d/epi_v${v}_r$r.err; fatal $? epi_$v; echo "epilogue variant $v r$r $(ms gpurun_out/r8d/epi_v${v}_r$r.json)"
 done; done
+for r in 1 2; do
+for v in 24 28; do
+timeout -k 10 300 python scripts/run_with_variant.py --adam $v -- bench.py --no-diag --optim adam > gpurun_out/r8d/adam_v${v}_r$r.json 2>gpurun_out/r8d/adam_v${v}_r$r.err; fatal $? adam_$v; echo "adam epilogue variant $v r$r $(ms gpurun_out/r8d/adam_v${v}_r$r.json)"
+done; done
 run mlp_syncbn_tdp 300 --syncbn
 run mlp_syncbn_torch 300 --syncbn --impl torch
 run mlp_accel_tdp 300 --api accelerate

@@ -63,7 +63,7 @@ def _reference(kind, init, batches, lr_change_at):
 
 
 SGD_VARIANTS = [(v, persist) for v in (0, 4, 8, 12, 16, 24, 28) for persist in (1, 0)]
-ADAM_VARIANTS = [(v, persist) for v in (0, 16, 24) for persist in (1, 0)]
+ADAM_VARIANTS = [(v, persist) for v in (0, 16, 24, 28) for persist in (1, 0)]
 
 
 @pytest.mark.parametrize("kind,variant,persist",

@@ -151,7 +151,7 @@ __device__ __forceinline__ f32x16 mfma_emu6(const bf8& ah, const bf8& am, const 
 }
 
 // optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
-constexpr int kOptWide = 4;  // SGD with paired columns: one batch covers both row tiles
+constexpr int kOptWide = 4;  // wider HBM batches: register SGD both row tiles, LDS paths 2x loads
 constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
 constexpr int kOptLds = 16;  // 128-wide paired tiles: gradient tile staged through LDS,
                              // float4 p / optimizer-state traffic (SGD and Adam)
@@ -834,7 +834,7 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
       __syncthreads();
       constexpr int C4 = BN / 4;
       constexpr int IT = BM * C4 / kT;
-      constexpr int HB = 4;
+      constexpr int HB = (OPTK & kOptWide) != 0 ? 8 : 4;  // kOptWide: twice the loads in flight
 #pragma unroll
       for (int i0 = 0; i0 < IT; i0 += HB) {
         int gi[HB];
@@ -1289,7 +1289,7 @@ static OptVariant& opt_variant() {
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs) {
   OptVariant& v = opt_variant();
   if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds);
-  if (adam >= 0) v.adam = adam & (kOptNT | kOptLds);
+  if (adam >= 0) v.adam = adam & (kOptWide | kOptNT | kOptLds);
   if (persist >= 0) v.persist = persist != 0;
   if (wgs > 0) v.wgs = wgs;
   return {v.sgd, v.adam, v.persist ? 1 : 0, v.wgs};
@@ -1402,6 +1402,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
       }
     } else if (adam_variant == (kOptLds | kOptNT)) {
       launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT>(p, fn, st, nb, s);
+    } else if (adam_variant == (kOptLds | kOptNT | kOptWide)) {
+      launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT | kOptWide>(p, fn, st, nb, s);
     } else if (adam_variant == kOptLds) {
       launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds>(p, fn, st, nb, s);
     } else {
