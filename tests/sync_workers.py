@@ -318,6 +318,8 @@ def factored_parity(rank, out_dir, kind="sgd", replicate=False, steps=5):
     model = ToyMLP(**FACTOR_DIMS)
     ref = copy.deepcopy(model)
     ddp = tdp.DDP(model, factor_sync=True)
+    if replicate == "mixed":  # per weight, by parameter name (survives the bucket rebuild)
+        replicate = {"fc1.weight": True, "fc2.weight": False}
     ddp.factor_replicate = replicate
     opt, ropt = _make_opts(kind, ddp.parameters(), ref.parameters(), 0.05 if kind == "sgd"
                            else 1e-2)
@@ -336,8 +338,10 @@ def factored_parity(rank, out_dir, kind="sgd", replicate=False, steps=5):
         F.cross_entropy(rddp(x), y).backward()
         ropt.step()
         plan = ddp.sync_plan()
-        want = "factored-replicated" if replicate else "factored-sharded"
-        assert [plan[n] for n in ("fc1.weight", "fc2.weight")] == [want, want], plan
+        for n in ("fc1.weight", "fc2.weight"):
+            rep = replicate.get(n) if isinstance(replicate, dict) else replicate
+            want = "factored-replicated" if rep else "factored-sharded"
+            assert plan[n] == want, (n, plan)
         assert plan["fc1.bias"] == "factored-bias" and plan["fc3.weight"] == "sharded", plan
     assert set(ddp._factor_cap.values()) == {4}, ddp._factor_cap
     _check_close(model, ref, f"factored {kind} replicate={replicate} W={W}", atol=3e-5)

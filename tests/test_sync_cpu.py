@@ -64,7 +64,7 @@ def test_bucket_rebuild_from_ready_order(tmp_path, fused):
 
 @pytest.mark.parametrize("world,kind,replicate", [
     (2, "sgd", True), (2, "adam", False), (3, "sgd", False), (3, "adam", True),
-    (4, "sgd", False), (4, "adam", True)])
+    (4, "sgd", False), (4, "adam", True), (3, "sgd", "mixed")])
 def test_factored_sync_matches_torch_ddp(tmp_path, world, kind, replicate):
     run(SW.factored_parity, tmp_path, n=world, kind=kind, replicate=replicate)
 

@@ -929,7 +929,10 @@ class DistributedDataParallel(nn.Module):
         if names is None or id(p) not in names:
             names = {id(q): n for n, q in self.module.named_parameters()}
             self._names_by_id = names
-        return names.get(id(p), f"param{self.arena.params.index(p)}")
+        n = names.get(id(p))
+        if n is None:
+            n = "param%d" % next(k for k, q in enumerate(self.arena.params) if q is p)
+        return n
 
     def _rep_rows_for(self, i, cap) -> int:
         """How many rows of factored weight ``i`` every rank computes itself: all of them
