@@ -484,3 +484,48 @@ def rebuild_moves_shards(rank, out_dir, kind="sgd"):
     _check_replicas(model)
     rddp = None  # noqa: F841
     _teardown()
+
+
+def factored_tuning(rank, out_dir, steps_after=2):
+    """DDP.tune_factor_replicate on the CPU twin: every replicated / sharded combination of the
+    two factored weights timed on real training steps (max over ranks), the choice recorded
+    by parameter NAME and applied (it survives the bucket rebuild the first step triggers);
+    every tuning step is a real step, so the model still matches torch DDP run over the same
+    batches, and the replicas stay identical."""
+    tdp.init_process_group("gloo")
+    r, W = rt.get_rank(), rt.get_world_size()
+    torch.manual_seed(0)
+    model = ToyMLP(**FACTOR_DIMS)
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, factor_sync=True)
+    opt, ropt = _make_opts("sgd", ddp.parameters(), ref.parameters(), 0.05)
+    assert ddp.register_fused_optimizer(opt)
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    k = [0]
+
+    def step():
+        x, y = _factor_batch(r, k[0], W, ragged_step=-1)
+        k[0] += 1
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        opt.step()
+
+    got = ddp.tune_factor_replicate(step, iters=1)
+    tun = ddp.factor_tuning
+    assert set(got) == {"fc1.weight", "fc2.weight"}, got
+    assert set(tun["chosen"]) == {"fc1.weight", "fc2.weight"}, tun
+    assert len(tun["timings_ms"]) == 4 and tun["captured"] is False, tun
+    for _ in range(steps_after):
+        step()
+    plan = ddp.sync_plan()
+    for n, c in tun["chosen"].items():
+        assert plan[n] == "factored-" + c, (n, c, plan)
+    for i in range(k[0]):
+        x, y = _factor_batch(r, i, W, ragged_step=-1)
+        ropt.zero_grad()
+        F.cross_entropy(rddp(x), y).backward()
+        ropt.step()
+    _check_close(model, ref, "factored after tuning", atol=3e-5)
+    ddp.check_replicas()
+    rddp = None  # noqa: F841
+    _teardown()

@@ -69,6 +69,11 @@ def test_factored_sync_matches_torch_ddp(tmp_path, world, kind, replicate):
     run(SW.factored_parity, tmp_path, n=world, kind=kind, replicate=replicate)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_factored_mode_tuning(tmp_path, world):
+    run(SW.factored_tuning, tmp_path, n=world)
+
+
 def test_factored_sync_refuses_foreign_gradient(tmp_path):
     run(SW.factored_foreign_gradient, tmp_path, n=2)
 
