@@ -634,10 +634,14 @@ def main():
             def tdp_step_eager():
                 x, y = gather_batch(data.x, data.y, cur["b"])
                 return body(x, y)
+            # also: 0 or 8 CUs left free for RCCL's kernels while the persistent epilogue GEMMs
+            # run (profiles/micro/comm_cus_ab.txt: 8 cost 3 % at dp1, whether they pay at N > 1
+            # only the real node can tell), unless --comm-cus fixed it
+            cus = (0, 8) if a.comm_cus is None else None
             if graph:
-                ddp.tune_factor_replicate(tdp_step, iters=10, capture=True)
+                ddp.tune_factor_replicate(tdp_step, iters=10, capture=True, comm_cus=cus)
             else:
-                ddp.tune_factor_replicate(eager_step, iters=3)
+                ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
         if graph:
             from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
 

@@ -66,7 +66,10 @@ def test_bench_world2_record(tmp_path):
     chosen = sync["factor_tuning"]["chosen"]
     assert set(chosen) == {"fc1.weight", "fc2.weight"}, sync  # a choice per factored weight
     assert set(chosen.values()) <= {"replicated", "sharded", "split"}, sync
-    assert len(sync["factor_tuning"]["timings_ms"]) == 9, sync  # 2 weights x 3 modes
+    # 2 weights x 3 modes, x 2 reserved-CU settings (bench.py tunes 0 / 8 CUs for RCCL)
+    assert len(sync["factor_tuning"]["timings_ms"]) == 18, sync
+    assert sync["factor_tuning"]["comm_cus"] in (0, 8), sync
+    assert rec["config"]["comm_cus"] == sync["factor_tuning"]["comm_cus"], rec["config"]
     _check_tuning_applied(sync)
 
 

@@ -975,7 +975,8 @@ class DistributedDataParallel(nn.Module):
             return o if f >= 0.5 else 0
         return self._split_rows(o, n, W, f)
 
-    def tune_factor_replicate(self, step_fn, iters: int = 3, capture: bool = False):
+    def tune_factor_replicate(self, step_fn, iters: int = 3, capture: bool = False,
+                              comm_cus=None):
         """Measure, don't guess: time ``step_fn`` (one full training step) under every
         replicated / sharded / split combination of the factored weights (each weight on its
         own: up to two weights, 3^k combinations; more: the three uniform plans), take the max
@@ -987,7 +988,12 @@ class DistributedDataParallel(nn.Module):
         at the same point (it issues collectives). Optimizer state is consolidated before each
         combination (a weight that was sharded has current state in its own rows only). No-op
         (returns None) without factored weights, at world size 1, or when TDP_FACTOR_REPLICATE
-        forces a mode. On the CPU twin (gloo tests) it times replicated / sharded eagerly."""
+        forces a mode. On the CPU twin (gloo tests) it times replicated / sharded eagerly.
+        ``comm_cus`` (GPU): also try these counts of CUs left free for the collectives' kernels
+        (grid-sized GEMMs -- the persistent optimizer-epilogue GEMM fills every CU's LDS -- plan
+        for CUs - N, native set_reserved_cus): a collective that overlaps such a GEMM can only
+        start on CUs it leaves free, which the one-GPU box cannot measure. The fastest
+        (modes, N) pair is kept."""
         import itertools
 
         if not self._factor or self.world_size == 1 or \
@@ -1004,11 +1010,17 @@ class DistributedDataParallel(nn.Module):
         # by NAME: arena indices move with a rebuild
         names = [self._param_name(self.arena.params[i]) for i in sorted(self._factor)]
         choices = (True, False, "split") if self._gpu else (True, False)
-        combos = list(itertools.product(choices, repeat=len(names))) if len(names) <= 2 \
+        modes = list(itertools.product(choices, repeat=len(names))) if len(names) <= 2 \
             else [(c,) * len(names) for c in choices]
+        C = native() if self._gpu else None
+        cus0 = int(C.reserved_cus()) if C is not None else 0
+        cus_list = [int(c) for c in comm_cus] if (comm_cus and C is not None) else [cus0]
+        combos = [(m, c) for c in cus_list for m in modes]
         ms = []
         captured = bool(capture)
-        for combo in combos:
+        for combo, cus in combos:
+            if C is not None:
+                C.set_reserved_cus(cus)  # planned at capture: each combination re-plans
             self.consolidate_optimizer_state()
             self.factor_replicate = dict(zip(names, combo))
             run = step_fn
@@ -1029,18 +1041,26 @@ class DistributedDataParallel(nn.Module):
         ms = [float(v) for v in t.tolist()]
         best = min(range(len(combos)), key=lambda k: ms[k])
         self.consolidate_optimizer_state()
-        self.factor_replicate = dict(zip(names, combos[best]))
+        self.factor_replicate = dict(zip(names, combos[best][0]))
+        if C is not None:
+            C.set_reserved_cus(combos[best][1])
 
         def label(combo):
             return {n: ("replicated" if c is True else "sharded" if c is False else "split")
                     for n, c in zip(names, combo)}
+        first = [k for k, (_, c) in enumerate(combos) if c == cus_list[0]]
         self.factor_tuning = {
             "captured": captured,  # every combination timed as a replayed hipGraph
-            "timings_ms": [{"modes": label(c), "ms": round(m, 4)} for c, m in zip(combos, ms)],
-            "chosen": label(combos[best]),
-            # the round-3 record's keys: all-replicated / all-sharded times
-            "replicated_ms": round(ms[combos.index((True,) * len(names))], 4),
-            "sharded_ms": round(ms[combos.index((False,) * len(names))], 4),
+            "timings_ms": [dict({"modes": label(m), "ms": round(t, 4)},
+                                **({"comm_cus": c} if len(cus_list) > 1 else {}))
+                           for (m, c), t in zip(combos, ms)],
+            "chosen": label(combos[best][0]),
+            "comm_cus": combos[best][1],
+            # the round-3 record's keys: all-replicated / all-sharded times (first CU setting)
+            "replicated_ms": round(min(ms[k] for k in first
+                                       if combos[k][0] == (True,) * len(names)), 4),
+            "sharded_ms": round(min(ms[k] for k in first
+                                    if combos[k][0] == (False,) * len(names)), 4),
         }
         return self.factor_replicate
 
