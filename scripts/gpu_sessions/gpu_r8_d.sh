@@ -12,6 +12,8 @@ run() {  # name, timeout, args...
 }
 # SGD epilogue: default (24 = LDS + non-temporal) vs 28 (+ one batch per tile), interleaved
 timeout -k 10 200 python -u -m pytest tests/test_sync_gpu.py -x -q --timeout 120 --timeout-method thread -k "epilogue_variants and 28" > gpurun_out/r8d/variant28_test.log 2>&1; fatal $? variant28_test; tail -1 gpurun_out/r8d/variant28_test.log
+timeout -k 10 240 python scripts/diag_adam_capture.py --runs 6 > gpurun_out/r8d/diag_adam_capture.jsonl 2>gpurun_out/r8d/diag_adam_capture.err; fatal $? diag_adam
+python3 -c "import json; [print(r['seed'], r['fused'], r['loss_max_diff'], {k: (v['max'], v['n_over_1e-5']) for k, v in r['params'].items() if v['max'] > 0}) for r in map(json.loads, open('gpurun_out/r8d/diag_adam_capture.jsonl'))]"
 for r in 1 2 3; do
 for v in 24 28; do
 timeout -k 10 300 python scripts/run_with_variant.py --sgd $v -- bench.py --no-diag > gpurun_out/r8d/epi_v${v}_r$r.json 2>gpurun_out/r8d/epi_v${v}_r$r.err; fatal $? epi_$v; echo "epilogue variant $v r$r $(ms gpurun_out/r8d/epi_v${v}_r$r.json)"
@@ -30,6 +32,4 @@ run r50_tdp 400 --model resnet50 --steps 20 --warmup 5
 run r50_torch 400 --model resnet50 --steps 20 --warmup 5 --impl torch
 run alexnet_tdp 300 --model alexnet --steps 20 --warmup 5
 run alexnet_torch 300 --model alexnet --steps 20 --warmup 5 --impl torch
-timeout -k 10 240 python scripts/diag_adam_capture.py --runs 6 > gpurun_out/r8d/diag_adam_capture.jsonl 2>gpurun_out/r8d/diag_adam_capture.err; fatal $? diag_adam
-python3 -c "import json; [print(r['seed'], r['fused'], r['loss_max_diff'], {k: (v['max'], v['n_over_1e-5']) for k, v in r['params'].items() if v['max'] > 0}) for r in map(json.loads, open('gpurun_out/r8d/diag_adam_capture.jsonl'))]"
 echo done

@@ -81,13 +81,20 @@ def main():
                          "kernels of every other queue")
     a = ap.parse_args()
     ks = load(a.trace)
+    # the hardware queue(s) that run collectives anywhere in the trace (a short window may hold
+    # none of the few collective KERNELS: a one-rank all-gather is a copy on that queue)
+    side_q = {k[3] for k in ks if is_coll(k[2])}
+    if len(side_q) > 1:  # a collective issued on the compute stream (eager): not a side queue
+        busy = {}
+        for k in ks:
+            busy[k[3]] = busy.get(k[3], 0) + k[1] - k[0]
+        side_q.discard(max(side_q, key=lambda q: busy.get(q, 0)))
     if a.step_marker and a.last_steps:
         starts = [k[0] for k in ks if a.step_marker in k[2]]
         if len(starts) >= a.last_steps:
             t_lo = starts[-a.last_steps]
             ks = [k for k in ks if k[0] >= t_lo]
     if a.by_queue:
-        side_q = {k[3] for k in ks if is_coll(k[2])}
         side = lambda k: k[3] in side_q  # noqa: E731
     else:
         side = lambda k: is_coll(k[2])  # noqa: E731
