@@ -460,9 +460,11 @@ def main():
             data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
             loader = DeviceLoader(data, a.batch, drop_last=True)
             model, opt, loader = accel.prepare(model, opt, loader)
-            ddp = model if isinstance(model, tdp.DDP) else None
+            # the prepared model's DDP: the wrapper at N > 1, the hidden world-1 DDP of the
+            # unwrapped one-process model (Accelerator.ddp_of)
+            ddp = accel.ddp_of(model)
             if use_gpu and want_fused and ddp is not None:
-                fused = model.register_fused_optimizer(opt.optimizer)
+                fused = accel.fuse_optimizer(model, opt)
             sampler = loader  # set_epoch lives on the prepared loader
 
             def body(x, y):  # REF/multi-GPU-training-accelerate.py:45-55

@@ -162,6 +162,7 @@ class Accelerator:
         self.sync_gradients = True
         self.end_of_dataloader = False
         self._models = []
+        self._hidden = {}  # id(prepared one-process model) -> its world-1 DDP
 
     # ------------------------------------------------------------------ process state
     @property
@@ -196,13 +197,45 @@ class Accelerator:
     # ------------------------------------------------------------------ prepare
     def prepare_model(self, model):
         model = model.to(self.device)
+        dev_ids = [self.device.index] if self.device.type == "cuda" else None
         if self.num_processes > 1:
-            dev_ids = [self.device.index] if self.device.type == "cuda" else None
             model = DistributedDataParallel(model, device_ids=dev_ids, **self.ddp_kwargs)
+        elif self.device.type == "cuda":
+            # one process: Accelerate hands the module back unwrapped, and so does this. A
+            # world-1 DDP still runs underneath (no collectives): its forward pre-hook does the
+            # per-iteration bookkeeping, and it is what a fused optimizer registers on, so the
+            # update can run in the weight-gradient GEMM epilogues as with the native DDP
+            # entry point (ddp_of / fuse_optimizer)
+            d = DistributedDataParallel(model, device_ids=dev_ids, **self.ddp_kwargs)
+
+            def pre(_m, _inp, _d=d):
+                _d._hidden_sample = _d._pre_forward()
+
+            def post(_m, _inp, _out, _d=d):
+                if getattr(_d, "_hidden_sample", False):
+                    _d._cur_ev["fwd1"] = _d._event()
+            model.register_forward_pre_hook(pre)
+            model.register_forward_hook(post)
+            self._hidden[id(model)] = d
         else:
-            flatten_module(model)  # single process: still one flat arena for the fused step
+            flatten_module(model)  # single CPU process: still one flat arena for the flat step
         self._models.append(model)
         return model
+
+    def ddp_of(self, model):
+        """The DDP behind a prepared model: the model itself when it is one (several
+        processes), the hidden world-1 DDP of a one-process GPU model, else None."""
+        if isinstance(model, DistributedDataParallel):
+            return model
+        return self._hidden.get(id(model))
+
+    def fuse_optimizer(self, model, optimizer) -> bool:
+        """Apply ``optimizer`` inside the gradient reduction of ``model``'s DDP (in the
+        weight-gradient GEMM epilogues at world size 1): ``DDP.register_fused_optimizer``.
+        False when the model has no DDP (a CPU process) or the optimizer is not fusable."""
+        d = self.ddp_of(model)
+        opt = optimizer.optimizer if isinstance(optimizer, AcceleratedOptimizer) else optimizer
+        return bool(d is not None and d.register_fused_optimizer(opt))
 
     def prepare_optimizer(self, opt):
         return AcceleratedOptimizer(opt, self)
@@ -252,14 +285,15 @@ class Accelerator:
         with contextlib.ExitStack() as stack:
             if not self.sync_gradients:
                 for m in models or self._models:
-                    if isinstance(m, DistributedDataParallel):
-                        stack.enter_context(m.no_sync())
+                    d = self.ddp_of(m)
+                    if d is not None:
+                        stack.enter_context(d.no_sync())
             yield
 
     @contextlib.contextmanager
     def no_sync(self, model):
-        with (model.no_sync() if isinstance(model, DistributedDataParallel)
-              else contextlib.nullcontext()):
+        d = self.ddp_of(model)
+        with (d.no_sync() if d is not None else contextlib.nullcontext()):
             yield
 
     def backward(self, loss, **kwargs):

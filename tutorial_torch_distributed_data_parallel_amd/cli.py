@@ -175,8 +175,9 @@ def train_accelerate(argv=None):
     optimizer = _optimizer(t, model.parameters())
     model, optimizer, train_loader = accelerator.prepare(model, optimizer, train_loader)
     world = accelerator.num_processes
-    if world > 1 and _want_fused(t, device):
-        model.register_fused_optimizer(optimizer.optimizer)
+    if _want_fused(t, device):
+        # the prepared model's DDP (the wrapper, or the hidden world-1 DDP of one process)
+        accelerator.fuse_optimizer(model, optimizer)
     run = torch.zeros(1, device=device)  # persistent: the captured step accumulates into it
 
     def body(inputs, labels):  # the reference's step (REF/multi-GPU-training-accelerate.py:45-55)

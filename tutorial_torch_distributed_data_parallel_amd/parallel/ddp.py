@@ -397,6 +397,18 @@ class DistributedDataParallel(nn.Module):
 
     # --------------------------------------------------------------------------- nn.Module
     def forward(self, *inputs, **kwargs):
+        sample = self._pre_forward()
+        out = self.module(*inputs, **kwargs)
+        if sample:
+            self._cur_ev["fwd1"] = self._event()
+        return out
+
+    def _pre_forward(self) -> bool:
+        """Per-iteration bookkeeping before the module runs (replica checks, a pending bucket
+        rebuild, fused-optimizer hyper-parameters, the reducer's next iteration, buffer
+        broadcast); True when this iteration's timing is sampled. Also driven by the forward
+        pre-hook of a model an ``Accelerator`` prepared in one process (accelerate/accelerator.py
+        ``prepare_model``: the module is returned unwrapped, as Accelerate does)."""
         if self.check_replicas_every and self._iter and \
                 self._iter % self.check_replicas_every == 0 and torch.is_grad_enabled() and \
                 not (self._gpu and torch.cuda.is_current_stream_capturing()):
@@ -435,10 +447,7 @@ class DistributedDataParallel(nn.Module):
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._sync_buffers()
-        out = self.module(*inputs, **kwargs)
-        if sample:
-            self._cur_ev["fwd1"] = self._event()
-        return out
+        return bool(sample)
 
     @contextlib.contextmanager
     def no_sync(self):
