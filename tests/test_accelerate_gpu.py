@@ -50,7 +50,9 @@ def test_one_process_accelerate_fused_matches_native_ddp(pg):
             for o in (o1, o2):
                 o.param_groups[0]["lr"] *= 0.5
         o1.zero_grad(set_to_none=True)
-        tdp.ops.cross_entropy(d1(x), y).backward()
+        # the native entry point's backward (bench.py): seeded like accelerator.backward, so the
+        # loss gradient comes from the same fused CE path
+        tdp.ops.backward(tdp.ops.cross_entropy(d1(x), y))
         o1.step()
         opt.zero_grad(set_to_none=True)
         acc.backward(tdp.ops.cross_entropy(model(x), y))
