@@ -288,7 +288,48 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   float rs = 0.f;
   if (p.db && bid == 0 && threadIdx.x < p.O)
     for (int k = 0; k < p.B; ++k) rs += smem[k * MMAX + threadIdx.x];
-  __syncthreads();
+  if (p.wopt.kind) {
+    // The update below overwrites W[:, cols] in place, and the input gradient needs the OLD W:
+    // dx[:, c] depends on column c of W only, so this workgroup computes dx for its own columns
+    // before updating them (no separate dx workgroups: they would read W while other
+    // workgroups write it -- a race). 8 column quads x 32 row groups per workgroup.
+    constexpr int CQ = CW / 4, RG = 256 / CQ;
+    const int c0 = bid * CW + (threadIdx.x % CQ) * 4;
+    if (c0 < p.I) {  // I % 4 == 0 (host-checked)
+      f32x4 wv[MMAX];
+#pragma unroll
+      for (int k = 0; k < MMAX; ++k)
+        wv[k] = k < p.O ? *reinterpret_cast<const f32x4*>(p.w + (long)k * p.ldw + c0)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int row = threadIdx.x / CQ; row < p.B; row += RG) {
+        const float* grow = smem + row * MMAX;
+        f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < MMAX; ++k) {
+          const float gv = grow[k];  // zero past O
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = fmaf(gv, wv[k][e], a4[e]);
+        }
+        if (p.gate) {
+          const f32x4 gt = *reinterpret_cast<const f32x4*>(p.gate + (long)row * p.ldgate + c0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a4[e] = gt[e] > 0.f ? a4[e] : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(p.dx + (long)row * p.lddx + c0) = a4;
+        if (p.dxp) {
+          typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+          unsigned h0, m0, l0, h1, m1, l1;
+          split4_pair(a4[0], a4[1], h0, m0, l0);
+          split4_pair(a4[2], a4[3], h1, m1, l1);
+          uint16_t* o = p.dxp + (long)row * p.I + c0;
+          *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
+          *reinterpret_cast<u32x2_*>(o + p.dxps) = u32x2_{m0, m1};
+          *reinterpret_cast<u32x2_*>(o + 2 * p.dxps) = u32x2_{l0, l1};
+        }
+      }
+    }
+  }
+  __syncthreads();  // also: every W[:, cols] read of this workgroup precedes its update
   float* red = smem;  // [NQ][MMAX][CW]
 #pragma unroll
   for (int m = 0; m < MMAX; ++m) red[(q * MMAX + m) * CW + cl] = acc[m];
@@ -353,7 +394,8 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
   if (wopt) p.wopt = *wopt;
   if (bopt && db) p.bopt = *bopt;
   const long threads = (long)B * (I / 4);
-  p.nb_dx = (int)((threads + 255) / 256);
+  // with the in-place update the weight workgroups compute dx themselves (kernel comment)
+  p.nb_dx = p.wopt.kind ? 0 : (int)((threads + 255) / 256);
   const int nb_dw = (I + kHeadCols - 1) / kHeadCols;
   // the 10-class heads get their own width (no FMAs on 6 padding classes)
   const int mm = O <= 8 ? 8 : O <= 10 ? 10 : kSkinnyMax;
