@@ -342,3 +342,36 @@ def test_bench_diagnostics_deadline():
     rec = json.loads(lines[0])
     assert rec["steps"] == 3 and rec["value"] > 0
     assert "exceeded" in rec["diagnostics"]["error"]
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_fused_step_is_deterministic(pg, kind):
+    """Two identical world-1 models with the fused optimizer (updates in the GEMM epilogues and
+    in the one-launch head backward) stay BITWISE identical. Regression: the head backward's dx
+    workgroups read W while its weight workgroups updated W in place -- a race that made
+    identical models diverge from the first step (profiles/r8/diag_accel_hidden_r8f_before_fix.jsonl)."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    data = [(torch.randn(64, 1024, device="cuda", generator=g),
+             torch.randint(0, 10, (64,), device="cuda", generator=g)) for _ in range(6)]
+    models = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        m = ToyMLP(in_features=1024, hidden=(512, 512), num_classes=10, device="cuda")
+        d = tdp.DDP(m, device_ids=[0])
+        o = (tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9) if kind == "sgd"
+             else tdp.optim.Adam(d.parameters(), lr=2e-3))
+        assert d.register_fused_optimizer(o) and d._epi_on
+        models.append((m, d, o))
+    for i, (x, y) in enumerate(data):
+        for m, d, o in models:
+            if i == 3:
+                o.param_groups[0]["lr"] *= 0.5
+            o.zero_grad(set_to_none=True)
+            tdp.ops.backward(tdp.ops.cross_entropy(d(x), y))
+            o.step()
+    torch.cuda.synchronize()
+    for (n, a), b in zip(models[0][0].named_parameters(), models[1][0].parameters()):
+        assert torch.equal(a, b), (n, float((a - b).abs().max()))
