@@ -92,3 +92,24 @@ def test_train_accelerate_two_ranks_on_one_gpu(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert len(_epoch_values(r.stdout)) == 2  # the local main process prints
     assert (out / "model.safetensors").exists()
+
+
+def test_train_accelerate_one_process_fused(tmp_path):
+    """scripts/train_accelerate.py under plain python (one process, the reference's default):
+    the module is prepared unwrapped with the hidden world-1 DDP, the fused optimizer updates in
+    the GEMM epilogues, and the run matches the same script with the fused optimizer off."""
+    outs = {}
+    for fused in (True, False):
+        p, out = _settings(tmp_path, f"acc1_{fused}", capture="auto",
+                           script="scripts/train_accelerate.py", fused_optimizer=fused)
+        txt = _run("scripts/train_accelerate.py", p, {}, rank_env=False)
+        outs[fused] = _epoch_values(txt)
+        assert (out / "model.safetensors").exists()
+        from safetensors.torch import load_file
+        keys = set(load_file(str(out / "model.safetensors")))
+        assert keys and not any(k.startswith("module.") for k in keys), keys
+    assert len(outs[True]) == len(outs[False]) == 2
+    for a, b in zip(outs[True], outs[False]):  # (epoch, train loss, test loss, accuracy %)
+        assert a[0] == b[0]
+        assert abs(a[1] - b[1]) <= 1e-2 * b[1] and abs(a[2] - b[2]) <= 1e-2 * b[2], outs
+        assert abs(a[3] - b[3]) <= 1.0, outs  # at most two of the 200 test samples
