@@ -25,8 +25,8 @@ def _settings(tmp_path, name, capture, world=1, script="scripts/train_ddp.py", *
     s = {"script_path": script, "out_dir": str(out),
          "optional_args": {"set_epoch": True, "print_rand": False},
          "local": {"device": "cuda", "condor": {"num_gpus": world}},
-         "train": dict(model="toy_mlp", num_epochs=2, checkpoint_epoch=5, optimizer="adam",
-                       lr=1e-3, n_train=1280, n_test=200, base_seed=7, capture=capture,
+         "train": dict(dict(model="toy_mlp", num_epochs=2, checkpoint_epoch=5, optimizer="adam",
+                            lr=1e-3, n_train=1280, n_test=200, base_seed=7, capture=capture),
                        **train)}
     p = tmp_path / f"{name}.yaml"
     p.write_text(yaml.safe_dump(s))
@@ -97,11 +97,15 @@ def test_train_accelerate_two_ranks_on_one_gpu(tmp_path):
 def test_train_accelerate_one_process_fused(tmp_path):
     """scripts/train_accelerate.py under plain python (one process, the reference's default):
     the module is prepared unwrapped with the hidden world-1 DDP, the fused optimizer updates in
-    the GEMM epilogues, and the run matches the same script with the fused optimizer off."""
+    the GEMM epilogues, and the run matches the same script with the fused optimizer off. SGD:
+    Adam turns the summation-order differences of the two update paths (epilogue vs split-K
+    weight gradient + flat pass) into O(lr) steps on near-zero gradients, and two epochs of
+    training on random labels amplify them (test_sync_gpu pins Adam's fused path per step)."""
     outs = {}
     for fused in (True, False):
         p, out = _settings(tmp_path, f"acc1_{fused}", capture="auto",
-                           script="scripts/train_accelerate.py", fused_optimizer=fused)
+                           script="scripts/train_accelerate.py", fused_optimizer=fused,
+                           optimizer="sgd", lr=0.01)
         txt = _run("scripts/train_accelerate.py", p, {}, rank_env=False)
         outs[fused] = _epoch_values(txt)
         assert (out / "model.safetensors").exists()
