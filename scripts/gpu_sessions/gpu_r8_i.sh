@@ -14,5 +14,4 @@ python3 scripts/step_kernels.py $T ce_fwd 40 > gpurun_out/r8i/reh_kernels.md
 python3 scripts/overlap_report.py $T --by-queue --step-marker ce_fwd --last-steps 4 --title "bench.py rehearsal of the multi-GPU step (TDP_FORCE_COLLECTIVE=1), side = the comm queue" > gpurun_out/r8i/reh_overlap.md
 head -14 gpurun_out/r8i/reh_kernels.md
 head -6 gpurun_out/r8i/reh_overlap.md
-rm -f $(find gpurun_out/r8i -name '*kernel_trace.csv')
 echo done
