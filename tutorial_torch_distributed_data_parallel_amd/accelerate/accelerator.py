@@ -198,7 +198,9 @@ class Accelerator:
     def prepare_model(self, model):
         model = model.to(self.device)
         dev_ids = [self.device.index] if self.device.type == "cuda" else None
-        if self.num_processes > 1:
+        if isinstance(model, DistributedDataParallel) or id(model) in self._hidden:
+            pass  # already prepared (or wrapped by the caller)
+        elif self.num_processes > 1:
             model = DistributedDataParallel(model, device_ids=dev_ids, **self.ddp_kwargs)
         elif self.device.type == "cuda":
             # one process: Accelerate hands the module back unwrapped, and so does this. A
