@@ -14,6 +14,7 @@
 //                (row sums of A) comes from workgroup 0.
 // All three apply the usual epilogue (bias, beta * C, ReLU) and need 16-B aligned rows.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -219,9 +220,12 @@ __device__ __forceinline__ void split4_pair(float x0, float x1, unsigned& h, uns
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{s0, s1}, bf2_));
 }
 
-constexpr int kHeadCols = 32;  // weight-gradient columns per head_bwd workgroup
+// weight-gradient columns per head_bwd workgroup: 32 when separate workgroups compute dx; 16
+// with the in-place update, where each weight workgroup also computes dx for its own columns
+// (twice the workgroups for the same work)
+constexpr int kHeadCols = 32, kHeadColsOpt = 16;
 
-template <int MMAX>
+template <int MMAX, int CW>
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   extern __shared__ float smem[];
   if ((int)blockIdx.x < p.nb_dx) {
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   // per workgroup, slices combined through LDS; workgroup 0 sums g for the bias. 32 columns x 8
   // slices (not skinny_m's 64 x 4): twice the workgroups and half of each thread's dependent
   // chain of x loads -- this part was the launch's long pole (64 workgroups for I = 4096)
-  constexpr int CW = kHeadCols, NQ = 256 / kHeadCols;
+  constexpr int NQ = 256 / CW;
   const int bid = blockIdx.x - p.nb_dx;
   const int cl = threadIdx.x % CW;
   const int q = threadIdx.x / CW;
@@ -396,14 +400,20 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
   const long threads = (long)B * (I / 4);
   // with the in-place update the weight workgroups compute dx themselves (kernel comment)
   p.nb_dx = p.wopt.kind ? 0 : (int)((threads + 255) / 256);
-  const int nb_dw = (I + kHeadCols - 1) / kHeadCols;
+  const int cw = p.wopt.kind ? kHeadColsOpt : kHeadCols;
+  const int nb_dw = (I + cw - 1) / cw;
   // the 10-class heads get their own width (no FMAs on 6 padding classes)
   const int mm = O <= 8 ? 8 : O <= 10 ? 10 : kSkinnyMax;
   const size_t lds = sizeof(float) * (size_t)std::max(B * mm, mm * 256);
   const dim3 grid(p.nb_dx + nb_dw);
-  if (mm == 8) hipLaunchKernelGGL(head_bwd_kernel<8>, grid, dim3(256), lds, s, p);
-  else if (mm == 10) hipLaunchKernelGGL(head_bwd_kernel<10>, grid, dim3(256), lds, s, p);
-  else hipLaunchKernelGGL(head_bwd_kernel<kSkinnyMax>, grid, dim3(256), lds, s, p);
+  auto launch = [&](auto cw_tag) {
+    constexpr int CW = decltype(cw_tag)::value;
+    if (mm == 8) hipLaunchKernelGGL((head_bwd_kernel<8, CW>), grid, dim3(256), lds, s, p);
+    else if (mm == 10) hipLaunchKernelGGL((head_bwd_kernel<10, CW>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((head_bwd_kernel<kSkinnyMax, CW>), grid, dim3(256), lds, s, p);
+  };
+  if (p.wopt.kind) launch(std::integral_constant<int, kHeadColsOpt>{});
+  else launch(std::integral_constant<int, kHeadCols>{});
   return true;
 }
 
