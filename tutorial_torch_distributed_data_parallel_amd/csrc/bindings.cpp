@@ -1733,7 +1733,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("arm_factor",
            [](SyncBackend& b, int bucket, Tensor& g_all, Tensor& x_all, int B, int out, int in,
               int64_t bias_off, int bias_bucket, bool replicate, bool x_ready, int rep_rows,
-              const c10::optional<Tensor>& g_src, double g_scale) {
+              const c10::optional<Tensor>& g_src, double g_scale, bool g_ready) {
              // device buffers for RcclOps; host buffers for PyOps (the CPU twin looks them up by
              // address in parallel/ddp.py _CpuSyncOps.factor_sync)
              TORCH_CHECK(g_all.is_cuda() == b.ops()->on_device() &&
@@ -1751,6 +1751,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              j.bias_off = bias_off;
              j.replicate = replicate;
              j.x_ready = x_ready;
+             j.g_ready = g_ready;
              j.rep_rows = replicate ? out : rep_rows;
              // g_scale: the factor of the update applied to the gathered g (1/W when the slots
              // hold unscaled g). Every rank must gather the same convention whichever way its own
@@ -1766,7 +1767,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("bucket"), py::arg("g_all"), py::arg("x_all"), py::arg("B"), py::arg("out"),
            py::arg("in"), py::arg("bias_off"), py::arg("bias_bucket"),
            py::arg("replicate") = false, py::arg("x_ready") = false, py::arg("rep_rows") = 0,
-           py::arg("g_src") = py::none(), py::arg("g_scale") = 1.0)
+           py::arg("g_src") = py::none(), py::arg("g_scale") = 1.0, py::arg("g_ready") = false)
       .def("prefetch_factor_x",
            [](SyncBackend& b, int bucket, Tensor& x_all, int B, int in,
               const c10::optional<Tensor>& x) {

@@ -244,13 +244,15 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
                           hipStream_t s, hipStream_t compute) {
   const int W = comm_->world(), r = comm_->rank();
   if (cnt <= 0 || cnt % j.in != 0) throw std::runtime_error("factor_sync: shard is not whole rows");
-  if (!skip_collectives) {
-    // in place: this rank's factor rows already sit at slot r (written on the compute stream);
-    // one RCCL group, so g and x share one launch and the links carry both back to back -- x
-    // only when it was not gathered at forward time already (prefetch_factor_x)
+  if (!skip_collectives && !(j.g_ready && j.x_ready)) {
+    // this rank's factor rows: out of place from the layer's buffer (g_src), or already at
+    // slot r (staged on the compute stream); one RCCL group, so g and x share one launch and
+    // the links carry both back to back -- each only when it was not gathered earlier
+    // (x at forward time, g before the layer's input-gradient GEMM: prefetch_factor_x)
     comm_->group_start();
-    comm_->all_gather(j.g_src ? j.g_src : j.g_all + (int64_t)r * j.B * j.out, j.g_all,
-                      (size_t)j.B * j.out, ncclFloat32, s);
+    if (!j.g_ready)
+      comm_->all_gather(j.g_src ? j.g_src : j.g_all + (int64_t)r * j.B * j.out, j.g_all,
+                        (size_t)j.B * j.out, ncclFloat32, s);
     if (!j.x_ready)
       comm_->all_gather(j.x_all + (int64_t)r * j.B * j.in, j.x_all, (size_t)j.B * j.in,
                         ncclFloat32, s);

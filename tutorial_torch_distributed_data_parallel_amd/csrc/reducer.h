@@ -93,6 +93,10 @@ struct FactorJob {
   // x_all was already all-gathered at forward time (SyncBackend::prefetch_factor_x): the job
   // gathers only g
   bool x_ready = false;
+  // g_all was already all-gathered at the start of the layer's backward, before its input-
+  // gradient GEMM (DDP.factor_prefetch_g -> SyncBackend::prefetch_factor_x with g): the gather
+  // overlaps that GEMM and the job gathers nothing
+  bool g_ready = false;
   // out-of-place g gather: this rank's g [B][out] straight from the layer's gradient buffer
   // (no staging copy into slot r)
   const float* g_src = nullptr;

@@ -154,6 +154,9 @@ class _LinearFn(torch.autograd.Function):
                 if pl is not None:
                     attach_planes(dx, pl)
                 return dx, dw, db, None, None, None
+        # a factored weight (world size > 1): its g all-gather starts now, ahead of the
+        # input-gradient GEMM it then overlaps (DDP.factor_prefetch_g)
+        g_pref = fac is not None and g.is_cuda and fac.factor_prefetch_g(w_param, g)
         if needs(ctx, 0):
             dx = torch.empty_like(x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
@@ -169,6 +172,8 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, weight, dx, True, False, gate=gate)
             if gate is not None:
                 _mark_gated(dx, x2)
+        if g_pref:
+            fac.factor_flush()  # the captured fork follows the GEMM's node
         if needs(ctx, 1):
             dw = grad_dest(w_param)
             # dW[out, in] = g^T . x : A = g stored [K=batch][M=out], B = x stored [K][N=in];

@@ -146,6 +146,7 @@ class DistributedDataParallel(nn.Module):
         self._factor_handed = {}
         # arena index -> per-rank batch whose x this iteration's forward staged and gathered
         self._factor_x_ready = {}
+        self._factor_g_ready = {}  # arena index -> B whose g gather was issued before the dgrad
         # factor sources gathered out of place (x, g): alive until the next iteration
         self._factor_keep = []
         self._epi_on = False
@@ -428,6 +429,7 @@ class DistributedDataParallel(nn.Module):
             self._rebuild_buckets()
         self._factor_handed.clear()
         self._factor_x_ready.clear()
+        self._factor_g_ready.clear()
         self._factor_keep.clear()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             if self._fused_opt is not None:
@@ -773,6 +775,31 @@ class DistributedDataParallel(nn.Module):
     def factor_flush(self) -> None:
         self._backend.flush()
 
+    def factor_prefetch_g(self, p, g: torch.Tensor) -> bool:
+        """Start of the backward of a factored weight ``p`` (device path): issue the all-gather
+        of this rank's output-gradient factor ``g`` [B][out] NOW, before the layer's input-
+        gradient GEMM, so the gather overlaps that GEMM instead of following it (the step model
+        of docs/COMM_MODEL.md assumes exactly this); :meth:`factor_submit` then arms the job
+        with nothing left to gather. Only for a full batch whose x went out at forward time
+        (out of place, every rank alike: the decision uses agreed values); the caller launches
+        the GEMM and then calls :meth:`factor_flush`. True when the gather was issued."""
+        i = self._epi_index.get(id(p))
+        if i is None or i not in self._factor or not self._gpu:
+            return False
+        o, n, _ = self._factor[i]
+        B = int(g.shape[0])
+        cap = self._factor_cap.get(i)
+        if cap is None or B != cap or self._factor_x_ready.get(i) != B or \
+                g.shape != (B, o) or not g.is_contiguous() or \
+                2 * self.world_size * cap * (o + n) > o * n:
+            return False
+        bufs = self._factor_buffers(i, cap)
+        self._factor_keep.append(g)  # read by the side stream; alive until the next forward
+        # the same generic rows all-gather as x's (W slots of cap rows)
+        self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o, g)
+        self._factor_g_ready[i] = B
+        return True
+
     def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor, dw=None) -> bool:
         """Stage this rank's factors of ``p``'s gradient (g [B][out] = dL/dy, x [B][in]) and
         arm its bucket; False when factoring does not pay at the agreed batch size (the caller
@@ -834,8 +861,11 @@ class DistributedDataParallel(nn.Module):
         # device path: the slots hold UNSCALED g on every rank and the update applies the 1/W
         # (g_scale) -- one convention whether a rank's slot is read in place (full batch) or
         # staged (ragged batch), since ranks may take different branches in the same step
+        g_ready = self._gpu and x_ready and B == cap and self._factor_g_ready.pop(i, None) == B
         g_src = None
-        if self._gpu and x_ready and B == cap:
+        if g_ready:
+            pass  # gathered before the dgrad GEMM (factor_prefetch_g), from g itself
+        elif self._gpu and x_ready and B == cap:
             # out of place: the all-gather reads this rank's g where the layer's backward wrote
             # it (no staging kernel at all)
             g_src = g
@@ -856,7 +886,7 @@ class DistributedDataParallel(nn.Module):
                                  -1 if bi is None else self.arena.offsets[bi],
                                  self._factor_bias_bucket.get(i, -1), replicate=rows == o,
                                  rep_rows=rows, g_src=g_src,
-                                 g_scale=1.0 / W if self._gpu else 1.0,
+                                 g_scale=1.0 / W if self._gpu else 1.0, g_ready=bool(g_ready),
                                  x_ready=bool(x_ready))
         self._factor_last_B[i] = B
         self._factor_rep[i] = rows
