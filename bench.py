@@ -641,7 +641,8 @@ def main():
             # only the real node can tell), unless --comm-cus fixed it
             cus = (0, 8) if a.comm_cus is None else None
             if graph:
-                ddp.tune_factor_replicate(tdp_step, iters=10, capture=True, comm_cus=cus)
+                ddp.tune_factor_replicate(tdp_step, iters=20, capture=True, comm_cus=cus,
+                                          repeats=2)
             else:
                 ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
         if graph:

@@ -1015,7 +1015,7 @@ class DistributedDataParallel(nn.Module):
         return self._split_rows(o, n, W, f)
 
     def tune_factor_replicate(self, step_fn, iters: int = 3, capture: bool = False,
-                              comm_cus=None):
+                              comm_cus=None, repeats: int = 1):
         """Measure, don't guess: time ``step_fn`` (one full training step) under every
         replicated / sharded / split combination of the factored weights (each weight on its
         own: up to two weights, 3^k combinations; more: the three uniform plans), take the max
@@ -1067,12 +1067,16 @@ class DistributedDataParallel(nn.Module):
             if capture:
                 run = try_capture(step_fn, warmup=1, log=lambda m: None)
                 captured = captured and isinstance(run, CapturedStep)
-            rt.barrier()
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                run()
-            sync()
-            ms.append((time.perf_counter() - t0) * 1000.0 / iters)
+            best_t = None
+            for _ in range(repeats):  # min of repeats: one slow window does not decide
+                rt.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    run()
+                sync()
+                t = (time.perf_counter() - t0) * 1000.0 / iters
+                best_t = t if best_t is None else min(best_t, t)
+            ms.append(best_t)
             if isinstance(run, CapturedStep):
                 del run
         t = torch.tensor(ms, dtype=torch.float64, device=self.device)
