@@ -322,32 +322,3 @@ def test_split_k_reduce_is_deterministic(C):
         ref = torch.relu((A.double() @ (B.double().t() if bk else B.double())) + bias.double())
         # |C| ~ sqrt(K): fp32 accumulation over K terms, scaled like the other planes tests
         torch.testing.assert_close(outs[0][0].double(), ref, rtol=1e-4, atol=2e-5 * K ** 0.5)
-
-
-def test_planes_carry_infinite_activations_like_fp32(C):
-    """an infinite activation split as x - inf = NaN made every product NaN.
-    The producers' split keeps only the head term of a non-finite value, so the planes GEMM
-    gives +-inf / NaN exactly where fp32 does (and the finite outputs stay fp32-accurate).
-    The in-kernel split of the other operand (weights) is unchanged:
-    profiles/r8/split_inf_select_cost_r8.md."""
-    torch.manual_seed(3)
-    x = torch.randn(128, 512, device="cuda")
-    x[3, 7] = float("inf")
-    x[9, 100] = float("-inf")
-    x[20, 5] = float("nan")
-    x[40, 0] = 3.0e38       # finite beyond bf16's range: its head term rounds to inf too
-    w = torch.randn(512, 512, device="cuda") * 0.05
-    p = C.split_planes(x)
-    assert torch.equal(p[0][3, 7].float(), torch.tensor(float("inf"), device="cuda"))
-    assert p[1][3, 7].item() == 0 and p[2][3, 7].item() == 0
-    y = torch.empty(128, 512, device="cuda")
-    C.gemm_planes(p, w, y, True)
-    ref = x @ w.t()
-    for r in (3, 9, 20):
-        assert torch.equal(torch.isinf(y[r]), torch.isinf(ref[r])), r
-        assert torch.equal(torch.isnan(y[r]), torch.isnan(ref[r])), r
-        inf = torch.isinf(ref[r])
-        assert torch.equal(torch.sign(y[r][inf]), torch.sign(ref[r][inf])), r
-    fin = torch.ones(128, dtype=torch.bool, device="cuda")
-    fin[[3, 9, 20, 40]] = False
-    assert _scaled_err(y[fin], x[fin], w.t()) < (8 + 2 * 512 ** 0.5) * U

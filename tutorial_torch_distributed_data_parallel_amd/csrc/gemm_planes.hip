@@ -36,7 +36,6 @@
 #include "common.h"
 #include "kernels.h"
 #include "planes.h"
-#include "split_bf16.h"
 
 namespace tdp {
 namespace {
@@ -131,8 +130,8 @@ __device__ __forceinline__ f32x4 finish4(const PParams& p, int row, int col, f32
   *reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + col) = v;
   if (p.op) {
     unsigned h0, m0, l0, h1, m1, l1;
-    split3_bits_nf(v[0], v[1], h0, m0, l0);
-    split3_bits_nf(v[2], v[3], h1, m1, l1);
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
     uint16_t* o = p.op + (long)row * p.N + col;
     *reinterpret_cast<u32x2*>(o) = u32x2{h0, h1};
     *reinterpret_cast<u32x2*>(o + p.ops) = u32x2{m0, m1};
@@ -530,8 +529,8 @@ __global__ __launch_bounds__(kT) void split_planes_kernel(const float* __restric
     const int row = (int)(e0 / cols), col = (int)(e0 - (long)row * cols);
     const f32x4 v = *reinterpret_cast<const f32x4*>(x + (long)row * ldx + col);
     unsigned h0, m0, l0, h1, m1, l1;
-    split3_bits_nf(v[0], v[1], h0, m0, l0);
-    split3_bits_nf(v[2], v[3], h1, m1, l1);
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
     uint16_t* o = planes + (long)row * cols + col;
     *reinterpret_cast<u32x2*>(o) = u32x2{h0, h1};
     *reinterpret_cast<u32x2*>(o + ps) = u32x2{m0, m1};
@@ -566,8 +565,8 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
     const f32x4 v = src[k];
     dst[k] = v;
     unsigned h0, m0, l0, h1, m1, l1;
-    split3_bits_nf(v[0], v[1], h0, m0, l0);
-    split3_bits_nf(v[2], v[3], h1, m1, l1);
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
     *reinterpret_cast<u32x2*>(o + 4 * k) = u32x2{h0, h1};
     *reinterpret_cast<u32x2*>(o + ps + 4 * k) = u32x2{m0, m1};
     *reinterpret_cast<u32x2*>(o + 2 * ps + 4 * k) = u32x2{l0, l1};

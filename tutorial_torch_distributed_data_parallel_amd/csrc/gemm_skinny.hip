@@ -20,7 +20,6 @@
 #include "kernels.h"
 #include "optim_elem.h"
 #include "planes.h"
-#include "split_bf16.h"
 
 namespace tdp {
 namespace {
@@ -208,6 +207,18 @@ __device__ __forceinline__ void opt_apply(const OptEpilogue& o, long i, float g)
   }
 }
 
+__device__ __forceinline__ void split4_pair(float x0, float x1, unsigned& h, unsigned& m,
+                                            unsigned& l) {
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf2_ __attribute__((ext_vector_type(2)));
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{x0, x1}, bf2_));
+  const float r0 = x0 - __uint_as_float(hu << 16), r1 = x1 - __uint_as_float(hu & 0xffff0000u);
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{r0, r1}, bf2_));
+  const float s0 = r0 - __uint_as_float(mu << 16), s1 = r1 - __uint_as_float(mu & 0xffff0000u);
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{s0, s1}, bf2_));
+}
 
 // weight-gradient columns per head_bwd workgroup: 32 when separate workgroups compute dx; 16
 // with the in-place update, where each weight workgroup also computes dx for its own columns
@@ -242,8 +253,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
     if (p.dxp) {
       typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
       unsigned h0, m0, l0, h1, m1, l1;
-      split3_bits_nf(acc[0], acc[1], h0, m0, l0);
-      split3_bits_nf(acc[2], acc[3], h1, m1, l1);
+      split4_pair(acc[0], acc[1], h0, m0, l0);
+      split4_pair(acc[2], acc[3], h1, m1, l1);
       uint16_t* o = p.dxp + (long)row * p.I + col;
       *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
       *reinterpret_cast<u32x2_*>(o + p.dxps) = u32x2_{m0, m1};
@@ -312,8 +323,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
         if (p.dxp) {
           typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
           unsigned h0, m0, l0, h1, m1, l1;
-          split3_bits_nf(a4[0], a4[1], h0, m0, l0);
-          split3_bits_nf(a4[2], a4[3], h1, m1, l1);
+          split4_pair(a4[0], a4[1], h0, m0, l0);
+          split4_pair(a4[2], a4[3], h1, m1, l1);
           uint16_t* o = p.dxp + (long)row * p.I + c0;
           *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
           *reinterpret_cast<u32x2_*>(o + p.dxps) = u32x2_{m0, m1};

@@ -22,28 +22,13 @@ __device__ __forceinline__ void split3_bits(float x0, float x1, unsigned& h, uns
   l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_{s0, s1}, bf2_));
 }
 
-// The producers' split (planes written next to an activation): a value whose head term is
-// +-inf (an infinite activation, or one beyond bf16's range) keeps only that head term -- its
-// residual x - hi would be inf - inf = NaN and turn every product of the planes GEMM into NaN
-// where fp32 gives +-inf. Finite values: bit-identical to split3_bits. (The GEMMs' in-kernel
-// splits of their other operand keep the bare sequence: a select there costs ~10 % more VALU
-// on the VALU-bound split, profiles/r8/split_inf_select_cost_r8.md.)
-__device__ __forceinline__ void split3_bits_nf(float x0, float x1, unsigned& h, unsigned& m,
-                                               unsigned& l) {
-  split3_bits(x0, x1, h, m, l);
-  const unsigned keep = (__builtin_isinf(__uint_as_float(h << 16)) ? 0u : 0x0000ffffu) |
-                        (__builtin_isinf(__uint_as_float(h & 0xffff0000u)) ? 0u : 0xffff0000u);
-  m &= keep;
-  l &= keep;
-}
-
 // four adjacent values -> their planes at o, o + ps, o + 2 ps (8-B stores)
 __device__ __forceinline__ void store_planes4(uint16_t* o, long ps, float v0, float v1, float v2,
                                               float v3) {
   typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
   unsigned h0, m0, l0, h1, m1, l1;
-  split3_bits_nf(v0, v1, h0, m0, l0);
-  split3_bits_nf(v2, v3, h1, m1, l1);
+  split3_bits(v0, v1, h0, m0, l0);
+  split3_bits(v2, v3, h1, m1, l1);
   *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
   *reinterpret_cast<u32x2_*>(o + ps) = u32x2_{m0, m1};
   *reinterpret_cast<u32x2_*>(o + 2 * ps) = u32x2_{l0, l1};
