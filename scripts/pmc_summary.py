@@ -5,8 +5,9 @@ by name.
 
     python scripts/pmc_summary.py <title> <pass_dir> [<pass_dir> ...] > out.md
 
-Derived columns when the counters are present (GRBM_GUI_ACTIVE is the GPU-clock count of the
-dispatch): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs), HBM GB/s from
+Derived columns when the counters are present (GRBM_GUI_ACTIVE is summed over the 8 XCDs: 8 x
+the dispatch's GPU clocks; SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs): MFMA busy =
+SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024), HBM GB/s from
 (FETCH_SIZE + WRITE_SIZE) KiB over the kernel's duration (FETCH_SIZE can read half the bytes of a
 wide coalesced stream on gfx950: a lower bound, CDNA4 guide §9).
 """
@@ -17,6 +18,7 @@ import sys
 from collections import defaultdict
 
 SIMDS = 256 * 4
+XCDS = 8
 
 
 def _load(d):
@@ -64,7 +66,8 @@ def main():
         row += [f"{v[c]:.3g}" if c in v else "" for c in counters]
         busy = ""
         if "SQ_VALU_MFMA_BUSY_CYCLES" in v and v.get("GRBM_GUI_ACTIVE"):
-            busy = f"{100 * v['SQ_VALU_MFMA_BUSY_CYCLES'] / (v['GRBM_GUI_ACTIVE'] * SIMDS):.0f} %"
+            clocks = v["GRBM_GUI_ACTIVE"] / XCDS
+            busy = f"{100 * v['SQ_VALU_MFMA_BUSY_CYCLES'] / (clocks * SIMDS):.0f} %"
         bw = ""
         if "FETCH_SIZE" in v or "WRITE_SIZE" in v:
             kib = v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)
