@@ -106,6 +106,10 @@ def parse():
                     help="tdp: capture the whole step into a hipGraph and replay it (the default "
                          "at world size > 1: bucket collectives then overlap backward on the comm "
                          "stream)")
+    ap.add_argument("--graph-steps", type=int, default=2,
+                    help="training steps per captured hipGraph replay (1 or 2: two steps per "
+                         "graph remove every other graph-launch gap; an epoch boundary falls "
+                         "between replays)")
     ap.add_argument("--eager", action="store_true",
                     help="tdp: run eagerly (the default at world size 1; collectives then run on "
                          "the compute stream without overlap)")
@@ -625,6 +629,7 @@ def main():
 
         advance()
         run = tdp_step
+        run_pair = [None]  # the two-step graph, when captured
         if a.impl == "tdp" and ddp is not None and world > 1 and use_gpu:
             # measured replicated-vs-sharded choice per factored Linear weight (untimed training
             # steps, agreed over ranks) before the step is captured -- timed the way the step
@@ -646,10 +651,21 @@ def main():
             else:
                 ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
         if graph:
-            from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
+            from tutorial_torch_distributed_data_parallel_amd.train.graph import (CapturedStep,
+                                                                                  try_capture)
 
             run = try_capture(tdp_step, warmup=3,
                               log=lambda m: print(m, file=sys.stderr, flush=True))
+            if ecur is not None and a.graph_steps == 2 and isinstance(run, CapturedStep):
+                # two training steps per replay (the device cursor advances per gather): half
+                # the graph launches; every step still runs all of its work
+                def two_steps():
+                    tdp_step()
+                    return tdp_step()
+                run2 = try_capture(two_steps, warmup=1,
+                                   log=lambda m: print(m, file=sys.stderr, flush=True))
+                if run2 is not two_steps:
+                    run_pair[0] = run2
             if ecur is not None:
                 # the warm-up / capture runs advanced the device cursor: restart the epoch's
                 # order so host and device positions agree from the first timed step on
@@ -659,7 +675,25 @@ def main():
         def step():
             advance()
             return run()
+
+        def steps(n):
+            """n training steps; pairs through the two-step graph while both fall in the
+            current epoch (the host advances its position for each)."""
+            k, out = 0, None
+            while k < n:
+                if run_pair[0] is not None and n - k >= 2 and \
+                        cur["pos"] + 2 * a.batch <= len(cur["idx"]):
+                    advance()
+                    advance()
+                    out = run_pair[0]()
+                    k += 2
+                else:
+                    out = step()
+                    k += 1
+            return out
         step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
+        step.many = steps
+        step.graph_steps = 2 if run_pair[0] is not None else (1 if graph else 0)
         if a.api == "accelerate":
             build_rehearsal = None
     else:
@@ -673,13 +707,20 @@ def main():
             scratch_warmup(a, dims, in_shape, dev)
         else:
             device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
-    for _ in range(a.warmup):
-        step()
+    many = getattr(step, "many", None)
+    if many is not None:
+        many(a.warmup)
+    else:
+        for _ in range(a.warmup):
+            step()
     barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss = step()
+    if many is not None:
+        loss = many(a.steps)
+    else:
+        for _ in range(a.steps):
+            loss = step()
     sync()
     barrier()
     sync()
@@ -757,6 +798,8 @@ def main():
                 "sync": sync,
                 "launched_by": launched_by(),
                 "comm_nranks": comm_nranks,
+                # training steps per hipGraph replay (0: eager)
+                "graph_steps": getattr(step, "graph_steps", None),
                 "baseline": {"samples_per_s": round(base, 2), "source": base_src}
                 if base else None,
             },

@@ -80,13 +80,13 @@ class CapturedStep:
         except Exception as e:
             raise CaptureFailed(repr(e)) from e
         finally:
-            self._ddps = []
+            self._ddps = []  # (DDP, iterations one replay runs: a graph may hold several steps)
             for d, it in before.values():
                 if d._iter != it:
-                    self._ddps.append(weakref.ref(d))
+                    self._ddps.append((weakref.ref(d), d._iter - it))
                     d._iter = it
         torch.cuda.synchronize()
-        if any(r().find_unused_parameters for r in self._ddps if r() is not None):
+        if any(r().find_unused_parameters for r, _ in self._ddps if r() is not None):
             # which parameters went unused is decided on the host every iteration (the reducer
             # zeroes their slots): a graph would freeze the capture-time answer. The flag is a
             # constructor argument, identical on every rank, so every rank refuses alike.
@@ -104,14 +104,17 @@ class CapturedStep:
         comm = rt.comm()
         if comm is not None and comm.world > 1:
             comm.watch_current("captured training step")  # RCCL watchdog covers the replay
-        for ref in self._ddps:
+        for ref, n in self._ddps:
             d = ref()
             if d is None:
                 continue
-            d._iter += 1
-            # the eager forward checks before the step whose count is a multiple: same cadence,
-            # run outside the graph (it is a collective: every rank replays in lock-step)
-            if d.check_replicas_every and d._iter % d.check_replicas_every == 0:
+            before = d._iter
+            d._iter += n
+            # the eager forward checks before the step whose count is a multiple: same cadence
+            # (once per replay that crosses a multiple), run outside the graph (it is a
+            # collective: every rank replays in lock-step)
+            k = d.check_replicas_every
+            if k and d._iter // k > before // k:
                 d.check_replicas()
         return self.output
 
