@@ -662,7 +662,9 @@ def main():
                 def two_steps():
                     tdp_step()
                     return tdp_step()
-                run2 = try_capture(two_steps, warmup=1,
+                # no eager warm-up: the one-step graph's warm-up already did it, and training
+                # steps outside the count would make the run differ from --graph-steps 1
+                run2 = try_capture(two_steps, warmup=0,
                                    log=lambda m: print(m, file=sys.stderr, flush=True))
                 if run2 is not two_steps:
                     run_pair[0] = run2
