@@ -21,7 +21,9 @@ Optimizer scalars live in device hyper blocks, so the captured step stays exact 
 Adam's step count). At world size 1 the toy-MLP step is captured as well (no collective, the
 optimizer runs in the weight-gradient GEMM epilogues; replay removes the host-side launch work
 the ~15-kernel eager step is bound by); the CNNs run eagerly. ``--graph`` / ``--eager`` force a
-mode.
+mode. A captured toy-MLP replay runs TWO training steps (``--graph-steps 2``, each with its own
+batch gather and update; an epoch boundary always falls between replays), which pays the
+graph-launch gap every other step; the trajectory is bit-identical to one step per replay.
 
 Diagnostics (after the timed region, in the JSON line's "diagnostics"): at world size > 1 the
 collectives of one step alone (``comm_ms``), the same captured step with its collectives turned
