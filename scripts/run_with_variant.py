@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--persist", type=int, default=-1)
     ap.add_argument("--wgs", type=int, default=-1)
     ap.add_argument("--planes", type=str, default=None, help="stages,pf,splits")
+    ap.add_argument("--no-early-g", action="store_true",
+                    help="factored g gathers only from the layer's own backward")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
@@ -32,6 +34,10 @@ def main():
         st, pf, sp = (int(v) for v in a.planes.split(","))
         if not C.gemm_planes_set_cfg(st, pf, sp):
             raise SystemExit(f"invalid planes config {a.planes}")
+    if a.no_early_g:
+        from tutorial_torch_distributed_data_parallel_amd.ops import linear
+
+        linear.set_early_prev_g(False)
     sys.argv = [script] + rest[1:]
     runpy.run_path(script if os.path.isabs(script) else os.path.join(ROOT, script),
                    run_name="__main__")

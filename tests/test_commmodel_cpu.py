@@ -29,6 +29,25 @@ def test_forward_x_gather_shortens_the_tail():
     assert early["exposed_us"] < late["exposed_us"]
 
 
+def test_early_g_gather_precedes_the_parameter_all_gather():
+    # fc1's g gathered from fc2's backward (after fc2's gated input-gradient GEMM) instead of
+    # queueing behind fc2's parameter all-gather on the side stream
+    layers = cm.toy_mlp_layers(128)
+    hw = cm.Hardware()
+    for W, mode in ((2, "factored-replicated"), (8, "factored-split"), (8, "factored-sharded")):
+        modes = {"fc1": mode, "fc2": mode}
+        on = cm.simulate(layers, modes, W, 128, hw, early_g=True)
+        off = cm.simulate(layers, modes, W, 128, hw, early_g=False)
+        assert on["step_us"] < off["step_us"], (W, mode)
+        fc1 = {j["layer"]: j for j in on["jobs"]}["fc1"]
+        fc1_off = {j["layer"]: j for j in off["jobs"]}["fc1"]
+        assert fc1["start_us"] < fc1_off["start_us"]
+    # bucket-mode neighbours have no factors to gather early: nothing changes
+    modes = {"fc1": "allreduce", "fc2": "allreduce"}
+    assert cm.simulate(layers, modes, 8, 128, hw, early_g=True)["step_us"] == \
+        cm.simulate(layers, modes, 8, 128, hw, early_g=False)["step_us"]
+
+
 def test_best_plan_beats_uniform_plans_and_follows_bandwidth():
     layers = cm.toy_mlp_layers(128)
     for W in (2, 4, 8):

@@ -122,6 +122,63 @@ def test_factored_captured_step(pg):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
 
 
+def test_early_prev_g_gather_captured_bitwise(pg, monkeypatch):
+    """fc1's g gather issued from fc2's backward (right after fc2's gated input-gradient GEMM,
+    ops/linear.py) instead of from fc1's own: the captured steps are bitwise identical to the
+    ones without it, and fc1's own backward finds its gather already issued."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.ops import linear
+    from tutorial_torch_distributed_data_parallel_amd.parallel.ddp import DistributedDataParallel
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    calls = []
+    orig = DistributedDataParallel.factor_prefetch_g
+
+    def spy(self, p, g):
+        r = orig(self, p, g)
+        calls.append((id(p), g.data_ptr(), r))
+        return r
+
+    monkeypatch.setattr(DistributedDataParallel, "factor_prefetch_g", spy)
+    X = torch.randn(256, DIMS[0], device="cuda")
+    Y = torch.randint(0, 10, (256,), device="cuda")
+    idx = torch.zeros(32, dtype=torch.long, device="cuda")
+    runs, counts = [], []
+    for early in (True, False):
+        old = linear.set_early_prev_g(early)
+        try:
+            m, d, o = _build(tdp, "sgd", True, seed=5)
+            fc1 = id(m.fc1.weight)
+
+            def step():
+                x, y = X.index_select(0, idx), Y.index_select(0, idx)
+                o.zero_grad(set_to_none=True)
+                loss = tdp.ops.cross_entropy(d(x), y)
+                loss.backward()
+                o.step()
+                return loss
+
+            calls.clear()
+            graph = CapturedStep(step, warmup=3)
+            n_fc1 = sum(1 for c in calls if c[0] == fc1 and c[2])
+        finally:
+            linear.set_early_prev_g(old)
+        counts.append(n_fc1)
+        torch.manual_seed(3)
+        losses = []
+        for _ in range(6):
+            idx.copy_(torch.randperm(256, device="cuda")[:32])
+            losses.append(graph.replay().clone())
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses), [p.detach().clone() for p in m.parameters()]))
+    # warmup + capture: fc1's gather is asked for twice per step when early (fc2's backward,
+    # then its own, which finds it issued), once otherwise
+    assert counts[1] >= 1 and counts[0] == 2 * counts[1], counts
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
+
+
 def test_factored_skips_when_not_profitable(pg):
     """A batch too large for the factors to be cheaper than the gradient falls back to the
     ordinary weight-gradient GEMM (and the bucket's normal collectives)."""

@@ -268,8 +268,12 @@ void RcclOps::factor_sync(int64_t begin, int64_t own, int64_t cnt, const FactorJ
   if (compute && compute != s) {
     for (auto& e : fac_ev_)
       if (!e) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventRecord(fac_ev_[0], s), "hipEventRecord(factor)");
-    check_hip(hipStreamWaitEvent(compute, fac_ev_[0], 0), "hipStreamWaitEvent(factor)");
+    if (j.gathered) {
+      check_hip(hipStreamWaitEvent(compute, j.gathered, 0), "hipStreamWaitEvent(gathered)");
+    } else {
+      check_hip(hipEventRecord(fac_ev_[0], s), "hipEventRecord(factor)");
+      check_hip(hipStreamWaitEvent(compute, fac_ev_[0], 0), "hipStreamWaitEvent(factor)");
+    }
     gs = compute;
   }
   const FactorPlan f = plan_factor(begin, own, cnt, j);
@@ -312,9 +316,12 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
     : ops_(std::move(ops)), numel_(numel), timing_(timing), skip_single_rank_(skip_single_rank) {
   factor_.resize(num_buckets);
   factor_skip_.assign(num_buckets, 0);
+  gdone_set_.assign(num_buckets, 0);
   if (ops_->on_device()) {
     ready_.resize(num_buckets);
     for (auto& e : ready_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    gdone_.resize(num_buckets);
+    for (auto& e : gdone_) check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     check_hip(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
     if (timing_) {
       check_hip(hipEventCreate(&t0_), "event");
@@ -327,6 +334,7 @@ SyncBackend::SyncBackend(std::shared_ptr<SyncOps> ops, int64_t numel, int num_bu
 
 SyncBackend::~SyncBackend() {
   for (auto& e : ready_) (void)hipEventDestroy(e);
+  for (auto& e : gdone_) (void)hipEventDestroy(e);
   if (done_) (void)hipEventDestroy(done_);
   if (t0_) (void)hipEventDestroy(t0_);
   if (t1_) (void)hipEventDestroy(t1_);
@@ -382,8 +390,12 @@ void SyncBackend::prefetch_factor_x(int bucket, float* x_all, const float* x_src
                                     hipStream_t compute) {
   if (!collective() || !ops_->on_device()) return;
   if (bucket < 0 || bucket >= (int)factor_.size()) throw std::runtime_error("prefetch: bucket");
-  issue(bucket, compute, [this, x_all, x_src, B, in](hipStream_t cs) {
+  issue(bucket, compute, [this, bucket, x_all, x_src, B, in, compute](hipStream_t cs) {
     ops_->factor_gather_x(x_all, x_src, B, in, cs);
+    if (cs != compute) {  // a side-stream gather: mark its end for the bucket's job
+      check_hip(hipEventRecord(gdone_[bucket], cs), "hipEventRecord(gathered)");
+      gdone_set_[bucket] = 1;
+    }
   });
 }
 
@@ -394,6 +406,7 @@ void SyncBackend::begin_iteration(hipStream_t compute) {
   forks_.clear();
   for (auto& f : factor_) f.B = 0;
   std::fill(factor_skip_.begin(), factor_skip_.end(), 0);
+  std::fill(gdone_set_.begin(), gdone_set_.end(), 0);
   epi_done_.clear();
   pending_.clear();
   deferred_.clear();
@@ -573,8 +586,13 @@ void SyncBackend::launch(int bucket, int64_t begin, int64_t end, hipStream_t com
       throw std::runtime_error("factored bucket: needs the fused optimizer, no clipping / "
                                "compression, and one whole-row-sharded weight per bucket");
     const int64_t own0 = own.first;
-    issue(bucket, compute, [this, begin, own0, cnt, j, compute](hipStream_t cs) {
-      ops_->factor_sync(begin, own0, cnt, j, cs, compute);
+    issue(bucket, compute, [this, bucket, begin, own0, cnt, j, compute](hipStream_t cs) {
+      FactorJob jj = j;
+      // runs after the bucket's gather forks (forks run in issue order): both factors gathered
+      // on the side stream -> the job waits for exactly those gathers
+      if (j.g_ready && j.x_ready && cs != compute && gdone_set_[bucket]) jj.gathered = gdone_[bucket];
+      gdone_set_[bucket] = 0;
+      ops_->factor_sync(begin, own0, cnt, jj, cs, compute);
     });
     return;
   }

@@ -103,6 +103,11 @@ struct FactorJob {
   // factor applied to the gathered g by the update (1/W on the device path, where every rank's
   // slot holds unscaled g whether it was read in place or staged; 1 on the CPU twin)
   float g_scale = 1.f;
+  // both factors were gathered by earlier side-stream forks and this event was recorded right
+  // after the last of them: the job's compute-stream arithmetic waits on it alone, not on
+  // everything queued on the side stream since (e.g. the previous job's parameter all-gather,
+  // when fc1's g gather was issued from fc2's backward: DDP.factor_prefetch_g)
+  hipEvent_t gathered = nullptr;
 };
 
 // Side effects of the sync algorithm. Offsets are arena elements; streams are ignored off-device.
@@ -293,6 +298,8 @@ class SyncBackend : public ReducerBackend {
   std::vector<Fork> forks_;               // deferred side-stream launches (capture only)
   std::vector<hipGraphNode_t> fork_deps_; // compute stream's capture frontier at the first one
   std::vector<hipEvent_t> ready_;
+  std::vector<hipEvent_t> gdone_;  // per bucket: recorded after its last factor gather fork
+  std::vector<char> gdone_set_;    // ... in this iteration, on the side stream
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool launched_any_ = false, timed_pending_ = false, launched_side_ = false;
 };

@@ -45,6 +45,17 @@ def _al16(*ts) -> bool:
                for t in ts)
 
 
+_EARLY_PREV_G = True  # the consumer's backward starts the previous layer's g gather
+
+
+def set_early_prev_g(on: bool) -> bool:
+    """Turn the one-layer-early g gather on/off (A/B: scripts/run_with_variant.py); returns the
+    previous setting."""
+    global _EARLY_PREV_G
+    old, _EARLY_PREV_G = _EARLY_PREV_G, bool(on)
+    return old
+
+
 def set_planes(on: bool) -> bool:
     """Turn the planes path on/off (tests, A/B); returns the previous setting."""
     global _PLANES
@@ -84,7 +95,7 @@ def _mark_gated(dx: torch.Tensor, gate: torch.Tensor) -> None:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None):
+    def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None, prev=None):
         C = native()
         M, K = x2.shape
         N = weight.shape[0]
@@ -107,6 +118,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.gate_in = gate_in
         ctx.params = (weight, bias)
+        ctx.prev_w = prev[0] if prev else None
         ctx.save_for_backward(x2, weight, y if relu else None)
         return y
 
@@ -153,7 +165,7 @@ class _LinearFn(torch.autograd.Function):
                     _mark_gated(dx, x2)
                 if pl is not None:
                     attach_planes(dx, pl)
-                return dx, dw, db, None, None, None
+                return dx, dw, db, None, None, None, None
         # a factored weight (world size > 1): its g all-gather starts now, ahead of the
         # input-gradient GEMM it then overlaps (DDP.factor_prefetch_g)
         g_pref = fac is not None and g.is_cuda and fac.factor_prefetch_g(w_param, g)
@@ -172,6 +184,17 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, weight, dx, True, False, gate=gate)
             if gate is not None:
                 _mark_gated(dx, x2)
+                # the gated dx IS the output gradient of the previous (fused Linear+ReLU) layer:
+                # a factored previous weight starts its g gather now, from here, so on the comm
+                # stream it precedes this layer's parameter all-gather instead of queueing
+                # behind it (DDP.factor_prefetch_g; docs/COMM_MODEL.md "early g gather")
+                prev = factor_target(ctx.prev_w) if ctx.prev_w is not None and _EARLY_PREV_G \
+                    else None
+                if prev is not None and dx.is_cuda and prev.factor_prefetch_g(ctx.prev_w, dx):
+                    if prev is not fac:
+                        prev.factor_flush()
+                    elif not g_pref:
+                        g_pref = True
         if g_pref:
             fac.factor_flush()  # the captured fork follows the GEMM's node
         if needs(ctx, 1):
@@ -198,7 +221,7 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 class _LinearCpuFn(torch.autograd.Function):
@@ -279,9 +302,13 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     if torch.is_grad_enabled():
         note_use(weight)
     fac = _factor_owner(weight) if torch.is_grad_enabled() else None
-    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, fac)
+    # the weight that produced x (a fused Linear+ReLU before this one): its g is this layer's
+    # gated dx, whose gather this layer's backward can start (a tuple: not an autograd input)
+    pw = getattr(x, "_tdp_prod_w", None) if gate_in else None
+    y = _LinearFn.apply(x2, weight, bias, relu, gate_in, fac, (pw,) if pw is not None else None)
     if x.dim() == 2:
         if relu:
             y._tdp_relu_out = True
+            y._tdp_prod_w = weight
         return y
     return y.reshape(*lead, weight.shape[0])

@@ -131,14 +131,17 @@ def job_cost(layer: Layer, mode: str, W: int, B: int, hw: Hardware) -> dict:
 
 
 def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
-             prefetch_x: bool = True) -> dict:
+             prefetch_x: bool = True, early_g: bool = True) -> dict:
     """Predicted captured W-rank step (reducer.cpp / ops/linear.py schedule): forward issues the
     factored x gathers on the side stream; backward runs, per weight from the last layer down,
     the layer's input gradient and then its job -- side-stream collectives (gathers, all-reduce,
     parameter all-gather) in FIFO order, the job's arithmetic on the compute stream once its
-    gathers are in. The step ends when both streams are done: ``exposed_us`` = step - compute
-    alone. ``modes``: layer name -> mode; layers absent (the small head) cost their compute time
-    and ride, as an all-reduce, with the first job."""
+    gathers are in. A factored layer's g gather goes out before its input-gradient GEMM, or with
+    ``early_g`` one layer earlier: right after the consumer's (gated) input-gradient GEMM, which
+    produces that g, so it precedes the consumer's parameter all-gather in the FIFO. The step
+    ends when both streams are done: ``exposed_us`` = step - compute alone. ``modes``: layer
+    name -> mode; layers absent (the small head) cost their compute time and ride, as an
+    all-reduce, with the first job."""
     tc = ts = 0.0
     costs = {L.name: job_cost(L, modes[L.name], W, B, hw) for L in layers if L.name in modes}
     for L in layers:  # forward
@@ -151,22 +154,36 @@ def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
     tc += sum(L.dgrad_us + L.wgrad_us for L in small)
     small_bytes = sum(4.0 * L.out * L.inp for L in small)
     jobs = []
-    for L in reversed([L for L in layers if L.name in modes]):
-        c = costs[L.name]
-        ready = tc                       # this layer's g exists
-        tc += L.dgrad_us                 # its input gradient (captured before the job's fork)
-        pre = c["pre_us"] + (0.0 if prefetch_x else c["x_us"])
+    order = list(reversed([L for L in layers if L.name in modes]))
+    gathered = {}  # layer -> (start, end) of its pre-job collectives on the side stream
+
+    def pre_of(L):
+        nonlocal small_bytes
+        pre = costs[L.name]["pre_us"] + (0.0 if prefetch_x else costs[L.name]["x_us"])
         if small_bytes:
             pre += _coll_us(hw, "all_reduce", W, small_bytes)
             small_bytes = 0.0
-        start = max(ts, ready)
-        ts = start + pre
-        tc = max(tc, ts if c["mode"].startswith("factored") else tc) + c["compute_us"]
+        return pre
+
+    for k, L in enumerate(order):
+        c = costs[L.name]
+        if L.name not in gathered:       # its g exists now: gathered before its dgrad
+            start = max(ts, tc)
+            ts = start + pre_of(L)
+            gathered[L.name] = (start, ts)
+        tc += L.dgrad_us                 # its input gradient (captured before the job's fork)
+        nxt = order[k + 1] if k + 1 < len(order) else None
+        if early_g and nxt is not None and costs[nxt.name]["mode"].startswith("factored"):
+            start = max(ts, tc)          # the gated dx is nxt's g
+            ts = start + pre_of(nxt)
+            gathered[nxt.name] = (start, ts)
+        start, done = gathered[L.name]
+        tc = max(tc, done if c["mode"].startswith("factored") else tc) + c["compute_us"]
         if c["post_us"] > 0:
             ts = max(ts, tc) + c["post_us"]
         tc += c["after_us"]  # replicated rows of a split job, while its all-gather runs
-        jobs.append({"layer": L.name, **{k: round(v, 2) if isinstance(v, float) else v
-                                         for k, v in c.items()},
+        jobs.append({"layer": L.name, **{k2: round(v, 2) if isinstance(v, float) else v
+                                         for k2, v in c.items()},
                      "start_us": round(start, 1), "end_us": round(max(ts, tc), 1)})
     step = max(tc, ts)
     return {"W": W, "B": B, "compute_us": round(alone, 1), "forward_us": round(fwd_end, 1),

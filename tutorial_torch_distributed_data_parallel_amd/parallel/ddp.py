@@ -146,7 +146,7 @@ class DistributedDataParallel(nn.Module):
         self._factor_handed = {}
         # arena index -> per-rank batch whose x this iteration's forward staged and gathered
         self._factor_x_ready = {}
-        self._factor_g_ready = {}  # arena index -> B whose g gather was issued before the dgrad
+        self._factor_g_ready = {}  # arena index -> (B, g's address) whose g gather was issued early
         # factor sources gathered out of place (x, g): alive until the next iteration
         self._factor_keep = []
         self._epi_on = False
@@ -782,12 +782,20 @@ class DistributedDataParallel(nn.Module):
         of docs/COMM_MODEL.md assumes exactly this); :meth:`factor_submit` then arms the job
         with nothing left to gather. Only for a full batch whose x went out at forward time
         (out of place, every rank alike: the decision uses agreed values); the caller launches
-        the GEMM and then calls :meth:`factor_flush`. True when the gather was issued."""
+        the GEMM and then calls :meth:`factor_flush`. True when the gather was issued.
+
+        Also called one layer EARLY, by the consumer of ``p``'s (fused ReLU) output, with its
+        gated input gradient -- which is ``p``'s g -- right after its input-gradient GEMM
+        (ops/linear.py): the gather then precedes the consumer's parameter all-gather on the
+        comm stream. ``p``'s own backward finds it issued for the same tensor and returns True;
+        for a different g (the output had other consumers) it gathers again."""
         i = self._epi_index.get(id(p))
         if i is None or i not in self._factor or not self._gpu:
             return False
         o, n, _ = self._factor[i]
         B = int(g.shape[0])
+        if self._factor_g_ready.get(i) == (B, g.data_ptr()):
+            return True  # issued early from the consumer's backward
         cap = self._factor_cap.get(i)
         if cap is None or B != cap or self._factor_x_ready.get(i) != B or \
                 g.shape != (B, o) or not g.is_contiguous() or \
@@ -797,7 +805,7 @@ class DistributedDataParallel(nn.Module):
         self._factor_keep.append(g)  # read by the side stream; alive until the next forward
         # the same generic rows all-gather as x's (W slots of cap rows)
         self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o, g)
-        self._factor_g_ready[i] = B
+        self._factor_g_ready[i] = (B, g.data_ptr())
         return True
 
     def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor, dw=None) -> bool:
@@ -861,7 +869,8 @@ class DistributedDataParallel(nn.Module):
         # device path: the slots hold UNSCALED g on every rank and the update applies the 1/W
         # (g_scale) -- one convention whether a rank's slot is read in place (full batch) or
         # staged (ragged batch), since ranks may take different branches in the same step
-        g_ready = self._gpu and x_ready and B == cap and self._factor_g_ready.pop(i, None) == B
+        g_ready = self._gpu and x_ready and B == cap and \
+            self._factor_g_ready.pop(i, None) == (B, g.data_ptr())
         g_src = None
         if g_ready:
             pass  # gathered before the dgrad GEMM (factor_prefetch_g), from g itself
