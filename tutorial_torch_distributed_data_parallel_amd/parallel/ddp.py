@@ -780,8 +780,9 @@ class DistributedDataParallel(nn.Module):
         of this rank's output-gradient factor ``g`` [B][out] NOW, before the layer's input-
         gradient GEMM, so the gather overlaps that GEMM instead of following it (the step model
         of docs/COMM_MODEL.md assumes exactly this); :meth:`factor_submit` then arms the job
-        with nothing left to gather. Only for a full batch whose x went out at forward time
-        (out of place, every rank alike: the decision uses agreed values); the caller launches
+        with nothing left to gather. Only when x went out at forward time (every rank alike:
+        the decision uses agreed values; a ragged batch is staged, a full one read in place);
+        the caller launches
         the GEMM and then calls :meth:`factor_flush`. True when the gather was issued.
 
         Also called one layer EARLY, by the consumer of ``p``'s (fused ReLU) output, with its
@@ -797,14 +798,22 @@ class DistributedDataParallel(nn.Module):
         if self._factor_g_ready.get(i) == (B, g.data_ptr()):
             return True  # issued early from the consumer's backward
         cap = self._factor_cap.get(i)
-        if cap is None or B != cap or self._factor_x_ready.get(i) != B or \
+        if cap is None or B > cap or self._factor_x_ready.get(i) != B or \
                 g.shape != (B, o) or not g.is_contiguous() or \
                 2 * self.world_size * cap * (o + n) > o * n:
             return False
         bufs = self._factor_buffers(i, cap)
-        self._factor_keep.append(g)  # read by the side stream; alive until the next forward
-        # the same generic rows all-gather as x's (W slots of cap rows)
-        self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o, g)
+        if B == cap:
+            self._factor_keep.append(g)  # read by the side stream; alive until the next forward
+            # the same generic rows all-gather as x's (W slots of cap rows), out of place
+            self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o, g)
+        else:
+            # a ragged batch on this rank: staged into slot r, zero-padded (unscaled, as in
+            # factor_submit), and gathered in place -- at the SAME point of the collective
+            # sequence as the full-batch ranks' gather (the early gather would otherwise run
+            # before the consumer's parameter all-gather on some ranks and after it on others)
+            native().factor_stage(g, None, bufs[0], bufs[1], self.rank, 1.0, cap)
+            self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o)
         self._factor_g_ready[i] = (B, g.data_ptr())
         return True
 
@@ -869,7 +878,7 @@ class DistributedDataParallel(nn.Module):
         # device path: the slots hold UNSCALED g on every rank and the update applies the 1/W
         # (g_scale) -- one convention whether a rank's slot is read in place (full batch) or
         # staged (ragged batch), since ranks may take different branches in the same step
-        g_ready = self._gpu and x_ready and B == cap and \
+        g_ready = self._gpu and x_ready and \
             self._factor_g_ready.pop(i, None) == (B, g.data_ptr())
         g_src = None
         if g_ready:
