@@ -93,6 +93,19 @@ def _mark_gated(dx: torch.Tensor, gate: torch.Tensor) -> None:
     dx._tdp_gated_by = (gate.data_ptr(), tuple(gate.shape))
 
 
+def _prefetch_prev_g(ctx, dx: torch.Tensor):
+    """The gated dx of a layer whose input is a fused Linear+ReLU output IS that previous
+    layer's output gradient g: a factored previous weight starts its g gather now, right after
+    the GEMM that produced dx, so on the comm stream it precedes this layer's own collectives
+    (parameter all-gather, bucket all-reduce) instead of queueing behind them
+    (DDP.factor_prefetch_g; docs/COMM_MODEL.md "early g gather"). Returns the DDP that issued
+    it (the caller flushes its fork after the GEMM's node), else None."""
+    if ctx.prev_w is None or not _EARLY_PREV_G or not dx.is_cuda:
+        return None
+    prev = factor_target(ctx.prev_w)
+    return prev if prev is not None and prev.factor_prefetch_g(ctx.prev_w, dx) else None
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None, prev=None):
@@ -163,6 +176,9 @@ class _LinearFn(torch.autograd.Function):
                         hand_off(b_param, db)
                 if gate is not None:
                     _mark_gated(dx, x2)
+                    prev = _prefetch_prev_g(ctx, dx)
+                    if prev is not None:
+                        prev.factor_flush()
                 if pl is not None:
                     attach_planes(dx, pl)
                 return dx, dw, db, None, None, None, None
@@ -184,13 +200,8 @@ class _LinearFn(torch.autograd.Function):
                 C.gemm_f32(g, weight, dx, True, False, gate=gate)
             if gate is not None:
                 _mark_gated(dx, x2)
-                # the gated dx IS the output gradient of the previous (fused Linear+ReLU) layer:
-                # a factored previous weight starts its g gather now, from here, so on the comm
-                # stream it precedes this layer's parameter all-gather instead of queueing
-                # behind it (DDP.factor_prefetch_g; docs/COMM_MODEL.md "early g gather")
-                prev = factor_target(ctx.prev_w) if ctx.prev_w is not None and _EARLY_PREV_G \
-                    else None
-                if prev is not None and dx.is_cuda and prev.factor_prefetch_g(ctx.prev_w, dx):
+                prev = _prefetch_prev_g(ctx, dx)
+                if prev is not None:
                     if prev is not fac:
                         prev.factor_flush()
                     elif not g_pref:
