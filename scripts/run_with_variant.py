@@ -35,9 +35,10 @@ def main():
         if not C.gemm_planes_set_cfg(st, pf, sp):
             raise SystemExit(f"invalid planes config {a.planes}")
     if a.no_early_g:
-        from tutorial_torch_distributed_data_parallel_amd.ops import linear
+        import importlib
 
-        linear.set_early_prev_g(False)
+        importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear") \
+            .set_early_prev_g(False)
     sys.argv = [script] + rest[1:]
     runpy.run_path(script if os.path.isabs(script) else os.path.join(ROOT, script),
                    run_name="__main__")

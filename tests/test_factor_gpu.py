@@ -127,7 +127,9 @@ def test_early_prev_g_gather_captured_bitwise(pg, monkeypatch):
     ops/linear.py) instead of from fc1's own: the captured steps are bitwise identical to the
     ones without it, and fc1's own backward finds its gather already issued."""
     tdp = pg
-    from tutorial_torch_distributed_data_parallel_amd.ops import linear
+    import importlib
+
+    linear = importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear")
     from tutorial_torch_distributed_data_parallel_amd.parallel.ddp import DistributedDataParallel
     from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
 
