@@ -161,6 +161,7 @@ def test_early_prev_g_gather_captured_bitwise(pg, monkeypatch):
                 return loss
 
             calls.clear()
+            idx.zero_()  # the same warm-up batches in both runs
             graph = CapturedStep(step, warmup=3)
             n_fc1 = sum(1 for c in calls if c[0] == fc1 and c[2])
         finally:
