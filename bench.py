@@ -755,6 +755,7 @@ def main():
             ident = False
         sync = {"replicas_identical": ident, "captured": isinstance(run, CapturedStep),
                 "backend": rt.get_backend(), "modes": ddp.sync_plan(),
+                "factor": ddp.factor_report() if ddp._factor else None,
                 "factor_tuning": ddp.factor_tuning}
 
     comm_nranks = None

@@ -529,3 +529,38 @@ def factored_tuning(rank, out_dir, steps_after=2):
     ddp.check_replicas()
     rddp = None  # noqa: F841
     _teardown()
+
+
+def factored_batch_over_slot(rank, out_dir, agree_first=False):
+    """a per-rank batch above the agreed factor slot on ONE rank only.
+    Without factor_capacity the over-slot rank raises cleanly (no collective from a subset of
+    the ranks, which would pair with the others' factor all-gathers and hang); the launcher's
+    fail-fast ends the job. With factor_capacity(6) agreed up front every rank runs the step
+    and matches stock torch DDP."""
+    tdp.init_process_group("gloo")
+    r, W = rt.get_rank(), rt.get_world_size()
+    torch.manual_seed(0)
+    model = ToyMLP(**FACTOR_DIMS)
+    ref = copy.deepcopy(model)
+    ddp = tdp.DDP(model, factor_sync=True)
+    opt, ropt = _make_opts("sgd", ddp.parameters(), ref.parameters(), 0.05)
+    ddp.register_fused_optimizer(opt)
+    if agree_first:
+        ddp.factor_capacity(6 if r == 0 else 4)  # the max over ranks is agreed
+    rddp = torch.nn.parallel.DistributedDataParallel(ref)
+    for step in range(3):
+        x, y = _factor_batch(r, step, W, ragged_step=-1)
+        if step == 1 and r == 0:  # one rank's batch grows past the first step's slot
+            g = torch.Generator().manual_seed(77)
+            x, y = torch.randn(6, 96, generator=g), torch.randint(0, 5, (6,), generator=g)
+        opt.zero_grad()
+        tdp.ops.cross_entropy(ddp(x), y).backward()
+        opt.step()
+        ropt.zero_grad()
+        F.cross_entropy(rddp(x), y).backward()
+        ropt.step()
+    assert set(ddp._factor_cap.values()) == {6}, ddp._factor_cap
+    _check_close(model, ref, "factored over-slot batch", atol=3e-5)
+    _check_replicas(model)
+    rddp = None  # noqa: F841
+    _teardown()

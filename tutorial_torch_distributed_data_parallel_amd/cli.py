@@ -144,10 +144,17 @@ def train_ddp(argv=None):
                                 s["out_dir"], optional_args, s["train"])
         return 0
     world = world_size_from(s)
-    if torch.cuda.is_available() and os.environ.get("TDP_GPU_RELAY", "0") != "1" and \
-            os.environ.get("TDP_GPU_PEER", "0") != "1":
-        # (the relay and peer vehicles share one GPU among ranks)
-        world = min(world, torch.cuda.device_count())
+    # counting devices does not initialise HIP in this (launcher) process
+    have = torch.cuda.device_count()
+    vehicle = os.environ.get("TDP_GPU_RELAY", "0") == "1" or \
+        os.environ.get("TDP_GPU_PEER", "0") == "1"  # (these share one GPU among ranks)
+    if have > 0 and world > have and not vehicle:
+        # the reference fails too (cuda:{rank} does not exist, REF/multi-GPU-training-torch.py
+        # :241); silently training at fewer ranks would change the global batch
+        print(f"train_ddp: local.condor.num_gpus = {world} but only {have} GPU(s) are visible; "
+              f"refusing to train with a different world size (set num_gpus <= {have})",
+              file=sys.stderr, flush=True)
+        return 2
     spawn(basic_ddp_training_loop, world, args=(world, s["out_dir"], optional_args, s["train"]))
     return 0
 

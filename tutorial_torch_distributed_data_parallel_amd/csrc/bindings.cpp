@@ -1423,6 +1423,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_set_bm", &gemm_f32_set_bm);
   m.def("gemm_f32_set_emu", &gemm_f32_set_emu);
   m.def("gemm_f32_emu", &gemm_f32_emu);
+  m.def("wgrad_opt_set_enabled", &wgrad_opt_set_enabled,
+        "A/B: the warp-specialised weight-gradient + optimizer kernel (default on)");
+  m.def("wgrad_opt_enabled", &wgrad_opt_enabled);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
   m.def("ce_fwd", &ce_fwd_op, py::arg("logits"), py::arg("labels"), py::arg("ignore_index"),

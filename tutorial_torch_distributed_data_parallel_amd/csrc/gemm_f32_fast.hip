@@ -1330,7 +1330,11 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (o_splits > 0 && a.rowsum == nullptr) splits = o_splits;
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   plan.grid = 0;
-  if (a.opt.kind != 0) {
+  plan.wgrad_ws = false;
+  if (a.opt.kind != 0 && !a.a_kcontig && !a.b_kcontig && wgrad_opt_ok(a)) {
+    plan.wgrad_ws = true;  // one 512-thread workgroup per CU, roles split (gemm_wgrad_opt.hip)
+    plan.grid = num_cus;
+  } else if (a.opt.kind != 0) {
     // persistent: 2 workgroups per CU (gemm_f32_set_opt_variant overrides, for measurements:
     // 3 fit with FN=1)
     const OptVariant& v = opt_variant();
@@ -1373,6 +1377,10 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   // the optimizer epilogue is instantiated for the weight-gradient layout only (A = dY^T and
   // B = X both MN-contiguous); any other use stores C and applies the flat update afterwards
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
+  if (opt && plan.wgrad_ws) {
+    wgrad_opt_run(a, plan.grid, s);
+    return;
+  }
   if (opt) {
     const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
     // SGD epilogue variant flags (kOptWide | kOptNT | kOptLds, gemm_f32_set_opt_variant).

@@ -140,6 +140,7 @@ class DistributedDataParallel(nn.Module):
         # arena index -> factor slot rows every rank agreed on (max over ranks of the first
         # factored step's batch, one all-reduce); smaller batches are zero-padded to it
         self._factor_cap = {}
+        self._factor_min_cap = 0   # factor_capacity(): a floor for the first step's agreement
         self._factor_mode = {}     # arena index -> sync mode of its last step (sync_plan)
         # arena index -> address of the weight gradient handed to autograd unwritten this step:
         # anything else in p.grad at the hook means another op contributed to the gradient
@@ -502,7 +503,30 @@ class DistributedDataParallel(nn.Module):
             self.world_size > 1
         self._clip_global = float(clip_grad_norm) if clip_grad_norm else None
         self.push_fused_hyper(optimizer, initial=True)
+        if self._factor:
+            # the replicated / sharded / split choice's xGMI input, measured HERE -- eagerly, on
+            # every rank at the same point (registration is part of the setup every rank runs) --
+            # never inside a backward hook: the choice is then fixed before the first
+            # step, and a pinned bandwidth (TDP_FACTOR_BUSBW=GB/s) makes it reproducible
+            self._probe_bandwidth(max(4 * o * n for o, n, _ in self._factor.values()))
         return True
+
+    def factor_capacity(self, rows: int) -> None:
+        """Agree the factored jobs' per-rank slot size (rows of g / x per rank) up front: the max
+        over ranks of ``rows`` and of any slot already agreed. Every rank must call it at the
+        same point, eagerly (one all-reduce). Needed when a later step's per-rank batch can
+        exceed the first factored step's (a resumed ragged batch first): such a step otherwise
+        raises (factor_submit) rather than re-agreeing from a subset of the ranks."""
+        t = torch.tensor([int(rows)] + [int(v) for v in self._factor_cap.values()],
+                         dtype=torch.int64, device=self.device)
+        rt.all_reduce(t, "max")
+        cap = int(t.max().item())
+        self._factor_min_cap = cap
+        for i in list(self._factor_cap):
+            if self._factor_cap[i] != cap:
+                self._factor_cap[i] = cap
+                for k in [k for k in self._factor_bufs if k[0] == i]:
+                    del self._factor_bufs[k]
 
     def _factor_candidates(self) -> dict:
         """Linear weights W[out][in] whose gradient synchronisation can be factored (reducer.h
@@ -795,7 +819,9 @@ class DistributedDataParallel(nn.Module):
             return False
         o, n, _ = self._factor[i]
         B = int(g.shape[0])
-        if self._factor_g_ready.get(i) == (B, g.data_ptr()):
+        # keyed by the tensor's version too: autograd may accumulate another consumer's
+        # gradient into the same storage in place after the early gather
+        if self._factor_g_ready.get(i) == (B, g.data_ptr(), g._version):
             return True  # issued early from the consumer's backward
         cap = self._factor_cap.get(i)
         if cap is None or B > cap or self._factor_x_ready.get(i) != B or \
@@ -814,7 +840,7 @@ class DistributedDataParallel(nn.Module):
             # before the consumer's parameter all-gather on some ranks and after it on others)
             native().factor_stage(g, None, bufs[0], bufs[1], self.rank, 1.0, cap)
             self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o)
-        self._factor_g_ready[i] = (B, g.data_ptr())
+        self._factor_g_ready[i] = (B, g.data_ptr(), g._version)
         return True
 
     def factor_submit(self, p, g: torch.Tensor, x: torch.Tensor, dw=None) -> bool:
@@ -844,26 +870,21 @@ class DistributedDataParallel(nn.Module):
                 raise RuntimeError("DDP factored synchronisation: the first step must run "
                                    "eagerly (it agrees the per-rank batch across ranks) before "
                                    "a hipGraph capture")
-            t = torch.tensor([B], dtype=torch.int64, device=self.device)
+            t = torch.tensor([max(B, self._factor_min_cap)], dtype=torch.int64,
+                             device=self.device)
             rt.all_reduce(t, "max")
             cap = int(t.item())
             self._factor_cap[i] = cap
-            self._probe_bandwidth(4 * o * n)
         if B > cap:
-            if self._gpu and torch.cuda.is_current_stream_capturing():
-                raise RuntimeError(
-                    f"DDP factored synchronisation: per-rank batch {B} exceeds the {cap} rows "
-                    "agreed before this hipGraph capture (the slots are baked into the graph)")
-            # eager: re-agree a larger slot (max over ranks) and reallocate. Under
-            # DistributedSampler / even_batches every rank sees the same batch size at the same
-            # step, so every rank enters this collective together (a first step smaller than
-            # later ones: a resumed ragged batch, a small warm-up batch)
-            t = torch.tensor([B], dtype=torch.int64, device=self.device)
-            rt.all_reduce(t, "max")
-            cap = int(t.item())
-            self._factor_cap[i] = cap
-            for k in [k for k in self._factor_bufs if k[0] == i]:
-                del self._factor_bufs[k]
+            # Fail fast, never re-agree here: only the ranks whose batch exceeds the slot reach
+            # this point, so a collective here would pair with the other ranks' factor
+            # all-gathers (mismatched collectives, a hang until the watchdog). The launcher's
+            # fail-fast then ends every rank. Agree a larger slot up front instead
+            # (factor_capacity, every rank at the same point).
+            raise RuntimeError(
+                f"DDP factored synchronisation: per-rank batch {B} exceeds the {cap} rows agreed "
+                f"at the first factored step; call ddp.factor_capacity({B}) on every rank before "
+                "the first step (or construct DDP with factor_sync=False)")
         if 2 * W * cap * (o + n) > o * n:
             self._factor_mode[i] = "bucket"
             return False
@@ -879,7 +900,7 @@ class DistributedDataParallel(nn.Module):
         # (g_scale) -- one convention whether a rank's slot is read in place (full batch) or
         # staged (ragged batch), since ranks may take different branches in the same step
         g_ready = self._gpu and x_ready and \
-            self._factor_g_ready.pop(i, None) == (B, g.data_ptr())
+            self._factor_g_ready.pop(i, None) == (B, g.data_ptr(), g._version)
         g_src = None
         if g_ready:
             pass  # gathered before the dgrad GEMM (factor_prefetch_g), from g itself
@@ -937,6 +958,18 @@ class DistributedDataParallel(nn.Module):
             plan[names.get(id(p), f"param{i}")] = mode
         return plan
 
+    def factor_report(self) -> dict:
+        """The factored weights' decision inputs and outcome, for the record: replicated rows
+        of each weight's last job (of its ``out`` rows; 0 = sharded), the agreed slot rows and
+        the all-gather bus bandwidth the choice was made with (measured at registration, or
+        pinned by TDP_FACTOR_BUSBW). Pin the rows for a reproducible run with
+        ``factor_replicate`` = {name: True / False / fraction}."""
+        rows = {self._param_name(self.arena.params[i]): {"rep_rows": int(r),
+                                                         "out_rows": int(self._factor[i][0])}
+                for i, r in self._factor_rep.items() if i in self._factor}
+        return {"rows": rows, "slot_rows": sorted(set(self._factor_cap.values())),
+                "busbw": self._busbw}
+
     # Fallback price model when no bandwidth was measured (CPU twin, tests): the replicated
     # update's extra GEMM rows cost 2*W*B*(1 - 1/W) FLOP at ~150 TF/s plus (1 - 1/W) * 16 B of
     # optimizer traffic at ~5 TB/s; the all-gather they replace moves 4 * (W - 1)/W B per element
@@ -953,6 +986,9 @@ class DistributedDataParallel(nn.Module):
         """Measure the all-gather bus bandwidth once (eager, every rank at the same point: the
         first factored step) and agree on the minimum: the measured xGMI input of the
         replicated-vs-sharded choice (parallel/commmodel.py) instead of an assumed constant."""
+        pinned = os.environ.get("TDP_FACTOR_BUSBW")
+        if pinned and self._busbw is None:
+            self._busbw = {"all_gather": float(pinned), "bytes": 0, "pinned": True}
         if self._busbw is not None or not self._gpu or self.world_size == 1 or \
                 rt.comm() is None:
             return

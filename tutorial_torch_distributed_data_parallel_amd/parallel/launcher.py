@@ -68,10 +68,25 @@ class ProcessExitedException(RuntimeError):
         self.rank, self.pid, self.exit_code = rank, pid, exit_code
 
 
+def _one_gpu_vehicle() -> bool:
+    """Several ranks share one GPU through the peer / relay vehicles (parallel/peer.py,
+    parallel/relay.py): they exchange device memory through IPC handles."""
+    return os.environ.get("TDP_GPU_PEER", "0") == "1" or \
+        os.environ.get("TDP_GPU_RELAY", "0") == "1"
+
+
 def _rank_env(rank, nprocs, addr, port, local_offset=0):
-    return {"RANK": str(rank), "LOCAL_RANK": str(rank + local_offset),
-            "WORLD_SIZE": str(nprocs), "LOCAL_WORLD_SIZE": str(nprocs), "MASTER_ADDR": addr,
-            "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    env = {"RANK": str(rank), "LOCAL_RANK": str(rank + local_offset),
+           "WORLD_SIZE": str(nprocs), "LOCAL_WORLD_SIZE": str(nprocs), "MASTER_ADDR": addr,
+           "MASTER_PORT": str(port)}
+    # HSA_ENABLE_IPC_MODE_LEGACY: the ranks inherit whatever the node's environment says (the
+    # MI355X pool this was built on exports 0 for every process: its host driver shares device
+    # memory between processes by dmabuf only, for RCCL's intra-node buffers as for tensors).
+    # The launcher sets it itself only for the one-GPU vehicles, whose cross-process device
+    # memory is the whole mechanism, and never overrides an operator's explicit value.
+    if _one_gpu_vehicle() and "HSA_ENABLE_IPC_MODE_LEGACY" not in os.environ:
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    return env
 
 
 def _child(fn, rank, args, env, err_q):

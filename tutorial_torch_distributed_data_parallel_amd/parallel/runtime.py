@@ -125,7 +125,12 @@ def init_process_group(backend: str | None = None, rank: int | None = None,
     else:
         raise ValueError(f"unknown backend {backend!r}")
 
-    if use_gpu:
+    if use_gpu and peer:
+        from .peer import peer_device
+
+        torch.cuda.set_device(peer_device())  # the one-GPU vehicle: every rank on one device
+        dev = torch.device("cuda", torch.cuda.current_device())
+    elif use_gpu:
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
         dev = torch.device("cuda", torch.cuda.current_device())
     else:

@@ -54,6 +54,7 @@ class CapturedStep:
         from ..parallel.ddp import _LIVE
 
         self.step_fn = step_fn
+        iter0 = {id(d): d._iter for d in list(_LIVE)}
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -63,6 +64,18 @@ class CapturedStep:
         # a bucket rebuild planned by the warm-up must happen now, eagerly: recorded into the
         # graph, its relayout would restore the pre-capture buffers at every replay
         live = list(_LIVE)
+        # the DDPs this step drives: those the warm-up advanced (without a warm-up: every live
+        # one, the conservative answer)
+        used = [d for d in live if warmup == 0 or d._iter != iter0.get(id(d), d._iter)]
+        if any(d.find_unused_parameters for d in used):
+            # which parameters went unused is decided on the host every iteration (the reducer
+            # zeroes their slots): a graph would freeze the capture-time answer. The flag is a
+            # constructor argument, identical on every rank, so every rank refuses alike -- and
+            # BEFORE recording: a recorded-but-never-replayed step would have advanced the
+            # reducer's, the optimizer's and the factored jobs' host-side state
+            torch.cuda.synchronize()
+            raise CaptureFailed("DDP(find_unused_parameters=True): the unused-parameter set is "
+                                "host bookkeeping per iteration; the step runs eagerly")
         for d in live:
             d.settle()
         torch.cuda.synchronize()
@@ -86,13 +99,6 @@ class CapturedStep:
                     self._ddps.append((weakref.ref(d), d._iter - it))
                     d._iter = it
         torch.cuda.synchronize()
-        if any(r().find_unused_parameters for r, _ in self._ddps if r() is not None):
-            # which parameters went unused is decided on the host every iteration (the reducer
-            # zeroes their slots): a graph would freeze the capture-time answer. The flag is a
-            # constructor argument, identical on every rank, so every rank refuses alike.
-            self.graph = None
-            raise CaptureFailed("DDP(find_unused_parameters=True): the unused-parameter set is "
-                                "host bookkeeping per iteration; the step runs eagerly")
 
     def replay(self):
         from ..optim.fused import sync_all_hyper
