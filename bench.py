@@ -393,6 +393,278 @@ def self_launch(a) -> int:
     return 0
 
 
+class BenchFault:
+    """TDP_BENCH_FAULT="name[,name...]" (tests of the fallback ladder): make that rung fail on
+    EVERY rank, at the first attempt only ("name@*": at every attempt). Names: ``tune`` (the
+    factored-mode tuning raises), ``factored`` (setup with factored weights raises), ``fused``
+    (setup with a fused optimizer raises), ``warmup`` (the first warm-up step raises). A capture
+    failure on one rank is TDP_FAULT_CAPTURE=<rank> (train/graph.py)."""
+
+    def __init__(self):
+        spec = [t.strip() for t in os.environ.get("TDP_BENCH_FAULT", "").split(",") if t.strip()]
+        self.once = {t for t in spec if not t.endswith("@*")}
+        self.always = {t[:-2] for t in spec if t.endswith("@*")}
+
+    def check(self, name: str, attempt: int) -> None:
+        if name in self.always or (name in self.once and attempt == 0):
+            raise RuntimeError(f"injected bench fault '{name}' (TDP_BENCH_FAULT)")
+
+
+# The fallback ladder at world size > 1 (VERDICT r4 next 2b): the first real N-GPU run must yield
+# a number, not a crash. Every rung is tried on every rank; a failure anywhere (setup, tuning,
+# warm-up steps) is agreed over all ranks (a host-side MIN all-reduce) and every rank moves to the
+# next rung together. Rung 0 is the full schedule; the last is the reference's own step (plain
+# bucketed all-reduce, optimizer.step(), eager). Inside a rung: a failed factored-mode tuning keeps
+# the model's choice, a failed capture runs that rung eagerly (both agreed, recorded).
+LADDER = (
+    {"name": "full", "factor": None, "fused": True, "graph": True},
+    {"name": "sharded-buckets", "factor": False, "fused": True, "graph": True},
+    {"name": "allreduce+optimizer.step", "factor": False, "fused": False, "graph": True},
+    {"name": "eager-allreduce", "factor": False, "fused": False, "graph": False},
+)
+
+
+def _agree(ok: bool) -> bool:
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import agree
+
+    return agree(ok)
+
+
+def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
+    """One rung's job: model, DDP (or the Accelerate facade), optimizer, data, step closures,
+    tuning and capture. Returns a namespace the caller times; raises on failure."""
+    import types
+
+    import tutorial_torch_distributed_data_parallel_amd as tdp
+    from tutorial_torch_distributed_data_parallel_amd.data import (DeviceLoader,
+                                                                    DistributedSampler,
+                                                                    SyntheticDataset)
+    from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
+        EpochCursor, gather_batch, gather_batch_cursor)
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
+
+    dims, in_shape, use_gpu = ctx.dims, ctx.in_shape, ctx.use_gpu
+    rank, world, dev = ctx.rank, ctx.world, ctx.dev
+    graph = ctx.graph and cfg["graph"]
+    torch.manual_seed(1234 + rank)
+    if a.model == "toy_mlp":
+        model = ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
+    else:
+        model = build_model(a.model, device=dev)
+    if a.syncbn:
+        model = tdp.nn.convert_sync_batchnorm(model)
+    bucket_mb = a.bucket_mb
+    fused = False
+
+    def make_opt(params):
+        if a.optim == "sgd":
+            return tdp.optim.SGD(params, lr=0.01, momentum=0.9)
+        return tdp.optim.Adam(params, lr=1e-3)
+
+    # auto = on: world > 1 shards the update inside the reduction; world 1 applies it in
+    # the weight-gradient GEMM epilogues (the local gradient is already the average)
+    want_fused = a.fused_opt in ("on", "auto") and not a.no_fused_opt and cfg["fused"]
+    acc = torch.zeros(3, device=dev)
+    factor_kw = {} if cfg["factor"] is None else {"factor_sync": cfg["factor"]}
+
+    def loss_fn(out_, y):
+        return tdp.ops.cross_entropy(out_, y, acc=acc)
+
+    if a.api == "accelerate":
+        # BASELINE.json config 4: the step through the Accelerate-style facade. One dataset
+        # shared by all ranks, dealt out by whole batches (Accelerate's BatchSamplerShard).
+        from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
+
+        accel = Accelerator(ddp_kwargs=dict(bucket_cap_mb=bucket_mb, **factor_kw))
+        opt = make_opt(model.parameters())
+        data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
+        loader = DeviceLoader(data, a.batch, drop_last=True)
+        model, opt, loader = accel.prepare(model, opt, loader)
+        # the prepared model's DDP: the wrapper at N > 1, the hidden world-1 DDP of the
+        # unwrapped one-process model (Accelerator.ddp_of)
+        ddp = accel.ddp_of(model)
+        if use_gpu and want_fused and ddp is not None:
+            fused = accel.fuse_optimizer(model, opt)
+        sampler = loader  # set_epoch lives on the prepared loader
+
+        def body(x, y):  # REF/multi-GPU-training-accelerate.py:45-55
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(model(x), y)
+            accel.backward(loss)
+            opt.step()
+            return loss
+    else:
+        ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
+                      bucket_cap_mb=bucket_mb, split_bucket_mb=a.split_mb,
+                      grad_compression=None if a.compression == "none" else a.compression,
+                      **factor_kw)
+        opt = make_opt(ddp.parameters())
+        if use_gpu and want_fused:
+            fused = ddp.register_fused_optimizer(opt)
+        data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
+        sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
+        loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+
+        def body(x, y):  # REF/multi-GPU-training-torch.py:118-126
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(ddp(x), y)
+            tdp.ops.backward(loss)  # loss.backward() seeded by a cached 1: no fill kernel
+            opt.step()
+            return loss
+    if fused:
+        fault.check("fused", attempt)
+    if ddp is not None and ddp._factor:
+        fault.check("factored", attempt)
+
+    def build_rehearsal():
+        """World size 1: the multi-GPU schedule on one GPU (RCCL collectives kept at world
+        size 1, per-bucket fused update instead of the GEMM epilogue, captured step)."""
+        torch.manual_seed(99)
+        m2 = (ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
+              if a.model == "toy_mlp" else build_model(a.model, device=dev))
+        if a.syncbn:
+            m2 = tdp.nn.convert_sync_batchnorm(m2)
+        d2 = tdp.DDP(m2, device_ids=[dev.index], bucket_cap_mb=bucket_mb,
+                     split_bucket_mb=a.split_mb, force_collective=True)
+        o2 = make_opt(d2.parameters())
+        if want_fused:
+            d2.register_fused_optimizer(o2)
+
+        def st():
+            x, y = gather_batch(data.x, data.y, idx_static)
+            o2.zero_grad(set_to_none=True)
+            tdp.ops.backward(loss_fn(d2(x), y))
+            o2.step()
+        return d2, st
+
+    # batches are gathered on the device by the sampler's indices (one H2D copy per epoch);
+    # a captured graph reads them from a static index tensor, eager steps from a slice
+    idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
+    cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices(), "b": None}
+    idx_static.copy_(cur["idx"][:a.batch])
+    # captured toy-MLP step: the gather reads the epoch order through a device-side cursor
+    # it advances itself (no per-step index copy node in the graph)
+    ecur = None
+    if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch):
+        ecur = EpochCursor(len(cur["idx"]), a.batch, dev)
+        ecur.set_order(cur["idx"])
+
+    def advance():
+        if cur["pos"] + a.batch > len(cur["idx"]):
+            cur["epoch"] += 1
+            sampler.set_epoch(cur["epoch"])
+            cur["idx"], cur["pos"] = loader.epoch_indices(), 0
+            if ecur is not None:
+                ecur.set_order(cur["idx"])
+        b = cur["idx"][cur["pos"]: cur["pos"] + a.batch]
+        if graph and ecur is None:
+            idx_static.copy_(b)
+            b = idx_static
+        cur["b"] = b
+        cur["pos"] += a.batch
+
+    def tdp_step():
+        if ecur is not None:
+            x, y = gather_batch_cursor(data.x, data.y, ecur)
+            return body(x, y)
+        b = idx_static if graph else cur["b"]
+        x, y = gather_batch(data.x, data.y, b)
+        return body(x, y)
+
+    advance()
+    run = tdp_step
+    run_pair = [None]  # the two-step graph, when captured
+    if ddp is not None and world > 1 and use_gpu:
+        # measured replicated-vs-sharded choice per factored Linear weight (untimed training
+        # steps, agreed over ranks) before the step is captured -- timed the way the step
+        # will run: captured and replayed when the bench captures it
+        def eager_step():
+            advance()
+            x, y = gather_batch(data.x, data.y, cur["b"])
+            return body(x, y)
+        # also: 0 or 8 CUs left free for RCCL's kernels while the persistent epilogue GEMMs
+        # run (profiles/micro/comm_cus_ab.txt: 8 cost 3 % at dp1, whether they pay at N > 1
+        # only the real node can tell), unless --comm-cus fixed it
+        cus = (0, 8) if a.comm_cus is None else None
+        from tutorial_torch_distributed_data_parallel_amd._native import native
+
+        cus0 = int(native().reserved_cus())
+        ok, err = True, None
+        try:
+            fault.check("tune", attempt)
+            if graph:
+                ddp.tune_factor_replicate(tdp_step, iters=20, capture=True, comm_cus=cus,
+                                          repeats=2)
+            else:
+                ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
+        except Exception as e:  # noqa: BLE001 - the ladder's first rung: keep the model's choice
+            ok, err = False, e
+        if not _agree(ok):
+            # every rank drops the tuning result alike: the auto rule decides each weight
+            native().set_reserved_cus(cus0)
+            ddp.factor_replicate = None
+            ddp.factor_tuning = None
+            if hasattr(ddp, "consolidate_optimizer_state"):
+                ddp.consolidate_optimizer_state()
+            fallbacks.append(f"{cfg['name']}: factored-mode tuning failed "
+                             f"({repr(err)[:160] if err else 'on another rank'}); kept the "
+                             "model's choice")
+    if graph:
+        from tutorial_torch_distributed_data_parallel_amd.train.graph import (CapturedStep,
+                                                                              try_capture)
+
+        run = try_capture(tdp_step, warmup=3,
+                          log=lambda m: print(m, file=sys.stderr, flush=True))
+        if not isinstance(run, CapturedStep):
+            fallbacks.append(f"{cfg['name']}: hipGraph capture failed (agreed over ranks); "
+                             "the step runs eagerly")
+        if ecur is not None and a.graph_steps == 2 and isinstance(run, CapturedStep):
+            # two training steps per replay (the device cursor advances per gather): half
+            # the graph launches; every step still runs all of its work
+            def two_steps():
+                tdp_step()
+                return tdp_step()
+            # no eager warm-up: the one-step graph's warm-up already did it, and training
+            # steps outside the count would make the run differ from --graph-steps 1
+            run2 = try_capture(two_steps, warmup=0,
+                               log=lambda m: print(m, file=sys.stderr, flush=True))
+            if run2 is not two_steps:
+                run_pair[0] = run2
+        if ecur is not None:
+            # the warm-up / capture runs advanced the device cursor: restart the epoch's
+            # order so host and device positions agree from the first timed step on
+            ecur.set_order(cur["idx"])
+            cur["pos"] = 0
+
+    def step():
+        advance()
+        return run()
+
+    def steps(n):
+        """n training steps; pairs through the two-step graph while both fall in the
+        current epoch (the host advances its position for each)."""
+        k, out = 0, None
+        while k < n:
+            if run_pair[0] is not None and n - k >= 2 and \
+                    cur["pos"] + 2 * a.batch <= len(cur["idx"]):
+                advance()
+                advance()
+                out = run_pair[0]()
+                k += 2
+            else:
+                out = step()
+                k += 1
+        return out
+    step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
+    step.many = steps
+    step.graph_steps = 2 if run_pair[0] is not None else (1 if graph else 0)
+    return types.SimpleNamespace(ddp=ddp, opt=opt, fused=fused, step=step, run=run,
+                                 graph=graph, rung=cfg["name"],
+                                 build_rehearsal=None if a.api == "accelerate"
+                                 else build_rehearsal)
+
+
 def main():
     a = parse()
     if a.gpus > 1 and not _launcher_env():
@@ -414,16 +686,14 @@ def main():
         a.impl == "tdp"
     in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
     fused = False
+    fallbacks = []
+    rung = None
+    job = None
 
     if a.impl == "tdp":
+        import types
+
         import tutorial_torch_distributed_data_parallel_amd as tdp
-        from tutorial_torch_distributed_data_parallel_amd.data import (DeviceLoader,
-                                                                        DistributedSampler,
-                                                                        SyntheticDataset)
-        from tutorial_torch_distributed_data_parallel_amd.data.synthetic import (
-            EpochCursor, gather_batch, gather_batch_cursor)
-        from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
-        from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
         from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
 
         if a.comm_cus is not None and use_gpu:
@@ -432,70 +702,11 @@ def main():
             _nat().set_reserved_cus(a.comm_cus)
         tdp.init_process_group("nccl" if use_gpu else "gloo")
         rank, world, dev = rt.get_rank(), rt.get_world_size(), rt.device()
-        torch.manual_seed(1234 + rank)
-        if a.model == "toy_mlp":
-            model = ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
-        else:
-            model = build_model(a.model, device=dev)
-        if a.syncbn:
-            model = tdp.nn.convert_sync_batchnorm(model)
-        bucket_mb = a.bucket_mb
-
-        def make_opt(params):
-            if a.optim == "sgd":
-                return tdp.optim.SGD(params, lr=0.01, momentum=0.9)
-            return tdp.optim.Adam(params, lr=1e-3)
-
-        # auto = on: world > 1 shards the update inside the reduction; world 1 applies it in
-        # the weight-gradient GEMM epilogues (the local gradient is already the average)
-        want_fused = a.fused_opt in ("on", "auto") and not a.no_fused_opt
         barrier = rt.barrier
         finish = tdp.destroy_process_group
-        acc = torch.zeros(3, device=dev)
-
-        def loss_fn(out_, y):
-            return tdp.ops.cross_entropy(out_, y, acc=acc)
-
-        if a.api == "accelerate":
-            # BASELINE.json config 4: the step through the Accelerate-style facade. One dataset
-            # shared by all ranks, dealt out by whole batches (Accelerate's BatchSamplerShard).
-            from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
-
-            accel = Accelerator(ddp_kwargs=dict(bucket_cap_mb=bucket_mb))
-            opt = make_opt(model.parameters())
-            data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
-            loader = DeviceLoader(data, a.batch, drop_last=True)
-            model, opt, loader = accel.prepare(model, opt, loader)
-            # the prepared model's DDP: the wrapper at N > 1, the hidden world-1 DDP of the
-            # unwrapped one-process model (Accelerator.ddp_of)
-            ddp = accel.ddp_of(model)
-            if use_gpu and want_fused and ddp is not None:
-                fused = accel.fuse_optimizer(model, opt)
-            sampler = loader  # set_epoch lives on the prepared loader
-
-            def body(x, y):  # REF/multi-GPU-training-accelerate.py:45-55
-                opt.zero_grad(set_to_none=True)
-                loss = loss_fn(model(x), y)
-                accel.backward(loss)
-                opt.step()
-                return loss
-        else:
-            ddp = tdp.DDP(model, device_ids=[dev.index] if use_gpu else None,
-                          bucket_cap_mb=bucket_mb, split_bucket_mb=a.split_mb,
-                          grad_compression=None if a.compression == "none" else a.compression)
-            opt = make_opt(ddp.parameters())
-            if use_gpu and want_fused:
-                fused = ddp.register_fused_optimizer(opt)
-            data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
-            sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
-            loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
-
-            def body(x, y):  # REF/multi-GPU-training-torch.py:118-126
-                opt.zero_grad(set_to_none=True)
-                loss = loss_fn(ddp(x), y)
-                tdp.ops.backward(loss)  # loss.backward() seeded by a cached 1: no fill kernel
-                opt.step()
-                return loss
+        ctx = types.SimpleNamespace(dims=dims, in_shape=in_shape, use_gpu=use_gpu, rank=rank,
+                                    world=world, dev=dev, graph=graph)
+        fault = BenchFault()
     else:
         import torch.distributed as dist
         import torch.nn as nn
@@ -560,163 +771,75 @@ def main():
             return loss
 
     sync = (torch.cuda.synchronize if use_gpu else (lambda: None))
-    epoch = [0]
-    it = [iter(loader)]
-
-    def next_batch():
-        try:
-            return next(it[0])
-        except StopIteration:
-            epoch[0] += 1
-            sampler.set_epoch(epoch[0])
-            it[0] = iter(loader)
-            return next(it[0])
-
     build_rehearsal = None
-    if a.impl == "tdp":
-        def build_rehearsal():
-            """World size 1: the multi-GPU schedule on one GPU (RCCL collectives kept at world
-            size 1, per-bucket fused update instead of the GEMM epilogue, captured step)."""
-            torch.manual_seed(99)
-            m2 = (ToyMLP(in_features=dims[0], hidden=dims[1:], batchnorm=a.syncbn, device=dev)
-                  if a.model == "toy_mlp" else build_model(a.model, device=dev))
-            if a.syncbn:
-                m2 = tdp.nn.convert_sync_batchnorm(m2)
-            d2 = tdp.DDP(m2, device_ids=[dev.index], bucket_cap_mb=bucket_mb,
-                         split_bucket_mb=a.split_mb, force_collective=True)
-            o2 = make_opt(d2.parameters())
-            if want_fused:
-                d2.register_fused_optimizer(o2)
+    if a.impl != "tdp":
+        epoch = [0]
+        it = [iter(loader)]
 
-            def st():
-                x, y = gather_batch(data.x, data.y, idx_static)
-                o2.zero_grad(set_to_none=True)
-                tdp.ops.backward(loss_fn(d2(x), y))
-                o2.step()
-            return d2, st
+        def next_batch():
+            try:
+                return next(it[0])
+            except StopIteration:
+                epoch[0] += 1
+                sampler.set_epoch(epoch[0])
+                it[0] = iter(loader)
+                return next(it[0])
 
-        # batches are gathered on the device by the sampler's indices (one H2D copy per epoch);
-        # a captured graph reads them from a static index tensor, eager steps from a slice
-        idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
-        cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices(), "b": None}
-        idx_static.copy_(cur["idx"][:a.batch])
-        # captured toy-MLP step: the gather reads the epoch order through a device-side cursor
-        # it advances itself (no per-step index copy node in the graph)
-        ecur = None
-        if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch):
-            ecur = EpochCursor(len(cur["idx"]), a.batch, dev)
-            ecur.set_order(cur["idx"])
-
-        def advance():
-            if cur["pos"] + a.batch > len(cur["idx"]):
-                cur["epoch"] += 1
-                sampler.set_epoch(cur["epoch"])
-                cur["idx"], cur["pos"] = loader.epoch_indices(), 0
-                if ecur is not None:
-                    ecur.set_order(cur["idx"])
-            b = cur["idx"][cur["pos"]: cur["pos"] + a.batch]
-            if graph and ecur is None:
-                idx_static.copy_(b)
-                b = idx_static
-            cur["b"] = b
-            cur["pos"] += a.batch
-
-        def tdp_step():
-            if ecur is not None:
-                x, y = gather_batch_cursor(data.x, data.y, ecur)
-                return body(x, y)
-            b = idx_static if graph else cur["b"]
-            x, y = gather_batch(data.x, data.y, b)
-            return body(x, y)
-
-        advance()
-        run = tdp_step
-        run_pair = [None]  # the two-step graph, when captured
-        if a.impl == "tdp" and ddp is not None and world > 1 and use_gpu:
-            # measured replicated-vs-sharded choice per factored Linear weight (untimed training
-            # steps, agreed over ranks) before the step is captured -- timed the way the step
-            # will run: captured and replayed when the bench captures it
-            def eager_step():
-                advance()
-                tdp_step_eager()
-
-            def tdp_step_eager():
-                x, y = gather_batch(data.x, data.y, cur["b"])
-                return body(x, y)
-            # also: 0 or 8 CUs left free for RCCL's kernels while the persistent epilogue GEMMs
-            # run (profiles/micro/comm_cus_ab.txt: 8 cost 3 % at dp1, whether they pay at N > 1
-            # only the real node can tell), unless --comm-cus fixed it
-            cus = (0, 8) if a.comm_cus is None else None
-            if graph:
-                ddp.tune_factor_replicate(tdp_step, iters=20, capture=True, comm_cus=cus,
-                                          repeats=2)
-            else:
-                ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
-        if graph:
-            from tutorial_torch_distributed_data_parallel_amd.train.graph import (CapturedStep,
-                                                                                  try_capture)
-
-            run = try_capture(tdp_step, warmup=3,
-                              log=lambda m: print(m, file=sys.stderr, flush=True))
-            if ecur is not None and a.graph_steps == 2 and isinstance(run, CapturedStep):
-                # two training steps per replay (the device cursor advances per gather): half
-                # the graph launches; every step still runs all of its work
-                def two_steps():
-                    tdp_step()
-                    return tdp_step()
-                # no eager warm-up: the one-step graph's warm-up already did it, and training
-                # steps outside the count would make the run differ from --graph-steps 1
-                run2 = try_capture(two_steps, warmup=0,
-                                   log=lambda m: print(m, file=sys.stderr, flush=True))
-                if run2 is not two_steps:
-                    run_pair[0] = run2
-            if ecur is not None:
-                # the warm-up / capture runs advanced the device cursor: restart the epoch's
-                # order so host and device positions agree from the first timed step on
-                ecur.set_order(cur["idx"])
-                cur["pos"] = 0
-
-        def step():
-            advance()
-            return run()
-
-        def steps(n):
-            """n training steps; pairs through the two-step graph while both fall in the
-            current epoch (the host advances its position for each)."""
-            k, out = 0, None
-            while k < n:
-                if run_pair[0] is not None and n - k >= 2 and \
-                        cur["pos"] + 2 * a.batch <= len(cur["idx"]):
-                    advance()
-                    advance()
-                    out = run_pair[0]()
-                    k += 2
-                else:
-                    out = step()
-                    k += 1
-            return out
-        step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
-        step.many = steps
-        step.graph_steps = 2 if run_pair[0] is not None else (1 if graph else 0)
-        if a.api == "accelerate":
-            build_rehearsal = None
-    else:
         def step():
             return run_step(*next_batch())
 
-    if use_gpu:
-        mode = a.warmup_mode if a.warmup_mode != "auto" else \
-            ("scratch" if a.model == "toy_mlp" else "gemm")
-        if a.impl == "tdp" and mode == "scratch":
-            scratch_warmup(a, dims, in_shape, dev)
+    def clock_warmup():
+        if use_gpu:
+            mode = a.warmup_mode if a.warmup_mode != "auto" else \
+                ("scratch" if a.model == "toy_mlp" else "gemm")
+            if a.impl == "tdp" and mode == "scratch":
+                scratch_warmup(a, dims, in_shape, dev)
+            else:
+                device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
+
+    if a.impl == "tdp":
+        # the fallback ladder (LADDER): build a rung, run its W warm-up steps; any failure on
+        # any rank moves every rank to the next rung. World size 1 has no collectives to lose
+        # and tries the full rung only, as before.
+        import gc
+
+        rungs = LADDER if world > 1 or os.environ.get("TDP_BENCH_LADDER") == "1" else LADDER[:1]
+        for attempt, cfg in enumerate(rungs):
+            ok, err = True, None
+            try:
+                job = build_tdp(a, ctx, cfg, attempt, fallbacks, fault)
+                if attempt == 0:
+                    clock_warmup()
+                fault.check("warmup", attempt)
+                job.step.many(a.warmup)
+                sync()
+            except Exception as e:  # noqa: BLE001 - agreed below, then the next rung
+                ok, err = False, e
+                if len(rungs) == 1:
+                    raise
+            if _agree(ok):
+                break
+            fallbacks.append(f"{cfg['name']} failed ({repr(err)[:200] if err else 'on another rank'})"
+                             "; next rung")
+            print(f"[bench] rung {cfg['name']} failed on some rank: {err!r}", file=sys.stderr,
+                  flush=True)
+            job = None
+            gc.collect()
+            if use_gpu:
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
         else:
-            device_warmup(dev, a.device_warmup_ms, a.impl == "tdp")
-    many = getattr(step, "many", None)
-    if many is not None:
-        many(a.warmup)
+            print("[bench] every rung of the fallback ladder failed: no timed step ran",
+                  file=sys.stderr, flush=True)
+            sys.exit(1)
+        ddp, opt, fused, step, run, graph = (job.ddp, job.opt, job.fused, job.step, job.run,
+                                             job.graph)
+        build_rehearsal, rung = job.build_rehearsal, job.rung
     else:
+        clock_warmup()
         for _ in range(a.warmup):
             step()
+    many = getattr(step, "many", None)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -805,6 +928,9 @@ def main():
                 "comm_nranks": comm_nranks,
                 # training steps per hipGraph replay (0: eager)
                 "graph_steps": getattr(step, "graph_steps", None),
+                # the fallback ladder (LADDER): the rung that ran and what failed before it
+                "rung": rung,
+                "fallbacks": fallbacks,
                 "baseline": {"samples_per_s": round(base, 2), "source": base_src}
                 if base else None,
             },

@@ -177,3 +177,245 @@ def rccl_watchdog_child():
 
 if __name__ == "__main__":
     rccl_watchdog_child()
+
+
+def _eager_vs_captured(step1, step2, batches, sx, sy, fill=None):
+    """Run step1 eagerly on each batch and step2 as a captured graph (one real warm-up step on
+    the first batch, then replays) on the same batches, fed through the static buffers."""
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    g = None
+    for x, y in batches:
+        step1(x, y)
+        if fill is not None:
+            fill(x, y)
+        else:
+            sx.copy_(x)
+            sy.copy_(y)
+        if g is None:
+            g = CapturedStep(step2, warmup=1)
+        else:
+            g.replay()
+    torch.cuda.synchronize()
+    return g
+
+
+def _assert_bitwise(m1, m2, tag):
+    r = rt.get_rank()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a, b), f"rank {r} {tag}: captured != eager for {n} " \
+                                  f"(max diff {float((a - b).abs().max())})"
+    for (n, a), b in zip(m1.named_buffers(), m2.buffers()):
+        if a.is_floating_point():
+            assert torch.equal(a, b), f"rank {r} {tag}: captured != eager for buffer {n}"
+
+
+def captured_syncbn_parity(rank, out_dir, steps=5):
+    """BASELINE config 3 (toy MLP + SyncBatchNorm) as a CAPTURED multi-rank step with real peers:
+    the forward statistics all-gather and the backward all-reduce of every BN layer are recorded
+    inline on the compute stream, the bucket / factored collectives on the side stream. Captured
+    == eager bitwise (parameters and running stats) on every rank; both == BN over the global
+    batch (the fp32 torch oracle); replicas identical."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    tdp.init_process_group("peer")
+    r, W = rt.get_rank(), rt.get_world_size()
+
+    def build():
+        torch.manual_seed(0)
+        m = tdp.nn.convert_sync_batchnorm(ToyMLP(**DIMS, batchnorm=True, device="cuda"))
+        d = tdp.DDP(m, device_ids=[rt.device().index])
+        o = tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+        assert d.register_fused_optimizer(o)
+        return m, d, o
+
+    m1, d1, o1 = build()
+    m2, d2, o2 = build()
+    ref = _torch_mlp(m1)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    sx = torch.empty(B, DIMS["in_features"], device="cuda")
+    sy = torch.empty(B, dtype=torch.long, device="cuda")
+
+    def step1(x, y):
+        o1.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d1(x), y))
+        o1.step()
+
+    def step2():
+        o2.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d2(sx), sy))
+        o2.step()
+
+    batches = [_batch(r, s) for s in range(steps)]
+    _eager_vs_captured(step1, step2, batches, sx, sy)
+    for s in range(steps):
+        ropt.zero_grad(set_to_none=True)
+        xs, ys = zip(*[_batch(k, s) for k in range(W)])
+        out = ref(torch.cat(xs))
+        sum(F.cross_entropy(o, t) for o, t in zip(out.split(B), ys)).div(W).backward()
+        ropt.step()
+    _assert_bitwise(m1, m2, f"SyncBN W={W}")
+    _close(m2, ref, f"captured SyncBN W={W}", atol=1e-4, rtol=1e-3)
+    bns = [m for m in m2.modules() if hasattr(m, "running_mean")]
+    rbns = [m for m in ref.modules() if isinstance(m, nn.BatchNorm1d)]
+    assert len(bns) == len(rbns) > 0
+    for a, b in zip(bns, rbns):
+        torch.testing.assert_close(a.running_mean, b.running_mean, atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(a.running_var, b.running_var, atol=1e-4, rtol=1e-4)
+    d1.check_replicas()
+    d2.check_replicas()
+    rt.barrier()
+    tdp.destroy_process_group()
+
+
+def captured_accelerate_parity(rank, out_dir, steps=5):
+    """BASELINE config 4: the step through the Accelerate-style facade (prepare -> DDP, fused
+    optimizer, accelerator.backward) CAPTURED with real peers == eager bitwise; both == the fp32
+    torch oracle (mean over ranks of each rank's mean-loss gradient)."""
+    from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
+
+    tdp.init_process_group("peer")
+    r, W = rt.get_rank(), rt.get_world_size()
+    accel = Accelerator()
+    assert accel.num_processes == W
+
+    def build():
+        torch.manual_seed(0)
+        m = ToyMLP(**DIMS, device="cuda")
+        o = tdp.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+        pm, po = accel.prepare(m, o)
+        assert accel.fuse_optimizer(pm, po)
+        return m, pm, po
+
+    m1, p1, o1 = build()
+    m2, p2, o2 = build()
+    ref = _torch_mlp(m1)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    sx = torch.empty(B, DIMS["in_features"], device="cuda")
+    sy = torch.empty(B, dtype=torch.long, device="cuda")
+
+    def step1(x, y):  # REF/multi-GPU-training-accelerate.py:45-55
+        o1.zero_grad()
+        accel.backward(tdp.ops.cross_entropy(p1(x), y))
+        o1.step()
+
+    def step2():
+        o2.zero_grad()
+        accel.backward(tdp.ops.cross_entropy(p2(sx), sy))
+        o2.step()
+
+    _eager_vs_captured(step1, step2, [_batch(r, s) for s in range(steps)], sx, sy)
+    for s in range(steps):
+        _oracle_step(ref, ropt, W, s, -1, -1)
+    _assert_bitwise(m1, m2, f"Accelerate W={W}")
+    _close(m2, ref, f"captured Accelerate W={W}")
+    accel.ddp_of(p2).check_replicas()
+    rt.barrier()
+    tdp.destroy_process_group()
+
+
+class SmallCNN(torch.nn.Module):
+    """conv -> SyncBN -> ReLU -> pool, twice, -> Linear: the ResNet-style CNN path (implicit-GEMM
+    convolutions, BN, pooling, several gradient buckets) at a size a unit test can run."""
+
+    def __init__(self):
+        super().__init__()
+        nn = tdp.nn
+        self.conv1 = nn.Conv2d(4, 32, 3, padding=1, device="cuda")
+        self.bn1 = nn.BatchNorm2d(32, device="cuda")
+        self.pool1 = nn.MaxPool2d(2)
+        self.conv2 = nn.Conv2d(32, 64, 3, padding=1, device="cuda")
+        self.bn2 = nn.BatchNorm2d(64, device="cuda")
+        self.pool2 = nn.MaxPool2d(2)
+        self.fc = nn.Linear(64 * 4 * 4, 10, device="cuda")
+
+    def forward(self, x):
+        from tutorial_torch_distributed_data_parallel_amd import ops
+
+        x = self.pool1(torch.relu(self.bn1(self.conv1(x))))
+        x = self.pool2(torch.relu(self.bn2(self.conv2(x))))
+        return self.fc(ops.flatten(x))
+
+
+def _torch_cnn(m):
+    import torch.nn as nn
+
+    ref = nn.Sequential(nn.Conv2d(4, 32, 3, padding=1), nn.BatchNorm2d(32), nn.ReLU(),
+                        nn.MaxPool2d(2), nn.Conv2d(32, 64, 3, padding=1), nn.BatchNorm2d(64),
+                        nn.ReLU(), nn.MaxPool2d(2), nn.Flatten(), nn.Linear(64 * 4 * 4, 10))
+    ref = ref.cuda()
+    src = [m.conv1, m.bn1, m.conv2, m.bn2, m.fc]
+    dst = [ref[0], ref[1], ref[4], ref[5], ref[9]]
+    with torch.no_grad():
+        for a, b in zip(src, dst):
+            for (n, p) in a.named_parameters():
+                getattr(b, n).copy_(p.contiguous())
+    return ref
+
+
+def _cnn_batch(r, step, n=8):
+    g = torch.Generator(device="cuda").manual_seed(100 * step + r)
+    x = torch.randn(n, 4, 16, 16, device="cuda", generator=g)
+    return x.contiguous(memory_format=torch.channels_last), \
+        torch.randint(0, 10, (n,), device="cuda", generator=g)
+
+
+def captured_cnn_parity(rank, out_dir, steps=4):
+    """BASELINE config 5 in miniature: a conv + SyncBN + pool + Linear CNN whose gradients go
+    through several buckets (small caps, split parameters) with the sharded fused update,
+    CAPTURED with real peers == eager bitwise (parameters, running stats); both == the global-
+    batch fp32 torch oracle."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    tdp.init_process_group("peer")
+    r, W = rt.get_rank(), rt.get_world_size()
+
+    def build():
+        torch.manual_seed(0)
+        m = tdp.nn.convert_sync_batchnorm(SmallCNN())
+        d = tdp.DDP(m, device_ids=[rt.device().index], bucket_cap_mb=0.02,
+                    first_bucket_cap_mb=0.004, split_bucket_mb=0.01)
+        o = tdp.optim.SGD(d.parameters(), lr=0.05, momentum=0.9)
+        assert d.register_fused_optimizer(o)
+        return m, d, o
+
+    m1, d1, o1 = build()
+    m2, d2, o2 = build()
+    assert len(d2._bounds) - 1 >= 4, d2._bounds  # several buckets, split parameters
+    ref = _torch_cnn(m1)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    sx = torch.empty(8, 4, 16, 16, device="cuda").contiguous(memory_format=torch.channels_last)
+    sy = torch.empty(8, dtype=torch.long, device="cuda")
+
+    def step1(x, y):
+        o1.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d1(x), y))
+        o1.step()
+
+    def step2():
+        o2.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(d2(sx), sy))
+        o2.step()
+
+    _eager_vs_captured(step1, step2, [_cnn_batch(r, s) for s in range(steps)], sx, sy)
+    for s in range(steps):
+        ropt.zero_grad(set_to_none=True)
+        xs, ys = zip(*[_cnn_batch(k, s) for k in range(W)])
+        out = ref(torch.cat(xs))
+        sum(F.cross_entropy(o, t) for o, t in zip(out.split(8), ys)).div(W).backward()
+        ropt.step()
+    _assert_bitwise(m1, m2, f"CNN W={W}")
+    for (n, p), q in zip(m2.named_parameters(),
+                         [ref[0].weight, ref[0].bias, ref[1].weight, ref[1].bias, ref[4].weight,
+                          ref[4].bias, ref[5].weight, ref[5].bias, ref[9].weight, ref[9].bias]):
+        torch.testing.assert_close(p.detach().contiguous(), q.detach().contiguous(), atol=1e-4,
+                                   rtol=1e-3, msg=lambda s: f"CNN W={W} {n}: {s}")
+    for a, b in ((m2.bn1, ref[1]), (m2.bn2, ref[5])):
+        torch.testing.assert_close(a.running_mean, b.running_mean, atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(a.running_var, b.running_var, atol=1e-4, rtol=1e-4)
+    d1.check_replicas()
+    d2.check_replicas()
+    rt.barrier()
+    tdp.destroy_process_group()

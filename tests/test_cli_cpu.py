@@ -141,3 +141,35 @@ def test_launcher_hosts_the_rendezvous_store():
     assert store.get("k") == b"v"
     one, _, env1 = _launcher_store("127.0.0.1", 1)
     assert one is None and env1 == {}
+
+
+def _bench_cpu2(env_extra):
+    env = {k: None for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    env.update(env_extra)
+    return _run(["bench.py", "--cpu", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                 "--dataset", "128", "--batch", "16", "--mlp-dims", "64,32,32"], env_extra=env)
+
+
+def test_bench_fallback_ladder_records_the_rung():
+    """a failure in a rung (here: the first warm-up step, on every rank)
+    moves every rank to the next rung, and the record says which rung ran and why."""
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert rec["config"]["rung"] == "sharded-buckets", rec["config"]
+    assert len(rec["config"]["fallbacks"]) == 1 and "full failed" in rec["config"]["fallbacks"][0]
+    assert rec["value"] > 0 and rec["steps"] == 2
+
+
+def test_bench_fallback_ladder_exhausted_exits_nonzero():
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"})
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "every rung of the fallback ladder failed" in r.stderr
+
+
+def test_bench_clean_run_reports_no_fallback():
+    r = _bench_cpu2({})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert rec["config"]["rung"] == "full" and rec["config"]["fallbacks"] == []

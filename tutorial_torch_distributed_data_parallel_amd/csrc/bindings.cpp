@@ -1426,6 +1426,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_opt_set_enabled", &wgrad_opt_set_enabled,
         "A/B: the warp-specialised weight-gradient + optimizer kernel (default on)");
   m.def("wgrad_opt_enabled", &wgrad_opt_enabled);
+  m.def("gemm_f32_set_lockstep", &gemm_f32_set_lockstep,
+        "A/B: the lockstep weight-gradient + optimizer kernel (default on)");
+  m.def("gemm_f32_lockstep", &gemm_f32_lockstep);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
   m.def("ce_fwd", &ce_fwd_op, py::arg("logits"), py::arg("labels"), py::arg("ignore_index"),

@@ -155,6 +155,8 @@ constexpr int kOptWide = 4;  // wider HBM batches: register SGD both row tiles, 
 constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
 constexpr int kOptLds = 16;  // 128-wide paired tiles: gradient tile staged through LDS,
                              // float4 p / optimizer-state traffic (SGD and Adam)
+constexpr int kOptG = 32;    // the lockstep kernel's math waves: the finished gradient tile goes
+                             // to the LDS buffer after the stages (wgrad_lockstep_kernel), no update
 
 template <bool NT>
 __device__ __forceinline__ f32x2 ld_epi(const float* q) {
@@ -742,6 +744,25 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
     // OPTK = kind (1 SGD, 2 Adam) | kOptWide (PAIR SGD: both row tiles in one batch, one HBM
     // round trip per tile) | kOptNT (non-temporal p / state traffic: touched once per step, so it
     // should not evict the L2-resident dY / X operand tiles)
+    if constexpr ((OPTK & kOptG) != 0) {
+      // lockstep kernel: the stream waves read the previous tile's gradient from G until the
+      // first barrier here; the second publishes this tile's. Two barriers, always (the stream
+      // waves count them).
+      static_assert(FN == 2 && FM == 2 && !AK && !BKC, "kOptG: the 128 x 128 MN x MN tile");
+      float* G = reinterpret_cast<float*>(smem + S * STG);
+      __syncthreads();
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int lr = wm * 64 + 2 * rl + f;
+          *reinterpret_cast<f32x2*>(G + lr * BN + wn * 64 + 2 * l31) =
+              f32x2{acc[f][0][r], acc[f][FN - 1][r]};
+        }
+      __syncthreads();
+      return;
+    }
     constexpr bool SGD = (OPTK & 3) == 1;
     constexpr bool NT = (OPTK & kOptNT) != 0;
     // per-step scalars from the device hyper block (graph-replay safe, kernels.h HyperSlot)
@@ -1203,6 +1224,157 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ge
   }
 }
 
+// Weight gradient + optimizer update with the roles split inside ONE 512-thread workgroup per
+// CU, in lockstep (profiles/r9/wgrad_lockstep_r9*.md). The persistent epilogue kernel above
+// alternates, in every workgroup, a K loop (no HBM traffic) with an HBM-bound update; the two
+// workgroups of a CU overlap those phases only by chance. Here waves 0-3 run exactly that K
+// loop (gemm_tile, kOptG: the 2-stage LDS-DMA pipeline, split-bf16 MFMAs -- bit-identical
+// gradients) for tile j while waves 4-7 stream the update of tile j - 1 (p / state loads of the
+// next chunk group always in flight, non-temporal), reading its gradient from an LDS buffer G.
+// Both roles execute the same barriers: the K loop's one per 32-deep K tile, two around the G
+// hand-over and one per tile -- the stream waves place their four chunk groups on the K loop's
+// barrier intervals, and a last step with no K work drains the final tile. No spin-waits, no
+// counters: the hardware barrier is the hand-over. (A version with independent roles and LDS
+// counters lost to the math waves' operand latency: gemm_wgrad_opt.hip.)
+template <int KIND>
+__global__ __launch_bounds__(2 * kT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+wgrad_lockstep_kernel(FastParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = smem_raw;
+  constexpr int S = 2, FN = 2, FM = 2;
+  constexpr int STG = 64 * FM * kBK * 4 + 64 * FN * kBK * 4;
+  constexpr int OPTK = KIND | kOptG;
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
+  const int T = p.tiles_m * p.tiles_n;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int per = q8 + (xcd < r8 ? 1 : 0);
+  const int before = xcd * q8 + (xcd < r8 ? xcd : r8);
+  const int t0 = (int)((long)T * before / nwg), t1 = (int)((long)T * (before + per) / nwg);
+  const int j0 = b / 8;
+  const int ntiles = t1 - t0 > j0 ? (t1 - t0 - j0 + per - 1) / per : 0;
+  const int nk = (p.K + kBK - 1) / kBK;  // the K loop's barriers per tile (K % 128 == 0: 4n)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < 4) {
+    for (int j = 0; j < ntiles; ++j) {
+      gemm_tile<FN, kDenseMN, kDenseMN, S, OPTK, FM, true>(p, t0 + j0 + j * per, smem);
+      __builtin_amdgcn_s_barrier();  // every wave is done with this tile's LDS stages
+    }
+    // the drain step: the stream waves update the last tile; match their barriers
+    if (ntiles > 0) {
+      for (int q = 0; q < nk + 3; ++q) __builtin_amdgcn_s_barrier();
+    }
+    return;
+  }
+  // ---------------------------------------------------------------- stream waves (4-7)
+  constexpr bool SGD = KIND == 1;
+  constexpr int BN = 64 * FN;
+  constexpr int IT = 128 * (BN / 4) / kT;  // 16-B chunks per thread per tile (16)
+  constexpr int GI = IT / 4;               // chunks per group (4 groups per tile)
+  constexpr int NS = SGD ? 2 : 3;
+  const float* G = reinterpret_cast<const float*>(smem + S * STG);
+  const int ts = threadIdx.x - kT;
+  OptEpilogue o = p.opt;
+  if constexpr (SGD) load_hyper(o.sgd);
+  else load_hyper(o.adam);
+  const bool mom_rd = SGD && o.sgd.momentum != 0.f && !o.sgd.first_step;
+  const bool mom_wr = SGD && o.sgd.momentum != 0.f;
+  const long step8 = 8 * p.ldc;
+  struct Tile {
+    long base;
+    int rows;
+    bool col_ok;
+  };
+  auto tile_of = [&](int j) -> Tile {
+    const int lid = t0 + j0 + j * per;
+    const int tm = lid / p.tiles_n, tn = lid - tm * p.tiles_n;  // gemm_tile's order
+    const int row = tm * 128 + (ts >> 5), col = tn * BN + (ts & 31) * 4;
+    Tile t;
+    t.col_ok = col < p.N;
+    t.rows = row < p.M ? min(IT, (p.M - row + 7) / 8) : 0;
+    t.base = (long)min(row, p.M - 1) * p.ldc + min(col, p.N - 4);
+    return t;
+  };
+  struct Set {
+    f32x4 v[NS][GI];
+  };
+  auto issue = [&](const Tile& t, int g, Set& s) {
+#pragma unroll
+    for (int u = 0; u < GI; ++u) {
+      const int it = g * GI + u;
+      const long q = t.base + (it < t.rows ? it * step8 : 0);
+      s.v[0][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.p + q));
+      if constexpr (SGD) {
+        if (mom_rd) s.v[1][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s0 + q));
+      } else {
+        s.v[1][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s0 + q));
+        s.v[2][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.s1 + q));
+      }
+    }
+  };
+  auto update = [&](const Tile& t, int g, Set& s) {
+    f32x4 gv[GI];
+#pragma unroll
+    for (int u = 0; u < GI; ++u) {
+      const int e = (g * GI + u) * kT + ts;
+      gv[u] = *reinterpret_cast<const f32x4*>(G + (e >> 5) * BN + (e & 31) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < GI; ++u) {
+      const int it = g * GI + u;
+      if (!t.col_ok || it >= t.rows) continue;
+      const long q = t.base + it * step8;
+      f32x4 pe = s.v[0][u];
+      if constexpr (SGD) {
+        f32x4 be = mom_rd ? s.v[1][u] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float pc = pe[c], bc = be[c];
+          sgd_elem(pc, gv[u][c], bc, o.sgd);
+          pe[c] = pc;
+          be[c] = bc;
+        }
+        __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + q));
+        if (mom_wr) __builtin_nontemporal_store(be, reinterpret_cast<f32x4*>(o.s0 + q));
+      } else {
+        f32x4 me = s.v[1][u], ve = s.v[2][u];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float pc = pe[c], mc = me[c], vc = ve[c];
+          adam_elem(pc, gv[u][c], mc, vc, nullptr, o.adam);
+          pe[c] = pc;
+          me[c] = mc;
+          ve[c] = vc;
+        }
+        __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + q));
+        __builtin_nontemporal_store(me, reinterpret_cast<f32x4*>(o.s0 + q));
+        __builtin_nontemporal_store(ve, reinterpret_cast<f32x4*>(o.s1 + q));
+      }
+    }
+  };
+  if (ntiles == 0) return;
+  const int ng = nk / 4;  // barrier intervals per chunk group
+  Set s0, s1;
+  Tile cur = tile_of(0);
+  issue(cur, 0, s0);  // tile 0's first group: in flight while the math waves compute tile 0
+  // step 0: no gradient yet -- the K loop's barriers and the three around G / the tile
+  for (int q = 0; q < nk + 3; ++q) __builtin_amdgcn_s_barrier();
+  for (int j = 1; j <= ntiles; ++j) {
+    // step j: update tile j - 1 (its gradient in G) while the math waves compute tile j
+    const Tile nt = tile_of(j < ntiles ? j : j - 1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Set& sc = (g & 1) ? s1 : s0;
+      Set& sn = (g & 1) ? s0 : s1;
+      if (g < 3) issue(cur, g + 1, sn);
+      else if (j < ntiles) issue(nt, 0, sn);  // the next tile's first group
+      update(cur, g, sc);
+      for (int q = 0; q < ng; ++q) __builtin_amdgcn_s_barrier();
+    }
+    for (int q = 0; q < 3; ++q) __builtin_amdgcn_s_barrier();  // G hand-over (2) + tile end
+    cur = nt;
+  }
+}
+
 template <int FN, int AKIND, int BKIND, int S, int OPT, int FM, bool EMU>
 void launch_fast(const FastParams& p, int nblocks, hipStream_t s) {
   constexpr int STG = 64 * FM * kBK * 4 + 64 * FN * kBK * 4;
@@ -1311,6 +1483,26 @@ static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int spl
   return ldc % 4 == 0 && al(C) && (bias == nullptr || al(bias));
 }
 
+// The lockstep weight-gradient + optimizer kernel (wgrad_lockstep_kernel): the optimizer
+// epilogue's layout (A = dY^T, B = X, both MN-contiguous), the split-bf16 products, K a
+// multiple of 128 (four chunk groups on the K loop's barrier intervals), SGD / Adam without
+// amsgrad. TDP_WGRAD_LOCKSTEP=0 / gemm_f32_set_lockstep(false) keep the persistent kernel.
+static bool o_lockstep = [] {
+  const char* e = std::getenv("TDP_WGRAD_LOCKSTEP");
+  return !(e && e[0] == '0');
+}();
+void gemm_f32_set_lockstep(bool on) { o_lockstep = on; }
+bool gemm_f32_lockstep() { return o_lockstep; }
+static bool lockstep_ok(const GemmF32Args& a) {
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (!o_lockstep || !o_emu || a.a_kcontig || a.b_kcontig || a.mask || a.gate) return false;
+  if (a.opt.kind != 1 && a.opt.kind != 2) return false;
+  if (a.opt.kind == 2 && (a.opt.adam.amsgrad || a.opt.s2)) return false;
+  if (a.K < 128 || a.K % 128 || a.M % 4 || a.N % 4 || a.ldc % 4) return false;
+  if (!al(a.opt.p) || (a.opt.s0 && !al(a.opt.s0)) || (a.opt.s1 && !al(a.opt.s1))) return false;
+  return true;
+}
+
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   // 128-wide tiles split the fewest fragments per MFMA; with split-bf16 products (VALU-heavy
   // per fragment) they win on the skinny-M GEMMs too (toy-MLP fc1 forward 84.5 -> 68.4 us,
@@ -1331,7 +1523,11 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   plan.grid = 0;
   plan.wgrad_ws = false;
-  if (a.opt.kind != 0 && !a.a_kcontig && !a.b_kcontig && wgrad_opt_ok(a)) {
+  plan.lockstep = false;
+  if (a.opt.kind != 0 && lockstep_ok(a)) {
+    plan.lockstep = true;  // one 512-thread workgroup per CU, roles in lockstep
+    plan.grid = num_cus;
+  } else if (a.opt.kind != 0 && !a.a_kcontig && !a.b_kcontig && wgrad_opt_ok(a)) {
     plan.wgrad_ws = true;  // one 512-thread workgroup per CU, roles split (gemm_wgrad_opt.hip)
     plan.grid = num_cus;
   } else if (a.opt.kind != 0) {
@@ -1379,6 +1575,29 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
   if (opt && plan.wgrad_ws) {
     wgrad_opt_run(a, plan.grid, s);
+    return;
+  }
+  if (opt && plan.lockstep) {
+    const int nb = std::max(1, std::min(plan.grid, nblocks));
+    constexpr int STG = 64 * 2 * kBK * 4 + 64 * 2 * kBK * 4;
+    const size_t lds = (size_t)2 * STG + 128 * 128 * 4;  // 2 stages + the gradient buffer G
+    if (a.opt.kind == 1) {
+      static bool cfg = false;
+      if (!cfg) {
+        (void)hipFuncSetAttribute((const void*)wgrad_lockstep_kernel<1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        cfg = true;
+      }
+      hipLaunchKernelGGL(wgrad_lockstep_kernel<1>, dim3(nb), dim3(2 * kT), lds, s, p);
+    } else {
+      static bool cfg = false;
+      if (!cfg) {
+        (void)hipFuncSetAttribute((const void*)wgrad_lockstep_kernel<2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        cfg = true;
+      }
+      hipLaunchKernelGGL(wgrad_lockstep_kernel<2>, dim3(nb), dim3(2 * kT), lds, s, p);
+    }
     return;
   }
   if (opt) {

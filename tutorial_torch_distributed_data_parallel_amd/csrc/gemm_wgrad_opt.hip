@@ -12,12 +12,12 @@
 // workgroups per CU overlap the phases only by chance, and the toy MLP's fc1 / fc2 updates ran
 // at 4.7 TB/s where a tile-shaped non-temporal stream of the same bytes reaches 5.3-5.5 TB/s
 // (dev/micro/stream_sgd.hip). Here ONE 512-thread workgroup per CU splits the roles:
-//   * waves 0-3 (math): tile t's gradient -- operands straight from L2 into registers (8-B loads
-//     in the MFMA layout: two 32 x 32 tiles per wave interleave their rows / columns so one
-//     float2 feeds both; the next 16-deep k-step's loads in flight behind this one's MFMAs), the
-//     exact 3-way bf16 split of both operands on the VALU, six v_mfma_f32_32x32x16_bf16 products
-//     per 32 x 32 x 16 step (split3 emulation of fp32: the same numerics as gemm_f32_fast.hip),
-//     then the finished 128 x 128 fp32 tile into one of two LDS buffers G (tile t -> t & 1);
+//   * waves 0-3 (math): tile t's gradient -- operands straight from L2 into registers (8-B
+//     buffer loads in the MFMA layout: two 32 x 32 tiles per wave interleave their rows /
+//     columns so one float2 feeds both; the next 16-deep k-step's loads in flight behind this
+//     one's MFMAs), native fp32 products on v_mfma_f32_32x32x2_f32 (no VALU at all: the math
+//     only has to stay under the stream's time per tile), then the finished 128 x 128 fp32 tile
+//     into one of two LDS buffers G (tile t -> t & 1);
 //   * waves 4-7 (stream): p / state loads of the NEXT batch are always in flight (they do not
 //     depend on the gradient, so the next tile's first batch is issued before this tile's last
 //     update), each batch's gradient chunks are read from G beside its update, and every 16-B p /
@@ -46,9 +46,6 @@ constexpr int kTM = 128, kTN = 128;
 constexpr int kGFloats = kTM * kTN;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct WsParams {
   const float* A;  // [K][M] (lda)
@@ -61,43 +58,8 @@ struct WsParams {
   float* rowsum;     // else, when set: rowsum = rowsum_beta * rowsum + sum_k A
   float rowsum_beta;
   int exp;           // timing experiments only (TDP_WS_EXP): 1 math skips its K loop, 2 stream
-                     // skips its HBM traffic (both keep the hand-over)
+                     // skips its HBM traffic (both keep the hand-over), 4 math loads nothing
 };
-
-// exact 3-way bf16 split of a pair: the instruction sequence of gemm_f32_fast.hip split3_pair
-__device__ __forceinline__ void split_pair(float x0, float x1, unsigned& h, unsigned& m,
-                                           unsigned& l) {
-  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf2));
-  const float r0 = x0 - __uint_as_float(hu << 16), r1 = x1 - __uint_as_float(hu & 0xffff0000u);
-  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{r0, r1}, bf2));
-  const float s0 = r0 - __uint_as_float(mu << 16), s1 = r1 - __uint_as_float(mu & 0xffff0000u);
-  h = hu;
-  m = mu;
-  l = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{s0, s1}, bf2));
-}
-
-// component c of 8 float2 (one k-step of one lane) -> the three bf16x8 MFMA operands
-template <int C>
-__device__ __forceinline__ void split_col(const f32x2 (&v)[8], bf8& h, bf8& m, bf8& l) {
-  unsigned hs[4], ms[4], ls[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) split_pair(v[2 * i][C], v[2 * i + 1][C], hs[i], ms[i], ls[i]);
-  h = __builtin_bit_cast(bf8, u32x4{hs[0], hs[1], hs[2], hs[3]});
-  m = __builtin_bit_cast(bf8, u32x4{ms[0], ms[1], ms[2], ms[3]});
-  l = __builtin_bit_cast(bf8, u32x4{ls[0], ls[1], ls[2], ls[3]});
-}
-
-// acc += a*b over the six kept split terms (smallest first; gemm_f32_fast.hip mfma_emu6)
-__device__ __forceinline__ f32x16 mfma6(const bf8& ah, const bf8& am, const bf8& al, const bf8& bh,
-                                        const bf8& bm, const bf8& bl, f32x16 acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-  return acc;
-}
 
 __device__ __forceinline__ int lds_load(const int* c) {
   return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -131,8 +93,12 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __syncthreads();  // the last barrier both roles share
 
   // XCD-aware persistent tile ranges (gemm_f32_fast.hip's persistent form): blocks b and b + 8
-  // share an XCD; each XCD walks a contiguous range of tiles (same row panel of g: L2 reuse),
-  // its workgroups interleaved over it
+  // share an XCD; each XCD walks a contiguous range of tiles, its workgroups interleaved over
+  // it. Tile order: row blocks fastest (tile = tn * tiles_m + tm), so the ~32 tiles an XCD runs
+  // at once share ONE column block of x (read from the MALL once per XCD) and walk the rows of
+  // g, which stays L2-resident (toy MLP: 2 MB): the math waves' operand loads hit L2. (Column
+  // blocks fastest streamed x through L2 once per row panel and exposed MALL latency on every
+  // k-step.)
   const int T = p.tiles_m * p.tiles_n;
   const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
   const int q8 = nwg / 8, r8 = nwg % 8;
@@ -150,9 +116,14 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int wm = wave >> 1, wn = wave & 1;
     const int h = lane >> 5, l31 = lane & 31;
     const int nks = (p.exp & 1) ? 0 : (p.K + 15) / 16;
+    // operand descriptors from kernel arguments only (wave-uniform: no waterfall loops)
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.A), 0, 0x7fffffff,
+                                                      0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.B), 0, 0x7fffffff,
+                                                      0x00020000);
     int i = 0;
     for (int lid = t0 + j0; lid < t1; lid += per, ++i) {
-      const int tm = lid / p.tiles_n, tn = lid - tm * p.tiles_n;
+      const int tn = lid / p.tiles_m, tm = lid - tn * p.tiles_m;
       const int m0 = tm * kTM, n0 = tn * kTN;
       // this lane's two rows (tile f = 0, 1) and two columns (tile g = 0, 1); clamped in range
       // (out-of-range rows / columns only feed outputs nobody stores)
@@ -163,27 +134,39 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // k = 8q + 4h + s of two consecutive q), so every MFMA sees the same operands in the same
       // slots and the gradient is bit-identical to the persistent epilogue kernel's
       auto kslot = [&](int e) { return 4 * h + e + (e >= 4 ? 4 : 0); };
-      // 32-bit element offsets from the (uniform) operand bases: no per-row 64-bit address kept
-      // live
+      // buffer loads: one per-lane byte offset (row pair / column pair of this lane half) and a
+      // uniform byte offset per k slot in an SGPR -- no per-slot address registers live
       const unsigned lda = (unsigned)p.lda, ldb = (unsigned)p.ldb;
+      const int va = (int)((4u * h * lda + (unsigned)am) * 4u);
+      const int vb = (int)((4u * h * ldb + (unsigned)bc) * 4u);
       auto load = [&](int ks, f32x2 (&a)[8], f32x2 (&bv)[8]) {
         const int k0 = ks * 16;
+        if (p.exp & 4) {  // timing experiment: no operand loads
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            a[e] = f32x2{1e-3f * e, 2e-3f};
+            bv[e] = f32x2{3e-3f, 1e-3f * e};
+          }
+          return;
+        }
         if (k0 + 16 <= p.K) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const unsigned k = (unsigned)(k0 + kslot(e));
-            a[e] = *reinterpret_cast<const f32x2*>(p.A + (k * lda + (unsigned)am));
-            bv[e] = *reinterpret_cast<const f32x2*>(p.B + (k * ldb + (unsigned)bc));
+            const int ke = k0 + e + (e >= 4 ? 4 : 0);  // + 4h in the lane offset
+            a[e] = __builtin_bit_cast(
+                f32x2, __builtin_amdgcn_raw_buffer_load_b64(ra, va, (int)(ke * lda * 4u), 0));
+            bv[e] = __builtin_bit_cast(
+                f32x2, __builtin_amdgcn_raw_buffer_load_b64(rb, vb, (int)(ke * ldb * 4u), 0));
           }
         } else {  // K tail: slots past K read row K - 1 and are zeroed
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const int k = k0 + kslot(e);
             const unsigned kc = (unsigned)min(k, p.K - 1);
-            const f32x2 va = *reinterpret_cast<const f32x2*>(p.A + (kc * lda + (unsigned)am));
-            const f32x2 vb = *reinterpret_cast<const f32x2*>(p.B + (kc * ldb + (unsigned)bc));
-            a[e] = k < p.K ? va : f32x2{0.f, 0.f};
-            bv[e] = k < p.K ? vb : f32x2{0.f, 0.f};
+            const f32x2 xa = *reinterpret_cast<const f32x2*>(p.A + (kc * lda + (unsigned)am));
+            const f32x2 xb = *reinterpret_cast<const f32x2*>(p.B + (kc * ldb + (unsigned)bc));
+            a[e] = k < p.K ? xa : f32x2{0.f, 0.f};
+            bv[e] = k < p.K ? xb : f32x2{0.f, 0.f};
           }
         }
       };
@@ -195,27 +178,36 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[f][g][r] = 0.f;
       const bool do_rs = tn == 0 && wn == 0 && (p.bopt.kind != 0 || p.rowsum != nullptr);
+      // Native fp32 products: v_mfma_f32_32x32x2_f32 (exact f32, an fmaf chain per output) at
+      // the f32 rate -- 256 MFMAs x 64 cycles per wave and tile, ~7 us at 2.4 GHz, under the
+      // ~12 us the stream waves need for the tile's 256 KB of p / momentum at their HBM share:
+      // the math stays off the critical path without any VALU split (the split-bf16 emulation
+      // needs ~1200 VALU per wave and tile and 100 more VGPRs, and lost to its own latency here).
+      // MFMA e of a 16-deep k-step takes k = k0 + 8 (e >> 2) + 4h + (e & 3) in lane half h:
+      // gemm_f32_fast.hip's native-f32 order, so the result is bit-identical to it.
       auto step = [&](const f32x2 (&a)[8], const f32x2 (&bv)[8]) {
-        bf8 ah0, am0, al0, ah1, am1, al1, bh0, bm0, bl0, bh1, bm1, bl1;
-        split_col<0>(a, ah0, am0, al0);
-        split_col<0>(bv, bh0, bm0, bl0);
-        acc[0][0] = mfma6(ah0, am0, al0, bh0, bm0, bl0, acc[0][0]);
-        split_col<1>(bv, bh1, bm1, bl1);
-        acc[0][1] = mfma6(ah0, am0, al0, bh1, bm1, bl1, acc[0][1]);
-        split_col<1>(a, ah1, am1, al1);
-        acc[1][0] = mfma6(ah1, am1, al1, bh0, bm0, bl0, acc[1][0]);
-        acc[1][1] = mfma6(ah1, am1, al1, bh1, bm1, bl1, acc[1][1]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e][0], bv[e][0], acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e][0], bv[e][1], acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e][1], bv[e][0], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e][1], bv[e][1], acc[1][1], 0, 0, 0);
+        }
       };
-      f32x2 a0[8], b0[8], a1[8], b1[8];
-      if (nks > 0) load(0, a0, b0);
+      // two k-steps of operands in registers: the next one in flight behind this one's MFMAs
+      // (32 MFMAs x 64 cycles of cover for the L2 latency); one loop exit, so the accumulators
+      // keep one register assignment
+      f32x2 ax[8], bx[8], ay[8], by[8];
+      if (nks > 0) load(0, ax, bx);
+      if (nks > 1) load(1, ay, by);
       int ks = 0;
-      for (; ks + 1 < nks; ks += 2) {
-        load(ks + 1, a1, b1);
-        step(a0, b0);
-        if (ks + 2 < nks) load(ks + 2, a0, b0);
-        step(a1, b1);
+      for (; ks + 2 <= nks; ks += 2) {
+        step(ax, bx);
+        if (ks + 2 < nks) load(ks + 2, ax, bx);
+        step(ay, by);
+        if (ks + 3 < nks) load(ks + 3, ay, by);
       }
-      if (ks < nks) step(a0, b0);
+      if (ks < nks) step(ax, bx);
 
       if (do_rs) {
         // bias gradient: lane l of the two wn == 0 waves sums row m0 + wm * 64 + l over k in
@@ -298,7 +290,7 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     bool col_ok;
   };
   auto tile_of = [&](int lid) -> Tile {
-    const int tm = lid / p.tiles_n, tn = lid - tm * p.tiles_n;
+    const int tn = lid / p.tiles_m, tm = lid - tn * p.tiles_m;
     const int row = tm * kTM + (ts >> 5), col = tn * kTN + (ts & 31) * 4;
     Tile t;
     t.col_ok = col < p.N;
@@ -424,6 +416,8 @@ bool wgrad_opt_ok(const GemmF32Args& a) {
   if (a.M < 4 || a.N < 4 || a.K < 1 || a.M % 4 || a.N % 4 || a.lda % 2 || a.ldb % 2 ||
       a.ldc % 4)
     return false;
+  // buffer-load byte offsets are 32-bit
+  if ((long)a.K * a.lda * 4 >= (1L << 31) || (long)a.K * a.ldb * 4 >= (1L << 31)) return false;
   if (!al(a.A, 8) || !al(a.B, 8) || !al(a.opt.p, 16) || (a.opt.s0 && !al(a.opt.s0, 16)) ||
       (a.opt.s1 && !al(a.opt.s1, 16)))
     return false;

@@ -121,6 +121,7 @@ struct GemmF32Args {
 struct GemmPlan {
   bool fast = false;    // LDS-DMA pipelined kernel (gemm_f32_fast.hip) vs generic
   bool wgrad_ws = false;  // optimizer epilogue by the warp-specialised kernel (gemm_wgrad_opt.hip)
+  bool lockstep = false;  // optimizer epilogue by wgrad_lockstep_kernel (gemm_f32_fast.hip)
   int tile = 0;         // generic: tile-table index; fast: FN (block tile 128 x 64*FN)
   int bm = 128, bn = 64;
   int stages = 2;       // fast kernel pipeline depth
@@ -150,6 +151,8 @@ bool wgrad_opt_ok(const GemmF32Args& a);
 void wgrad_opt_run(const GemmF32Args& a, int num_cus, hipStream_t s);
 void wgrad_opt_set_enabled(bool on);  // A/B: false = the persistent epilogue kernel
 bool wgrad_opt_enabled();
+void gemm_f32_set_lockstep(bool on);  // A/B: false = the persistent epilogue kernel
+bool gemm_f32_lockstep();
 // set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel
 void gemm_f32_set_mode(int mode);
 // benchmarking knob: force the fast kernel's tile width / split-K / stages (0 = planner's choice)

@@ -32,8 +32,6 @@ def planes_fit(M: int, N: int, K: int) -> bool:
     return _PLANES and M <= 256 and K % 32 == 0 and K >= 256 and N % 4 == 0 and N >= 512
 
 
-
-
 def planes_input_fit(M: int, K: int) -> bool:
     """A [M, K] activation may feed a planes GEMM (its producer should emit the planes)."""
     return _PLANES and M <= 256 and K % 32 == 0 and K >= 256
@@ -49,7 +47,7 @@ _EARLY_PREV_G = True  # the consumer's backward starts the previous layer's g ga
 
 
 def set_early_prev_g(on: bool) -> bool:
-    """Turn the one-layer-early g gather on/off (A/B: scripts/run_with_variant.py); returns the
+    """Turn the one-layer-early g gather on/off (A/B: scripts/archive/run_with_variant.py); returns the
     previous setting."""
     global _EARLY_PREV_G
     old, _EARLY_PREV_G = _EARLY_PREV_G, bool(on)
