@@ -1,7 +1,8 @@
 """Multi-rank workers for the peer-memory vehicle (parallel/peer.py, csrc/peer.hip): W rank
 processes on ONE GPU whose collectives are device kernels over IPC-mapped windows -- so, unlike
 the host relay, the multi-rank training step can be CAPTURED into a hipGraph and replayed with
-real peers. Oracles: closed-form collective results, the eager run of the same step (bitwise)
+real peers. The captured-parity workers also take backend="nccl": the multi-GPU RCCL tier
+(tests/test_multigpu_rccl.py) runs the same bodies with one rank per GPU. Oracles: closed-form collective results, the eager run of the same step (bitwise)
 and the fp32 torch DDP-semantics oracle of relay_workers."""
 import os
 import time
@@ -80,13 +81,13 @@ def chunked_collectives(rank, out_dir):
     tdp.destroy_process_group()
 
 
-def captured_ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, steps=6):
+def captured_ddp_parity(rank, out_dir, kind="sgd", factor=True, replicate=None, steps=6, backend="peer"):
     """The multi-rank DDP step captured into a hipGraph and replayed with real peers (bucket
     collectives / factored gathers on the side stream, deferred forks, join) == the same step
     run eagerly, BITWISE, on every rank; both match the fp32 torch oracle; replicas identical."""
     from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
 
-    tdp.init_process_group("peer")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
     lr = 0.05 if kind == "sgd" else 2e-3
 
@@ -210,7 +211,7 @@ def _assert_bitwise(m1, m2, tag):
             assert torch.equal(a, b), f"rank {r} {tag}: captured != eager for buffer {n}"
 
 
-def captured_syncbn_parity(rank, out_dir, steps=5):
+def captured_syncbn_parity(rank, out_dir, steps=5, backend="peer"):
     """BASELINE config 3 (toy MLP + SyncBatchNorm) as a CAPTURED multi-rank step with real peers:
     the forward statistics all-gather and the backward all-reduce of every BN layer are recorded
     inline on the compute stream, the bucket / factored collectives on the side stream. Captured
@@ -219,7 +220,7 @@ def captured_syncbn_parity(rank, out_dir, steps=5):
     import torch.nn as nn
     import torch.nn.functional as F
 
-    tdp.init_process_group("peer")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
 
     def build():
@@ -269,13 +270,13 @@ def captured_syncbn_parity(rank, out_dir, steps=5):
     tdp.destroy_process_group()
 
 
-def captured_accelerate_parity(rank, out_dir, steps=5):
+def captured_accelerate_parity(rank, out_dir, steps=5, backend="peer"):
     """BASELINE config 4: the step through the Accelerate-style facade (prepare -> DDP, fused
     optimizer, accelerator.backward) CAPTURED with real peers == eager bitwise; both == the fp32
     torch oracle (mean over ranks of each rank's mean-loss gradient)."""
     from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
 
-    tdp.init_process_group("peer")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
     accel = Accelerator()
     assert accel.num_processes == W
@@ -361,7 +362,7 @@ def _cnn_batch(r, step, n=8):
         torch.randint(0, 10, (n,), device="cuda", generator=g)
 
 
-def captured_cnn_parity(rank, out_dir, steps=4):
+def captured_cnn_parity(rank, out_dir, steps=4, backend="peer"):
     """BASELINE config 5 in miniature: a conv + SyncBN + pool + Linear CNN whose gradients go
     through several buckets (small caps, split parameters) with the sharded fused update,
     CAPTURED with real peers == eager bitwise (parameters, running stats); both == the global-
@@ -369,7 +370,7 @@ def captured_cnn_parity(rank, out_dir, steps=4):
     import torch.nn as nn
     import torch.nn.functional as F
 
-    tdp.init_process_group("peer")
+    tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
 
     def build():

@@ -85,7 +85,8 @@ def collectives(rank, out_dir, backend="relay"):
     included."""
     tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
-    assert rt.get_backend() == backend and not rt.comm().native_rccl
+    want = "rccl" if backend in ("nccl", "rccl") else backend  # RCCL: the multi-GPU tier
+    assert rt.get_backend() == want and bool(rt.comm().native_rccl) == (want == "rccl")
     t = torch.full((5,), float(r + 1), device="cuda")
     rt.all_reduce(t, "sum")
     assert torch.equal(t, torch.full_like(t, W * (W + 1) / 2))

@@ -1423,11 +1423,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_set_bm", &gemm_f32_set_bm);
   m.def("gemm_f32_set_emu", &gemm_f32_set_emu);
   m.def("gemm_f32_emu", &gemm_f32_emu);
-  m.def("wgrad_opt_set_enabled", &wgrad_opt_set_enabled,
-        "A/B: the warp-specialised weight-gradient + optimizer kernel (default on)");
-  m.def("wgrad_opt_enabled", &wgrad_opt_enabled);
   m.def("gemm_f32_set_lockstep", &gemm_f32_set_lockstep,
-        "A/B: the lockstep weight-gradient + optimizer kernel (default on)");
+        "A/B: the lockstep weight-gradient + optimizer kernel (default off)");
   m.def("gemm_f32_lockstep", &gemm_f32_lockstep);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
         py::arg("db") = py::none(), py::arg("beta_db") = 0.0);

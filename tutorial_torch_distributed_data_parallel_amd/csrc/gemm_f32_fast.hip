@@ -1234,8 +1234,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ge
 // Both roles execute the same barriers: the K loop's one per 32-deep K tile, two around the G
 // hand-over and one per tile -- the stream waves place their four chunk groups on the K loop's
 // barrier intervals, and a last step with no K work drains the final tile. No spin-waits, no
-// counters: the hardware barrier is the hand-over. (A version with independent roles and LDS
-// counters lost to the math waves' operand latency: gemm_wgrad_opt.hip.)
+// counters: the hardware barrier is the hand-over. (A version with independent roles handing
+// the tile over through LDS counters lost to the math waves' operand latency and their VALU /
+// MFMA interference with the stream: profiles/r9/wgrad_split_roles_r9.md.)
 template <int KIND>
 __global__ __launch_bounds__(2 * kT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 wgrad_lockstep_kernel(FastParams p) {
@@ -1353,9 +1354,14 @@ wgrad_lockstep_kernel(FastParams p) {
   };
   if (ntiles == 0) return;
   const int ng = nk / 4;  // barrier intervals per chunk group
-  Set s0, s1;
+  // one register set per chunk group: the loads of the next TWO groups are in flight while a
+  // group is updated (HBM latency under load spans more than one barrier interval: one group
+  // ahead measured 223 us for the two toy-MLP kernels, two 194, three 204); group g of every
+  // tile lives in set g, so the issue two ahead wraps into the next tile's groups 0 / 1
+  Set st[4];
   Tile cur = tile_of(0);
-  issue(cur, 0, s0);  // tile 0's first group: in flight while the math waves compute tile 0
+  issue(cur, 0, st[0]);  // tile 0's first groups: in flight while the math waves compute tile 0
+  issue(cur, 1, st[1]);
   // step 0: no gradient yet -- the K loop's barriers and the three around G / the tile
   for (int q = 0; q < nk + 3; ++q) __builtin_amdgcn_s_barrier();
   for (int j = 1; j <= ntiles; ++j) {
@@ -1363,11 +1369,9 @@ wgrad_lockstep_kernel(FastParams p) {
     const Tile nt = tile_of(j < ntiles ? j : j - 1);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      Set& sc = (g & 1) ? s1 : s0;
-      Set& sn = (g & 1) ? s0 : s1;
-      if (g < 3) issue(cur, g + 1, sn);
-      else if (j < ntiles) issue(nt, 0, sn);  // the next tile's first group
-      update(cur, g, sc);
+      if (g < 2) issue(cur, g + 2, st[g + 2]);
+      else if (j < ntiles) issue(nt, g - 2, st[g - 2]);  // the next tile's groups 0 and 1
+      update(cur, g, st[g]);
       for (int q = 0; q < ng; ++q) __builtin_amdgcn_s_barrier();
     }
     for (int q = 0; q < 3; ++q) __builtin_amdgcn_s_barrier();  // G hand-over (2) + tile end
@@ -1486,10 +1490,10 @@ static bool c_vec_ok(int N, long ldc, const float* C, const float* bias, int spl
 // The lockstep weight-gradient + optimizer kernel (wgrad_lockstep_kernel): the optimizer
 // epilogue's layout (A = dY^T, B = X, both MN-contiguous), the split-bf16 products, K a
 // multiple of 128 (four chunk groups on the K loop's barrier intervals), SGD / Adam without
-// amsgrad. TDP_WGRAD_LOCKSTEP=0 / gemm_f32_set_lockstep(false) keep the persistent kernel.
-static bool o_lockstep = [] {
-  const char* e = std::getenv("TDP_WGRAD_LOCKSTEP");
-  return !(e && e[0] == '0');
+// amsgrad. Opt-in: TDP_WGRAD_LOCKSTEP=1 / gemm_f32_set_lockstep(true).
+static bool o_lockstep = [] {  // opt-in: measured at parity with the persistent kernel, not
+  const char* e = std::getenv("TDP_WGRAD_LOCKSTEP");  // better (profiles/r9/wgrad_split_roles_r9.md)
+  return e && e[0] == '1';
 }();
 void gemm_f32_set_lockstep(bool on) { o_lockstep = on; }
 bool gemm_f32_lockstep() { return o_lockstep; }
@@ -1522,13 +1526,9 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (o_splits > 0 && a.rowsum == nullptr) splits = o_splits;
   if (a.opt.kind != 0) splits = 1;  // the optimizer epilogue needs the complete K sum
   plan.grid = 0;
-  plan.wgrad_ws = false;
   plan.lockstep = false;
   if (a.opt.kind != 0 && lockstep_ok(a)) {
     plan.lockstep = true;  // one 512-thread workgroup per CU, roles in lockstep
-    plan.grid = num_cus;
-  } else if (a.opt.kind != 0 && !a.a_kcontig && !a.b_kcontig && wgrad_opt_ok(a)) {
-    plan.wgrad_ws = true;  // one 512-thread workgroup per CU, roles split (gemm_wgrad_opt.hip)
     plan.grid = num_cus;
   } else if (a.opt.kind != 0) {
     // persistent: 2 workgroups per CU (gemm_f32_set_opt_variant overrides, for measurements:
@@ -1573,10 +1573,6 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   // the optimizer epilogue is instantiated for the weight-gradient layout only (A = dY^T and
   // B = X both MN-contiguous); any other use stores C and applies the flat update afterwards
   const bool opt = a.opt.kind != 0 && plan.splits == 1 && !ak && !bk;
-  if (opt && plan.wgrad_ws) {
-    wgrad_opt_run(a, plan.grid, s);
-    return;
-  }
   if (opt && plan.lockstep) {
     const int nb = std::max(1, std::min(plan.grid, nblocks));
     constexpr int STG = 64 * 2 * kBK * 4 + 64 * 2 * kBK * 4;

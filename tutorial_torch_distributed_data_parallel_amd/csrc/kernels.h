@@ -120,7 +120,6 @@ struct GemmF32Args {
 
 struct GemmPlan {
   bool fast = false;    // LDS-DMA pipelined kernel (gemm_f32_fast.hip) vs generic
-  bool wgrad_ws = false;  // optimizer epilogue by the warp-specialised kernel (gemm_wgrad_opt.hip)
   bool lockstep = false;  // optimizer epilogue by wgrad_lockstep_kernel (gemm_f32_fast.hip)
   int tile = 0;         // generic: tile-table index; fast: FN (block tile 128 x 64*FN)
   int bm = 128, bn = 64;
@@ -144,13 +143,6 @@ void gemm_skinny_run(int kind, const GemmF32Args& a, hipStream_t s);
 void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s);
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
-// weight gradient + optimizer update, warp-specialised (csrc/gemm_wgrad_opt.hip): the optimizer-
-// epilogue case of gemm_f32_fast (A = dY^T [K][M], B = X [K][N], SGD / Adam without amsgrad);
-// gemm_f32_fast_plan picks it when wgrad_opt_ok. One 512-thread workgroup per CU (num_cus).
-bool wgrad_opt_ok(const GemmF32Args& a);
-void wgrad_opt_run(const GemmF32Args& a, int num_cus, hipStream_t s);
-void wgrad_opt_set_enabled(bool on);  // A/B: false = the persistent epilogue kernel
-bool wgrad_opt_enabled();
 void gemm_f32_set_lockstep(bool on);  // A/B: false = the persistent epilogue kernel
 bool gemm_f32_lockstep();
 // set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel
