@@ -21,9 +21,9 @@ Optimizer scalars live in device hyper blocks, so the captured step stays exact 
 Adam's step count). At world size 1 the toy-MLP step is captured as well (no collective, the
 optimizer runs in the weight-gradient GEMM epilogues; replay removes the host-side launch work
 the ~15-kernel eager step is bound by); the CNNs run eagerly. ``--graph`` / ``--eager`` force a
-mode. A captured toy-MLP replay runs TWO training steps (``--graph-steps 2``, each with its own
+mode. A captured toy-MLP replay runs FOUR training steps (``--graph-steps 4``, each with its own
 batch gather and update; an epoch boundary always falls between replays), which pays the
-graph-launch gap every other step; the trajectory is bit-identical to one step per replay.
+graph-launch gap once per four steps; the trajectory is bit-identical to one step per replay.
 
 Diagnostics (after the timed region, in the JSON line's "diagnostics"): at world size > 1 the
 collectives of one step alone (``comm_ms``), the same captured step with its collectives turned
@@ -108,10 +108,10 @@ def parse():
                     help="tdp: capture the whole step into a hipGraph and replay it (the default "
                          "at world size > 1: bucket collectives then overlap backward on the comm "
                          "stream)")
-    ap.add_argument("--graph-steps", type=int, default=2,
-                    help="training steps per captured hipGraph replay (1 or 2: two steps per "
-                         "graph remove every other graph-launch gap; an epoch boundary falls "
-                         "between replays)")
+    ap.add_argument("--graph-steps", type=int, default=4,
+                    help="training steps per captured hipGraph replay (G steps per graph pay "
+                         "the graph-launch gap once per G steps; a group that would cross an "
+                         "epoch boundary runs step by step)")
     ap.add_argument("--eager", action="store_true",
                     help="tdp: run eagerly (the default at world size 1; collectives then run on "
                          "the compute stream without overlap)")
@@ -319,7 +319,22 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
         g = CapturedStep(st, warmup=3)
         out["rehearsal_ms"] = round(_time_steps(g.replay, n), 4)
         out["rehearsal_buckets"] = len(d2._bounds) - 1
-        del g, d2
+        del g
+        # the same schedule with its one-rank collectives turned into no-ops: at world size 1 an
+        # all-gather / reduce-scatter is a local copy on the comm queue (factors, buckets) that
+        # competes for HBM with the compute stream -- traffic a W-rank job moves over xGMI
+        # instead. What remains over dp1 is the schedule itself (side-stream forks and joins,
+        # per-bucket / factored updates instead of the GEMM epilogue).
+        d2._ops.skip_collectives = True
+        try:
+            g = CapturedStep(st, warmup=2)
+            out["rehearsal_schedule_ms"] = round(_time_steps(g.replay, n), 4)
+            del g
+        finally:
+            d2._ops.skip_collectives = False
+        out["rehearsal_over_dp1"] = round(out["rehearsal_ms"] / step_ms, 4)
+        out["rehearsal_schedule_over_dp1"] = round(out["rehearsal_schedule_ms"] / step_ms, 4)
+        del d2
     return out
 
 
@@ -574,7 +589,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
 
     advance()
     run = tdp_step
-    run_pair = [None]  # the two-step graph, when captured
+    run_pair = [None]  # the G-step graph, when captured
     if ddp is not None and world > 1 and use_gpu:
         # measured replicated-vs-sharded choice per factored Linear weight (untimed training
         # steps, agreed over ranks) before the step is captured -- timed the way the step
@@ -619,17 +634,20 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         if not isinstance(run, CapturedStep):
             fallbacks.append(f"{cfg['name']}: hipGraph capture failed (agreed over ranks); "
                              "the step runs eagerly")
-        if ecur is not None and a.graph_steps == 2 and isinstance(run, CapturedStep):
-            # two training steps per replay (the device cursor advances per gather): half
-            # the graph launches; every step still runs all of its work
-            def two_steps():
-                tdp_step()
-                return tdp_step()
+        G = max(1, int(a.graph_steps))
+        if ecur is not None and G > 1 and isinstance(run, CapturedStep):
+            # G training steps per replay (the device cursor advances per gather): 1/G of the
+            # graph launches; every step still runs all of its work
+            def g_steps():
+                out = None
+                for _ in range(G):
+                    out = tdp_step()
+                return out
             # no eager warm-up: the one-step graph's warm-up already did it, and training
             # steps outside the count would make the run differ from --graph-steps 1
-            run2 = try_capture(two_steps, warmup=0,
+            run2 = try_capture(g_steps, warmup=0,
                                log=lambda m: print(m, file=sys.stderr, flush=True))
-            if run2 is not two_steps:
+            if run2 is not g_steps:
                 run_pair[0] = run2
         if ecur is not None:
             # the warm-up / capture runs advanced the device cursor: restart the epoch's
@@ -642,23 +660,24 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         return run()
 
     def steps(n):
-        """n training steps; pairs through the two-step graph while both fall in the
+        """n training steps; groups of G through the G-step graph while they fall in the
         current epoch (the host advances its position for each)."""
         k, out = 0, None
         while k < n:
-            if run_pair[0] is not None and n - k >= 2 and \
-                    cur["pos"] + 2 * a.batch <= len(cur["idx"]):
-                advance()
-                advance()
+            G = a.graph_steps
+            if run_pair[0] is not None and n - k >= G and \
+                    cur["pos"] + G * a.batch <= len(cur["idx"]):
+                for _ in range(G):
+                    advance()
                 out = run_pair[0]()
-                k += 2
+                k += G
             else:
                 out = step()
                 k += 1
         return out
     step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
     step.many = steps
-    step.graph_steps = 2 if run_pair[0] is not None else (1 if graph else 0)
+    step.graph_steps = a.graph_steps if run_pair[0] is not None else (1 if graph else 0)
     return types.SimpleNamespace(ddp=ddp, opt=opt, fused=fused, step=step, run=run,
                                  graph=graph, rung=cfg["name"],
                                  build_rehearsal=None if a.api == "accelerate"

@@ -191,6 +191,9 @@ class DistributedDataParallel(nn.Module):
             if comm is None:
                 raise RuntimeError("GPU DDP needs the RCCL backend (init_process_group('nccl'))")
             self._ops = C.RcclOps(comm, self.arena.grad, self.arena.data, compression=comp)
+            # profiling only: the W-rank schedule with its collectives as no-ops (the one-GPU
+            # rehearsal without its one-rank copies; bench.py diagnostics rehearsal_schedule_ms)
+            self._ops.skip_collectives = os.environ.get("TDP_SKIP_COLLECTIVES", "0") == "1"
         else:
             self._cpu_ops = _CpuSyncOps(self, compression=comp)
             self._ops = C.PyOps(self.rank, self.world_size, self._cpu_ops)
