@@ -2,14 +2,14 @@
 same process -- the A/B switches are setters, not environment knobs (README "Environment
 knobs"). Example (optimizer-epilogue variant 28 = LDS + non-temporal + one batch per tile):
 
-    python scripts/run_with_variant.py --sgd 28 -- bench.py --steps 100
+    python scripts/archive/run_with_variant.py --sgd 28 -- bench.py --steps 100
 """
 import argparse
 import os
 import runpy
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

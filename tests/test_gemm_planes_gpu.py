@@ -62,6 +62,31 @@ def test_planes_gemm_matches_fp64(C, M, N, K, bk):
     assert e < 4 * e_fast + 16 * U, (e, e_fast)
 
 
+@pytest.mark.parametrize("M,N,K,bk", SHAPES)
+def test_planes_single_group_kernel_matches_fp64(C, M, N, K, bk):
+    """The one-wave-group 3-stage variant (gemm_planes_set_cfg stages 3; the default, stages 4,
+    sums each half of every K tile in its own wave group, so the two are not bitwise equal): the
+    same fp32 bound, epilogues and split-K partials through the same paths."""
+    torch.manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn((N, K) if bk else (K, N), device="cuda")
+    Bm = B.t() if bk else B
+    out = torch.empty(M, N, device="cuda")
+    assert C.gemm_planes_set_cfg(3, 0, 0)
+    try:
+        C.gemm_planes(C.split_planes(A), B, out, bk)
+        b = torch.randn(N, device="cuda")
+        y = torch.empty(M, N, device="cuda")
+        C.gemm_planes(C.split_planes(A), B, y, bk, bias=b, relu=True)
+        torch.cuda.synchronize()
+    finally:
+        C.gemm_planes_set_cfg(4, 0, 0)
+    e = _scaled_err(out, A, Bm)
+    assert e < (8 + 2 * K ** 0.5) * U, e
+    ref = torch.relu(A.double() @ Bm.double() + b.double())
+    torch.testing.assert_close(y.double(), ref, rtol=1e-4, atol=1e-4 * K ** 0.5)
+
+
 def test_planes_gemm_epilogues_and_out_planes(C):
     torch.manual_seed(1)
     M, N, K = 128, 512, 1024

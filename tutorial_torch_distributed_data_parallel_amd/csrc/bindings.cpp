@@ -1415,7 +1415,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("planes") = false, py::arg("backend") = nullptr, py::arg("w_offset") = -1,
         py::arg("b_offset") = -1, py::arg("b_span") = 0);
   m.def("gemm_planes_plan", &gemm_planes_plan_op);
-  m.def("gemm_planes_set_cfg", &gemm_planes_set_cfg, py::arg("stages") = 3, py::arg("pf") = 0,
+  m.def("gemm_planes_set_cfg", &gemm_planes_set_cfg,
+        "planes GEMM variant: stages 2 / 3 (one wave group), 4 = default (3 stages, two wave "
+        "groups); pf = B prefetch (2 stages only); splits > 0 = split-K override",
+        py::arg("stages") = 4, py::arg("pf") = 0,
         py::arg("splits") = 0);
   m.def("gemm_f32_set_mode", &gemm_f32_set_mode);
   m.def("gemm_f32_set_override", &gemm_f32_set_override);

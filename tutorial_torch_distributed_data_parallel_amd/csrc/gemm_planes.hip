@@ -504,6 +504,171 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 :
   }
 }
 
+// Two waves per SIMD (gemm_planes_set_cfg stages = 4): the same tile, LDS image and three stages
+// as the S = 3 kernel, but 512 threads -- wave group q = wave >> 2 computes MFMA step q (k 16q ..
+// 16q + 15) of every 32-deep K tile into its own accumulators; the groups are summed through LDS
+// at the end. The single-group kernel keeps one wave per SIMD behind its own LDS reads, split and
+// MFMA issue (52 % of wave cycles waiting on dependencies, MFMA busy 37 %:
+// profiles/r8/mlp_dp1_pmc_r8m.md); here each SIMD has a second wave to issue from while one
+// waits (profiles/r9/planes_dual_r9.md). Registers: the S = 3 kernel's 234 fit two waves' 256.
+template <bool BKC>
+__global__ __launch_bounds__(2 * kT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+gemm_planes_dual_kernel(PParams p) {
+  constexpr int S = 3;
+  constexpr int BN = kBN;
+  constexpr int BBYTES = BN * kBK * 4;
+  constexpr int STG = kABytes + BBYTES;
+  constexpr int NCH = kABytes / 1024 + BBYTES / 1024;  // 1-KiB DMA chunks per stage (40)
+  constexpr int GW = NCH / 8;                          // per wave (5)
+  static_assert(NCH % 8 == 0, "chunks split evenly over the 8 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = wave >> 2, w = wave & 3;  // MFMA step, column slice
+  const int h = lane >> 5, l31 = lane & 31;
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  const int z = lid / p.tiles_mn, t = lid % p.tiles_mn;
+  const int m0 = (t / p.tiles_n) * kBM, n0 = (t % p.tiles_n) * BN;
+  const int kb = z * p.kps;
+  const int ke = min(p.K, kb + p.kps);
+  const int nk = (ke - kb) / kBK;
+
+  // per-lane DMA sources: chunk j = wave * GW + i; chunks 0-23 are A (plane j >> 3, row block
+  // j & 7), 24-39 are B (8 rows of 128 B, K-contiguous; or 1 KiB of [32 k][BN] rows)
+  const char* src[GW];
+  int dst[GW];
+  long kbytes[GW];  // source bytes per unit of k
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int j = wave * GW + i;
+    if (j < 24) {
+      const int plane = j >> 3, rb = j & 7;
+      const int row = rb * 16 + (lane >> 2);
+      const int gr = min(m0 + row, p.M - 1);
+      const int c = (lane & 3) ^ aswz(row);
+      src[i] = reinterpret_cast<const char*>(p.Ap + plane * p.ps + (long)gr * p.lda + c * 8);
+      dst[i] = plane * kAPlane + rb * 1024;
+      kbytes[i] = 2;
+    } else {
+      const int jb = j - 24;
+      if (BKC) {
+        const int row = jb * 8 + (lane >> 3);
+        const int gr = min(n0 + row, p.N - 1);
+        src[i] = reinterpret_cast<const char*>(p.B + (long)gr * p.ldb +
+                                               ((lane & 7) ^ bswz(row)) * 4);
+        kbytes[i] = 4;
+      } else {
+        constexpr int LPR = BN / 4, RPC = 1024 / (BN * 4);
+        const int krow = RPC * jb + lane / LPR;
+        const int gc = min(n0 + (lane % LPR) * 4, p.N - 4);
+        src[i] = reinterpret_cast<const char*>(p.B + (long)krow * p.ldb + gc);
+        kbytes[i] = 4 * p.ldb;
+      }
+      dst[i] = kABytes + jb * 1024;
+    }
+  }
+  auto issue = [&](int kt) {
+    lds_char* st = smem + (kt % S) * STG;
+    const long k0 = kb + min(kt, nk - 1) * kBK;
+#pragma unroll
+    for (int i = 0; i < GW; ++i) glds16(src[i] + k0 * kbytes[i], st + dst[i]);
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[f][r] = 0.f;
+
+  auto compute = [&](int kt) {
+    const lds_char* st = smem + (kt % S) * STG;
+    float bv[8];
+    const int bcol = w * 32 + l31;
+    if (BKC) {
+      const int c0 = 4 * q + 2 * h;
+      const f32x4 v0 =
+          *reinterpret_cast<const f32x4*>(st + kABytes + bcol * 128 + ((c0 ^ bswz(bcol)) * 16));
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(st + kABytes + bcol * 128 +
+                                                       (((c0 + 1) ^ bswz(bcol)) * 16));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bv[j] = v0[j];
+        bv[4 + j] = v1[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bv[j] = *reinterpret_cast<const float*>(st + kABytes +
+                                                ((16 * q + 8 * h + j) * BN + bcol) * 4);
+    }
+    bf8 a[4][3];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int row = f * 32 + l31;
+      const int off = row * 64 + (((2 * q + h) ^ aswz(row)) * 16);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[f][pl] = *reinterpret_cast<const bf8*>(st + pl * kAPlane + off);
+    }
+    bf8 x0, x1, x2;
+    split_x8(bv, x0, x1, x2);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] = mfma6(a[f][0], a[f][1], a[f][2], x0, x1, x2, acc[f]);
+  };
+
+  if (nk > 0) {
+#pragma unroll
+    for (int t0 = 0; t0 < S - 1; ++t0) issue(t0);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt<(S - 2) * GW>();  // tile kt landed (tile kt + 1 may still be in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the stage refilled below
+    __builtin_amdgcn_s_barrier();
+    issue(kt + S - 1);
+    compute(kt);
+  }
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  // sum the two groups' accumulators, then the S = 3 kernel's LDS-staged epilogue (512 threads)
+  constexpr int TS = BN + 4;
+  static_assert(kBM * TS * 4 <= S * STG, "the C tile must fit in the stages");
+  float* T = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  if (q == 1) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        T[(f * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * TS + w * 32 + l31] = acc[f][r];
+  }
+  __syncthreads();
+  if (q == 0) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float* e = T + (f * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * TS + w * 32 + l31;
+        *e = acc[f][r] + *e;
+      }
+  }
+  __syncthreads();
+  constexpr int C4 = BN / 4;
+  constexpr int IT = kBM * C4 / (2 * kT);
+  float* ws = p.ws + (long)z * p.M * p.N;
+#pragma unroll 4
+  for (int i = 0; i < IT; ++i) {
+    const int e = i * 2 * kT + threadIdx.x;
+    const int lr = e / C4, lc = (e % C4) * 4;
+    const int row = m0 + lr, col = n0 + lc;
+    if (row >= p.M || col >= p.N) continue;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + lr * TS + lc);
+    if (p.splits > 1) *reinterpret_cast<f32x4*>(ws + (long)row * p.N + col) = v;
+    else finish4(p, row, col, v);
+  }
+}
+
 // C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread
 __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
   const long ng = (long)p.M * p.N / 4;
@@ -595,24 +760,27 @@ __global__ __launch_bounds__(kT) void gather_planes_kernel(const float* __restri
 
 inline bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
-// variant: pipeline depth (2 stages: 80 KiB, two workgroups per CU; 3: 120 KiB, one) and the
-// B prefetch distance in tiles (0 = off; two stages only), set by gemm_planes_set_cfg
-// (measurements; with a split-K override). Default 3,0: one workgroup per CU halves the split-K count (8 for the toy
-// MLP), hence the partial-sum traffic of the reduce; the captured toy-MLP step measured
-// 0.371-0.374 ms vs 0.383-0.386 with 2,0 (profiles/r6/bench_modes_r6j.txt). The B prefetch
-// measured nothing (the K loop is not HBM-latency bound: TDP_PLANES_EXP experiments,
+// variant: pipeline depth (2 stages: 80 KiB, two workgroups per CU; 3: 120 KiB, one; 4: the
+// 3-stage image computed by two wave groups, gemm_planes_dual_kernel) and the B prefetch distance
+// in tiles (0 = off; two stages only), set by gemm_planes_set_cfg (measurements; with a split-K
+// override). One workgroup per CU halves the split-K count (8 for the toy MLP), hence the
+// partial-sum traffic of the reduce; the captured toy-MLP step measured 0.371-0.374 ms with 3,0
+// vs 0.383-0.386 with 2,0 (profiles/r6/bench_modes_r6j.txt). Default 4,0: 0.3624-0.3637 ms vs
+// 0.3657-0.3677 with 3,0, interleaved on one box (profiles/r9/planes_dual_r9k.md). The B
+// prefetch measured nothing (the K loop is not HBM-latency bound: TDP_PLANES_EXP experiments,
 // profiles/r6/planes_gemm_experiments.md)
 struct PlanesCfg {
   int stages, pf, splits;  // splits > 0: split-K override
 };
 PlanesCfg& planes_cfg() {
-  static PlanesCfg c{3, 0, 0};
+  static PlanesCfg c{4, 0, 0};
   return c;
 }
 }  // namespace
 
 bool gemm_planes_set_cfg(int stages, int pf, int splits) {
-  if (!((stages == 2 || stages == 3) && pf >= 0 && pf <= 4 && (stages == 2 || pf == 0) &&
+  // stages 4 = the two-waves-per-SIMD kernel (gemm_planes_dual_kernel: 3 stages, 512 threads)
+  if (!((stages >= 2 && stages <= 4) && pf >= 0 && pf <= 4 && (stages == 2 || pf == 0) &&
         splits >= 0))
     return false;
   planes_cfg() = {stages, pf, splits};
@@ -634,8 +802,21 @@ void launch_planes(const PParams& p, int nblocks, hipStream_t s) {
 }
 
 template <bool BKC>
+void launch_dual(const PParams& p, int nblocks, hipStream_t s) {
+  const size_t lds = (size_t)3 * (kABytes + kBN * kBK * 4);
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)gemm_planes_dual_kernel<BKC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    configured = true;
+  }
+  hipLaunchKernelGGL((gemm_planes_dual_kernel<BKC>), dim3(nblocks), dim3(2 * kT), lds, s, p);
+}
+
+template <bool BKC>
 void launch_cfg(const PParams& p, const PlanesCfg& c, int nblocks, hipStream_t s) {
-  if (c.stages == 3) launch_planes<BKC, 3, 0>(p, nblocks, s);
+  if (c.stages == 4) launch_dual<BKC>(p, nblocks, s);
+  else if (c.stages == 3) launch_planes<BKC, 3, 0>(p, nblocks, s);
   else if (c.pf == 1) launch_planes<BKC, 2, 1>(p, nblocks, s);
   else if (c.pf == 2) launch_planes<BKC, 2, 2>(p, nblocks, s);
   else if (c.pf >= 3) launch_planes<BKC, 2, 3>(p, nblocks, s);
