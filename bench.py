@@ -122,6 +122,12 @@ def parse():
                          "the optimizer's HBM traffic); with world_size 1 in the weight-gradient "
                          "GEMM epilogues (no gradient write/re-read). auto = on")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
+    ap.add_argument("--parallel", choices=["auto", "ddp", "tensor"], default="auto",
+                    help="N > 1 toy MLP: 'tensor' = the tensor-sharded step "
+                         "(parallel/tensor_parallel.py: activations cross xGMI, not weights), "
+                         "'ddp' = the DDP reducer's ladder, 'auto' = time both, keep the faster")
+    ap.add_argument("--select-steps", type=int, default=20,
+                    help="timed steps per candidate of --parallel auto")
     ap.add_argument("--comm-cus", type=int, default=None,
                     help="CUs left to RCCL: grid-sized kernels (persistent GEMMs, split-K "
                          "planners) plan for (CUs - N) (TDP_COMM_CUS; default 0)")
@@ -439,6 +445,13 @@ LADDER = (
 )
 
 
+# The tensor-sharded step (parallel/tensor_parallel.py): tried before the ladder at N > 1 for the
+# toy MLP; with --parallel auto both it and the ladder's first working rung are timed, the faster
+# one is measured.
+TENSOR_RUNG = {"name": "tensor-sharded", "factor": None, "fused": False, "graph": True,
+               "tensor": True}
+
+
 def _agree(ok: bool) -> bool:
     from tutorial_torch_distributed_data_parallel_amd.train.graph import agree
 
@@ -486,7 +499,28 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
     def loss_fn(out_, y):
         return tdp.ops.cross_entropy(out_, y, acc=acc)
 
-    if a.api == "accelerate":
+    tp = None
+    if cfg.get("tensor"):
+        from tutorial_torch_distributed_data_parallel_amd.parallel.tensor_parallel import \
+            TensorParallelMLP
+
+        if a.model != "toy_mlp" or a.api != "ddp":
+            raise RuntimeError("tensor-sharded step: the toy MLP through the native DDP API only")
+        tp = TensorParallelMLP(model)
+        ddp = None
+        opt = make_opt(tp.parameters())
+        data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
+        sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
+        loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+
+        def body(x, y):  # REF/multi-GPU-training-torch.py:118-126, sharded execution
+            opt.zero_grad(set_to_none=True)
+            loss = loss_fn(tp(x), y)
+            tdp.ops.backward(loss)
+            tp.sync_grads()  # the replicated head / bias: averaged all-reduce
+            opt.step()
+            return loss
+    elif a.api == "accelerate":
         # BASELINE.json config 4: the step through the Accelerate-style facade. One dataset
         # shared by all ranks, dealt out by whole batches (Accelerate's BatchSamplerShard).
         from tutorial_torch_distributed_data_parallel_amd.accelerate import Accelerator
@@ -678,9 +712,9 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
     step.raw = tdp_step  # the uncaptured body (diagnostics re-capture it)
     step.many = steps
     step.graph_steps = a.graph_steps if run_pair[0] is not None else (1 if graph else 0)
-    return types.SimpleNamespace(ddp=ddp, opt=opt, fused=fused, step=step, run=run,
+    return types.SimpleNamespace(ddp=ddp, tp=tp, opt=opt, fused=fused, step=step, run=run,
                                  graph=graph, rung=cfg["name"],
-                                 build_rehearsal=None if a.api == "accelerate"
+                                 build_rehearsal=None if (a.api == "accelerate" or tp is not None)
                                  else build_rehearsal)
 
 
@@ -822,7 +856,46 @@ def main():
         # and tries the full rung only, as before.
         import gc
 
+        def timed_ms(j, n):
+            """ms per step of n steps of job j, max over ranks (the selection's clock)."""
+            barrier()
+            sync()
+            t0 = time.perf_counter()
+            j.step.many(n)
+            sync()
+            barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                             device=dev if use_gpu else "cpu")
+            rt.all_reduce(t, "max")
+            return float(t.item()) * 1000.0 / n
+
+        tensor_job, selection = None, None
+        if world > 1 and a.parallel != "ddp" and a.model == "toy_mlp" and a.api == "ddp":
+            ok, err = True, None
+            try:
+                tj = build_tdp(a, ctx, TENSOR_RUNG, 0, fallbacks, fault)
+                clock_warmup()
+                tj.step.many(a.warmup)
+                sync()
+            except Exception as e:  # noqa: BLE001 - agreed below; the ladder follows
+                ok, err = False, e
+            if _agree(ok):
+                tensor_job = tj
+            else:
+                fallbacks.append(f"tensor-sharded failed ({repr(err)[:200] if err else 'on another rank'}); DDP ladder")
+                print(f"[bench] tensor-sharded step failed on some rank: {err!r}",
+                      file=sys.stderr, flush=True)
+                tj = None
+                gc.collect()
+                if use_gpu:
+                    torch.cuda.synchronize()
+                    torch.cuda.empty_cache()
         rungs = LADDER if world > 1 or os.environ.get("TDP_BENCH_LADDER") == "1" else LADDER[:1]
+        if tensor_job is not None and a.parallel == "tensor":
+            rungs = ()
+            job = tensor_job
+        elif tensor_job is not None:
+            selection = {"tensor-sharded_ms": round(timed_ms(tensor_job, a.select_steps), 4)}
         for attempt, cfg in enumerate(rungs):
             ok, err = True, None
             try:
@@ -848,9 +921,22 @@ def main():
                 torch.cuda.synchronize()
                 torch.cuda.empty_cache()
         else:
-            print("[bench] every rung of the fallback ladder failed: no timed step ran",
-                  file=sys.stderr, flush=True)
-            sys.exit(1)
+            if rungs and tensor_job is None:
+                print("[bench] every rung of the fallback ladder failed: no timed step ran",
+                      file=sys.stderr, flush=True)
+                sys.exit(1)
+            job = tensor_job if job is None else job
+        if selection is not None and job is not tensor_job:
+            selection[f"{job.rung}_ms"] = round(timed_ms(job, a.select_steps), 4)
+            if selection["tensor-sharded_ms"] < selection[f"{job.rung}_ms"]:
+                job = tensor_job
+            selection["chosen"] = job.rung
+            # the loser's graphs and buffers go before the timed run
+            gc.collect()
+            if use_gpu:
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+        tensor_job = None
         ddp, opt, fused, step, run, graph = (job.ddp, job.opt, job.fused, job.step, job.run,
                                              job.graph)
         build_rehearsal, rung = job.build_rehearsal, job.rung
@@ -900,6 +986,18 @@ def main():
                 "factor": ddp.factor_report() if ddp._factor else None,
                 "factor_tuning": ddp.factor_tuning}
 
+    if a.impl == "tdp" and getattr(job, "tp", None) is not None:
+        from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+        try:
+            job.tp.check_replicas()
+            ident = True
+        except RuntimeError:
+            ident = False
+        sync = {"replicas_identical": ident, "captured": isinstance(run, CapturedStep),
+                "backend": rt.get_backend(),
+                "modes": {"fc1": "column-sharded", "fc2": "row-sharded (reduce-scatter of "
+                          "activations)", "head": "replicated (averaged all-reduce)"}}
     comm_nranks = None
     if a.impl == "tdp" and rt.comm() is not None:
         comm_nranks = int(rt.comm().nranks)
@@ -950,6 +1048,8 @@ def main():
                 # the fallback ladder (LADDER): the rung that ran and what failed before it
                 "rung": rung,
                 "fallbacks": fallbacks,
+                # --parallel auto at N > 1: ms/step of each candidate, and the one measured
+                "selection": selection if a.impl == "tdp" else None,
                 "baseline": {"samples_per_s": round(base, 2), "source": base_src}
                 if base else None,
             },

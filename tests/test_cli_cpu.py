@@ -143,17 +143,18 @@ def test_launcher_hosts_the_rendezvous_store():
     assert one is None and env1 == {}
 
 
-def _bench_cpu2(env_extra):
+def _bench_cpu2(env_extra, *args):
     env = {k: None for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     env.update(env_extra)
     return _run(["bench.py", "--cpu", "--gpus", "2", "--steps", "2", "--warmup", "1",
-                 "--dataset", "128", "--batch", "16", "--mlp-dims", "64,32,32"], env_extra=env)
+                 "--dataset", "128", "--batch", "16", "--mlp-dims", "64,32,32", *args],
+                env_extra=env)
 
 
 def test_bench_fallback_ladder_records_the_rung():
     """a failure in a rung (here: the first warm-up step, on every rank)
     moves every rank to the next rung, and the record says which rung ran and why."""
-    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup"})
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup"}, "--parallel", "ddp")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     assert rec["config"]["rung"] == "sharded-buckets", rec["config"]
@@ -162,14 +163,45 @@ def test_bench_fallback_ladder_records_the_rung():
 
 
 def test_bench_fallback_ladder_exhausted_exits_nonzero():
-    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"})
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"}, "--parallel", "ddp")
     assert r.returncode != 0
     assert r.stdout.strip() == ""
     assert "every rung of the fallback ladder failed" in r.stderr
 
 
 def test_bench_clean_run_reports_no_fallback():
-    r = _bench_cpu2({})
+    r = _bench_cpu2({}, "--parallel", "ddp")
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     assert rec["config"]["rung"] == "full" and rec["config"]["fallbacks"] == []
+
+
+def test_bench_parallel_auto_times_both_and_records_the_choice():
+    """--parallel auto (the default) at N > 1: the tensor-sharded step and the DDP ladder's
+    first working rung are both timed; the faster one is measured and the record says so."""
+    r = _bench_cpu2({}, "--select-steps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
+    sel = c["selection"]
+    assert set(sel) == {"tensor-sharded_ms", "full_ms", "chosen"}, sel
+    fast = min(("tensor-sharded", "full"), key=lambda k: sel[k + "_ms"])
+    assert sel["chosen"] == fast == c["rung"], c
+    assert c["sync"]["replicas_identical"] is True, c["sync"]
+
+
+def test_bench_parallel_tensor_runs_the_sharded_step():
+    r = _bench_cpu2({}, "--parallel", "tensor")
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
+    assert c["rung"] == "tensor-sharded" and c["selection"] is None, c
+    assert c["sync"]["modes"]["fc1"] == "column-sharded" and c["parallelism"] == "dp2"
+    assert c["sync"]["replicas_identical"] is True
+
+
+def test_bench_parallel_auto_survives_an_exhausted_ladder():
+    """Every DDP rung fails its warm-up: the tensor-sharded step (built first) still yields the
+    number."""
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
+    assert c["rung"] == "tensor-sharded" and len(c["fallbacks"]) == 4, c

@@ -101,7 +101,7 @@ def _peer_bench(extra_env, *args):
     env.update(TDP_GPU_PEER="1", **extra_env)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
            "--warmup", "2", "--mlp-dims", "1024,512,512", "--dataset", "1024", "--batch", "32",
-           "--no-diag", "--device-warmup-ms", "0", *args]
+           "--no-diag", "--device-warmup-ms", "0", "--parallel", "ddp", *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])

@@ -1,0 +1,54 @@
+"""MI355X: the tensor-sharded toy-MLP step (parallel/tensor_parallel.py) with real peers on one
+GPU (the peer-memory vehicle: collectives as device kernels, capturable): captured == eager
+bitwise, both == the one-process global-batch step; and bench.py's --parallel tensor / auto."""
+import functools
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import spawn
+
+import tp_workers as TW  # noqa: E402  (tests/ is on sys.path via conftest)
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(fn, tmp_path, n=2, **kw):
+    spawn(functools.partial(fn, **kw) if kw else fn, n, args=(str(tmp_path),), grace=5.0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tensor_parallel_captured_with_real_peers(tmp_path, world):
+    run(TW.captured_parity, tmp_path, n=world)
+
+
+def test_tensor_parallel_syncbn_captured_with_real_peers(tmp_path):
+    run(TW.captured_parity, tmp_path, n=2, bn=True)
+
+
+def _peer_bench(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    env.update(TDP_GPU_PEER="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+           "--warmup", "2", "--mlp-dims", "1024,512,512", "--dataset", "1024", "--batch", "32",
+           "--no-diag", "--device-warmup-ms", "0", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+
+
+def test_bench_tensor_sharded_step_captured():
+    c = _peer_bench("--parallel", "tensor")["config"]
+    assert c["rung"] == "tensor-sharded" and c["fallbacks"] == [], c
+    assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
+
+
+def test_bench_parallel_auto_records_selection():
+    c = _peer_bench("--select-steps", "4")["config"]
+    sel = c["selection"]
+    assert sel is not None and sel["chosen"] == c["rung"], c
+    assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]

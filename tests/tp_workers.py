@@ -1,0 +1,172 @@
+"""Multi-rank workers for the tensor-sharded toy-MLP step (parallel/tensor_parallel.py) on
+CPU/gloo. Oracle: the one-process step of the FULL model on the node's batch (every rank's
+batch in rank order, mean loss) with torch.optim -- what DDP's averaged all-reduce computes."""
+import copy
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+import tutorial_torch_distributed_data_parallel_amd as tdp
+from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+from tutorial_torch_distributed_data_parallel_amd.parallel.tensor_parallel import \
+    TensorParallelMLP
+
+DIMS = dict(in_features=37, hidden=(32, 20), num_classes=5)
+B = 6
+
+
+def _batch(r, step):
+    g = torch.Generator().manual_seed(1000 * step + r)
+    return torch.randn(B, 37, generator=g) * (1 + r), torch.randint(0, 5, (B,), generator=g)
+
+
+def _ref_model(bn):
+    torch.manual_seed(0)
+    return ToyMLP(batchnorm=bn, **DIMS)
+
+
+def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4):
+    tdp.init_process_group("gloo")
+    W = rt.get_world_size()
+    ref = _ref_model(bn)
+    model = copy.deepcopy(ref)
+    if bn:
+        model = tdp.nn.convert_sync_batchnorm(model)
+    tp = TensorParallelMLP(model, global_batch=global_batch)
+    hp = dict(lr=0.05, momentum=0.9, weight_decay=1e-3)
+    opt = tdp.optim.SGD(tp.parameters(), **hp)
+    ropt = torch.optim.SGD(ref.parameters(), **hp)
+    for step in range(steps):
+        xs, ys = zip(*[_batch(r, step) for r in range(W)])
+        X, Y = torch.cat(xs), torch.cat(ys)
+        x, y = (X, Y) if global_batch else (xs[rank], ys[rank])
+        opt.zero_grad()
+        out = tp(x)
+        assert out.shape == (B, 5)
+        tdp.ops.cross_entropy(out, ys[rank]).backward()
+        tp.sync_grads()
+        opt.step()
+        ropt.zero_grad()
+        F.cross_entropy(ref(X), Y).backward()
+        ropt.step()
+    full = tp.full_state_dict()
+    sd = ref.state_dict()
+    assert set(full) == set(sd), (sorted(full), sorted(sd))
+    for k, v in sd.items():
+        torch.testing.assert_close(full[k].float(), v.float(), atol=2e-5, rtol=1e-4,
+                                   msg=lambda m: f"{k}: {m}")
+    # every rank holds the same full model
+    if W > 1:
+        allsd = [None] * W
+        dist.all_gather_object(allsd, {k: v.clone() for k, v in full.items()})
+        for other in allsd[1:]:
+            for k in full:
+                assert torch.equal(other[k], allsd[0][k]), k
+    # load the full state into a differently initialised wrapper: same full state back
+    torch.manual_seed(5)
+    fresh = ToyMLP(batchnorm=bn, **DIMS)
+    if bn:
+        fresh = tdp.nn.convert_sync_batchnorm(fresh)
+    tp2 = TensorParallelMLP(fresh, global_batch=global_batch)
+    tp2.load_full_state_dict(full)
+    back = tp2.full_state_dict()
+    for k in full:
+        assert torch.equal(back[k], full[k]), k
+    tdp.destroy_process_group()
+
+
+def refuses_plain_bn(rank, out_dir):
+    tdp.init_process_group("gloo")
+    try:
+        TensorParallelMLP(ToyMLP(batchnorm=True, **DIMS))
+    except ValueError as e:
+        assert "SyncBN" in str(e)
+    else:
+        raise AssertionError("plain BatchNorm1d before the row-parallel layer was accepted")
+    tdp.destroy_process_group()
+
+
+GDIMS = dict(in_features=256, hidden=(128, 64), num_classes=10)
+GB = 16
+
+
+def _gbatch(r, step):
+    g = torch.Generator().manual_seed(77 * step + r)
+    return (torch.randn(GB, 256, generator=g) * (1 + 0.5 * r)).cuda(), \
+        torch.randint(0, 10, (GB,), generator=g).cuda()
+
+
+def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5):
+    """GPU, W ranks (peer vehicle on one GPU, or RCCL): the tensor-sharded step captured into a
+    hipGraph and replayed == the same step run eagerly, BITWISE; both match the one-process
+    global-batch step of the full model (torch fp32 on the GPU) to fp32 accuracy."""
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    tdp.init_process_group(backend)
+    W = rt.get_world_size()
+
+    def build():
+        torch.manual_seed(0)
+        m = ToyMLP(batchnorm=bn, device="cuda", **GDIMS)
+        if bn:
+            m = tdp.nn.convert_sync_batchnorm(m)
+        t = TensorParallelMLP(m)
+        return t, tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+
+    t1, o1 = build()
+    t2, o2 = build()
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential()
+    full = ToyMLP(batchnorm=bn, device="cuda", **GDIMS)
+    rsd = {k: v.clone() for k, v in full.state_dict().items()}
+    import torch.nn as nn
+    layers = [nn.Linear(256, 128), nn.BatchNorm1d(128) if bn else nn.Identity(), nn.ReLU(),
+              nn.Linear(128, 64), nn.BatchNorm1d(64) if bn else nn.Identity(), nn.ReLU(),
+              nn.Linear(64, 10)]
+    ref = nn.Sequential(*layers).cuda()
+    keymap = {"0": "fc1", "1": "bn1", "3": "fc2", "4": "bn2", "6": "fc3"}
+    ref.load_state_dict({f"{i}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
+                         for k, v in rsd.items() if k.split(".")[0] == n}, strict=True)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    sx = torch.empty(GB, 256, device="cuda")
+    sy = torch.empty(GB, dtype=torch.long, device="cuda")
+
+    def step2():
+        o2.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(t2(sx), sy))
+        t2.sync_grads()
+        o2.step()
+
+    g = None
+    for step in range(steps):
+        xs, ys = zip(*[_gbatch(r, step) for r in range(W)])
+        x, y = xs[rank], ys[rank]
+        o1.zero_grad(set_to_none=True)
+        tdp.ops.backward(tdp.ops.cross_entropy(t1(x), y))
+        t1.sync_grads()
+        o1.step()
+        sx.copy_(x)
+        sy.copy_(y)
+        if g is None:
+            g = CapturedStep(step2, warmup=1)
+        else:
+            g.replay()
+        ropt.zero_grad()
+        F.cross_entropy(ref(torch.cat(xs)), torch.cat(ys)).backward()
+        ropt.step()
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(t1.parameters(), t2.parameters())):
+        assert torch.equal(a, b), f"rank {rank}: captured != eager for param {i} " \
+                                  f"(max diff {float((a - b).abs().max())})"
+    got = t2.full_state_dict()
+    want = {f"{n}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
+            for k, v in ref.state_dict().items() if k.split(".")[0] == i}
+    for k, v in want.items():
+        torch.testing.assert_close(got[k].float(), v.float(), atol=5e-5, rtol=1e-3,
+                                   msg=lambda m: f"W={W} bn={bn} {k}: {m}")
+    t1.check_replicas()
+    t2.check_replicas()
+    rt.barrier()
+    tdp.destroy_process_group()

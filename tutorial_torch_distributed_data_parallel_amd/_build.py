@@ -93,7 +93,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _needs(o, s, headers):
             # the split-bf16 GEMM keeps its f32 residual subtractions scalar: packed f32 VALU
             # (v_pk_add_f32) costs ~4x a v_sub_f32's issue slot beside MFMAs
-            extra = ["-fno-slp-vectorize"] if s.name in ("gemm_f32_fast.hip", "gemm_planes.hip") else []
+            extra = ["-fno-slp-vectorize"] if s.name in ("gemm_f32_fast.hip", "gemm_planes.hip", "gemm_emu8.hip") else []
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common, "-ffp-contract=fast",
                               *extra, "-c", str(s), "-o", str(o)])
     for s in cpp_srcs:

@@ -14,6 +14,7 @@
 
 #include "comm.h"
 #include "conv.h"
+#include "emu8.h"
 #include "kernels.h"
 #include "planes.h"
 #include "loader.h"
@@ -214,6 +215,30 @@ void gemm_planes_op(const Tensor& Ap, const Tensor& B, Tensor& C, bool b_kcontig
 }
 
 // x [rows, cols] fp32 (unit inner stride) -> its exact bf16 split planes [3, rows, cols]
+// large-tile split-bf16 GEMM (csrc/gemm_emu8.hip): A [M,K]; B [N,K] if b_kcontig else [K,N]
+void gemm_emu8_op(const Tensor& A, const Tensor& B, Tensor& C, bool b_kcontig, double beta) {
+  CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
+  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
+  CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_ROWMAJOR(C);
+  GemmEmu8Args a;
+  a.M = (int)C.size(0);
+  a.N = (int)C.size(1);
+  a.K = (int)A.size(1);
+  TORCH_CHECK(A.size(0) == a.M, "gemm_emu8: A rows != C rows");
+  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == a.N, "gemm_emu8: B cols != C cols");
+  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == a.K, "gemm_emu8: inner dims differ");
+  a.A = A.data_ptr<float>();
+  a.B = B.data_ptr<float>();
+  a.C = C.data_ptr<float>();
+  a.lda = A.stride(0);
+  a.ldb = B.stride(0);
+  a.ldc = C.stride(0);
+  a.b_kcontig = b_kcontig;
+  a.beta = (float)beta;
+  TORCH_CHECK(gemm_emu8_ok(a), "gemm_emu8: K % 32 == 0 and 16-B aligned rows required");
+  gemm_emu8_run(a, cur_stream());
+}
+
 Tensor split_planes_op(const Tensor& x) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_ROWMAJOR(x);
   const int rows = (int)x.size(0), cols = (int)x.size(1);
@@ -1410,6 +1435,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,
         py::arg("gate") = py::none(), py::arg("out_planes") = py::none());
   m.def("split_planes", &split_planes_op);
+  m.def("gemm_emu8", &gemm_emu8_op, py::arg("A"), py::arg("B"), py::arg("C"),
+        py::arg("b_kcontig") = true, py::arg("beta") = 0.0);
+  m.def("gemm_emu8_set_waves", &gemm_emu8_set_waves);
   m.def("head_bwd", &head_bwd_op, py::arg("g"), py::arg("x"), py::arg("w"), py::arg("dx"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("gate") = py::none(),
         py::arg("planes") = false, py::arg("backend") = nullptr, py::arg("w_offset") = -1,

@@ -1,0 +1,321 @@
+"""Tensor-sharded execution of the toy MLP with data-parallel training semantics.
+
+What the reference does: ``DDP(model)`` (/root/reference/multi-GPU-training-torch.py:245), then
+per step ``loss.backward()`` -- every rank all-reduces the full 218 MB gradient -- and
+``optimizer.step()`` on a full replica (:125-126). Same math here, different execution: the
+hidden Linear pair is split Megatron-style over the W ranks of the node, so what crosses xGMI
+each step is ACTIVATIONS (a few MB), not weights:
+
+  X   = all-gather of every rank's batch            [W*B, in]      (no gradient)
+  H1  = relu?(X . W1[own rows]^T + b1[own])         [W*B, h1/W]    column-parallel fc1
+        (BatchNorm1d here sees the GLOBAL batch: SyncBN statistics with no collective)
+  P2  = H1 . W2[:, own cols]^T                      [W*B, h2]      row-parallel fc2 (partial)
+  H2  = relu?(reduce_scatter_rows(P2) + b2)         [B, h2]        this rank's samples
+  out = fc3(H2)                                     [B, classes]   replicated head
+
+Backward is autograd through the same ops: the reduce-scatter's gradient is the all-gather of
+dH2, scaled by 1/W so that every sharded gradient is the global-batch MEAN that DDP's averaged
+all-reduce produces; the replicated parameters (b2, the head, a BatchNorm after fc2) get the
+usual averaged all-reduce (``sync_grads``, ~0.2 MB). Each rank then updates only its shard
+with the ordinary optimizer: 1/W of the optimizer's HBM traffic, the dominant cost of the dp1
+step (profiles/r9/wgrad_split_roles_r9.md).
+
+Per step and rank at W ranks, B samples each (toy MLP 9216-4096-4096-10, fp32): X all-gather
+(W-1) B 9216 x 4 B (33 MB at W = 8), reduce-scatter and all-gather of [W*B, 4096] (2 x 14.7 MB
+at W = 8) -- against (W-1)/W x 218 MB x 2 for a gradient all-reduce or the factored modes'
+parameter all-gathers (parallel/commmodel.py, docs/COMM_MODEL.md "Tensor-sharded"). GEMM work
+per rank equals dp1's; numerics are fp32 (the same kernels), summation order differs from the
+replicated step (tests/test_tensor_parallel_cpu.py checks the step against the one-process
+global-batch step).
+
+``state_dict()`` of the wrapper is the full model's (rank-order all-gathers), so checkpoints
+stay those of the unsharded ToyMLP (utils/checkpoint.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import runtime
+from .arena import ParamArena
+from ..nn import BatchNorm1d, Linear, SyncBatchNorm
+
+
+# Measurement only (scripts/tp_rank_proxy.py): one process plays rank 0 of a W-rank job -- shard
+# shapes of W ranks, every collective replaced by its local copy (no peer traffic): the per-rank
+# compute of the W-rank step on one GPU.
+_FAKE_WORLD = 0
+
+
+def set_fake_world(w: int) -> None:
+    global _FAKE_WORLD
+    _FAKE_WORLD = int(w)
+
+
+def _ranks():
+    if _FAKE_WORLD:
+        return 0, _FAKE_WORLD
+    return runtime.get_rank(), runtime.get_world_size()
+
+
+def _all_gather_rows(out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """out[r*n:(r+1)*n] = rank r's x (ordered on the current stream on the GPU)."""
+    rank, world = _ranks()
+    if world == 1:
+        out.copy_(x)
+        return out
+    if _FAKE_WORLD:
+        out.view((world,) + tuple(x.shape)).copy_(x.unsqueeze(0).expand((world,) + tuple(x.shape)))
+        return out
+    comm = runtime.comm()
+    if x.is_cuda and comm is not None:
+        comm.all_gather(out, x.contiguous())
+    else:
+        dist.all_gather(list(out.chunk(world)), x.contiguous())
+    return out
+
+
+def _reduce_scatter_rows(out: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """out = sum over ranks of rank r's p[rank*n:(rank+1)*n] (this rank's row block)."""
+    rank, world = _ranks()
+    if world == 1 or _FAKE_WORLD:
+        out.copy_(p[: out.shape[0]])
+        return out
+    comm = runtime.comm()
+    if p.is_cuda and comm is not None:
+        comm.reduce_scatter(out, p.contiguous(), "sum")
+    else:  # gloo has no reduce-scatter: all-reduce, keep the own block
+        full = p.contiguous().clone()
+        dist.all_reduce(full)
+        out.copy_(full.chunk(world)[rank])
+    return out
+
+
+class _GatherRows(torch.autograd.Function):
+    """Every rank's rows, in rank order; the gradient of this rank's rows is the sum over ranks
+    of their gradient blocks (a reduce-scatter)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _, world = _ranks()
+        out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), device=x.device,
+                          dtype=x.dtype)
+        return _all_gather_rows(out, x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        _, world = _ranks()
+        out = torch.empty((dy.shape[0] // world,) + tuple(dy.shape[1:]), device=dy.device,
+                          dtype=dy.dtype)
+        return _reduce_scatter_rows(out, dy)
+
+
+class _ScatterRowsSum(torch.autograd.Function):
+    """This rank's row block of the sum over ranks; the gradient is the all-gather of the row
+    blocks' gradients, times ``scale`` (1/W: sum of per-rank mean losses -> global mean)."""
+
+    @staticmethod
+    def forward(ctx, p, scale: float):
+        _, world = _ranks()
+        ctx.scale = scale
+        out = torch.empty((p.shape[0] // world,) + tuple(p.shape[1:]), device=p.device,
+                          dtype=p.dtype)
+        return _reduce_scatter_rows(out, p)
+
+    @staticmethod
+    def backward(ctx, dy):
+        _, world = _ranks()
+        out = torch.empty((world * dy.shape[0],) + tuple(dy.shape[1:]), device=dy.device,
+                          dtype=dy.dtype)
+        _all_gather_rows(out, dy)
+        if ctx.scale != 1.0:
+            out.mul_(ctx.scale)
+        return out, None
+
+
+def _linears(model):
+    order = getattr(model, "_order", None)
+    if order is None:
+        raise TypeError("TensorParallelMLP: expects a ToyMLP-like module (an ordered stack of "
+                        "Linear [+ BatchNorm1d] layers)")
+    mods = [(n, getattr(model, n)) for n in order]
+    return mods
+
+
+class TensorParallelMLP(nn.Module):
+    """Wrap a (full, identically initialised) ToyMLP with two hidden layers for tensor-sharded
+    training at the current world size; ``forward`` takes this rank's batch and returns this
+    rank's logits, exactly like ``DDP(model)(x)``. Call ``sync_grads()`` after backward (the
+    averaged all-reduce of the replicated parameters' gradients), then ``optimizer.step()`` on
+    ``parameters()``.
+
+    ``global_batch=True``: ``forward`` receives the whole node's batch [W*B, in] in rank order
+    (every rank gathered it from its replica of the dataset) and skips the input all-gather."""
+
+    def __init__(self, model: nn.Module, global_batch: bool = False):
+        super().__init__()
+        rank, world = _ranks()
+        self.rank, self.world = rank, world
+        self.global_batch = bool(global_batch)
+        mods = _linears(model)
+        lin = [(n, m) for n, m in mods if isinstance(m, nn.Linear)]
+        bns = {n: m for n, m in mods if isinstance(m, nn.modules.batchnorm._BatchNorm)}
+        if len(lin) != 3:
+            raise ValueError("TensorParallelMLP: supports the toy MLP's shape (two hidden "
+                             f"Linear layers and a head), got {len(lin)} Linear layers")
+        (n1, fc1), (n2, fc2), (n3, fc3) = lin
+        h1 = fc1.out_features
+        if h1 % world or (h1 // world) % 4:
+            raise ValueError(f"TensorParallelMLP: hidden width {h1} must split into W = "
+                             f"{world} shards of a multiple of 4")
+        names = [n for n, _ in mods]
+        bn1 = bns.get(names[names.index(n1) + 1]) if names.index(n1) + 1 < len(names) else None
+        bn2 = bns.get(names[names.index(n2) + 1]) if names.index(n2) + 1 < len(names) else None
+        if bn1 is not None and world > 1 and not isinstance(bn1, SyncBatchNorm):
+            raise ValueError("TensorParallelMLP: the BatchNorm after fc1 normalises over the "
+                             "node's batch here (SyncBN statistics); per-rank statistics "
+                             "(plain BatchNorm1d) are not supported -- convert_sync_batchnorm")
+        # every shard is cut from rank 0's weights (DDP's construction-time broadcast)
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                runtime.broadcast(t.data, 0)
+        self._names = (n1, n2, n3)
+        self._bn_names = (names[names.index(n1) + 1] if bn1 is not None else None,
+                          names[names.index(n2) + 1] if bn2 is not None else None)
+        self._dims = (fc1.in_features, h1, fc2.out_features, fc3.out_features)
+        s = h1 // world
+        lo, hi = rank * s, (rank + 1) * s
+        dev = fc1.weight.device
+        with torch.no_grad():
+            relu1 = bn1 is None
+            self.fc1 = Linear(fc1.in_features, s, bias=fc1.bias is not None, relu=relu1,
+                              device=dev)
+            self.fc1.weight.copy_(fc1.weight[lo:hi])
+            if fc1.bias is not None:
+                self.fc1.bias.copy_(fc1.bias[lo:hi])
+            self.bn1 = None
+            if bn1 is not None:
+                self.bn1 = BatchNorm1d(s, eps=bn1.eps, momentum=bn1.momentum,
+                                       affine=bn1.affine,
+                                       track_running_stats=bn1.track_running_stats,
+                                       relu=getattr(bn1, "relu", False), device=dev)
+                for name in ("weight", "bias", "running_mean", "running_var"):
+                    src = getattr(bn1, name, None)
+                    if src is not None:
+                        getattr(self.bn1, name).copy_(src[lo:hi])
+                if bn1.num_batches_tracked is not None:
+                    self.bn1.num_batches_tracked.copy_(bn1.num_batches_tracked)
+                self.bn1._nbt = getattr(bn1, "_nbt", 0)
+            self.fc2 = Linear(s, fc2.out_features, bias=False, device=dev)
+            self.fc2.weight.copy_(fc2.weight[:, lo:hi])
+            self.b2 = nn.Parameter(fc2.bias.detach().clone()) if fc2.bias is not None else None
+            self.relu2 = bn2 is None and getattr(fc2, "relu", False)
+            self.bn2 = bn2  # replicated: normalises this rank's rows (sync or not, as given)
+            self.fc3 = fc3
+        self._replicated = [p for p in ([self.b2] if self.b2 is not None else [])] + \
+            (list(bn2.parameters()) if bn2 is not None else []) + list(fc3.parameters())
+        # one flat arena, replicated parameters first: their gradients are ONE contiguous range
+        # (a single all-reduce, no packing), every gradient has its slot (the optimizer's
+        # single-kernel, capture-safe flat step: optim/fused.py)
+        rep = {id(q) for q in self._replicated}
+        self._arena = ParamArena(self._replicated +
+                                 [q for q in self.parameters() if id(q) not in rep])
+        last = len(self._replicated) - 1
+        self._rep_end = self._arena.offsets[last] + self._arena.numels[last]
+
+    # ---------------------------------------------------------------------------- forward
+    def forward(self, x):
+        x = x.reshape(x.shape[0], -1)
+        X = x if (self.world == 1 or self.global_batch) else _GatherRows.apply(x)
+        h = self.fc1(X)
+        if self.bn1 is not None:
+            h = self.bn1(h)
+        p = self.fc2(h)
+        y = _ScatterRowsSum.apply(p, 1.0 / self.world) if self.world > 1 else p
+        if self.b2 is not None:
+            y = y + self.b2
+        if self.bn2 is not None:
+            y = self.bn2(y)
+        elif self.relu2:
+            y = torch.relu(y)
+        return self.fc3(y)
+
+    def sync_grads(self) -> None:
+        """Every gradient into its arena slot (a gradient autograd produced elsewhere -- the
+        broadcast bias add -- is copied in), then the averaged all-reduce of the replicated
+        parameters' gradients: one collective over the arena's leading range."""
+        a = self._arena
+        with torch.no_grad():
+            for i, q in enumerate(a.params):
+                if q.grad is not None and not a.is_arena_grad(i):
+                    g = a.grad_view(i)
+                    g.copy_(q.grad)
+                    q.grad = g
+        if self.world == 1 or _FAKE_WORLD:
+            return
+        runtime.all_reduce(a.grad[: self._rep_end], "avg")
+
+    def check_replicas(self) -> None:
+        """Raise unless every rank holds bit-identical replicated parameters (collective)."""
+        if self.world == 1 or _FAKE_WORLD:
+            return
+        flat = torch.cat([p.detach().reshape(-1) for p in self._replicated])
+        out = torch.empty(self.world * flat.numel(), device=flat.device, dtype=flat.dtype)
+        _all_gather_rows(out, flat)
+        for r, part in enumerate(out.chunk(self.world)):
+            if not torch.equal(part, flat):
+                raise RuntimeError(f"tensor-sharded step: replicated parameters of rank {r} "
+                                   f"differ from rank {self.rank}'s")
+
+    # ----------------------------------------------------------------------- checkpoints
+    def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t.detach().clone()
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), device=t.device,
+                          dtype=t.dtype)
+        return _all_gather_rows(out, t.detach().contiguous())
+
+    def full_state_dict(self) -> dict:
+        """The unsharded ToyMLP state_dict (collective: every rank must call it)."""
+        n1, n2, n3 = self._names
+        b1n, b2n = self._bn_names
+        sd = {f"{n1}.weight": self._gather_rows(self.fc1.weight)}
+        if self.fc1.bias is not None:
+            sd[f"{n1}.bias"] = self._gather_rows(self.fc1.bias)
+        if self.bn1 is not None:
+            for k, v in self.bn1.state_dict().items():
+                sd[f"{b1n}.{k}"] = v.clone() if k == "num_batches_tracked" else \
+                    self._gather_rows(v)
+        # fc2 columns: gather the [h2, s] shards as rows of their transposes
+        sd[f"{n2}.weight"] = self._gather_rows(self.fc2.weight.t().contiguous()).t().contiguous()
+        if self.b2 is not None:
+            sd[f"{n2}.bias"] = self.b2.detach().clone()
+        if self.bn2 is not None:
+            for k, v in self.bn2.state_dict().items():
+                sd[f"{b2n}.{k}"] = v.clone()
+        for k, v in self.fc3.state_dict().items():
+            sd[f"{n3}.{k}"] = v.clone()
+        return sd
+
+    def load_full_state_dict(self, sd: dict) -> None:
+        n1, n2, n3 = self._names
+        b1n, b2n = self._bn_names
+        s = self._dims[1] // self.world
+        lo, hi = self.rank * s, (self.rank + 1) * s
+        with torch.no_grad():
+            self.fc1.weight.copy_(sd[f"{n1}.weight"][lo:hi])
+            if self.fc1.bias is not None:
+                self.fc1.bias.copy_(sd[f"{n1}.bias"][lo:hi])
+            if self.bn1 is not None:
+                for k, v in self.bn1.state_dict().items():
+                    src = sd[f"{b1n}.{k}"]
+                    v.copy_(src if k == "num_batches_tracked" else src[lo:hi])
+            self.fc2.weight.copy_(sd[f"{n2}.weight"][:, lo:hi])
+            if self.b2 is not None:
+                self.b2.copy_(sd[f"{n2}.bias"])
+            if self.bn2 is not None:
+                self.bn2.load_state_dict({k[len(b2n) + 1:]: v for k, v in sd.items()
+                                          if k.startswith(b2n + ".")})
+            self.fc3.load_state_dict({k[len(n3) + 1:]: v for k, v in sd.items()
+                                      if k.startswith(n3 + ".")})
