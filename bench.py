@@ -500,22 +500,53 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         return tdp.ops.cross_entropy(out_, y, acc=acc)
 
     tp = None
+    bsz = a.batch  # rows one step gathers (the tensor-sharded step: the node's batch)
     if cfg.get("tensor"):
         from tutorial_torch_distributed_data_parallel_amd.parallel.tensor_parallel import \
             TensorParallelMLP
 
         if a.model != "toy_mlp" or a.api != "ddp":
             raise RuntimeError("tensor-sharded step: the toy MLP through the native DDP API only")
-        tp = TensorParallelMLP(model)
+        # every rank holds the same dataset and every rank's DistributedSampler: it gathers the
+        # node's batch (rank 0's samples, rank 1's, ...) from its own HBM instead of receiving
+        # the other ranks' inputs over xGMI (33 MB per step at W = 8); the loss stays on this
+        # rank's samples. TDP_TP_GLOBAL=0: each rank gathers its own batch, the wrapper
+        # all-gathers the inputs.
+        shared = os.environ.get("TDP_TP_GLOBAL", "1") == "1"
+        tp = TensorParallelMLP(model, global_batch=shared)
         ddp = None
         opt = make_opt(tp.parameters())
-        data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
-        sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
-        loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+        if shared:
+            data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
+            samplers = [DistributedSampler(data, num_replicas=world, rank=r, shuffle=True)
+                        for r in range(world)]
+            loaders = [DeviceLoader(data, a.batch, sampler=s_, drop_last=True)
+                       for s_ in samplers]
+
+            class _NodeOrder:
+                """The node's batch order: step s = rank 0's batch s, rank 1's batch s, ..."""
+
+                def set_epoch(self, e):
+                    for s_ in samplers:
+                        s_.set_epoch(e)
+
+                def epoch_indices(self):
+                    idx = torch.stack([ld.epoch_indices() for ld in loaders])
+                    nb = idx.shape[1] // a.batch
+                    return idx[:, :nb * a.batch].reshape(world, nb, a.batch).transpose(0, 1) \
+                        .reshape(-1).contiguous()
+            sampler = loader = _NodeOrder()
+            bsz = a.batch * world
+            own = slice(rank * a.batch, (rank + 1) * a.batch)
+        else:
+            data = SyntheticDataset(a.dataset, in_shape, 10, seed=rank, device=dev)
+            sampler = DistributedSampler(data, num_replicas=world, rank=rank, shuffle=True)
+            loader = DeviceLoader(data, a.batch, sampler=sampler, drop_last=True)
+            own = slice(None)
 
         def body(x, y):  # REF/multi-GPU-training-torch.py:118-126, sharded execution
             opt.zero_grad(set_to_none=True)
-            loss = loss_fn(tp(x), y)
+            loss = loss_fn(tp(x), y[own])
             tdp.ops.backward(loss)
             tp.sync_grads()  # the replicated head / bias: averaged all-reduce
             opt.step()
@@ -589,29 +620,29 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
 
     # batches are gathered on the device by the sampler's indices (one H2D copy per epoch);
     # a captured graph reads them from a static index tensor, eager steps from a slice
-    idx_static = torch.empty(a.batch, dtype=torch.long, device=dev)
+    idx_static = torch.empty(bsz, dtype=torch.long, device=dev)
     cur = {"epoch": 0, "pos": 0, "idx": loader.epoch_indices(), "b": None}
-    idx_static.copy_(cur["idx"][:a.batch])
+    idx_static.copy_(cur["idx"][:bsz])
     # captured toy-MLP step: the gather reads the epoch order through a device-side cursor
     # it advances itself (no per-step index copy node in the graph)
     ecur = None
-    if graph and use_gpu and EpochCursor.fits(data.x, data.y, a.batch):
-        ecur = EpochCursor(len(cur["idx"]), a.batch, dev)
+    if graph and use_gpu and EpochCursor.fits(data.x, data.y, bsz):
+        ecur = EpochCursor(len(cur["idx"]), bsz, dev)
         ecur.set_order(cur["idx"])
 
     def advance():
-        if cur["pos"] + a.batch > len(cur["idx"]):
+        if cur["pos"] + bsz > len(cur["idx"]):
             cur["epoch"] += 1
             sampler.set_epoch(cur["epoch"])
             cur["idx"], cur["pos"] = loader.epoch_indices(), 0
             if ecur is not None:
                 ecur.set_order(cur["idx"])
-        b = cur["idx"][cur["pos"]: cur["pos"] + a.batch]
+        b = cur["idx"][cur["pos"]: cur["pos"] + bsz]
         if graph and ecur is None:
             idx_static.copy_(b)
             b = idx_static
         cur["b"] = b
-        cur["pos"] += a.batch
+        cur["pos"] += bsz
 
     def tdp_step():
         if ecur is not None:
@@ -700,7 +731,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         while k < n:
             G = a.graph_steps
             if run_pair[0] is not None and n - k >= G and \
-                    cur["pos"] + G * a.batch <= len(cur["idx"]):
+                    cur["pos"] + G * bsz <= len(cur["idx"]):
                 for _ in range(G):
                     advance()
                 out = run_pair[0]()

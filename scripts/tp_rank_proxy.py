@@ -39,11 +39,12 @@ def run(W):
     TPm.set_fake_world(W)
     torch.manual_seed(0)
     m = ToyMLP(device=dev)
-    net = TPm.TensorParallelMLP(m) if W > 0 else tdp.DDP(m, device_ids=[0])
+    # the bench's form: every rank gathers the node's batch itself (no input all-gather)
+    net = TPm.TensorParallelMLP(m, global_batch=True) if W > 0 else tdp.DDP(m, device_ids=[0])
     opt = tdp.optim.SGD(net.parameters(), lr=0.01, momentum=0.9)
     if W == 0:
         net.register_fused_optimizer(opt)
-    x = torch.randn(B, 9216, device=dev)
+    x = torch.randn(B * max(W, 1), 9216, device=dev)
     y = torch.randint(0, 10, (B,), device=dev)
 
     def step():

@@ -104,6 +104,22 @@ def _prefetch_prev_g(ctx, dx: torch.Tensor):
     return prev if prev is not None and prev.factor_prefetch_g(ctx.prev_w, dx) else None
 
 
+_WGRAD_SPLITS: dict = {}
+
+
+def _wgrad_splits(out: int, inp: int, k: int, device) -> int:
+    """Split-K count the weight-gradient GEMM dW[out, in] (depth k) gets WITHOUT a fused bias
+    row sum (cached per shape): > 1 means the row sum would cost it its split-K (the
+    tensor-sharded step's fc1 at W = 8: 288 tiles for 512 slots)."""
+    key = (out, inp, k, device.index)
+    v = _WGRAD_SPLITS.get(key)
+    if v is None:
+        C = native()
+        v = _WGRAD_SPLITS[key] = int(C.gemm_f32_plan(out, inp, k, False,
+                                                     C.num_cus(device.index or 0))[5])
+    return v
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None, prev=None):
@@ -143,11 +159,19 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
-        # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU) -- unless the
-        # consumer's input-gradient epilogue already applied this mask (idempotent either way)
-        g = C.relu_bias_bwd(dy, y) if ctx.relu and not _pregated(dy, y) else dy
         fac = factor_target(w_param) if needs(ctx, 1) else None
         epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
+        # the bias gradient comes from the mask pass instead of the weight-gradient GEMM when
+        # that GEMM would otherwise be denied split-K (its in-kernel row sum needs one split)
+        sep_db = db is not None and needs(ctx, 1) and fac is None and epi is None and \
+            weight.shape[0] > 16 and _wgrad_splits(weight.shape[0], x2.shape[1], x2.shape[0],
+                                                   x2.device) > 1
+        # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU) -- unless the
+        # consumer's input-gradient epilogue already applied this mask (idempotent either way)
+        if ctx.relu and not _pregated(dy, y):
+            g = C.relu_bias_bwd(dy, y, db if sep_db else None)
+        else:
+            g = C.relu_bias_bwd(dy, None, db) if sep_db else dy
         if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16:
             # classifier head (out <= 16): input gradient (gated, + its planes for the next skinny
             # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd). At
@@ -227,7 +251,7 @@ class _LinearFn(torch.autograd.Function):
                     if be is not None:
                         hand_off(b_param, db)
             else:
-                C.gemm_f32(g, x2, dw, False, False, rowsum=db)
+                C.gemm_f32(g, x2, dw, False, False, rowsum=None if sep_db else db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
         return dx, dw, db, None, None, None, None

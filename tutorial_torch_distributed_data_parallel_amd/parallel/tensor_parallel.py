@@ -128,10 +128,44 @@ class _ScatterRowsSum(torch.autograd.Function):
         _, world = _ranks()
         out = torch.empty((world * dy.shape[0],) + tuple(dy.shape[1:]), device=dy.device,
                           dtype=dy.dtype)
-        _all_gather_rows(out, dy)
         if ctx.scale != 1.0:
-            out.mul_(ctx.scale)
+            dy = dy * ctx.scale  # on this rank's rows: 1/W of the gathered tensor's bytes
+        _all_gather_rows(out, dy.contiguous())
         return out, None
+
+
+class _BiasReLU(torch.autograd.Function):
+    """``relu?(y + b)`` for the reduce-scattered fc2 output; backward is ONE native pass (the
+    ReLU mask and the bias gradient, written into b's arena slot: csrc relu_bias_bwd)."""
+
+    @staticmethod
+    def forward(ctx, y, b, relu: bool):
+        out = y + b
+        if relu:
+            out.clamp_min_(0.0)
+        ctx.relu = relu
+        ctx.b = b
+        ctx.save_for_backward(out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .._native import native
+        from ..ops._grad import grad_dest
+
+        (out,) = ctx.saved_tensors
+        db = grad_dest(ctx.b) if ctx.needs_input_grad[1] else None
+        if dy.is_cuda:
+            dy = dy.contiguous()
+            if ctx.relu or db is not None:
+                g = native().relu_bias_bwd(dy, out if ctx.relu else None, db)
+            else:
+                g = dy
+        else:
+            g = dy * (out > 0) if ctx.relu else dy
+            if db is not None:
+                db.copy_(g.sum(0))
+        return g, db, None
 
 
 def _linears(model):
@@ -234,11 +268,11 @@ class TensorParallelMLP(nn.Module):
         p = self.fc2(h)
         y = _ScatterRowsSum.apply(p, 1.0 / self.world) if self.world > 1 else p
         if self.b2 is not None:
-            y = y + self.b2
-        if self.bn2 is not None:
-            y = self.bn2(y)
+            y = _BiasReLU.apply(y, self.b2, self.relu2)
         elif self.relu2:
             y = torch.relu(y)
+        if self.bn2 is not None:
+            y = self.bn2(y)
         return self.fc3(y)
 
     def sync_grads(self) -> None:
