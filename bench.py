@@ -448,8 +448,12 @@ LADDER = (
 # The tensor-sharded step (parallel/tensor_parallel.py): tried before the ladder at N > 1 for the
 # toy MLP; with --parallel auto both it and the ladder's first working rung are timed, the faster
 # one is measured.
-TENSOR_RUNG = {"name": "tensor-sharded", "factor": None, "fused": False, "graph": True,
-               "tensor": True}
+TENSOR_RUNGS = (
+    {"name": "tensor-sharded", "factor": None, "fused": False, "graph": True, "tensor": 1},
+    # fc2's reduce-scatter / all-gather in column chunks behind the chunk GEMMs
+    {"name": "tensor-overlap", "factor": None, "fused": False, "graph": True,
+     "tensor": int(os.environ.get("TDP_TP_CHUNKS", "4"))},
+)
 
 
 def _agree(ok: bool) -> bool:
@@ -513,7 +517,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         # rank's samples. TDP_TP_GLOBAL=0: each rank gathers its own batch, the wrapper
         # all-gathers the inputs.
         shared = os.environ.get("TDP_TP_GLOBAL", "1") == "1"
-        tp = TensorParallelMLP(model, global_batch=shared)
+        tp = TensorParallelMLP(model, global_batch=shared, overlap_chunks=int(cfg["tensor"]))
         ddp = None
         opt = make_opt(tp.parameters())
         if shared:
@@ -902,21 +906,28 @@ def main():
 
         tensor_job, selection = None, None
         if world > 1 and a.parallel != "ddp" and a.model == "toy_mlp" and a.api == "ddp":
-            ok, err = True, None
-            try:
-                tj = build_tdp(a, ctx, TENSOR_RUNG, 0, fallbacks, fault)
-                clock_warmup()
-                tj.step.many(a.warmup)
-                sync()
-            except Exception as e:  # noqa: BLE001 - agreed below; the ladder follows
-                ok, err = False, e
-            if _agree(ok):
-                tensor_job = tj
-            else:
-                fallbacks.append(f"tensor-sharded failed ({repr(err)[:200] if err else 'on another rank'}); DDP ladder")
-                print(f"[bench] tensor-sharded step failed on some rank: {err!r}",
-                      file=sys.stderr, flush=True)
-                tj = None
+            # every tensor-sharded variant that builds is timed; the fastest is kept
+            selection = {}
+            for tcfg in TENSOR_RUNGS:
+                ok, err, tj = True, None, None
+                try:
+                    tj = build_tdp(a, ctx, tcfg, 0, fallbacks, fault)
+                    clock_warmup()
+                    tj.step.many(a.warmup)
+                    sync()
+                except Exception as e:  # noqa: BLE001 - agreed below; the ladder follows
+                    ok, err = False, e
+                if not _agree(ok):
+                    fallbacks.append(f"{tcfg['name']} failed ({repr(err)[:200] if err else 'on another rank'})")
+                    print(f"[bench] {tcfg['name']} failed on some rank: {err!r}",
+                          file=sys.stderr, flush=True)
+                    tj = None
+                else:
+                    selection[f"{tcfg['name']}_ms"] = round(timed_ms(tj, a.select_steps), 4)
+                    if tensor_job is None or selection[f"{tcfg['name']}_ms"] < \
+                            selection[f"{tensor_job.rung}_ms"]:
+                        tensor_job = tj
+                    tj = None
                 gc.collect()
                 if use_gpu:
                     torch.cuda.synchronize()
@@ -925,8 +936,9 @@ def main():
         if tensor_job is not None and a.parallel == "tensor":
             rungs = ()
             job = tensor_job
-        elif tensor_job is not None:
-            selection = {"tensor-sharded_ms": round(timed_ms(tensor_job, a.select_steps), 4)}
+            selection["chosen"] = job.rung
+        elif tensor_job is None:
+            selection = None
         for attempt, cfg in enumerate(rungs):
             ok, err = True, None
             try:
@@ -959,7 +971,7 @@ def main():
             job = tensor_job if job is None else job
         if selection is not None and job is not tensor_job:
             selection[f"{job.rung}_ms"] = round(timed_ms(job, a.select_steps), 4)
-            if selection["tensor-sharded_ms"] < selection[f"{job.rung}_ms"]:
+            if selection[f"{tensor_job.rung}_ms"] < selection[f"{job.rung}_ms"]:
                 job = tensor_job
             selection["chosen"] = job.rung
             # the loser's graphs and buffers go before the timed run

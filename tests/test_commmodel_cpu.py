@@ -100,3 +100,18 @@ def test_cnn_bucket_model_resnet50():
     assert exp[4] <= exp[25] <= exp[64] <= exp[1024] and exp[1024] > 1000.0, exp
     r8 = cm.simulate_buckets(fwd, grads, 8, hw)  # the default plan: 1 MiB first, 25 MiB
     assert r8["exposed_us"] < 0.01 * r8["compute_us"], r8
+
+
+def test_tensor_sharded_model_beats_factored_at_w8():
+    """The tensor-sharded step (activations over xGMI) against the best factored plan at W = 8
+    under the same assumed hardware: shorter predicted step, >= 70 % of dp1, and the chunked
+    overlap hides part of its two big collectives."""
+    hw = cm.Hardware()
+    t1 = cm.simulate_tensor(8, hw=hw)
+    t4 = cm.simulate_tensor(8, hw=hw, chunks=4)
+    fac = cm.best_plan(cm.toy_mlp_layers(), 8, 128, hw)
+    assert t1["step_us"] < fac["step_us"]
+    assert t1["scaling_eff"] >= 0.70 and t4["exposed_us"] < t1["exposed_us"]
+    # gathering the node's batch locally saves the 33 MB input all-gather
+    assert cm.simulate_tensor(8, hw=hw, global_batch=False)["step_us"] > t1["step_us"] + 90
+    assert cm.simulate_tensor(1)["exposed_us"] == 0.0

@@ -29,3 +29,8 @@ def test_tensor_parallel_global_batch_input(tmp_path):
 
 def test_tensor_parallel_refuses_per_rank_bn(tmp_path):
     run(TW.refuses_plain_bn, tmp_path, n=2)
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 4), (4, 2)])
+def test_tensor_parallel_overlapped_chunks_match_global_batch(tmp_path, world, chunks):
+    run(TW.step_parity, tmp_path, n=world, chunks=chunks)

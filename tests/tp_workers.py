@@ -27,14 +27,14 @@ def _ref_model(bn):
     return ToyMLP(batchnorm=bn, **DIMS)
 
 
-def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4):
+def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4, chunks=1):
     tdp.init_process_group("gloo")
     W = rt.get_world_size()
     ref = _ref_model(bn)
     model = copy.deepcopy(ref)
     if bn:
         model = tdp.nn.convert_sync_batchnorm(model)
-    tp = TensorParallelMLP(model, global_batch=global_batch)
+    tp = TensorParallelMLP(model, global_batch=global_batch, overlap_chunks=chunks)
     hp = dict(lr=0.05, momentum=0.9, weight_decay=1e-3)
     opt = tdp.optim.SGD(tp.parameters(), **hp)
     ropt = torch.optim.SGD(ref.parameters(), **hp)
@@ -98,7 +98,7 @@ def _gbatch(r, step):
         torch.randint(0, 10, (GB,), generator=g).cuda()
 
 
-def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5):
+def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1):
     """GPU, W ranks (peer vehicle on one GPU, or RCCL): the tensor-sharded step captured into a
     hipGraph and replayed == the same step run eagerly, BITWISE; both match the one-process
     global-batch step of the full model (torch fp32 on the GPU) to fp32 accuracy."""
@@ -112,7 +112,7 @@ def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5):
         m = ToyMLP(batchnorm=bn, device="cuda", **GDIMS)
         if bn:
             m = tdp.nn.convert_sync_batchnorm(m)
-        t = TensorParallelMLP(m)
+        t = TensorParallelMLP(m, overlap_chunks=chunks)
         return t, tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
 
     t1, o1 = build()

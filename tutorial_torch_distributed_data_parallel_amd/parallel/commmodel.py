@@ -191,6 +191,49 @@ def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
             "step_us": round(step, 1), "jobs": jobs}
 
 
+# Per-rank compute of the tensor-sharded step (parallel/tensor_parallel.py), measured on one GPU
+# with the shard shapes of W ranks and the collectives replaced by local copies
+# (scripts/tp_rank_proxy.py, profiles/r9/tp_rank_proxy_r9o.jsonl; dp1 of that run: 347.6 us)
+TP_RANK_US = {1: 467.9, 2: 377.4, 4: 369.5, 8: 363.0}
+TP_DP1_US = 347.6
+
+
+def simulate_tensor(W: int, B: int = 128, dims=(9216, 4096, 4096), classes: int = 10,
+                    hw: Hardware | None = None, chunks: int = 1, global_batch: bool = True,
+                    rank_us: float | None = None, fc2_gemm_us: float = 42.0) -> dict:
+    """Predicted step of the tensor-sharded toy MLP at W ranks: the measured per-rank compute
+    plus the collectives on its critical path -- the reduce-scatter of fc2's partial output
+    [W*B, h2] (forward) and the all-gather of its gradient (backward), the averaged all-reduce
+    of the replicated head, and (without ``global_batch``) the input all-gather. With ``chunks``
+    > 1 each of the two big collectives runs in column chunks behind fc2's chunk GEMMs
+    (``fc2_gemm_us``: that layer's forward GEMM time, the backward has two such GEMMs)."""
+    hw = hw or Hardware()
+    d0, h1, h2 = dims
+    if W <= 1:
+        c = rank_us if rank_us is not None else TP_RANK_US.get(1, TP_DP1_US)
+        return {"W": 1, "compute_us": c, "exposed_us": 0.0, "step_us": c, "wire_MB": 0.0}
+    comp = rank_us if rank_us is not None else TP_RANK_US.get(W, TP_RANK_US[8])
+    big = 4.0 * W * B * h2
+    rs = _coll_us(hw, "reduce_scatter", W, big)
+    ag = _coll_us(hw, "all_gather", W, big)
+    head = _coll_us(hw, "all_reduce", W, 4.0 * (h2 * classes + classes + h2))
+    xg = 0.0 if global_batch else _coll_us(hw, "all_gather", W, 4.0 * W * B * d0)
+
+    def hidden(coll, gemm):
+        """Exposed part of a collective split into ``chunks`` behind as many GEMM chunks."""
+        if chunks <= 1:
+            return coll
+        g, c = gemm / chunks, (coll - hw.latency_us) / chunks + hw.latency_us
+        return g + (chunks - 1) * max(g, c) + c - gemm
+
+    exposed = hidden(rs, fc2_gemm_us) + hidden(ag, 2 * fc2_gemm_us) + head + xg
+    wire = (W - 1) / W * (2 * big + (0 if global_batch else 4.0 * W * B * d0)) + \
+        2 * (W - 1) / W * 4.0 * (h2 * classes + classes + h2)
+    return {"W": W, "compute_us": round(comp, 1), "exposed_us": round(exposed, 1),
+            "step_us": round(comp + exposed, 1), "wire_MB": round(wire / 1e6, 1),
+            "scaling_eff": round(TP_DP1_US / (comp + exposed), 3)}
+
+
 def best_plan(layers: list[Layer], W: int, B: int, hw: Hardware,
               candidates: dict | None = None) -> dict:
     """The cheapest mode per weight (exhaustive over the candidates; the toy MLP has two)."""

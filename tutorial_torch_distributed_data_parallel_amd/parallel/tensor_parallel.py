@@ -134,6 +134,95 @@ class _ScatterRowsSum(torch.autograd.Function):
         return out, None
 
 
+class _RowParallelOverlap(torch.autograd.Function):
+    """``reduce_scatter_rows(h1 . w2^T)`` in ``nc`` column chunks of fc2's output: chunk c's
+    GEMM runs on the compute stream while chunk c-1's reduce-scatter runs on the communication
+    stream. Backward mirrors it: chunk c's all-gather of dY (scaled by ``scale``) overlaps chunk
+    c-1's two GEMMs (dW2 rows of chunk c, dH1 accumulated over chunks). On CPU the same chunk
+    loop runs without streams (the gloo tests of the indexing)."""
+
+    @staticmethod
+    def forward(ctx, h1, w2, scale: float, nc: int, side):
+        from .._native import native
+
+        _, world = _ranks()
+        M, s = h1.shape
+        h2 = w2.shape[0]
+        hc = h2 // nc
+        B = M // world
+        parts = torch.empty((nc, B, hc), device=h1.device, dtype=h1.dtype)
+        ctx.save_for_backward(h1, w2)
+        ctx.scale, ctx.nc, ctx.side = scale, nc, side
+        if not h1.is_cuda:
+            for c in range(nc):
+                _reduce_scatter_rows(parts[c], h1 @ w2[c * hc:(c + 1) * hc].t())
+        else:
+            C = native()
+            comp = torch.cuda.current_stream()
+            keep = []
+            for c in range(nc):
+                pc = torch.empty((M, hc), device=h1.device, dtype=h1.dtype)
+                C.gemm_f32(h1, w2[c * hc:(c + 1) * hc], pc, True, True)
+                ev = torch.cuda.Event()
+                ev.record(comp)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    _reduce_scatter_rows(parts[c], pc)
+                keep.append(pc)  # alive until the join below orders their reuse after it
+            done = torch.cuda.Event()
+            done.record(side)
+            comp.wait_event(done)
+            del keep
+        return parts.transpose(0, 1).reshape(B, h2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .._native import native
+        from ..ops._grad import grad_dest
+
+        h1, w2 = ctx.saved_tensors
+        nc, scale, side = ctx.nc, ctx.scale, ctx.side
+        _, world = _ranks()
+        M, s = h1.shape
+        h2 = w2.shape[0]
+        hc = h2 // nc
+        B = dy.shape[0]
+        # this rank's rows of dY, scaled, chunk-major: [nc][B][hc]
+        dyc = (dy * scale).reshape(B, nc, hc).transpose(0, 1).contiguous()
+        dp = torch.empty((nc, M, hc), device=dy.device, dtype=dy.dtype)
+        dh1 = torch.empty_like(h1) if ctx.needs_input_grad[0] else None
+        dw2 = grad_dest(w2) if ctx.needs_input_grad[1] else None
+        if not dy.is_cuda:
+            for c in range(nc):
+                _all_gather_rows(dp[c], dyc[c])
+                if dw2 is not None:
+                    dw2[c * hc:(c + 1) * hc].copy_(dp[c].t() @ h1)
+                if dh1 is not None:
+                    t = dp[c] @ w2[c * hc:(c + 1) * hc]
+                    dh1.copy_(t) if c == 0 else dh1.add_(t)
+            return dh1, dw2, None, None, None
+        C = native()
+        comp = torch.cuda.current_stream()
+        ready = torch.cuda.Event()
+        ready.record(comp)
+        side.wait_event(ready)
+        evs = []
+        with torch.cuda.stream(side):
+            for c in range(nc):
+                _all_gather_rows(dp[c], dyc[c])
+                e = torch.cuda.Event()
+                e.record(side)
+                evs.append(e)
+        for c in range(nc):
+            comp.wait_event(evs[c])
+            if dw2 is not None:  # dW2[rows of chunk c] = dP_c^T . H1
+                C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
+            if dh1 is not None:  # dH1 (+)= dP_c . W2[rows of chunk c]
+                C.gemm_f32(dp[c], w2[c * hc:(c + 1) * hc], dh1, True, False,
+                           beta=0.0 if c == 0 else 1.0)
+        return dh1, dw2, None, None, None
+
+
 class _BiasReLU(torch.autograd.Function):
     """``relu?(y + b)`` for the reduce-scattered fc2 output; backward is ONE native pass (the
     ReLU mask and the bias gradient, written into b's arena slot: csrc relu_bias_bwd)."""
@@ -187,8 +276,9 @@ class TensorParallelMLP(nn.Module):
     ``global_batch=True``: ``forward`` receives the whole node's batch [W*B, in] in rank order
     (every rank gathered it from its replica of the dataset) and skips the input all-gather."""
 
-    def __init__(self, model: nn.Module, global_batch: bool = False):
+    def __init__(self, model: nn.Module, global_batch: bool = False, overlap_chunks: int = 1):
         super().__init__()
+        self.overlap_chunks = int(overlap_chunks)
         rank, world = _ranks()
         self.rank, self.world = rank, world
         self.global_batch = bool(global_batch)
@@ -218,6 +308,11 @@ class TensorParallelMLP(nn.Module):
         self._bn_names = (names[names.index(n1) + 1] if bn1 is not None else None,
                           names[names.index(n2) + 1] if bn2 is not None else None)
         self._dims = (fc1.in_features, h1, fc2.out_features, fc3.out_features)
+        self._side = None  # communication stream of the overlapped fc2 (created on first use)
+        if fc2.out_features % max(1, self.overlap_chunks) or (fc2.weight.is_cuda and (
+                fc2.out_features // max(1, self.overlap_chunks)) % 4):
+            raise ValueError(f"TensorParallelMLP: fc2 width {fc2.out_features} does not split "
+                             f"into {self.overlap_chunks} chunks of a multiple of 4")
         s = h1 // world
         lo, hi = rank * s, (rank + 1) * s
         dev = fc1.weight.device
@@ -265,8 +360,14 @@ class TensorParallelMLP(nn.Module):
         h = self.fc1(X)
         if self.bn1 is not None:
             h = self.bn1(h)
-        p = self.fc2(h)
-        y = _ScatterRowsSum.apply(p, 1.0 / self.world) if self.world > 1 else p
+        nc = self.overlap_chunks
+        if self.world > 1 and nc > 1:
+            if self._side is None and h.is_cuda:
+                self._side = torch.cuda.Stream(device=h.device, priority=-1)
+            y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 / self.world, nc, self._side)
+        else:
+            p = self.fc2(h)
+            y = _ScatterRowsSum.apply(p, 1.0 / self.world) if self.world > 1 else p
         if self.b2 is not None:
             y = _BiasReLU.apply(y, self.b2, self.relu2)
         elif self.relu2:
