@@ -341,6 +341,26 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
         out["rehearsal_over_dp1"] = round(out["rehearsal_ms"] / step_ms, 4)
         out["rehearsal_schedule_over_dp1"] = round(out["rehearsal_schedule_ms"] / step_ms, 4)
         del d2
+        if a.model == "toy_mlp" and not a.syncbn and a.api == "ddp":
+            # the tensor-sharded step's per-rank compute at W = 2 / 8 on this GPU (shard
+            # shapes, collectives as local copies) and the step it predicts with the assumed
+            # xGMI figures (docs/COMM_MODEL.md "Tensor-sharded")
+            from tutorial_torch_distributed_data_parallel_amd.parallel import commmodel as cm
+            from tutorial_torch_distributed_data_parallel_amd.parallel.tensor_parallel import \
+                rank_compute_ms
+
+            dims = tuple(int(v) for v in a.mlp_dims.split(",")) if a.mlp_dims else \
+                (9216, 4096, 4096)
+            rk, pred = {}, {}
+            for W in (2, 8):
+                ms = rank_compute_ms(W, dims=dims, B=a.batch, steps=n, optim=a.optim)
+                rk[str(W)] = round(ms, 4)
+                pred[str(W)] = round(cm.simulate_tensor(W, B=a.batch, dims=dims,
+                                                        rank_us=ms * 1000.0, chunks=4)
+                                     ["step_us"] / 1000.0, 4)
+            out["tensor_rank_compute_ms"] = rk
+            out["tensor_predicted_step_ms"] = pred
+            out["tensor_predicted_eff"] = {k: round(step_ms / v, 3) for k, v in pred.items()}
     return out
 
 

@@ -41,7 +41,9 @@ SHAPES = [(128, 4096, 9216, True),   # toy-MLP fc1 forward
           (128, 4096, 4096, False),  # fc2 input gradient (W stored [out][in])
           (130, 200, 64, True),      # ragged M / N edges
           (32, 128, 256, False),
-          (300, 256, 512, True)]     # several row tiles
+          (300, 256, 512, True),     # several row tiles
+          (1024, 512, 9216, True),   # tensor-sharded fc1 at W = 8 (the node's batch)
+          (1024, 4096, 512, True)]   # its fc2 partial GEMM
 
 
 @pytest.mark.parametrize("M,N,K,bk", SHAPES)

@@ -57,31 +57,3 @@ def test_bench_parallel_auto_records_selection():
     sel = c["selection"]
     assert sel is not None and sel["chosen"] == c["rung"], c
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
-
-
-@pytest.mark.parametrize("relu", [True, False])
-def test_linear_bias_grad_from_mask_pass_when_wgrad_splits(relu):
-    """ops.linear: a weight-gradient GEMM that would be denied split-K by its fused bias row sum
-    (few tiles, deep K: the tensor-sharded fc1) takes the bias gradient from the mask pass
-    instead; weight / bias / input gradients match fp64."""
-    import torch
-
-    from tutorial_torch_distributed_data_parallel_amd import ops
-    from tutorial_torch_distributed_data_parallel_amd.ops import linear as L
-
-    torch.manual_seed(3)
-    x = torch.randn(1024, 2048, device="cuda", requires_grad=True)
-    w = (torch.randn(256, 2048, device="cuda") / 45).requires_grad_()
-    b = (torch.randn(256, device="cuda") / 10).requires_grad_()
-    assert L._wgrad_splits(256, 2048, 1024, x.device) > 1
-    y = ops.linear(x, w, b, relu=relu)
-    go = torch.randn_like(y)
-    y.backward(go)
-    xd, wd, bd = (t.detach().double().requires_grad_() for t in (x, w, b))
-    yd = xd @ wd.t() + bd
-    if relu:
-        yd = torch.relu(yd)
-    yd.backward(go.double())
-    for got, want, name in ((x.grad, xd.grad, "dx"), (w.grad, wd.grad, "dw"),
-                            (b.grad, bd.grad, "db")):
-        torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=1e-4, msg=name)

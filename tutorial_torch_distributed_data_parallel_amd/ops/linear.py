@@ -27,14 +27,20 @@ from ._grad import (bias_epilogue, epilogue_target, factor_target, grad_dest, ha
 _PLANES = True
 
 
+# Rows up to which the activation operand goes pre-split: a batch per rank (M = 128), or the
+# node's batch of the tensor-sharded step (M = W * 128 <= 1024: profiles/r9/tp_planes_r9.md)
+PLANES_MAX_ROWS = 1024
+
+
 def planes_fit(M: int, N: int, K: int) -> bool:
     """The planes GEMM applies: few rows (a batch), K a multiple of its 32-deep tile, wide N."""
-    return _PLANES and M <= 256 and K % 32 == 0 and K >= 256 and N % 4 == 0 and N >= 512
+    return _PLANES and M <= PLANES_MAX_ROWS and K % 32 == 0 and K >= 256 and N % 4 == 0 and \
+        N >= 512
 
 
 def planes_input_fit(M: int, K: int) -> bool:
     """A [M, K] activation may feed a planes GEMM (its producer should emit the planes)."""
-    return _PLANES and M <= 256 and K % 32 == 0 and K >= 256
+    return _PLANES and M <= PLANES_MAX_ROWS and K % 32 == 0 and K >= 256
 
 
 def _al16(*ts) -> bool:
@@ -64,6 +70,15 @@ def set_planes(on: bool) -> bool:
 def attach_planes(t: torch.Tensor, planes: torch.Tensor) -> None:
     """Record that ``planes`` are the bf16 split of ``t``'s current contents."""
     t._tdp_planes = (planes, t._version, t.data_ptr(), tuple(t.shape))
+
+
+def has_planes(t: torch.Tensor) -> bool:
+    """``t`` carries its producer's split planes (planes_of would not split it)."""
+    for src in (t, t._base):
+        rec = getattr(src, "_tdp_planes", None) if src is not None else None
+        if rec is not None and rec[1] == src._version and rec[2] == t.data_ptr():
+            return True
+    return False
 
 
 def planes_of(t: torch.Tensor) -> torch.Tensor:
@@ -102,22 +117,6 @@ def _prefetch_prev_g(ctx, dx: torch.Tensor):
         return None
     prev = factor_target(ctx.prev_w)
     return prev if prev is not None and prev.factor_prefetch_g(ctx.prev_w, dx) else None
-
-
-_WGRAD_SPLITS: dict = {}
-
-
-def _wgrad_splits(out: int, inp: int, k: int, device) -> int:
-    """Split-K count the weight-gradient GEMM dW[out, in] (depth k) gets WITHOUT a fused bias
-    row sum (cached per shape): > 1 means the row sum would cost it its split-K (the
-    tensor-sharded step's fc1 at W = 8: 288 tiles for 512 slots)."""
-    key = (out, inp, k, device.index)
-    v = _WGRAD_SPLITS.get(key)
-    if v is None:
-        C = native()
-        v = _WGRAD_SPLITS[key] = int(C.gemm_f32_plan(out, inp, k, False,
-                                                     C.num_cus(device.index or 0))[5])
-    return v
 
 
 class _LinearFn(torch.autograd.Function):
@@ -159,19 +158,11 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         want_db = b_param is not None and needs(ctx, 2)
         db = grad_dest(b_param) if want_db else None
-        fac = factor_target(w_param) if needs(ctx, 1) else None
-        epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
-        # the bias gradient comes from the mask pass instead of the weight-gradient GEMM when
-        # that GEMM would otherwise be denied split-K (its in-kernel row sum needs one split)
-        sep_db = db is not None and needs(ctx, 1) and fac is None and epi is None and \
-            weight.shape[0] > 16 and _wgrad_splits(weight.shape[0], x2.shape[1], x2.shape[0],
-                                                   x2.device) > 1
         # ReLU backward: g = dy * (y > 0), one pass (g is dy itself without ReLU) -- unless the
         # consumer's input-gradient epilogue already applied this mask (idempotent either way)
-        if ctx.relu and not _pregated(dy, y):
-            g = C.relu_bias_bwd(dy, y, db if sep_db else None)
-        else:
-            g = C.relu_bias_bwd(dy, None, db) if sep_db else dy
+        g = C.relu_bias_bwd(dy, y) if ctx.relu and not _pregated(dy, y) else dy
+        fac = factor_target(w_param) if needs(ctx, 1) else None
+        epi = epilogue_target(w_param) if needs(ctx, 1) and fac is None else None
         if needs(ctx, 0) and needs(ctx, 1) and fac is None and weight.shape[0] <= 16:
             # classifier head (out <= 16): input gradient (gated, + its planes for the next skinny
             # GEMM), weight and bias gradient in ONE launch (csrc/gemm_skinny.hip head_bwd). At
@@ -215,8 +206,11 @@ class _LinearFn(torch.autograd.Function):
             # also applies that layer's mask (x > 0): its backward then skips its mask pass
             gate = x2 if ctx.gate_in else None
             M, K = g.shape
+            # (a batch-sized g arrives with its planes from the head backward; a larger one
+            # without them would pay a split pass the planes GEMM does not win back:
+            # profiles/r9/tp_planes_r9.md)
             if planes_fit(M, x2.shape[1], K) and weight.stride(1) == 1 and \
-                    _al16(weight, gate, dx):
+                    _al16(weight, gate, dx) and (M <= 256 or has_planes(g)):
                 C.gemm_planes(planes_of(g), weight, dx, False, gate=gate)
             else:
                 C.gemm_f32(g, weight, dx, True, False, gate=gate)
@@ -251,7 +245,7 @@ class _LinearFn(torch.autograd.Function):
                     if be is not None:
                         hand_off(b_param, db)
             else:
-                C.gemm_f32(g, x2, dw, False, False, rowsum=None if sep_db else db)
+                C.gemm_f32(g, x2, dw, False, False, rowsum=db)
         elif want_db:
             C.relu_bias_bwd(g, None, db)
         return dx, dw, db, None, None, None, None

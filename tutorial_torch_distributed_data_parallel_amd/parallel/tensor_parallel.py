@@ -157,12 +157,18 @@ class _RowParallelOverlap(torch.autograd.Function):
             for c in range(nc):
                 _reduce_scatter_rows(parts[c], h1 @ w2[c * hc:(c + 1) * hc].t())
         else:
+            from ..ops.linear import planes_fit, planes_of
+
             C = native()
             comp = torch.cuda.current_stream()
             keep = []
+            hp = planes_of(h1) if planes_fit(M, hc, s) else None
             for c in range(nc):
                 pc = torch.empty((M, hc), device=h1.device, dtype=h1.dtype)
-                C.gemm_f32(h1, w2[c * hc:(c + 1) * hc], pc, True, True)
+                if hp is not None:  # H1's pre-split planes (fc1's epilogue emitted them)
+                    C.gemm_planes(hp, w2[c * hc:(c + 1) * hc], pc, True)
+                else:
+                    C.gemm_f32(h1, w2[c * hc:(c + 1) * hc], pc, True, True)
                 ev = torch.cuda.Event()
                 ev.record(comp)
                 side.wait_event(ev)
@@ -454,3 +460,52 @@ class TensorParallelMLP(nn.Module):
                                           if k.startswith(b2n + ".")})
             self.fc3.load_state_dict({k[len(n3) + 1:]: v for k, v in sd.items()
                                       if k.startswith(n3 + ".")})
+
+
+def rank_compute_ms(W: int, dims=(9216, 4096, 4096), classes: int = 10, B: int = 128,
+                    steps: int = 100, optim: str = "sgd", device=None) -> float:
+    """Measured per-rank compute of the W-rank tensor-sharded step on THIS one GPU: rank 0's
+    shard shapes, every collective replaced by its local copy (set_fake_world), the node's batch
+    gathered from a device dataset each step, SGD momentum (or Adam), captured and replayed as
+    bench.py runs it. The W-rank step is this plus its exposed collectives
+    (parallel/commmodel.py simulate_tensor). World size 1 only (no process group peers)."""
+    import time
+
+    from .. import optim as toptim
+    from .. import ops
+    from ..data.synthetic import gather_batch
+    from ..models import ToyMLP
+    from ..train.graph import CapturedStep
+
+    if runtime.get_world_size() != 1:
+        raise RuntimeError("rank_compute_ms: a one-process measurement")
+    dev = device or runtime.device()
+    set_fake_world(W)
+    try:
+        torch.manual_seed(0)
+        net = TensorParallelMLP(ToyMLP(in_features=dims[0], hidden=dims[1:],
+                                       num_classes=classes, device=dev), global_batch=True)
+        opt = toptim.SGD(net.parameters(), lr=0.01, momentum=0.9) if optim == "sgd" else \
+            toptim.Adam(net.parameters(), lr=1e-3)
+        n = max(4 * W * B, 1024)
+        data = torch.randn(n, dims[0], device=dev)
+        labels = torch.randint(0, classes, (n,), device=dev)
+        idx = torch.randperm(n, device=dev)[:W * B]
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            x, y = gather_batch(data, labels, idx)
+            ops.backward(ops.cross_entropy(net(x), y[:B]))
+            net.sync_grads()
+            opt.step()
+        g = CapturedStep(step, warmup=3)
+        for _ in range(10):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1000.0 / steps
+    finally:
+        set_fake_world(0)
