@@ -364,6 +364,47 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
     return out
 
 
+def tensor_diagnostics(a, job, step_ms, world, barrier):
+    """N > 1, tensor-sharded step measured: the same step with every collective replaced by its
+    local copy (re-captured; rank 0's shard shapes on every rank) = this rank's compute; the
+    exposed communication is the measured step minus it. Plus the RCCL bus-bandwidth sweep and
+    the model's prediction from it (docs/COMM_MODEL.md "Tensor-sharded")."""
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commbench
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commmodel as cm
+    from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
+    from tutorial_torch_distributed_data_parallel_amd.parallel import tensor_parallel as TPm
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import try_capture
+
+    n = max(10, min(a.steps, 50))
+    out = {"mode": "graph" if job.graph else "eager", "execution": job.rung}
+    TPm.set_fake_world(world)
+    try:
+        st = getattr(job.step, "raw", job.step)
+        if job.graph:
+            st = try_capture(st, warmup=2, log=lambda m: None)
+        barrier()
+        compute_ms = _time_steps(st, n)
+    finally:
+        TPm.set_fake_world(0)
+    t = torch.tensor([compute_ms], dtype=torch.float64, device=rt.device())
+    rt.all_reduce(t, "max")
+    compute_ms = float(t.item())
+    out.update(compute_ms=round(compute_ms, 4), exposed_comm_ms=round(step_ms - compute_ms, 4))
+    sweep = commbench.collective_busbw([m * 2 ** 20 for m in DIAG_SWEEP_MB], iters=5, warmup=2)
+    out["busbw_GBps"] = {f"{r['op']}@{r['bytes'] >> 20}MiB": r["busbw_GBps"] for r in sweep}
+    big = {}
+    for r in sweep:
+        if r["bytes"] >= big.get(r["op"], (0, 0))[0]:
+            big[r["op"]] = (r["bytes"], r["busbw_GBps"])
+    dims = tuple(int(v) for v in a.mlp_dims.split(",")) if a.mlp_dims else (9216, 4096, 4096)
+    hw = cm.Hardware(busbw_GBps={op: bw for op, (_, bw) in big.items()})
+    pred = cm.simulate_tensor(world, B=a.batch, dims=dims, hw=hw, rank_us=compute_ms * 1e3,
+                              chunks=int(job.tp.overlap_chunks))
+    out.update(predicted_step_ms=round(pred["step_us"] / 1e3, 4),
+               predicted_exposed_ms=round(pred["exposed_us"] / 1e3, 4))
+    return out
+
+
 def _launcher_env() -> bool:
     """True when a launcher (torchrun, parallel/launcher.py, this script's own parent) already
     made this process one rank of a job."""
@@ -1122,6 +1163,23 @@ def main():
         return rec
 
     diag = None
+    tp_job = job if (a.impl == "tdp" and getattr(job, "tp", None) is not None) else None
+    if tp_job is not None and use_gpu and not a.no_diag:
+        limit = float(os.environ.get("TDP_DIAG_TIMEOUT_S", "120"))
+
+        def expire_tp():
+            if rank == 0:
+                print(json.dumps(record({"error": f"diagnostics exceeded {limit:g} s"})),
+                      file=out, flush=True)
+            os._exit(0)
+        timer = threading.Timer(limit, expire_tp)
+        timer.daemon = True
+        timer.start()
+        try:
+            diag = tensor_diagnostics(a, tp_job, ms, world, barrier)
+        except Exception as e:  # diagnostics never cost the measurement
+            diag = {"error": repr(e)[:300]}
+        timer.cancel()
     if a.impl == "tdp" and ddp is not None and use_gpu and not a.no_diag:
         # The measurement is final here. Diagnostics run more collectives, and a peer that
         # stalls in them must not cost the result: past the deadline every rank exits 0, and

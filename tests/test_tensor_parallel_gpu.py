@@ -35,12 +35,12 @@ def test_tensor_parallel_syncbn_captured_with_real_peers(tmp_path):
     run(TW.captured_parity, tmp_path, n=2, bn=True)
 
 
-def _peer_bench(*args):
+def _peer_bench(*args, diag=False):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     env.update(TDP_GPU_PEER="1")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
            "--warmup", "2", "--mlp-dims", "1024,512,512", "--dataset", "1024", "--batch", "32",
-           "--no-diag", "--device-warmup-ms", "0", *args]
+           "--device-warmup-ms", "0", *([] if diag else ["--no-diag"]), *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
@@ -57,3 +57,13 @@ def test_bench_parallel_auto_records_selection():
     sel = c["selection"]
     assert sel is not None and sel["chosen"] == c["rung"], c
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
+
+
+def test_bench_tensor_sharded_diagnostics():
+    """N > 1 diagnostics of the tensor-sharded step: compute with local-copy collectives, the
+    exposed remainder, the busbw sweep and the model's prediction from it."""
+    rec = _peer_bench("--parallel", "tensor", diag=True)
+    d = rec["diagnostics"]
+    assert "error" not in d, d
+    assert d["execution"] == rec["config"]["rung"] and d["compute_ms"] > 0, d
+    assert d["predicted_step_ms"] > 0 and d["busbw_GBps"], d
