@@ -78,7 +78,7 @@ def test_bench_self_launch_peer_captured():
     env.update(TDP_GPU_PEER="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
            "--warmup", "3", "--mlp-dims", "1024,512,512", "--dataset", "1024", "--batch", "32",
-           "--no-diag", "--device-warmup-ms", "0"]
+           "--no-diag", "--device-warmup-ms", "0", "--parallel", "ddp"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]

@@ -54,7 +54,8 @@ def test_bench_world2_record(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "2", "--mlp-dims", "1024,512,512",
-           "--dataset", "1024", "--batch", "32", "--no-diag", "--device-warmup-ms", "0"]
+           "--dataset", "1024", "--batch", "32", "--no-diag", "--device-warmup-ms", "0",
+           "--parallel", "ddp"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
