@@ -116,9 +116,10 @@ class _ScatterRowsSum(torch.autograd.Function):
     blocks' gradients, times ``scale`` (1/W: sum of per-rank mean losses -> global mean)."""
 
     @staticmethod
-    def forward(ctx, p, scale: float):
+    def forward(ctx, p, scale: float, owner=None):
         _, world = _ranks()
         ctx.scale = scale
+        ctx.owner = owner
         out = torch.empty((p.shape[0] // world,) + tuple(p.shape[1:]), device=p.device,
                           dtype=p.dtype)
         return _reduce_scatter_rows(out, p)
@@ -130,8 +131,28 @@ class _ScatterRowsSum(torch.autograd.Function):
                           dtype=dy.dtype)
         if ctx.scale != 1.0:
             dy = dy * ctx.scale  # on this rank's rows: 1/W of the gathered tensor's bytes
-        _all_gather_rows(out, dy.contiguous())
-        return out, None
+        dy = dy.contiguous()
+        owner = ctx.owner
+        if owner is not None and dy.is_cuda and owner.comm_stream() is not None:
+            # on the communication stream: the all-gather, then the replicated parameters'
+            # all-reduce (their gradients are complete: the head's backward ran before this
+            # node), which then runs behind fc2's / fc1's gradient GEMMs (joined in sync_grads)
+            side = owner.comm_stream()
+            comp = torch.cuda.current_stream()
+            ready = torch.cuda.Event()
+            ready.record(comp)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                _all_gather_rows(out, dy)
+                gathered = torch.cuda.Event()
+                gathered.record(side)
+                owner._reduce_replicated_async()
+            comp.wait_event(gathered)
+            keep = owner._keep
+            keep.append(dy)  # read on the side stream: alive until sync_grads' join
+        else:
+            _all_gather_rows(out, dy)
+        return out, None, None
 
 
 class _RowParallelOverlap(torch.autograd.Function):
@@ -142,7 +163,7 @@ class _RowParallelOverlap(torch.autograd.Function):
     loop runs without streams (the gloo tests of the indexing)."""
 
     @staticmethod
-    def forward(ctx, h1, w2, scale: float, nc: int, side):
+    def forward(ctx, h1, w2, scale: float, nc: int, side, owner=None):
         from .._native import native
 
         _, world = _ranks()
@@ -152,7 +173,7 @@ class _RowParallelOverlap(torch.autograd.Function):
         B = M // world
         parts = torch.empty((nc, B, hc), device=h1.device, dtype=h1.dtype)
         ctx.save_for_backward(h1, w2)
-        ctx.scale, ctx.nc, ctx.side = scale, nc, side
+        ctx.scale, ctx.nc, ctx.side, ctx.owner = scale, nc, side, owner
         if not h1.is_cuda:
             for c in range(nc):
                 _reduce_scatter_rows(parts[c], h1 @ w2[c * hc:(c + 1) * hc].t())
@@ -206,7 +227,7 @@ class _RowParallelOverlap(torch.autograd.Function):
                 if dh1 is not None:
                     t = dp[c] @ w2[c * hc:(c + 1) * hc]
                     dh1.copy_(t) if c == 0 else dh1.add_(t)
-            return dh1, dw2, None, None, None
+            return dh1, dw2, None, None, None, None
         C = native()
         comp = torch.cuda.current_stream()
         ready = torch.cuda.Event()
@@ -219,6 +240,9 @@ class _RowParallelOverlap(torch.autograd.Function):
                 e = torch.cuda.Event()
                 e.record(side)
                 evs.append(e)
+            if ctx.owner is not None:
+                ctx.owner._reduce_replicated_async()
+                ctx.owner._keep.append(dyc)
         for c in range(nc):
             comp.wait_event(evs[c])
             if dw2 is not None:  # dW2[rows of chunk c] = dP_c^T . H1
@@ -226,7 +250,7 @@ class _RowParallelOverlap(torch.autograd.Function):
             if dh1 is not None:  # dH1 (+)= dP_c . W2[rows of chunk c]
                 C.gemm_f32(dp[c], w2[c * hc:(c + 1) * hc], dh1, True, False,
                            beta=0.0 if c == 0 else 1.0)
-        return dh1, dw2, None, None, None
+        return dh1, dw2, None, None, None, None
 
 
 class _BiasReLU(torch.autograd.Function):
@@ -314,7 +338,10 @@ class TensorParallelMLP(nn.Module):
         self._bn_names = (names[names.index(n1) + 1] if bn1 is not None else None,
                           names[names.index(n2) + 1] if bn2 is not None else None)
         self._dims = (fc1.in_features, h1, fc2.out_features, fc3.out_features)
-        self._side = None  # communication stream of the overlapped fc2 (created on first use)
+        self._side = None  # communication stream (comm_stream)
+        self._reduced = None  # event: the replicated all-reduce issued from the backward
+        self._keep = []  # tensors read on the communication stream, alive until the join
+        self._fresh = False
         if fc2.out_features % max(1, self.overlap_chunks) or (fc2.weight.is_cuda and (
                 fc2.out_features // max(1, self.overlap_chunks)) % 4):
             raise ValueError(f"TensorParallelMLP: fc2 width {fc2.out_features} does not split "
@@ -361,6 +388,9 @@ class TensorParallelMLP(nn.Module):
 
     # ---------------------------------------------------------------------------- forward
     def forward(self, x):
+        # every replicated gradient is empty: this backward writes them into their arena slots
+        # (ops/_grad.py grad_dest), so the backward may all-reduce the slots early
+        self._fresh = all(q.grad is None for q in self._replicated)
         x = x.reshape(x.shape[0], -1)
         X = x if (self.world == 1 or self.global_batch) else _GatherRows.apply(x)
         h = self.fc1(X)
@@ -368,12 +398,12 @@ class TensorParallelMLP(nn.Module):
             h = self.bn1(h)
         nc = self.overlap_chunks
         if self.world > 1 and nc > 1:
-            if self._side is None and h.is_cuda:
-                self._side = torch.cuda.Stream(device=h.device, priority=-1)
-            y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 / self.world, nc, self._side)
+            self.comm_stream()
+            y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 / self.world, nc, self._side,
+                                          self)
         else:
             p = self.fc2(h)
-            y = _ScatterRowsSum.apply(p, 1.0 / self.world) if self.world > 1 else p
+            y = _ScatterRowsSum.apply(p, 1.0 / self.world, self) if self.world > 1 else p
         if self.b2 is not None:
             y = _BiasReLU.apply(y, self.b2, self.relu2)
         elif self.relu2:
@@ -382,18 +412,45 @@ class TensorParallelMLP(nn.Module):
             y = self.bn2(y)
         return self.fc3(y)
 
-    def sync_grads(self) -> None:
-        """Every gradient into its arena slot (a gradient autograd produced elsewhere -- the
-        broadcast bias add -- is copied in), then the averaged all-reduce of the replicated
-        parameters' gradients: one collective over the arena's leading range."""
+    def comm_stream(self):
+        """The communication stream (GPU, W > 1): fc2's overlapped collectives, the backward
+        all-gather and the replicated gradients' all-reduce; created on first use."""
+        if self.world == 1 or _FAKE_WORLD or not self.fc1.weight.is_cuda:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.fc1.weight.device, priority=-1)
+        return self._side
+
+    def _reduce_replicated_async(self) -> None:
+        """(On the communication stream, from the backward:) the replicated parameters'
+        averaged all-reduce; ``sync_grads`` joins it."""
+        if not self._fresh:
+            # gradients accumulate across backward passes (no zero_grad(set_to_none=True)):
+            # autograd adds this pass's into .grad after this node -- sync_grads reduces them
+            return
         a = self._arena
+        runtime.all_reduce(a.grad[: self._rep_end], "avg")
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._reduced = ev
+
+    def sync_grads(self) -> None:
+        """Every gradient into its arena slot (a gradient autograd produced elsewhere is copied
+        in), then the averaged all-reduce of the replicated parameters' gradients: one
+        collective over the arena's leading range -- already issued from the backward on the
+        communication stream (joined here), or run here."""
+        a = self._arena
+        ev, self._reduced = self._reduced, None
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+            self._keep.clear()
         with torch.no_grad():
             for i, q in enumerate(a.params):
                 if q.grad is not None and not a.is_arena_grad(i):
                     g = a.grad_view(i)
                     g.copy_(q.grad)
                     q.grad = g
-        if self.world == 1 or _FAKE_WORLD:
+        if self.world == 1 or _FAKE_WORLD or ev is not None:
             return
         runtime.all_reduce(a.grad[: self._rep_end], "avg")
 
