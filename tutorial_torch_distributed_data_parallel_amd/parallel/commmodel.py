@@ -226,7 +226,10 @@ def simulate_tensor(W: int, B: int = 128, dims=(9216, 4096, 4096), classes: int 
         g, c = gemm / chunks, (coll - hw.latency_us) / chunks + hw.latency_us
         return g + (chunks - 1) * max(g, c) + c - gemm
 
-    exposed = hidden(rs, fc2_gemm_us) + hidden(ag, 2 * fc2_gemm_us) + head + xg
+    # the head's all-reduce is issued on the communication stream right after the backward
+    # all-gather and runs behind fc2's / fc1's gradient GEMMs (~4 x fc2_gemm_us of work)
+    exposed = hidden(rs, fc2_gemm_us) + hidden(ag, 2 * fc2_gemm_us) + \
+        max(0.0, head - 4 * fc2_gemm_us) + xg
     wire = (W - 1) / W * (2 * big + (0 if global_batch else 4.0 * W * B * d0)) + \
         2 * (W - 1) / W * 4.0 * (h2 * classes + classes + h2)
     return {"W": W, "compute_us": round(comp, 1), "exposed_us": round(exposed, 1),
