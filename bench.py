@@ -356,7 +356,7 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
                 ms = rank_compute_ms(W, dims=dims, B=a.batch, steps=n, optim=a.optim)
                 rk[str(W)] = round(ms, 4)
                 pred[str(W)] = round(cm.simulate_tensor(W, B=a.batch, dims=dims,
-                                                        rank_us=ms * 1000.0, chunks=4)
+                                                        rank_us=ms * 1000.0, chunks=2)
                                      ["step_us"] / 1000.0, 4)
             out["tensor_rank_compute_ms"] = rk
             out["tensor_predicted_step_ms"] = pred
@@ -513,7 +513,7 @@ TENSOR_RUNGS = (
     {"name": "tensor-sharded", "factor": None, "fused": False, "graph": True, "tensor": 1},
     # fc2's reduce-scatter / all-gather in column chunks behind the chunk GEMMs
     {"name": "tensor-overlap", "factor": None, "fused": False, "graph": True,
-     "tensor": int(os.environ.get("TDP_TP_CHUNKS", "4"))},
+     "tensor": int(os.environ.get("TDP_TP_CHUNKS", "2"))},
 )
 
 
