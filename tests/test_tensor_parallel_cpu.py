@@ -34,3 +34,11 @@ def test_tensor_parallel_refuses_per_rank_bn(tmp_path):
 @pytest.mark.parametrize("world,chunks", [(2, 4), (4, 2)])
 def test_tensor_parallel_overlapped_chunks_match_global_batch(tmp_path, world, chunks):
     run(TW.step_parity, tmp_path, n=world, chunks=chunks)
+
+
+def test_tensor_parallel_adam_matches_global_batch(tmp_path):
+    run(TW.step_parity, tmp_path, n=2, kind="adam")
+
+
+def test_tensor_parallel_checkpoint_is_the_full_models(tmp_path):
+    run(TW.checkpoint_roundtrip, tmp_path, n=2)

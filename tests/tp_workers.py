@@ -27,7 +27,7 @@ def _ref_model(bn):
     return ToyMLP(batchnorm=bn, **DIMS)
 
 
-def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4, chunks=1):
+def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4, chunks=1, kind="sgd"):
     tdp.init_process_group("gloo")
     W = rt.get_world_size()
     ref = _ref_model(bn)
@@ -35,9 +35,14 @@ def step_parity(rank, out_dir, bn=False, global_batch=False, steps=4, chunks=1):
     if bn:
         model = tdp.nn.convert_sync_batchnorm(model)
     tp = TensorParallelMLP(model, global_batch=global_batch, overlap_chunks=chunks)
-    hp = dict(lr=0.05, momentum=0.9, weight_decay=1e-3)
-    opt = tdp.optim.SGD(tp.parameters(), **hp)
-    ropt = torch.optim.SGD(ref.parameters(), **hp)
+    if kind == "sgd":
+        hp = dict(lr=0.05, momentum=0.9, weight_decay=1e-3)
+        opt = tdp.optim.SGD(tp.parameters(), **hp)
+        ropt = torch.optim.SGD(ref.parameters(), **hp)
+    else:
+        hp = dict(lr=1e-2, weight_decay=1e-3)
+        opt = tdp.optim.Adam(tp.parameters(), **hp)
+        ropt = torch.optim.Adam(ref.parameters(), **hp)
     for step in range(steps):
         xs, ys = zip(*[_batch(r, step) for r in range(W)])
         X, Y = torch.cat(xs), torch.cat(ys)
@@ -169,4 +174,36 @@ def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1):
     t1.check_replicas()
     t2.check_replicas()
     rt.barrier()
+    tdp.destroy_process_group()
+
+
+def checkpoint_roundtrip(rank, out_dir):
+    """save_ddp_checkpoint of the sharded job = the unsharded ToyMLP's checkpoint: it loads into
+    a plain ToyMLP (equal to the gathered state) and back into a fresh sharded wrapper."""
+    import os
+
+    from tutorial_torch_distributed_data_parallel_amd.utils.checkpoint import (
+        load_checkpoint, save_ddp_checkpoint)
+
+    tdp.init_process_group("gloo")
+    torch.manual_seed(0)
+    tp = TensorParallelMLP(ToyMLP(**DIMS))
+    opt = tdp.optim.SGD(tp.parameters(), lr=0.05, momentum=0.9)
+    x, y = _batch(rank, 0)
+    tdp.ops.cross_entropy(tp(x), y).backward()
+    tp.sync_grads()
+    opt.step()
+    path = save_ddp_checkpoint(tp, out_dir, 0)
+    assert os.path.exists(path)
+    full = tp.state_dict()
+    plain = ToyMLP(**DIMS)
+    load_checkpoint(plain, path)
+    for k, v in plain.state_dict().items():
+        assert torch.equal(v, full[k]), k
+    torch.manual_seed(9)
+    tp2 = TensorParallelMLP(ToyMLP(**DIMS))
+    load_checkpoint(tp2, path)
+    back = tp2.state_dict()
+    for k in full:
+        assert torch.equal(back[k], full[k]), k
     tdp.destroy_process_group()

@@ -496,6 +496,39 @@ class TensorParallelMLP(nn.Module):
             sd[f"{n3}.{k}"] = v.clone()
         return sd
 
+    def state_dict(self, *args, **kwargs):  # noqa: D401 - the full model's (collective)
+        """The unsharded ToyMLP state_dict, every rank must call it (all-gathers): checkpoints
+        of the tensor-sharded job are those of the replicated model (utils/checkpoint.py)."""
+        if args or kwargs.get("destination") is not None or kwargs.get("prefix"):
+            return super().state_dict(*args, **kwargs)  # nn.Module internals: local shards
+        return self.full_state_dict()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """Load an unsharded ToyMLP state_dict (this rank keeps its slices)."""
+        n1, n2, n3 = self._names
+        want = set(self.full_state_dict_keys())
+        missing = sorted(want - set(state_dict))
+        unexpected = sorted(set(state_dict) - want)
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"TensorParallelMLP.load_state_dict: missing {missing}, "
+                               f"unexpected {unexpected}")
+        self.load_full_state_dict(state_dict)
+        from torch.nn.modules.module import _IncompatibleKeys
+
+        return _IncompatibleKeys(missing, unexpected)
+
+    def full_state_dict_keys(self):
+        n1, n2, n3 = self._names
+        b1n, b2n = self._bn_names
+        keys = [f"{n1}.weight"] + ([f"{n1}.bias"] if self.fc1.bias is not None else [])
+        if self.bn1 is not None:
+            keys += [f"{b1n}.{k}" for k in self.bn1.state_dict()]
+        keys += [f"{n2}.weight"] + ([f"{n2}.bias"] if self.b2 is not None else [])
+        if self.bn2 is not None:
+            keys += [f"{b2n}.{k}" for k in self.bn2.state_dict()]
+        keys += [f"{n3}.{k}" for k in self.fc3.state_dict()]
+        return keys
+
     def load_full_state_dict(self, sd: dict) -> None:
         n1, n2, n3 = self._names
         b1n, b2n = self._bn_names

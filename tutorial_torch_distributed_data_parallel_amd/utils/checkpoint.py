@@ -36,7 +36,13 @@ def save_on_main(obj, path: str) -> None:
 
 def save_ddp_checkpoint(ddp_model, save_dir: str, epoch: int) -> str:
     path = os.path.join(save_dir, f"ckpt_{epoch}.pt")
-    sd = _detach_clone(ddp_model.state_dict()) if rt.get_rank() == 0 else None
+    if getattr(ddp_model, "full_state_dict", None) is not None:
+        # a sharded model (parallel/tensor_parallel.py): assembling the full state dict is a
+        # collective every rank joins; rank 0 writes it
+        full = ddp_model.full_state_dict()
+        sd = _detach_clone(full) if rt.get_rank() == 0 else None
+    else:
+        sd = _detach_clone(ddp_model.state_dict()) if rt.get_rank() == 0 else None
     save_on_main(sd, path)
     return path
 
