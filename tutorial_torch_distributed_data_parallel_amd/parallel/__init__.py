@@ -2,7 +2,6 @@
 from . import runtime
 from .arena import ParamArena, flatten_module
 from .ddp import DDP, DistributedDataParallel
-from .tensor_parallel import TensorParallelMLP
 from .runtime import (all_gather_flat, all_reduce, all_reduce_coalesced, barrier, broadcast,
                       destroy_process_group, get_local_rank, get_rank, get_world_size,
                       init_process_group, is_initialized, is_main_process)
@@ -12,3 +11,12 @@ __all__ = ["runtime", "ParamArena", "flatten_module", "DDP", "DistributedDataPar
            "init_process_group", "destroy_process_group", "get_rank", "get_world_size",
            "get_local_rank", "is_initialized", "is_main_process", "all_reduce",
            "all_reduce_coalesced", "broadcast", "all_gather_flat", "barrier"]
+
+
+def __getattr__(name):
+    # tensor_parallel builds on nn/ (which imports this package): resolved on first use
+    if name == "TensorParallelMLP":
+        from .tensor_parallel import TensorParallelMLP
+
+        return TensorParallelMLP
+    raise AttributeError(name)
