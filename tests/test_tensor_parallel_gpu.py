@@ -67,3 +67,27 @@ def test_bench_tensor_sharded_diagnostics():
     assert "error" not in d, d
     assert d["execution"] == rec["config"]["rung"] and d["compute_ms"] > 0, d
     assert d["predicted_step_ms"] > 0 and d["busbw_GBps"], d
+
+
+def test_bias_act_and_scaled_relu_bias_bwd():
+    """csrc bias_act (y = relu?(x + b)) and relu_bias_bwd's gscale (g scaled, db not) against
+    torch."""
+    import torch
+
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    torch.manual_seed(4)
+    x = torch.randn(128, 512, device="cuda")
+    b = torch.randn(512, device="cuda")
+    for relu in (True, False):
+        ref = x + b
+        ref = torch.relu(ref) if relu else ref
+        assert torch.equal(C.bias_act(x, b, relu), ref)
+    y = torch.relu(x + b)
+    dy = torch.randn_like(y)
+    db = torch.empty(512, device="cuda")
+    g = C.relu_bias_bwd(dy, y, db, gscale=0.125)
+    m = dy * (y > 0)
+    assert torch.equal(g, m * 0.125)
+    torch.testing.assert_close(db, m.sum(0), rtol=1e-5, atol=1e-4)

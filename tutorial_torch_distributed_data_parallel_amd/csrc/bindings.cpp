@@ -515,10 +515,11 @@ void adam_multi_op(const std::vector<Tensor>& ps, const std::vector<Tensor>& gs,
 
 // g = dy*(y>0) (new tensor; dy itself when y is None), db (optional) = sum over rows of g
 Tensor relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
-                        const c10::optional<Tensor>& db, double beta_db) {
+                        const c10::optional<Tensor>& db, double beta_db, double gscale) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_ROWMAJOR(dy);
   const int B = (int)dy.size(0), N = (int)dy.size(1);
   const bool has_y = y.has_value() && y->defined();
+  TORCH_CHECK(gscale == 1.0 || has_y, "relu_bias_bwd: gscale needs the ReLU output y");
   Tensor g = dy;
   if (has_y) {
     CHECK_ROWMAJOR(*y);
@@ -532,8 +533,22 @@ Tensor relu_bias_bwd_op(const Tensor& dy, const c10::optional<Tensor>& y,
   if (dbp) part = at::empty({(int64_t)slices * N}, dy.options());
   relu_bias_bwd_ws(dy.data_ptr<float>(), has_y ? y->data_ptr<float>() : nullptr, B, N,
                    dy.stride(0), g.data_ptr<float>(), dbp, (float)beta_db,
-                   dbp ? part.data_ptr<float>() : nullptr, slices, cur_stream());
+                   dbp ? part.data_ptr<float>() : nullptr, slices, cur_stream(), (float)gscale);
   return g;
+}
+
+// y = relu?(x + b) row-wise (x [B, N] row-major, N % 4 == 0, 16-B aligned)
+Tensor bias_act_op(const Tensor& x, const Tensor& b, bool relu) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_ROWMAJOR(x); CHECK_GPU(b); CHECK_F32(b); CHECK_CONTIG(b);
+  const int B = (int)x.size(0), N = (int)x.size(1);
+  TORCH_CHECK(b.numel() == N && N % 4 == 0 && x.stride(0) % 4 == 0 &&
+                  x.data_ptr<float>() != nullptr && ((uintptr_t)x.data_ptr() & 15) == 0 &&
+                  ((uintptr_t)b.data_ptr() & 15) == 0,
+              "bias_act: N % 4 == 0 and 16-B aligned rows / bias required");
+  Tensor y = at::empty({B, N}, x.options());
+  bias_act_rows(x.data_ptr<float>(), x.stride(0), b.data_ptr<float>(), y.data_ptr<float>(), N,
+                B, N, relu, cur_stream());
+  return y;
 }
 
 // ------------------------------------------------------------------------------------ misc ops
@@ -1458,7 +1473,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: the lockstep weight-gradient + optimizer kernel (default off)");
   m.def("gemm_f32_lockstep", &gemm_f32_lockstep);
   m.def("relu_bias_bwd", &relu_bias_bwd_op, py::arg("dy"), py::arg("y") = py::none(),
-        py::arg("db") = py::none(), py::arg("beta_db") = 0.0);
+        py::arg("db") = py::none(), py::arg("beta_db") = 0.0, py::arg("gscale") = 1.0);
+  m.def("bias_act", &bias_act_op, py::arg("x"), py::arg("b"), py::arg("relu") = false);
   m.def("ce_fwd", &ce_fwd_op, py::arg("logits"), py::arg("labels"), py::arg("ignore_index"),
         py::arg("smoothing"), py::arg("mean"), py::arg("acc"), py::arg("with_grad") = false);
   m.def("ce_bwd", &ce_bwd_op);

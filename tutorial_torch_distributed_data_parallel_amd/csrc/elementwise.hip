@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void relu_bias_part_kernel(const float* __rest
                                                              int B, int N, long ld,
                                                              float* __restrict__ g,
                                                              float* __restrict__ part,
-                                                             int rows_per, int cgb) {
+                                                             int rows_per, int cgb, float gscale) {
   constexpr int W = VEC ? 4 : 1;
   __shared__ f32x4 red[256];
   const int rgn = 256 / cgb;
@@ -39,14 +39,14 @@ __global__ __launch_bounds__(256) void relu_bias_part_kernel(const float* __rest
           const f32x4 m = *reinterpret_cast<const f32x4*>(y + off);
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-          *reinterpret_cast<f32x4*>(g + (long)r * N + col) = d;
+          *reinterpret_cast<f32x4*>(g + (long)r * N + col) = d * gscale;
         }
         s += d;
       } else {
         float d = dy[off];
         if (y) {
           d = y[off] > 0.f ? d : 0.f;
-          g[(long)r * N + col] = d;
+          g[(long)r * N + col] = d * gscale;
         }
         s[0] += d;
       }
@@ -73,7 +73,8 @@ int relu_bias_cgb(int N) {
 
 // `part` is carved from `g`'s tail when the caller provides db; see bindings (workspace).
 void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, float* g,
-                      float* db, float beta_db, float* part, int slices, hipStream_t s) {
+                      float* db, float beta_db, float* part, int slices, hipStream_t s,
+                      float gscale) {
   const bool vec = (N % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)dy & 15) == 0) &&
                    (y == nullptr || ((uintptr_t)y & 15) == 0) && (((uintptr_t)g & 15) == 0);
   const int rows_per = (B + slices - 1) / slices;
@@ -82,12 +83,41 @@ void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, fl
   dim3 grid((cols + cgb - 1) / cgb, slices);
   if (vec)
     hipLaunchKernelGGL(relu_bias_part_kernel<true>, grid, dim3(256), 0, s, dy, y, B, N, ld, g,
-                       db ? part : nullptr, rows_per, cgb);
+                       db ? part : nullptr, rows_per, cgb, gscale);
   else
     hipLaunchKernelGGL(relu_bias_part_kernel<false>, grid, dim3(256), 0, s, dy, y, B, N, ld, g,
-                       db ? part : nullptr, rows_per, cgb);
+                       db ? part : nullptr, rows_per, cgb, gscale);
   // db = beta*db + column sums of the partials: the split-axis-parallel split-K combine
   if (db) splitk_reduce(part, slices, 1, N, db, false, N, nullptr, beta_db, false, s);
+}
+
+// y[r][c] = relu?(x[r][c] + b[c]) over [B][N] (N % 4 == 0, 16-B aligned rows): the bias + ReLU
+// of an output that no GEMM epilogue produced (the tensor-sharded step's reduce-scattered fc2
+// output, parallel/tensor_parallel.py) in one pass
+namespace {
+__global__ __launch_bounds__(256) void bias_act_rows_kernel(const float* __restrict__ x, long ldx,
+                                                            const float* __restrict__ b,
+                                                            float* __restrict__ y, long ldy,
+                                                            int B, int N4, int relu) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long)B * N4) return;
+  const int r = (int)(t / N4), c = (int)(t % N4) * 4;
+  f32x4 v = *reinterpret_cast<const f32x4*>(x + (long)r * ldx + c) +
+            *reinterpret_cast<const f32x4*>(b + c);
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(y + (long)r * ldy + c) = v;
+}
+}  // namespace
+
+void bias_act_rows(const float* x, long ldx, const float* b, float* y, long ldy, int B, int N,
+                   bool relu, hipStream_t s) {
+  const long n = (long)B * (N / 4);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(bias_act_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
+                     ldx, b, y, ldy, B, N / 4, relu ? 1 : 0);
 }
 
 int relu_bias_slices(int B, int N, int num_cus) {

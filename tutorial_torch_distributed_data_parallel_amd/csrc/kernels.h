@@ -240,8 +240,12 @@ void scale_inplace(float* x, long n, float a, hipStream_t s);
 //   g[B][N] = dy * (y > 0) (written only when y != null), db = beta_db*db + sum_rows(g).
 //   `part` holds slices*N floats of column partial sums (slices from relu_bias_slices).
 int relu_bias_slices(int B, int N, int num_cus);
+// y = relu?(x + b) row-wise over [B][N] (N % 4 == 0, 16-B aligned rows and bias)
+void bias_act_rows(const float* x, long ldx, const float* b, float* y, long ldy, int B, int N,
+                   bool relu, hipStream_t s);
 void relu_bias_bwd_ws(const float* dy, const float* y, int B, int N, long ld, float* g,
-                      float* db, float beta_db, float* part, int slices, hipStream_t s);
+                      float* db, float beta_db, float* part, int slices, hipStream_t s,
+                      float gscale = 1.f);  // g = gscale * dy * (y > 0) (db unscaled)
 void fill_f32(float* x, long n, float v, hipStream_t s);
 // 4-D strided copy over dst's logical shape; elements outside src's shape are written as 0
 // (accumulate: dst += src, and elements outside src's shape are left alone)

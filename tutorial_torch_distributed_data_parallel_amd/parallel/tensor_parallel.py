@@ -215,7 +215,7 @@ class _RowParallelOverlap(torch.autograd.Function):
         hc = h2 // nc
         B = dy.shape[0]
         # this rank's rows of dY, scaled, chunk-major: [nc][B][hc]
-        dyc = (dy * scale).reshape(B, nc, hc).transpose(0, 1).contiguous()
+        dyc = (dy * scale if scale != 1.0 else dy).reshape(B, nc, hc).transpose(0, 1).contiguous()
         dp = torch.empty((nc, M, hc), device=dy.device, dtype=dy.dtype)
         dh1 = torch.empty_like(h1) if ctx.needs_input_grad[0] else None
         dw2 = grad_dest(w2) if ctx.needs_input_grad[1] else None
@@ -254,15 +254,22 @@ class _RowParallelOverlap(torch.autograd.Function):
 
 
 class _BiasReLU(torch.autograd.Function):
-    """``relu?(y + b)`` for the reduce-scattered fc2 output; backward is ONE native pass (the
-    ReLU mask and the bias gradient, written into b's arena slot: csrc relu_bias_bwd)."""
+    """``relu?(y + b)`` for the reduce-scattered fc2 output, one native pass each way: forward
+    csrc bias_act, backward relu_bias_bwd (the ReLU mask, the bias gradient into b's arena slot,
+    and the input gradient times ``gscale`` -- the 1/W of the sharded gradients, folded here
+    instead of a separate scaling pass; the bias gradient itself stays unscaled)."""
 
     @staticmethod
-    def forward(ctx, y, b, relu: bool):
-        out = y + b
-        if relu:
-            out.clamp_min_(0.0)
-        ctx.relu = relu
+    def forward(ctx, y, b, relu: bool, gscale: float = 1.0):
+        if y.is_cuda:
+            from .._native import native
+
+            out = native().bias_act(y, b, relu)
+        else:
+            out = y + b
+            if relu:
+                out.clamp_min_(0.0)
+        ctx.relu, ctx.gscale = relu, gscale
         ctx.b = b
         ctx.save_for_backward(out if relu else None)
         return out
@@ -276,15 +283,20 @@ class _BiasReLU(torch.autograd.Function):
         db = grad_dest(ctx.b) if ctx.needs_input_grad[1] else None
         if dy.is_cuda:
             dy = dy.contiguous()
-            if ctx.relu or db is not None:
-                g = native().relu_bias_bwd(dy, out if ctx.relu else None, db)
+            if ctx.relu:
+                g = native().relu_bias_bwd(dy, out, db, gscale=ctx.gscale)
+            elif db is not None:
+                g = native().relu_bias_bwd(dy, None, db)
+                g = g * ctx.gscale if ctx.gscale != 1.0 else g
             else:
-                g = dy
+                g = dy * ctx.gscale if ctx.gscale != 1.0 else dy
         else:
             g = dy * (out > 0) if ctx.relu else dy
             if db is not None:
                 db.copy_(g.sum(0))
-        return g, db, None
+            if ctx.gscale != 1.0:
+                g = g * ctx.gscale
+        return g, db, None, None
 
 
 def _linears(model):
@@ -397,15 +409,19 @@ class TensorParallelMLP(nn.Module):
         if self.bn1 is not None:
             h = self.bn1(h)
         nc = self.overlap_chunks
+        # the 1/W of the sharded gradients: folded into the bias + ReLU backward when there is
+        # one (no separate scaling pass), else applied before the backward all-gather
+        inv = 1.0 / self.world
+        fold = self.world > 1 and self.b2 is not None
         if self.world > 1 and nc > 1:
             self.comm_stream()
-            y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 / self.world, nc, self._side,
-                                          self)
+            y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 if fold else inv, nc,
+                                          self._side, self)
         else:
             p = self.fc2(h)
-            y = _ScatterRowsSum.apply(p, 1.0 / self.world, self) if self.world > 1 else p
+            y = _ScatterRowsSum.apply(p, 1.0 if fold else inv, self) if self.world > 1 else p
         if self.b2 is not None:
-            y = _BiasReLU.apply(y, self.b2, self.relu2)
+            y = _BiasReLU.apply(y, self.b2, self.relu2, inv if fold else 1.0)
         elif self.relu2:
             y = torch.relu(y)
         if self.bn2 is not None:
