@@ -193,9 +193,9 @@ def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
 
 # Per-rank compute of the tensor-sharded step (parallel/tensor_parallel.py), measured on one GPU
 # with the shard shapes of W ranks and the collectives replaced by local copies
-# (scripts/tp_rank_proxy.py, profiles/r9/tp_rank_proxy_r9o.jsonl; dp1 of that run: 347.6 us)
-TP_RANK_US = {1: 467.9, 2: 377.4, 4: 369.5, 8: 363.0}
-TP_DP1_US = 347.6
+# (scripts/tp_rank_proxy.py, profiles/r9/tp_rank_proxy_r9x.jsonl; dp1 of that run: 357.6 us)
+TP_RANK_US = {1: 490.0, 2: 371.0, 4: 360.4, 8: 354.6}
+TP_DP1_US = 357.6
 
 
 def simulate_tensor(W: int, B: int = 128, dims=(9216, 4096, 4096), classes: int = 10,
