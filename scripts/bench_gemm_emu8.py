@@ -53,8 +53,10 @@ for name, M, N, K, bk in SHAPES:
             C.gemm_emu8_set_waves(w)
             best[f"w{w}"] = min(best.get(f"w{w}", 1e30),
                                 timeit(lambda: C.gemm_emu8(A, B, o, bk), reps))
+        C.gemm_f32_set_mode(2)  # the 128 x 128 fast kernel (auto dispatch may pick emu8)
         best["fast"] = min(best.get("fast", 1e30),
                            timeit(lambda: C.gemm_f32(A, B, of, True, bk), reps))
+        C.gemm_f32_set_mode(0)
     C.gemm_emu8_set_waves(8)
     torch.cuda.synchronize()
     Bm = B.t() if bk else B

@@ -183,3 +183,38 @@ def test_emu_non_finite_inputs_stay_non_finite(C):
     assert torch.isfinite(out).all(), (big.abs().max().item(), (~torch.isfinite(out)).sum().item())
     e_emu = _scaled_err(out, big, small, True, True)
     assert e_emu < (8 + 2 * K ** 0.5) * U, e_emu
+
+
+
+@pytest.mark.parametrize("bk", [True, False])
+def test_gemm_f32_dispatches_large_plain_gemms_to_emu8(bk):
+    """gemm_f32 on a large plain GEMM (>= 256 256x256 tiles in whole waves) runs the 256 x 256
+    kernel (csrc/gemm_emu8.hip): bias + ReLU epilogue, bitwise equal to the 128 x 128 fast
+    kernel (same six products in the same k order), within the fp32 bound against fp64."""
+    import torch
+
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    torch.manual_seed(11)
+    M, N, K = 4096, 4096, 1024
+    A = torch.randn(M, K, device="cuda")
+    B = torch.randn((N, K) if bk else (K, N), device="cuda")
+    bias = torch.randn(N, device="cuda")
+    auto = torch.empty(M, N, device="cuda")
+    fast = torch.empty(M, N, device="cuda")
+    direct = torch.empty(M, N, device="cuda")
+    C.gemm_f32(A, B, auto, True, bk, bias=bias, relu=True)
+    C.gemm_f32_set_mode(2)
+    try:
+        C.gemm_f32(A, B, fast, True, bk, bias=bias, relu=True)
+    finally:
+        C.gemm_f32_set_mode(0)
+    C.gemm_emu8(A, B, direct, bk)
+    torch.cuda.synchronize()
+    assert torch.equal(auto, fast)
+    assert torch.equal(auto, torch.relu(direct + bias))
+    Bm = B.t() if bk else B
+    rows = torch.randperm(M, device="cuda")[:128]
+    ref = torch.relu(A[rows].double() @ Bm.double() + bias.double())
+    torch.testing.assert_close(auto[rows].double(), ref, rtol=1e-4, atol=1e-3)

@@ -14,7 +14,12 @@ struct GemmEmu8Args {
   bool b_kcontig = true;
   int M = 0, N = 0, K = 0;
   float beta = 0.f;
+  const float* bias = nullptr;  // C = relu?(A.B^T + bias + beta C)
+  bool relu = false;
 };
+// The 256 x 256 kernel fills the chip on this shape: one plain-epilogue GEMM with >= 256 output
+// tiles in nearly whole waves (gemm_f32's planner prefers it there; profiles/r9/gemm_emu8_r9.md)
+bool gemm_emu8_fits(int M, int N, int K, int num_cus);
 bool gemm_emu8_ok(const GemmEmu8Args& a);
 void gemm_emu8_run(const GemmEmu8Args& a, hipStream_t s);
 // variant: 8 waves (wave tile 128 x 64, default) or 4 (128 x 128, one wave per SIMD)

@@ -50,6 +50,8 @@ struct E8Params {
   int M, N, K;
   int tiles_n, tiles;
   float beta;
+  const float* bias;  // optional [N]
+  int relu;
 };
 
 __device__ __forceinline__ void split_pair8(float x0, float x1, unsigned& h, unsigned& m,
@@ -220,7 +222,9 @@ gemm_emu8_kernel(E8Params p) {
         const int row = m0 + wm * 128 + f * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row < p.M) {
           float* c = p.C + (long)row * p.ldc + col;
-          *c = p.beta != 0.f ? p.beta * *c + acc[f][g][r] : acc[f][g][r];
+          float v = acc[f][g][r] + (p.bias ? p.bias[col] : 0.f);
+          if (p.beta != 0.f) v += p.beta * *c;
+          *c = p.relu ? fmaxf(v, 0.f) : v;
         }
       }
     }
@@ -251,6 +255,13 @@ bool gemm_emu8_set_waves(int w) {
   return true;
 }
 
+bool gemm_emu8_fits(int M, int N, int K, int num_cus) {
+  if (K < 1024 || K % kBK8 || M < 2048 || N < 2048) return false;
+  const long tiles = (long)ceil_div(M, kTile) * ceil_div(N, kTile);
+  const long waves = (tiles + num_cus - 1) / num_cus;
+  return tiles >= num_cus && tiles * 10 >= waves * num_cus * 9;  // >= 90 % of the last wave
+}
+
 bool gemm_emu8_ok(const GemmEmu8Args& a) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (a.M <= 0 || a.N < 4 || a.K < kBK8 || a.K % kBK8) return false;
@@ -274,6 +285,8 @@ void gemm_emu8_run(const GemmEmu8Args& a, hipStream_t s) {
   p.tiles_n = ceil_div(a.N, kTile);
   p.tiles = ceil_div(a.M, kTile) * p.tiles_n;
   p.beta = a.beta;
+  p.bias = a.bias;
+  p.relu = a.relu ? 1 : 0;
   const bool w4 = e8_waves() == 4;
   if (a.b_kcontig) w4 ? launch_e8<true, 4>(p, s) : launch_e8<true, 8>(p, s);
   else w4 ? launch_e8<false, 4>(p, s) : launch_e8<false, 8>(p, s);

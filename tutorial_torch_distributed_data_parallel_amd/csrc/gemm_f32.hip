@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "emu8.h"
 
 namespace tdp {
 namespace {
@@ -346,6 +347,21 @@ GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus) {
     if (plan.skinny) return plan;
   }
   if (g_mode != 1 && gemm_f32_fast_ok(a)) {
+    // a large plain GEMM that fills the chip with 256 x 256 tiles: the one-workgroup-per-CU
+    // kernel, bitwise equal and 15-20 % faster (profiles/r9/gemm_emu8_r9.md)
+    if ((g_mode == 0 || g_mode == 3) && gemm_f32_emu() && a.a_kcontig && !a.mask && !a.rowsum &&
+        !a.gate &&
+        a.opt.kind == 0 && gemm_emu8_fits(a.M, a.N, a.K, num_cus)) {
+      GemmEmu8Args e;
+      e.A = a.A; e.B = a.B; e.C = a.C; e.lda = a.lda; e.ldb = a.ldb; e.ldc = a.ldc;
+      e.b_kcontig = a.b_kcontig; e.M = a.M; e.N = a.N; e.K = a.K; e.beta = a.beta;
+      if (gemm_emu8_ok(e)) {
+        plan.emu8 = true;
+        plan.fast = true;
+        plan.bm = plan.bn = 256;
+        return plan;
+      }
+    }
     gemm_f32_fast_plan(a, num_cus, plan);
     return plan;
   }
@@ -377,6 +393,14 @@ void gemm_f32_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStre
   if (plan.skinny) {
     gemm_skinny_run(plan.skinny, a, s);
     if (a.opt.kind != 0) gemm_opt_fallback(a, s);
+    return;
+  }
+  if (plan.emu8) {
+    GemmEmu8Args e;
+    e.A = a.A; e.B = a.B; e.C = a.C; e.lda = a.lda; e.ldb = a.ldb; e.ldc = a.ldc;
+    e.b_kcontig = a.b_kcontig; e.M = a.M; e.N = a.N; e.K = a.K; e.beta = a.beta;
+    e.bias = a.bias; e.relu = a.relu;
+    gemm_emu8_run(e, s);
     return;
   }
   if (plan.fast) {

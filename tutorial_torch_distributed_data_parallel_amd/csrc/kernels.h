@@ -129,6 +129,7 @@ struct GemmPlan {
   long ws_floats = 0;   // split-K workspace needed (0 when splits == 1)
   int skinny = 0;       // > 0: one of the skinny kernels (gemm_skinny.hip) runs instead
   int grid = 0;         // fast kernel: > 0 = persistent launch of this many workgroups
+  bool emu8 = false;    // the 256 x 256 split-bf16 kernel (gemm_emu8.hip) runs instead
 };
 
 GemmPlan gemm_f32_plan(const GemmF32Args& a, int num_cus);
