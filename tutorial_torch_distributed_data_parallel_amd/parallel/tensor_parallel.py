@@ -459,7 +459,9 @@ class TensorParallelMLP(nn.Module):
         ev, self._reduced = self._reduced, None
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
-            self._keep.clear()
+        # the compute stream is ordered after every side-stream read of these (the gathered
+        # event, or the join above): their memory may be reused from here on
+        self._keep.clear()
         with torch.no_grad():
             for i, q in enumerate(a.params):
                 if q.grad is not None and not a.is_arena_grad(i):
