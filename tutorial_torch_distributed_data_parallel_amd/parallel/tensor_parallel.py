@@ -111,55 +111,15 @@ class _GatherRows(torch.autograd.Function):
         return _reduce_scatter_rows(out, dy)
 
 
-class _ScatterRowsSum(torch.autograd.Function):
-    """This rank's row block of the sum over ranks; the gradient is the all-gather of the row
-    blocks' gradients, times ``scale`` (1/W: sum of per-rank mean losses -> global mean)."""
-
-    @staticmethod
-    def forward(ctx, p, scale: float, owner=None):
-        _, world = _ranks()
-        ctx.scale = scale
-        ctx.owner = owner
-        out = torch.empty((p.shape[0] // world,) + tuple(p.shape[1:]), device=p.device,
-                          dtype=p.dtype)
-        return _reduce_scatter_rows(out, p)
-
-    @staticmethod
-    def backward(ctx, dy):
-        _, world = _ranks()
-        out = torch.empty((world * dy.shape[0],) + tuple(dy.shape[1:]), device=dy.device,
-                          dtype=dy.dtype)
-        if ctx.scale != 1.0:
-            dy = dy * ctx.scale  # on this rank's rows: 1/W of the gathered tensor's bytes
-        dy = dy.contiguous()
-        owner = ctx.owner
-        if owner is not None and dy.is_cuda and owner.comm_stream() is not None:
-            # on the communication stream: the all-gather, then the replicated parameters'
-            # all-reduce (their gradients are complete: the head's backward ran before this
-            # node), which then runs behind fc2's / fc1's gradient GEMMs (joined in sync_grads)
-            side = owner.comm_stream()
-            comp = torch.cuda.current_stream()
-            ready = torch.cuda.Event()
-            ready.record(comp)
-            side.wait_event(ready)
-            with torch.cuda.stream(side):
-                _all_gather_rows(out, dy)
-                gathered = torch.cuda.Event()
-                gathered.record(side)
-                owner._reduce_replicated_async()
-            comp.wait_event(gathered)
-            keep = owner._keep
-            keep.append(dy)  # read on the side stream: alive until sync_grads' join
-        else:
-            _all_gather_rows(out, dy)
-        return out, None, None
-
-
 class _RowParallelOverlap(torch.autograd.Function):
-    """``reduce_scatter_rows(h1 . w2^T)`` in ``nc`` column chunks of fc2's output: chunk c's
-    GEMM runs on the compute stream while chunk c-1's reduce-scatter runs on the communication
-    stream. Backward mirrors it: chunk c's all-gather of dY (scaled by ``scale``) overlaps chunk
-    c-1's two GEMMs (dW2 rows of chunk c, dH1 accumulated over chunks). On CPU the same chunk
+    """fc2 of the sharded pair: ``reduce_scatter_rows(h1 . w2^T)``, in ``nc`` column chunks of
+    fc2's output when nc > 1 (chunk c's GEMM on the compute stream while chunk c-1's
+    reduce-scatter runs on the communication stream; nc = 1: one GEMM, the reduce-scatter on
+    the compute stream). Backward: the all-gather(s) of dY (times ``scale``) on the
+    communication stream; dW2 = dP^T H1 on an auxiliary stream, so its GEMMs fill the CUs that
+    fc1's weight-gradient GEMM (fewer tiles than slots: 288 for 512 at W = 8) leaves idle (joined
+    in ``sync_grads``); dH1 = dP W2 on the compute stream, gated by fc1's ReLU in its epilogue
+    when fc1's output is one (fc1's backward then skips its mask pass). On CPU the same chunk
     loop runs without streams (the gloo tests of the indexing)."""
 
     @staticmethod
@@ -174,41 +134,56 @@ class _RowParallelOverlap(torch.autograd.Function):
         parts = torch.empty((nc, B, hc), device=h1.device, dtype=h1.dtype)
         ctx.save_for_backward(h1, w2)
         ctx.scale, ctx.nc, ctx.side, ctx.owner = scale, nc, side, owner
+        ctx.gate = bool(getattr(h1, "_tdp_relu_out", False)) and h1.is_cuda
         if not h1.is_cuda:
             for c in range(nc):
                 _reduce_scatter_rows(parts[c], h1 @ w2[c * hc:(c + 1) * hc].t())
-        else:
-            from ..ops.linear import planes_fit, planes_of
+            return parts.transpose(0, 1).reshape(B, h2)
+        from ..ops.linear import planes_fit, planes_of
 
-            C = native()
-            comp = torch.cuda.current_stream()
-            keep = []
-            hp = planes_of(h1) if planes_fit(M, hc, s) else None
+        C = native()
+        hp = planes_of(h1) if planes_fit(M, hc, s) else None
+
+        def chunk(c, out):
+            if hp is not None:  # H1's pre-split planes (fc1's epilogue emitted them)
+                C.gemm_planes(hp, w2[c * hc:(c + 1) * hc], out, True)
+            else:
+                C.gemm_f32(h1, w2[c * hc:(c + 1) * hc], out, True, True)
+        if nc == 1:
+            pc = torch.empty((M, h2), device=h1.device, dtype=h1.dtype)
+            chunk(0, pc)
+            return _reduce_scatter_rows(parts[0], pc)
+        if side is None:  # no communication stream (local-copy measurement): in order
             for c in range(nc):
                 pc = torch.empty((M, hc), device=h1.device, dtype=h1.dtype)
-                if hp is not None:  # H1's pre-split planes (fc1's epilogue emitted them)
-                    C.gemm_planes(hp, w2[c * hc:(c + 1) * hc], pc, True)
-                else:
-                    C.gemm_f32(h1, w2[c * hc:(c + 1) * hc], pc, True, True)
-                ev = torch.cuda.Event()
-                ev.record(comp)
-                side.wait_event(ev)
-                with torch.cuda.stream(side):
-                    _reduce_scatter_rows(parts[c], pc)
-                keep.append(pc)  # alive until the join below orders their reuse after it
-            done = torch.cuda.Event()
-            done.record(side)
-            comp.wait_event(done)
-            del keep
+                chunk(c, pc)
+                _reduce_scatter_rows(parts[c], pc)
+            return parts.transpose(0, 1).reshape(B, h2)
+        comp = torch.cuda.current_stream()
+        keep = []
+        for c in range(nc):
+            pc = torch.empty((M, hc), device=h1.device, dtype=h1.dtype)
+            chunk(c, pc)
+            ev = torch.cuda.Event()
+            ev.record(comp)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                _reduce_scatter_rows(parts[c], pc)
+            keep.append(pc)  # alive until the join below orders their reuse after it
+        done = torch.cuda.Event()
+        done.record(side)
+        comp.wait_event(done)
+        del keep
         return parts.transpose(0, 1).reshape(B, h2)
 
     @staticmethod
     def backward(ctx, dy):
         from .._native import native
         from ..ops._grad import grad_dest
+        from ..ops.linear import _mark_gated
 
         h1, w2 = ctx.saved_tensors
-        nc, scale, side = ctx.nc, ctx.scale, ctx.side
+        nc, scale, side, owner = ctx.nc, ctx.scale, ctx.side, ctx.owner
         _, world = _ranks()
         M, s = h1.shape
         h2 = w2.shape[0]
@@ -230,26 +205,58 @@ class _RowParallelOverlap(torch.autograd.Function):
             return dh1, dw2, None, None, None, None
         C = native()
         comp = torch.cuda.current_stream()
+        side = owner.comm_stream() if owner is not None else side
+        aux = owner.aux_stream() if owner is not None else None
         ready = torch.cuda.Event()
         ready.record(comp)
-        side.wait_event(ready)
         evs = []
-        with torch.cuda.stream(side):
+        if side is not None:
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                for c in range(nc):
+                    _all_gather_rows(dp[c], dyc[c])
+                    e = torch.cuda.Event()
+                    e.record(side)
+                    evs.append(e)
+                if owner is not None:
+                    owner._reduce_replicated_async()
+        else:
             for c in range(nc):
                 _all_gather_rows(dp[c], dyc[c])
-                e = torch.cuda.Event()
-                e.record(side)
-                evs.append(e)
-            if ctx.owner is not None:
-                ctx.owner._reduce_replicated_async()
-                ctx.owner._keep.append(dyc)
-        for c in range(nc):
-            comp.wait_event(evs[c])
-            if dw2 is not None:  # dW2[rows of chunk c] = dP_c^T . H1
-                C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
-            if dh1 is not None:  # dH1 (+)= dP_c . W2[rows of chunk c]
+            ready = torch.cuda.Event()  # the gathered dP (compute stream) for the aux stream
+            ready.record(comp)
+        if owner is not None:
+            owner._keep += [dyc, dp, h1]
+        if dh1 is not None:
+            for c in range(nc):
+                if evs:
+                    comp.wait_event(evs[c])
+                last = c == nc - 1
+                # dH1 (+)= dP_c . W2[rows of chunk c]; the last chunk's epilogue applies fc1's
+                # ReLU mask to the finished sum
                 C.gemm_f32(dp[c], w2[c * hc:(c + 1) * hc], dh1, True, False,
-                           beta=0.0 if c == 0 else 1.0)
+                           beta=0.0 if c == 0 else 1.0, gate=h1 if (ctx.gate and last) else None)
+            if ctx.gate:
+                _mark_gated(dh1, h1)
+        if dw2 is not None:
+            if aux is not None:
+                # dW2[rows of chunk c] = dP_c^T . H1 on the aux stream, released only once dH1
+                # is done: it then runs beside fc1's weight-gradient GEMM (next on the compute
+                # stream, fewer tiles than slots) instead of competing with dH1 for the CUs
+                after_dh1 = torch.cuda.Event()
+                after_dh1.record(comp)
+                with torch.cuda.stream(aux):
+                    aux.wait_event(after_dh1)
+                    for c in range(nc):
+                        C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
+                    done = torch.cuda.Event()
+                    done.record(aux)
+                owner._aux_done = done
+            else:
+                for c in range(nc):
+                    if evs:
+                        comp.wait_event(evs[c])
+                    C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
         return dh1, dw2, None, None, None, None
 
 
@@ -354,6 +361,8 @@ class TensorParallelMLP(nn.Module):
         self._reduced = None  # event: the replicated all-reduce issued from the backward
         self._keep = []  # tensors read on the communication stream, alive until the join
         self._fresh = False
+        self._aux = None  # auxiliary stream (aux_stream)
+        self._aux_done = None  # event: fc2's weight-gradient GEMMs on it
         if fc2.out_features % max(1, self.overlap_chunks) or (fc2.weight.is_cuda and (
                 fc2.out_features // max(1, self.overlap_chunks)) % 4):
             raise ValueError(f"TensorParallelMLP: fc2 width {fc2.out_features} does not split "
@@ -413,13 +422,11 @@ class TensorParallelMLP(nn.Module):
         # one (no separate scaling pass), else applied before the backward all-gather
         inv = 1.0 / self.world
         fold = self.world > 1 and self.b2 is not None
-        if self.world > 1 and nc > 1:
-            self.comm_stream()
+        if self.world > 1:
             y = _RowParallelOverlap.apply(h, self.fc2.weight, 1.0 if fold else inv, nc,
-                                          self._side, self)
+                                          self.comm_stream() if nc > 1 else None, self)
         else:
-            p = self.fc2(h)
-            y = _ScatterRowsSum.apply(p, 1.0 if fold else inv, self) if self.world > 1 else p
+            y = self.fc2(h)
         if self.b2 is not None:
             y = _BiasReLU.apply(y, self.b2, self.relu2, inv if fold else 1.0)
         elif self.relu2:
@@ -436,6 +443,15 @@ class TensorParallelMLP(nn.Module):
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.fc1.weight.device, priority=-1)
         return self._side
+
+    def aux_stream(self):
+        """A second side stream (GPU, W > 1) for fc2's weight-gradient GEMMs, which run beside
+        fc1's backward; joined in ``sync_grads``."""
+        if self.world == 1 or not self.fc1.weight.is_cuda:
+            return None
+        if self._aux is None:
+            self._aux = torch.cuda.Stream(device=self.fc1.weight.device)
+        return self._aux
 
     def _reduce_replicated_async(self) -> None:
         """(On the communication stream, from the backward:) the replicated parameters'
@@ -459,6 +475,9 @@ class TensorParallelMLP(nn.Module):
         ev, self._reduced = self._reduced, None
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
+        aux, self._aux_done = self._aux_done, None
+        if aux is not None:
+            torch.cuda.current_stream().wait_event(aux)
         # the compute stream is ordered after every side-stream read of these (the gathered
         # event, or the join above): their memory may be reused from here on
         self._keep.clear()
