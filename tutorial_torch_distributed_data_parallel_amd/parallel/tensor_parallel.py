@@ -6,7 +6,8 @@ per step ``loss.backward()`` -- every rank all-reduces the full 218 MB gradient 
 hidden Linear pair is split Megatron-style over the W ranks of the node, so what crosses xGMI
 each step is ACTIVATIONS (a few MB), not weights:
 
-  X   = all-gather of every rank's batch            [W*B, in]      (no gradient)
+  X   = every rank's batch, in rank order           [W*B, in]      (gathered from the rank's
+        own dataset replica with global_batch=True -- bench.py -- else all-gathered)
   H1  = relu?(X . W1[own rows]^T + b1[own])         [W*B, h1/W]    column-parallel fc1
         (BatchNorm1d here sees the GLOBAL batch: SyncBN statistics with no collective)
   P2  = H1 . W2[:, own cols]^T                      [W*B, h2]      row-parallel fc2 (partial)
@@ -14,11 +15,17 @@ each step is ACTIVATIONS (a few MB), not weights:
   out = fc3(H2)                                     [B, classes]   replicated head
 
 Backward is autograd through the same ops: the reduce-scatter's gradient is the all-gather of
-dH2, scaled by 1/W so that every sharded gradient is the global-batch MEAN that DDP's averaged
-all-reduce produces; the replicated parameters (b2, the head, a BatchNorm after fc2) get the
-usual averaged all-reduce (``sync_grads``, ~0.2 MB). Each rank then updates only its shard
-with the ordinary optimizer: 1/W of the optimizer's HBM traffic, the dominant cost of the dp1
-step (profiles/r9/wgrad_split_roles_r9.md).
+dH2, scaled by 1/W (folded into the bias + ReLU backward pass) so that every sharded gradient is
+the global-batch MEAN that DDP's averaged all-reduce produces; the replicated parameters (b2,
+the head, a BatchNorm after fc2) get the usual averaged all-reduce (~0.2 MB). Each rank then
+updates only its shard with the ordinary optimizer: 1/W of the optimizer's HBM traffic, the
+dominant cost of the dp1 step (profiles/r9/wgrad_split_roles_r9.md).
+
+Streams (GPU, W > 1): the backward all-gather and then the replicated all-reduce run on a
+communication stream (the all-reduce behind the gradient GEMMs); fc2's weight-gradient GEMM runs
+on an auxiliary stream beside fc1's, which has fewer tiles than workgroup slots; both are joined
+in ``sync_grads``. ``overlap_chunks`` > 1 splits fc2's reduce-scatter / all-gather into column
+chunks behind the chunk GEMMs. Captured into the step's hipGraph like everything else.
 
 Per step and rank at W ranks, B samples each (toy MLP 9216-4096-4096-10, fp32): X all-gather
 (W-1) B 9216 x 4 B (33 MB at W = 8), reduce-scatter and all-gather of [W*B, 4096] (2 x 14.7 MB
