@@ -517,6 +517,17 @@ TENSOR_RUNGS = (
 )
 
 
+def _report_local(name: str, e: BaseException) -> None:
+    """The failing rank's own traceback, printed BEFORE the agreement collective: when only some
+    ranks fail, the others may be inside a collective of the rung and the agreement never lands
+    (the watchdog then ends the job), so this line is the only record of the cause."""
+    import traceback
+
+    r = os.environ.get("RANK", "0")
+    print(f"[bench] rank {r}: {name} raised:\n{traceback.format_exc()}", file=sys.stderr,
+          flush=True)
+
+
 def _agree(ok: bool) -> bool:
     from tutorial_torch_distributed_data_parallel_amd.train.graph import agree
 
@@ -745,6 +756,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
                 ddp.tune_factor_replicate(eager_step, iters=3, comm_cus=cus)
         except Exception as e:  # noqa: BLE001 - the ladder's first rung: keep the model's choice
             ok, err = False, e
+            _report_local(f"{cfg['name']}: factored-mode tuning", e)
         if not _agree(ok):
             # every rank drops the tuning result alike: the auto rule decides each weight
             native().set_reserved_cus(cus0)
@@ -978,6 +990,7 @@ def main():
                     sync()
                 except Exception as e:  # noqa: BLE001 - agreed below; the ladder follows
                     ok, err = False, e
+                    _report_local(tcfg["name"], e)
                 if not _agree(ok):
                     fallbacks.append(f"{tcfg['name']} failed ({repr(err)[:200] if err else 'on another rank'})")
                     print(f"[bench] {tcfg['name']} failed on some rank: {err!r}",
@@ -1011,6 +1024,7 @@ def main():
                 sync()
             except Exception as e:  # noqa: BLE001 - agreed below, then the next rung
                 ok, err = False, e
+                _report_local(cfg["name"], e)
                 if len(rungs) == 1:
                     raise
             if _agree(ok):

@@ -18,6 +18,7 @@ from tutorial_torch_distributed_data_parallel_amd.parallel.launcher import spawn
 
 import peer_workers as PW  # noqa: E402  (tests/ is on sys.path via conftest)
 import relay_workers as RW  # noqa: E402
+import tp_workers as TW  # noqa: E402
 
 NGPU = torch.cuda.device_count()
 pytestmark = [pytest.mark.gpu,
@@ -72,9 +73,37 @@ def test_rccl_cnn_captured(tmp_path, world):
 
 
 @pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("bn,chunks", [(False, 1), (False, 2), (True, 1)])
+def test_rccl_tensor_parallel_captured(tmp_path, world, bn, chunks):
+    """The tensor-sharded step (parallel/tensor_parallel.py) on RCCL: reduce-scatter / all-gather
+    of activations over xGMI inside hipGraph capture, captured == eager bitwise, both == the
+    one-process global-batch step to fp32 accuracy."""
+    run(TW.captured_parity, tmp_path, world, backend="nccl", bn=bn, chunks=chunks)
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_rccl_bench_tensor_record(world):
+    """``python bench.py --gpus N --parallel tensor`` on N real GPUs: a tensor-sharded rung,
+    captured, replicas identical, RCCL saw N ranks."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "TDP_GPU_PEER", "TDP_GPU_RELAY")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "6",
+           "--warmup", "3", "--mlp-dims", "1024,512,512", "--dataset", "2048", "--batch", "32",
+           "--device-warmup-ms", "0", "--parallel", "tensor"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    c = rec["config"]
+    assert rec["n_gpus"] == world and c["comm_nranks"] == world, c
+    assert c["rung"].startswith("tensor-") and c["fallbacks"] == [], c
+    assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
+
+
+@pytest.mark.parametrize("world", WORLDS)
 def test_rccl_bench_record(world):
     """``python bench.py --gpus N`` on N real GPUs: one valid record, captured, replicas
-    bit-identical, RCCL saw N ranks, no fallback taken."""
+    bit-identical, RCCL saw N ranks, no fallback taken (``--parallel auto``: whichever of the
+    tensor-sharded and DDP executions timed faster)."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "TDP_GPU_PEER", "TDP_GPU_RELAY")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "6",

@@ -21,12 +21,12 @@ def run(fn, tmp_path, n=2, **kw):
     spawn(functools.partial(fn, **kw) if kw else fn, n, args=(str(tmp_path),), grace=5.0)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_tensor_parallel_captured_with_real_peers(tmp_path, world):
     run(TW.captured_parity, tmp_path, n=world)
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 4), (4, 2)])
+@pytest.mark.parametrize("world,chunks", [(2, 4), (4, 2), (8, 2)])
 def test_tensor_parallel_overlap_captured_with_real_peers(tmp_path, world, chunks):
     run(TW.captured_parity, tmp_path, n=world, chunks=chunks)
 

@@ -1436,6 +1436,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950-native kernels, RCCL communicator and gradient reducer";
   m.def("num_cus", &num_cus);
   m.def("reserved_cus", &reserved_cus);
+  // a failed stream capture leaves its error as the thread's last HIP error; the next checked
+  // launch would report it although the eager fallback is fine: read (and so clear) it
+  m.def("take_last_hip_error", []() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
+  });
   m.def("set_reserved_cus", &set_reserved_cus);
   m.def("gemm_f32", &gemm_f32_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("mask") = py::none(),

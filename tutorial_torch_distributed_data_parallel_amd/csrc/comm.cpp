@@ -140,6 +140,11 @@ int Communicator::pending_watches() {
 
 void Communicator::watchdog_loop() {
   check_hip(hipSetDevice(device_), "hipSetDevice(watchdog)");
+  // this thread polls events (hipEventQuery) while the main thread may be recording a hipGraph
+  // in global capture mode: relaxed, its queries no longer invalidate that capture (seen as a
+  // one-rank capture failure right after replays left watches pending)
+  hipStreamCaptureMode relaxed = hipStreamCaptureModeRelaxed;
+  check_hip(hipThreadExchangeStreamCaptureMode(&relaxed), "hipThreadExchangeStreamCaptureMode");
   std::unique_lock<std::mutex> lk(mu_);
   while (!stop_) {
     // retire finished work in order; the oldest unfinished watch decides

@@ -83,6 +83,9 @@ static inline uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
 }
 
 void HostBatchLoader::worker() {
+  // event queries from this thread must not invalidate a step the main thread is capturing
+  hipStreamCaptureMode relaxed = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&relaxed);
   std::unique_lock<std::mutex> lk(mu_);
   std::vector<int64_t> rows;
   while (!stop_) {

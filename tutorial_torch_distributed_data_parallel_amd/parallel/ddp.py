@@ -16,10 +16,10 @@ a bucket may split a large tensor, all-reduces run on a dedicated high-priority 
 """
 from __future__ import annotations
 
-import os
-
 import contextlib
 import hashlib
+import os
+import sys
 import time
 import weakref
 
@@ -1122,7 +1122,8 @@ class DistributedDataParallel(nn.Module):
             run = step_fn
             step_fn()  # one eager step in this mode (sizes its buffers)
             if capture:
-                run = try_capture(step_fn, warmup=1, log=lambda m: None)
+                run = try_capture(step_fn, warmup=1,
+                                  log=lambda m: print(m, file=sys.stderr, flush=True))
                 captured = captured and isinstance(run, CapturedStep)
             best_t = None
             for _ in range(repeats):  # min of repeats: one slow window does not decide

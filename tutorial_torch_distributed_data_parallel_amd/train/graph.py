@@ -139,6 +139,23 @@ def agree(ok: bool) -> bool:
     return bool(int(t[0]))
 
 
+def _clear_capture_error() -> None:
+    """Clear the thread's sticky HIP error a failed capture leaves (torch.cuda.graph's exit has
+    ended the capture): otherwise the next checked launch of the EAGER fallback reports the
+    capture's error (seen at W = 4 after a one-rank capture failure: the barrier that followed
+    raised, the other ranks stalled)."""
+    try:
+        from .._native import native
+
+        msg = native().take_last_hip_error()
+    except Exception:  # noqa: BLE001 - an older build without the binding
+        msg = ""
+    if msg:
+        import sys
+
+        print(f"[tdp] cleared the failed capture's HIP error: {msg}", file=sys.stderr, flush=True)
+
+
 def try_capture(step_fn, warmup: int = 3, log=print, capture=CapturedStep):
     """Capture if possible, else run eagerly -- decided for ALL ranks together: one rank
     replaying a graph while another runs eagerly would issue collectives in a different order
@@ -150,6 +167,7 @@ def try_capture(step_fn, warmup: int = 3, log=print, capture=CapturedStep):
     except CaptureFailed as e:
         err = e
         if torch.cuda.is_available():
+            _clear_capture_error()
             torch.cuda.synchronize()
     if agree(graph is not None):
         return graph
