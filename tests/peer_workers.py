@@ -5,6 +5,7 @@ real peers. The captured-parity workers also take backend="nccl": the multi-GPU 
 (tests/test_multigpu_rccl.py) runs the same bodies with one rank per GPU. Oracles: closed-form collective results, the eager run of the same step (bitwise)
 and the fp32 torch DDP-semantics oracle of relay_workers."""
 import os
+import sys
 import time
 
 import torch
@@ -176,7 +177,37 @@ def rccl_watchdog_child():
     raise SystemExit(0)
 
 
+def capture_beside_pending_watch_child():
+    """One rank on RCCL with a watch pending (a 1.5 s device spin on a side stream) while the main
+    thread records a hipGraph in global capture mode for 0.35 s: the watchdog thread polls the
+    pending event meanwhile (every 100 ms). Its queries must not invalidate the capture (they did
+    before the watchdog thread switched itself to relaxed capture mode)."""
+    os.environ["TDP_TIMEOUT_S"] = "30"
+    tdp.init_process_group("nccl", rank=0, world_size=1, local_rank=0)
+    comm = rt.comm()
+    comm.set_watch_single_rank(True)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        native().debug_spin_ms(1500)
+        comm.watch_current("pending spin")
+    assert comm.pending_watches() == 1
+    x = torch.ones(1 << 16, device="cuda")
+    torch.cuda.current_stream().synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = x * 2.0
+        time.sleep(0.35)  # the watchdog wakes at least three times during the capture
+        y += 1.0
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(y.sum()) == 3.0 * x.numel()
+    print("capture-ok", flush=True)
+    raise SystemExit(0)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["capture_beside_pending_watch"]:
+        capture_beside_pending_watch_child()
     rccl_watchdog_child()
 
 

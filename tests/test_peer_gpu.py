@@ -71,6 +71,18 @@ def test_rccl_watchdog_fires_on_stalled_collective():
     assert "RCCL watchdog" in r.stderr and "stalled collective" in r.stderr, r.stderr[-2000:]
 
 
+def test_capture_beside_pending_watch():
+    """The communicator's watchdog thread polls a pending watch while the main thread records a
+    hipGraph: the capture succeeds (the thread runs in relaxed capture mode; before, its event
+    queries invalidated a concurrent capture -- a one-rank capture failure in bench's tuning)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "peer_workers.py"),
+                        "capture_beside_pending_watch"], capture_output=True, text=True,
+                       timeout=120, cwd=ROOT,
+                       env=dict(os.environ, PYTHONPATH=os.path.join(ROOT, "tests") + os.pathsep +
+                                ROOT))
+    assert r.returncode == 0 and "capture-ok" in r.stdout, (r.returncode, r.stderr[-2000:])
+
+
 def test_bench_self_launch_peer_captured():
     """``TDP_GPU_PEER=1 python bench.py --gpus 2``: bench.py spawns its two ranks itself, the
     multi-rank step is CAPTURED with real peers, replicas end bit-identical."""
