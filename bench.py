@@ -510,9 +510,9 @@ LADDER = (
 # toy MLP; with --parallel auto both it and the ladder's first working rung are timed, the faster
 # one is measured.
 TENSOR_RUNGS = (
-    {"name": "tensor-sharded", "factor": None, "fused": False, "graph": True, "tensor": 1},
+    {"name": "tensor-sharded", "factor": None, "fused": True, "graph": True, "tensor": 1},
     # fc2's reduce-scatter / all-gather in column chunks behind the chunk GEMMs
-    {"name": "tensor-overlap", "factor": None, "fused": False, "graph": True,
+    {"name": "tensor-overlap", "factor": None, "fused": True, "graph": True,
      "tensor": int(os.environ.get("TDP_TP_CHUNKS", "2"))},
 )
 
@@ -592,6 +592,9 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         tp = TensorParallelMLP(model, global_batch=shared, overlap_chunks=int(cfg["tensor"]))
         ddp = None
         opt = make_opt(tp.parameters())
+        if use_gpu and want_fused:
+            # the shards' SGD inside their weight-gradient GEMMs (complete gradients per rank)
+            fused = tp.register_fused_optimizer(opt)
         if shared:
             data = SyntheticDataset(a.dataset * world, in_shape, 10, seed=0, device=dev)
             samplers = [DistributedSampler(data, num_replicas=world, rank=r, shuffle=True)
@@ -1149,7 +1152,9 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "impl": impl,
-                "optimizer": a.optim + (" (fused into the gradient reduction)"
+                "optimizer": a.optim + ((" (shards: fused into their weight-gradient GEMMs)"
+                                         if job.tp is not None else
+                                         " (fused into the gradient reduction)")
                                         if a.impl == "tdp" and fused else ""),
                 "final_loss": final_loss,
                 "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,

@@ -3,7 +3,7 @@
 copies, captured step, the node's batch gathered per step), next to the captured dp1 step of the
 replicated model (DDP, fused optimizer). One JSON line each.
 
-python scripts/tp_rank_proxy.py [--no-dp1] [W ...]"""
+python scripts/tp_rank_proxy.py [--no-dp1] [--unfused] [W ...]"""
 import json
 import sys
 
@@ -51,10 +51,12 @@ a = torch.randn(4096, 4096, device=dev)  # clock warm-up
 for _ in range(50):
     a @ a
 torch.cuda.synchronize()
-args = [v for v in sys.argv[1:] if v != "--no-dp1"]
+args = [v for v in sys.argv[1:] if v not in ("--no-dp1", "--unfused")]
+FUSED = "--unfused" not in sys.argv
 ws = [int(v) for v in args] or [1, 2, 4, 8]
 if "--no-dp1" not in sys.argv:
     print(json.dumps({"W": "dp1 (DDP, fused optimizer)", "ms": round(dp1_ms(), 4)}), flush=True)
 for W in ws:
-    print(json.dumps({"W": W, "rank_compute_ms": round(rank_compute_ms(W, steps=200), 4)}),
+    print(json.dumps({"W": W, "fused": FUSED,
+                      "rank_compute_ms": round(rank_compute_ms(W, steps=200, fused=FUSED), 4)}),
           flush=True)

@@ -73,12 +73,14 @@ def test_rccl_cnn_captured(tmp_path, world):
 
 
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("bn,chunks", [(False, 1), (False, 2), (True, 1)])
-def test_rccl_tensor_parallel_captured(tmp_path, world, bn, chunks):
+@pytest.mark.parametrize("bn,chunks,fused", [(False, 1, False), (False, 2, False),
+                                              (True, 1, False), (False, 2, True),
+                                              (True, 1, True)])
+def test_rccl_tensor_parallel_captured(tmp_path, world, bn, chunks, fused):
     """The tensor-sharded step (parallel/tensor_parallel.py) on RCCL: reduce-scatter / all-gather
     of activations over xGMI inside hipGraph capture, captured == eager bitwise, both == the
     one-process global-batch step to fp32 accuracy."""
-    run(TW.captured_parity, tmp_path, world, backend="nccl", bn=bn, chunks=chunks)
+    run(TW.captured_parity, tmp_path, world, backend="nccl", bn=bn, chunks=chunks, fused=fused)
 
 
 @pytest.mark.parametrize("world", WORLDS)

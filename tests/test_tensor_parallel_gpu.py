@@ -35,6 +35,16 @@ def test_tensor_parallel_syncbn_captured_with_real_peers(tmp_path):
     run(TW.captured_parity, tmp_path, n=2, bn=True)
 
 
+@pytest.mark.parametrize("world,chunks,bn", [(1, 1, False), (2, 1, False), (4, 2, False),
+                                             (2, 1, True), (8, 2, False)])
+def test_tensor_parallel_fused_optimizer_captured(tmp_path, world, chunks, bn):
+    """register_fused_optimizer: SGD of the shards inside their weight-gradient GEMM
+    epilogues, the rest (replicated head, BatchNorm shards) in optimizer.step(): captured ==
+    eager bitwise, both == the one-process global-batch step of the full model."""
+    run(TW.captured_parity, tmp_path, n=world, chunks=chunks, bn=bn, fused=True,
+        backend="nccl" if world == 1 else "peer")
+
+
 def _peer_bench(*args, diag=False):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     env.update(TDP_GPU_PEER="1")

@@ -103,7 +103,7 @@ def _gbatch(r, step):
         torch.randint(0, 10, (GB,), generator=g).cuda()
 
 
-def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1):
+def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1, fused=False):
     """GPU, W ranks (peer vehicle on one GPU, or RCCL): the tensor-sharded step captured into a
     hipGraph and replayed == the same step run eagerly, BITWISE; both match the one-process
     global-batch step of the full model (torch fp32 on the GPU) to fp32 accuracy."""
@@ -118,7 +118,10 @@ def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1):
         if bn:
             m = tdp.nn.convert_sync_batchnorm(m)
         t = TensorParallelMLP(m, overlap_chunks=chunks)
-        return t, tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        o = tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        if fused:  # the shards' update inside their weight-gradient GEMMs
+            assert t.register_fused_optimizer(o)
+        return t, o
 
     t1, o1 = build()
     t2, o2 = build()

@@ -1430,6 +1430,69 @@ float* block_ptr(const c10::optional<Tensor>& blk) {
   return const_cast<float*>(hyper_ptr(blk));
 }
 
+// Weight-gradient GEMM whose epilogue applies SGD to explicit tensors (the tensor-sharded
+// wrapper's shards: their gradient is complete on this rank, no reduction precedes the update):
+// p / buf are C-shaped contiguous slices of the parameter and momentum arenas, the scalars come
+// from the optimizer's device hyper block. With rowsum and bias_p the bias is updated from the
+// row sums by the same kernel. Returns whether the epilogue ran; if not, C (and rowsum) hold the
+// gradient as from gemm_f32 and the caller updates them another way.
+bool gemm_f32_sgd_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
+                     const Tensor& p, const c10::optional<Tensor>& buf, const Tensor& hyper,
+                     bool nesterov, bool maximize, const c10::optional<Tensor>& rowsum,
+                     const c10::optional<Tensor>& bias_p, const c10::optional<Tensor>& bias_buf) {
+  CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C); CHECK_GPU(p); CHECK_GPU(hyper);
+  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C); CHECK_F32(p);
+  CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_CONTIG(C); CHECK_CONTIG(p);
+  const int M = (int)C.size(0), N = (int)C.size(1);
+  const int K = (int)(a_kcontig ? A.size(1) : A.size(0));
+  TORCH_CHECK((a_kcontig ? A.size(0) : A.size(1)) == M, "gemm: A rows != C rows");
+  TORCH_CHECK((b_kcontig ? B.size(0) : B.size(1)) == N, "gemm: B cols != C cols");
+  TORCH_CHECK((b_kcontig ? B.size(1) : B.size(0)) == K, "gemm: inner dims differ");
+  TORCH_CHECK(p.numel() == (int64_t)M * N, "gemm_f32_sgd: p must have C's elements");
+  const bool mom = buf.has_value() && buf->defined();
+  if (mom) {
+    CHECK_GPU(*buf); CHECK_F32(*buf); CHECK_CONTIG(*buf);
+    TORCH_CHECK(buf->numel() == p.numel(), "gemm_f32_sgd: momentum buffer size");
+  }
+  TORCH_CHECK((int64_t)M * N < (int64_t)1 << 31, "gemm_f32_sgd: parameter too large");
+  GemmF32Args a;
+  a.A = A.data_ptr<float>(); a.B = B.data_ptr<float>(); a.C = C.data_ptr<float>();
+  a.lda = A.stride(0); a.ldb = B.stride(0); a.ldc = N;
+  a.M = M; a.N = N; a.K = K;
+  a.a_kcontig = a_kcontig; a.b_kcontig = b_kcontig;
+  if (rowsum.has_value() && rowsum->defined()) {
+    CHECK_GPU(*rowsum); CHECK_F32(*rowsum); CHECK_CONTIG(*rowsum);
+    TORCH_CHECK(rowsum->numel() == M, "gemm: rowsum must have M elements");
+    a.rowsum = rowsum->data_ptr<float>();
+  }
+  GemmF32Args probe = a;
+  probe.opt.kind = 1;
+  const GemmPlan pp = gemm_f32_plan(probe, num_cus(C.get_device()));
+  const bool epi = pp.fast && !pp.skinny && pp.splits == 1 && !a_kcontig && !b_kcontig;
+  if (epi) {
+    const SgdHyper h{0.f, mom ? 1.f : 0.f, 0.f, 0.f, nesterov, maximize, false, 1.f,
+                     block_ptr(hyper)};
+    a.opt.kind = 1;
+    a.opt.p = p.data_ptr<float>();
+    a.opt.s0 = mom ? buf->data_ptr<float>() : nullptr;
+    a.opt.sgd = h;
+    if (a.rowsum != nullptr && bias_p.has_value() && bias_p->defined()) {
+      CHECK_GPU(*bias_p); CHECK_F32(*bias_p); CHECK_CONTIG(*bias_p);
+      TORCH_CHECK(bias_p->numel() == M, "gemm_f32_sgd: the bias must have M elements");
+      TORCH_CHECK(!mom || (bias_buf.has_value() && bias_buf->defined() &&
+                           bias_buf->numel() == M), "gemm_f32_sgd: bias momentum buffer");
+      a.bias_opt.kind = 1;
+      a.bias_opt.p = bias_p->data_ptr<float>();
+      a.bias_opt.s0 = mom ? bias_buf->data_ptr<float>() : nullptr;
+    }
+  }
+  const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  Tensor ws;
+  if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
+  gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  return epi;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1451,6 +1514,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
         py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0,
         py::arg("bias_offset") = -1, py::arg("bias_span") = 0);
+  m.def("gemm_f32_sgd", &gemm_f32_sgd_op, py::arg("A"), py::arg("B"), py::arg("C"),
+        py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("p"), py::arg("buf"),
+        py::arg("hyper"), py::arg("nesterov") = false, py::arg("maximize") = false,
+        py::arg("rowsum") = py::none(), py::arg("bias_p") = py::none(),
+        py::arg("bias_buf") = py::none());
   m.def("gemm_f32_plan", &gemm_f32_plan_op);
   m.def("gemm_planes", &gemm_planes_op, py::arg("Ap"), py::arg("B"), py::arg("C"),
         py::arg("b_kcontig"), py::arg("bias") = py::none(), py::arg("relu") = false,

@@ -174,7 +174,7 @@ class _LinearFn(torch.autograd.Function):
             dw = grad_dest(w_param)
             gate = x2 if ctx.gate_in else None
             kw = {}
-            if epi is not None and dw.is_contiguous():
+            if epi is not None and dw.is_contiguous() and not _tp_epilogue(epi):
                 # world size 1 + fused optimizer: the kernel updates W (and b) in place
                 kw = dict(backend=epi[0], w_offset=epi[1])
                 be = bias_epilogue(b_param) if db is not None else None
@@ -233,6 +233,15 @@ class _LinearFn(torch.autograd.Function):
                 # gradient from the all-gathered factors (g, x), and the averaged bias gradient
                 # from the gathered g; dw / db are handed to autograd unwritten
                 pass
+            elif epi is not None and _tp_epilogue(epi):
+                # a tensor-sharded weight (parallel/tensor_parallel.py register_fused_optimizer):
+                # the same epilogue on the shard, whose gradient is complete on this rank
+                be = bias_epilogue(b_param) if db is not None else None
+                if epi[0].epilogue_gemm(g, x2, dw, w_param, db=db,
+                                        b=b_param if be is not None else None):
+                    hand_off(w_param, dw)
+                    if be is not None:
+                        hand_off(b_param, db)
             elif epi is not None:
                 # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
                 # from the accumulators; the gradient itself is never written to HBM
@@ -249,6 +258,11 @@ class _LinearFn(torch.autograd.Function):
         elif want_db:
             C.relu_bias_bwd(g, None, db)
         return dx, dw, db, None, None, None, None
+
+
+def _tp_epilogue(epi) -> bool:
+    """The epilogue target is a tensor-sharded wrapper (not a DDP reducer backend)."""
+    return hasattr(epi[0], "epilogue_gemm")
 
 
 class _LinearCpuFn(torch.autograd.Function):

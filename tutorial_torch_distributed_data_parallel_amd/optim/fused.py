@@ -287,6 +287,12 @@ class SGD(_FusedBase):
                 loss = closure()
         if self._fused_step():
             return loss
+        tp = getattr(self, "_fused_tp", None)
+        tp = tp() if tp is not None else None
+        if tp is not None:
+            # tensor-sharded wrapper with the shards' update in their GEMM epilogues: the rest
+            tp._fused_step(self)
+            return loss
         for gi, g in enumerate(self.param_groups):
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:

@@ -193,9 +193,11 @@ def simulate(layers: list[Layer], modes: dict, W: int, B: int, hw: Hardware,
 
 # Per-rank compute of the tensor-sharded step (parallel/tensor_parallel.py), measured on one GPU
 # with the shard shapes of W ranks and the collectives replaced by local copies
-# (scripts/tp_rank_proxy.py, profiles/r9/tp_rank_proxy_r9x.jsonl; dp1 of that run: 357.6 us)
-TP_RANK_US = {1: 490.0, 2: 371.0, 4: 360.4, 8: 354.6}
-TP_DP1_US = 357.6
+# (scripts/tp_rank_proxy.py, profiles/r9/tp_rank_proxy_fused_r9ak.jsonl: the shards' SGD in their
+# weight-gradient GEMM epilogues, TensorParallelMLP.register_fused_optimizer; dp1 of that run:
+# 349.8 us. Before the fused update, r9x: 371.0 / 360.4 / 354.6 against dp1 357.6)
+TP_RANK_US = {1: 490.0, 2: 341.8, 4: 331.3, 8: 339.4}
+TP_DP1_US = 349.8
 
 
 def simulate_tensor(W: int, B: int = 128, dims=(9216, 4096, 4096), classes: int = 10,

@@ -40,6 +40,9 @@ stay those of the unsharded ToyMLP (utils/checkpoint.py).
 """
 from __future__ import annotations
 
+import contextlib
+import weakref
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -146,8 +149,10 @@ class _RowParallelOverlap(torch.autograd.Function):
             for c in range(nc):
                 _reduce_scatter_rows(parts[c], h1 @ w2[c * hc:(c + 1) * hc].t())
             return parts.transpose(0, 1).reshape(B, h2)
+        from ..ops._grad import note_use
         from ..ops.linear import planes_fit, planes_of
 
+        note_use(w2)  # the fused optimizer's epilogue needs exactly one use per step
         C = native()
         hp = planes_of(h1) if planes_fit(M, hc, s) else None
 
@@ -186,7 +191,7 @@ class _RowParallelOverlap(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from .._native import native
-        from ..ops._grad import grad_dest
+        from ..ops._grad import epilogue_target, grad_dest, hand_off
         from ..ops.linear import _mark_gated
 
         h1, w2 = ctx.saved_tensors
@@ -245,6 +250,17 @@ class _RowParallelOverlap(torch.autograd.Function):
                            beta=0.0 if c == 0 else 1.0, gate=h1 if (ctx.gate and last) else None)
             if ctx.gate:
                 _mark_gated(dh1, h1)
+        # the fused optimizer (register_fused_optimizer): each chunk's epilogue updates its rows
+        # of W2 in place instead of writing the gradient
+        epi = epilogue_target(w2) if dw2 is not None else None
+        handed = []
+
+        def dw2_chunk(c):
+            out = dw2[c * hc:(c + 1) * hc]
+            if epi is not None and epi[0].epilogue_gemm(dp[c], h1, out, w2, row0=c * hc):
+                handed.append(c)
+            else:
+                C.gemm_f32(dp[c], h1, out, False, False)
         if dw2 is not None:
             if aux is not None:
                 # dW2[rows of chunk c] = dP_c^T . H1 on the aux stream, released only once dH1
@@ -255,7 +271,7 @@ class _RowParallelOverlap(torch.autograd.Function):
                 with torch.cuda.stream(aux):
                     aux.wait_event(after_dh1)
                     for c in range(nc):
-                        C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
+                        dw2_chunk(c)
                     done = torch.cuda.Event()
                     done.record(aux)
                 owner._aux_done = done
@@ -263,7 +279,9 @@ class _RowParallelOverlap(torch.autograd.Function):
                 for c in range(nc):
                     if evs:
                         comp.wait_event(evs[c])
-                    C.gemm_f32(dp[c], h1, dw2[c * hc:(c + 1) * hc], False, False)
+                    dw2_chunk(c)
+            if handed:
+                hand_off(w2, dw2)
         return dh1, dw2, None, None, None, None
 
 
@@ -413,12 +431,20 @@ class TensorParallelMLP(nn.Module):
                                  [q for q in self.parameters() if id(q) not in rep])
         last = len(self._replicated) - 1
         self._rep_end = self._arena.offsets[last] + self._arena.numels[last]
+        self._index = {id(q): i for i, q in enumerate(self._arena.params)}
+        self._fopt = None     # optimizer applied in the shards' weight-gradient GEMM epilogues
+        self._fstate = None   # (momentum arena or None, hyper block, param group) of this step
+        self._uses = {}       # forward uses per parameter (an epilogue needs exactly one)
+        self._done = {}       # arena index -> elements the epilogues updated in this step
+        self._epi_on = True   # off inside no_sync()
 
     # ---------------------------------------------------------------------------- forward
     def forward(self, x):
         # every replicated gradient is empty: this backward writes them into their arena slots
         # (ops/_grad.py grad_dest), so the backward may all-reduce the slots early
         self._fresh = all(q.grad is None for q in self._replicated)
+        if self._fopt is not None and torch.is_grad_enabled() and self.training:
+            self._begin_fused_step()
         x = x.reshape(x.shape[0], -1)
         X = x if (self.world == 1 or self.global_batch) else _GatherRows.apply(x)
         h = self.fc1(X)
@@ -497,6 +523,142 @@ class TensorParallelMLP(nn.Module):
         if self.world == 1 or _FAKE_WORLD or ev is not None:
             return
         runtime.all_reduce(a.grad[: self._rep_end], "avg")
+
+    # ------------------------------------------------------------------ fused optimizer
+    def register_fused_optimizer(self, optimizer) -> bool:
+        """Apply ``optimizer`` to the SHARDED weights inside their weight-gradient GEMMs: the
+        epilogue reads p and the momentum at each gradient element, updates them and never
+        writes the gradient (csrc/gemm_f32_fast.hip OptEpilogue). A shard's gradient is complete
+        on its own rank -- nothing is reduced before the update -- so this holds at any world
+        size, where DDP can do it at world size 1 only (parallel/ddp.py register_fused_optimizer).
+        ``optimizer.step()`` then updates what no epilogue did: the replicated parameters after
+        their all-reduce, BatchNorm shards, a weight whose GEMM plan has no epilogue. Saves the
+        gradient's HBM write and re-read and the separate update pass (profiles/r9: 0.386 ->
+        see tp_fused_r9*.md). tdp SGD, one parameter group over ``parameters()``, GPU; returns
+        False and changes nothing otherwise. Each backward applies the update: run the earlier
+        passes of a gradient accumulation under ``no_sync()``."""
+        from ..optim.fused import SGD
+
+        if not self.fc1.weight.is_cuda or not isinstance(optimizer, SGD) or \
+                len(optimizer.param_groups) != 1:
+            return False
+        g = optimizer.param_groups[0]
+        if {id(q) for q in g["params"]} != set(self._index) or g["grad_scale"] != 1.0:
+            return False
+        self._fopt = optimizer
+        optimizer._fused_tp = weakref.ref(self)
+        me = weakref.ref(self)
+        for q in (self.fc1.weight, self.fc1.bias, self.fc2.weight):
+            if q is not None:
+                q._tdp_epi = me
+        return True
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside store their gradients (accumulated by autograd) instead of
+        applying the update; the pass after it -- whose gradients then accumulate too -- leaves
+        every update to ``optimizer.step()``."""
+        prev, self._epi_on = self._epi_on, False
+        try:
+            yield
+        finally:
+            self._epi_on = prev
+
+    def _begin_fused_step(self) -> None:
+        """(forward, before any epilogue of this step:) the momentum arena, the device hyper
+        block with the current scalars, and the block's per-step advance (first-step flag)."""
+        from .._native import native
+
+        opt, a = self._fopt, self._arena
+        g = opt.param_groups[0]
+        buf, fresh = None, False
+        if g["momentum"] != 0:
+            bufs, fresh = opt._flat_state(a, ("momentum_buffer",))
+            buf = bufs["momentum_buffer"]
+        if 0 in opt._blocks:
+            blk = opt._blocks[0][0]
+            opt.sync_hyper()
+            if fresh:
+                opt._request_first(blk)
+        else:
+            blk = opt.hyper_block(0, device=self.fc1.weight.device, first=fresh)
+        native().opt_step_begin(blk, 1)
+        self._fstate = (buf, blk, g)
+        self._uses = {}
+        self._done = {}
+
+    def _note_use(self, p) -> None:  # ops/_grad.py note_use
+        self._uses[id(p)] = self._uses.get(id(p), 0) + 1
+
+    def epilogue_slot(self, p):  # ops/_grad.py epilogue_target
+        if self._fstate is None or not self._epi_on or self._uses.get(id(p), 0) != 1:
+            return None
+        return self, self._index[id(p)]
+
+    def bias_epilogue(self, b):  # ops/_grad.py bias_epilogue
+        if self._fstate is None or not self._epi_on or id(b) not in self._index:
+            return None
+        return self, self._index[id(b)], None
+
+    def note_handed(self, p, t) -> None:  # ops/_grad.py hand_off: tracked in epilogue_gemm
+        pass
+
+    def epilogue_gemm(self, A, B, C, w, row0: int = 0, db=None, b=None) -> bool:
+        """C = A^T B (both MN-contiguous: the weight-gradient layout) for rows ``row0 ..`` of the
+        sharded weight ``w``, with SGD applied to those rows in the epilogue (and to the bias
+        ``b`` from the row sums ``db``). False: the plan had no epilogue, C / db hold the
+        gradient and ``optimizer.step()`` updates them."""
+        from .._native import native
+
+        buf, blk, g = self._fstate
+        a = self._arena
+        i = self._index[id(w)]
+        n = C.numel()
+        start = a.offsets[i] + row0 * C.shape[1]
+        bp = bb = None
+        if b is not None and db is not None:
+            j = self._index[id(b)]
+            bo = a.offsets[j]
+            bp = a.data[bo:bo + b.numel()]
+            bb = buf[bo:bo + b.numel()] if buf is not None else None
+        done = native().gemm_f32_sgd(A, B, C, False, False, a.data[start:start + n],
+                                     buf[start:start + n] if buf is not None else None, blk,
+                                     nesterov=g["nesterov"], maximize=g["maximize"], rowsum=db,
+                                     bias_p=bp, bias_buf=bb)
+        if done:
+            self._done[i] = self._done.get(i, 0) + n
+            if bp is not None:
+                self._done[j] = a.numels[j]
+        return done
+
+    def _fused_step(self, opt) -> None:
+        """``optimizer.step()`` with the fused optimizer: one flat update per run of arena
+        parameters no epilogue updated (gradients in their slots: sync_grads ran)."""
+        from .._native import native
+
+        if self._fstate is None:
+            self._begin_fused_step()
+        buf, blk, g = self._fstate
+        a = self._arena
+        spans = []
+        for i in range(len(a.params)):
+            done = self._done.get(i, 0)
+            if done == a.numels[i] or a.params[i].grad is None:
+                continue
+            if done:
+                raise RuntimeError("tensor-sharded fused optimizer: a weight was updated in part")
+            end = a.offsets[i + 1] if i + 1 < len(a.params) else a.numel
+            if spans and spans[-1][1] == a.offsets[i]:
+                spans[-1][1] = end
+            else:
+                spans.append([a.offsets[i], end])
+        C = native()
+        for lo, hi in spans:
+            C.sgd_flat(a.data[lo:hi], a.grad[lo:hi], buf[lo:hi] if buf is not None else None,
+                       g["lr"], g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"],
+                       g["maximize"], False, 1.0, hyper=blk)
+        self._fstate = None
+        self._done = {}
 
     def check_replicas(self) -> None:
         """Raise unless every rank holds bit-identical replicated parameters (collective)."""
@@ -597,11 +759,11 @@ class TensorParallelMLP(nn.Module):
 
 
 def rank_compute_ms(W: int, dims=(9216, 4096, 4096), classes: int = 10, B: int = 128,
-                    steps: int = 100, optim: str = "sgd", device=None) -> float:
+                    steps: int = 100, optim: str = "sgd", device=None, fused: bool = True) -> float:
     """Measured per-rank compute of the W-rank tensor-sharded step on THIS one GPU: rank 0's
     shard shapes, every collective replaced by its local copy (set_fake_world), the node's batch
-    gathered from a device dataset each step, SGD momentum (or Adam), captured and replayed as
-    bench.py runs it. The W-rank step is this plus its exposed collectives
+    gathered from a device dataset each step, SGD momentum (in the shards' GEMM epilogues unless
+    ``fused=False``; or Adam), captured and replayed as bench.py runs it. The W-rank step is this plus its exposed collectives
     (parallel/commmodel.py simulate_tensor). World size 1 only (no process group peers)."""
     import time
 
@@ -621,6 +783,8 @@ def rank_compute_ms(W: int, dims=(9216, 4096, 4096), classes: int = 10, B: int =
                                        num_classes=classes, device=dev), global_batch=True)
         opt = toptim.SGD(net.parameters(), lr=0.01, momentum=0.9) if optim == "sgd" else \
             toptim.Adam(net.parameters(), lr=1e-3)
+        if fused:
+            net.register_fused_optimizer(opt)  # as bench.py runs it (SGD only)
         n = max(4 * W * B, 1024)
         data = torch.randn(n, dims[0], device=dev)
         labels = torch.randint(0, classes, (n,), device=dev)
