@@ -45,6 +45,13 @@ def test_tensor_parallel_fused_optimizer_captured(tmp_path, world, chunks, bn):
         backend="nccl" if world == 1 else "peer")
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_tensor_parallel_gradient_accumulation(tmp_path, world):
+    """Two micro-batches per step (fused + no_sync, unfused, unfused + no_sync) == the torch
+    step of the full model on the summed global-batch gradients."""
+    run(TW.accumulation_parity, tmp_path, n=world)
+
+
 def _peer_bench(*args, diag=False):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     env.update(TDP_GPU_PEER="1")

@@ -1,6 +1,7 @@
 """Multi-rank workers for the tensor-sharded toy-MLP step (parallel/tensor_parallel.py) on
 CPU/gloo. Oracle: the one-process step of the FULL model on the node's batch (every rank's
 batch in rank order, mean loss) with torch.optim -- what DDP's averaged all-reduce computes."""
+import contextlib
 import copy
 
 import torch
@@ -209,4 +210,64 @@ def checkpoint_roundtrip(rank, out_dir):
     back = tp2.state_dict()
     for k in full:
         assert torch.equal(back[k], full[k]), k
+    tdp.destroy_process_group()
+
+
+def accumulation_parity(rank, out_dir, backend="peer", steps=3):
+    """GPU: gradient accumulation over two micro-batches, three ways -- the fused optimizer with
+    the first micro-batch under ``no_sync()``; unfused without no_sync (the first backward
+    all-reduces the replicated gradients early, the second waits for it and sync_grads reduces
+    the sum again; fc2's accumulated weight gradient is computed on the compute stream, where
+    autograd adds it); unfused with no_sync -- each == the torch step of the full model on the
+    summed global-batch gradients (r9an: before the fix of the aux-stream race, fc2.weight was
+    0.3-0.5 off)."""
+    import torch.nn as nn
+
+    tdp.init_process_group(backend)
+    W = rt.get_world_size()
+
+    def build(fused):
+        torch.manual_seed(0)
+        t = TensorParallelMLP(ToyMLP(device="cuda", **GDIMS))
+        o = tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        if fused:
+            assert t.register_fused_optimizer(o)
+        return t, o
+
+    torch.manual_seed(0)
+    full = ToyMLP(device="cuda", **GDIMS)
+    rsd = {k: v.clone() for k, v in full.state_dict().items()}
+    ref = nn.Sequential(nn.Linear(256, 128), nn.ReLU(), nn.Linear(128, 64), nn.ReLU(),
+                        nn.Linear(64, 10)).cuda()
+    keymap = {"0": "fc1", "2": "fc2", "4": "fc3"}
+    ref.load_state_dict({f"{i}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
+                         for k, v in rsd.items() if k.split(".")[0] == n}, strict=True)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    var = {"A fused+no_sync": (build(True), True), "B unfused": (build(False), False),
+           "C unfused+no_sync": (build(False), True)}
+    for step in range(steps):
+        for (t, o), ns in var.values():
+            o.zero_grad(set_to_none=True)
+            for micro in range(2):
+                xs, ys = zip(*[_gbatch(r, 2 * step + micro) for r in range(W)])
+                ctx = t.no_sync() if micro == 0 and ns else contextlib.nullcontext()
+                with ctx:
+                    tdp.ops.backward(tdp.ops.cross_entropy(t(xs[rank]), ys[rank]))
+            t.sync_grads()
+            o.step()
+        ropt.zero_grad()
+        for micro in range(2):
+            xs, ys = zip(*[_gbatch(r, 2 * step + micro) for r in range(W)])
+            F.cross_entropy(ref(torch.cat(xs)), torch.cat(ys)).backward()
+        ropt.step()
+    torch.cuda.synchronize()
+    want = {f"{n}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
+            for k, v in ref.state_dict().items() if k.split(".")[0] == i}
+    for name, ((t, o), ns) in var.items():
+        got = t.full_state_dict()
+        for k, v in want.items():
+            torch.testing.assert_close(got[k].float(), v.float(), atol=5e-5, rtol=1e-3,
+                                       msg=lambda m: f"{name} {k}: {m}")
+        t.check_replicas()
+    rt.barrier()
     tdp.destroy_process_group()

@@ -262,7 +262,10 @@ class _RowParallelOverlap(torch.autograd.Function):
             else:
                 C.gemm_f32(dp[c], h1, out, False, False)
         if dw2 is not None:
-            if aux is not None:
+            if aux is not None and w2.grad is None:
+                # (only into W2's arena slot: a fresh gradient tensor -- accumulation -- goes
+                # straight to autograd's AccumulateGrad on the compute stream, so it is computed
+                # there)
                 # dW2[rows of chunk c] = dP_c^T . H1 on the aux stream, released only once dH1
                 # is done: it then runs beside fc1's weight-gradient GEMM (next on the compute
                 # stream, fewer tiles than slots) instead of competing with dH1 for the CUs
@@ -442,9 +445,18 @@ class TensorParallelMLP(nn.Module):
     def forward(self, x):
         # every replicated gradient is empty: this backward writes them into their arena slots
         # (ops/_grad.py grad_dest), so the backward may all-reduce the slots early
-        self._fresh = all(q.grad is None for q in self._replicated)
+        ev = self._reduced
+        if ev is not None:
+            # an earlier backward of this accumulation already all-reduced its replicated
+            # gradients (on the communication stream): order this pass's accumulation after it;
+            # sync_grads then reduces the sum again (averaging averaged values is exact)
+            torch.cuda.current_stream().wait_event(ev)
+            self._reduced = None
+        self._fresh = self._epi_on and all(q.grad is None for q in self._replicated)
         if self._fopt is not None and torch.is_grad_enabled() and self.training:
-            self._begin_fused_step()
+            if self._fstate is None:  # once per optimizer step (accumulation: several forwards)
+                self._begin_fused_step()
+            self._uses = {}
         x = x.reshape(x.shape[0], -1)
         X = x if (self.world == 1 or self.global_batch) else _GatherRows.apply(x)
         h = self.fc1(X)
@@ -533,8 +545,8 @@ class TensorParallelMLP(nn.Module):
         size, where DDP can do it at world size 1 only (parallel/ddp.py register_fused_optimizer).
         ``optimizer.step()`` then updates what no epilogue did: the replicated parameters after
         their all-reduce, BatchNorm shards, a weight whose GEMM plan has no epilogue. Saves the
-        gradient's HBM write and re-read and the separate update pass (profiles/r9: 0.386 ->
-        see tp_fused_r9*.md). tdp SGD, one parameter group over ``parameters()``, GPU; returns
+        gradient's HBM write and re-read and the separate update pass (per-rank compute at W = 2:
+        391 -> 342 us, profiles/r9/tp_fused_r9ak.md). tdp SGD, one parameter group over ``parameters()``, GPU; returns
         False and changes nothing otherwise. Each backward applies the update: run the earlier
         passes of a gradient accumulation under ``no_sync()``."""
         from ..optim.fused import SGD
@@ -555,9 +567,10 @@ class TensorParallelMLP(nn.Module):
 
     @contextlib.contextmanager
     def no_sync(self):
-        """Backward passes inside store their gradients (accumulated by autograd) instead of
-        applying the update; the pass after it -- whose gradients then accumulate too -- leaves
-        every update to ``optimizer.step()``."""
+        """Gradient accumulation (DDP.no_sync): backward passes inside neither all-reduce the
+        replicated gradients early nor apply the fused update -- they store their gradients,
+        which autograd accumulates; the pass after it accumulates too and leaves the whole update
+        to ``sync_grads()`` + ``optimizer.step()``."""
         prev, self._epi_on = self._epi_on, False
         try:
             yield
@@ -584,7 +597,6 @@ class TensorParallelMLP(nn.Module):
             blk = opt.hyper_block(0, device=self.fc1.weight.device, first=fresh)
         native().opt_step_begin(blk, 1)
         self._fstate = (buf, blk, g)
-        self._uses = {}
         self._done = {}
 
     def _note_use(self, p) -> None:  # ops/_grad.py note_use
