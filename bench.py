@@ -359,6 +359,9 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
                                                         rank_us=ms * 1000.0, chunks=2)
                                      ["step_us"] / 1000.0, 4)
             out["tensor_rank_compute_ms"] = rk
+            # the rehearsal of the execution --parallel auto can pick at N > 1 (per-rank compute
+            # of the tensor-sharded step over dp1; the DDP schedule's is rehearsal_over_dp1)
+            out["tensor_rank_over_dp1"] = {k: round(v / step_ms, 4) for k, v in rk.items()}
             out["tensor_predicted_step_ms"] = pred
             out["tensor_predicted_eff"] = {k: round(step_ms / v, 3) for k, v in pred.items()}
     return out
