@@ -353,7 +353,8 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
                 (9216, 4096, 4096)
             rk, pred = {}, {}
             for W in (2, 8):
-                ms = rank_compute_ms(W, dims=dims, B=a.batch, steps=n, optim=a.optim)
+                # (>= 200 replays: a 20-step window read 4-7 % high against the proxy's)
+                ms = rank_compute_ms(W, dims=dims, B=a.batch, steps=max(n, 200), optim=a.optim)
                 rk[str(W)] = round(ms, 4)
                 pred[str(W)] = round(cm.simulate_tensor(W, B=a.batch, dims=dims,
                                                         rank_us=ms * 1000.0, chunks=2)
