@@ -42,3 +42,11 @@ def test_tensor_parallel_adam_matches_global_batch(tmp_path):
 
 def test_tensor_parallel_checkpoint_is_the_full_models(tmp_path):
     run(TW.checkpoint_roundtrip, tmp_path, n=2)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tensor_parallel_gradient_accumulation_cpu(tmp_path, world):
+    """Two micro-batches per step through the wrapper (with and without no_sync; the fused
+    optimizer is GPU-only and refuses here) == the torch step on the summed global-batch
+    gradients."""
+    run(TW.accumulation_parity, tmp_path, n=world, backend="gloo", device="cpu")

@@ -98,10 +98,10 @@ GDIMS = dict(in_features=256, hidden=(128, 64), num_classes=10)
 GB = 16
 
 
-def _gbatch(r, step):
+def _gbatch(r, step, device="cuda"):
     g = torch.Generator().manual_seed(77 * step + r)
-    return (torch.randn(GB, 256, generator=g) * (1 + 0.5 * r)).cuda(), \
-        torch.randint(0, 10, (GB,), generator=g).cuda()
+    return (torch.randn(GB, 256, generator=g) * (1 + 0.5 * r)).to(device), \
+        torch.randint(0, 10, (GB,), generator=g).to(device)
 
 
 def captured_parity(rank, out_dir, backend="peer", bn=False, steps=5, chunks=1, fused=False):
@@ -213,7 +213,7 @@ def checkpoint_roundtrip(rank, out_dir):
     tdp.destroy_process_group()
 
 
-def accumulation_parity(rank, out_dir, backend="peer", steps=3):
+def accumulation_parity(rank, out_dir, backend="peer", steps=3, device="cuda"):
     """GPU: gradient accumulation over two micro-batches, three ways -- the fused optimizer with
     the first micro-batch under ``no_sync()``; unfused without no_sync (the first backward
     all-reduces the replicated gradients early, the second waits for it and sync_grads reduces
@@ -228,17 +228,17 @@ def accumulation_parity(rank, out_dir, backend="peer", steps=3):
 
     def build(fused):
         torch.manual_seed(0)
-        t = TensorParallelMLP(ToyMLP(device="cuda", **GDIMS))
+        t = TensorParallelMLP(ToyMLP(device=device, **GDIMS))
         o = tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
         if fused:
-            assert t.register_fused_optimizer(o)
+            assert t.register_fused_optimizer(o) == (device != "cpu")
         return t, o
 
     torch.manual_seed(0)
-    full = ToyMLP(device="cuda", **GDIMS)
+    full = ToyMLP(device=device, **GDIMS)
     rsd = {k: v.clone() for k, v in full.state_dict().items()}
     ref = nn.Sequential(nn.Linear(256, 128), nn.ReLU(), nn.Linear(128, 64), nn.ReLU(),
-                        nn.Linear(64, 10)).cuda()
+                        nn.Linear(64, 10)).to(device)
     keymap = {"0": "fc1", "2": "fc2", "4": "fc3"}
     ref.load_state_dict({f"{i}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
                          for k, v in rsd.items() if k.split(".")[0] == n}, strict=True)
@@ -249,7 +249,7 @@ def accumulation_parity(rank, out_dir, backend="peer", steps=3):
         for (t, o), ns in var.values():
             o.zero_grad(set_to_none=True)
             for micro in range(2):
-                xs, ys = zip(*[_gbatch(r, 2 * step + micro) for r in range(W)])
+                xs, ys = zip(*[_gbatch(r, 2 * step + micro, device) for r in range(W)])
                 ctx = t.no_sync() if micro == 0 and ns else contextlib.nullcontext()
                 with ctx:
                     tdp.ops.backward(tdp.ops.cross_entropy(t(xs[rank]), ys[rank]))
@@ -257,10 +257,11 @@ def accumulation_parity(rank, out_dir, backend="peer", steps=3):
             o.step()
         ropt.zero_grad()
         for micro in range(2):
-            xs, ys = zip(*[_gbatch(r, 2 * step + micro) for r in range(W)])
+            xs, ys = zip(*[_gbatch(r, 2 * step + micro, device) for r in range(W)])
             F.cross_entropy(ref(torch.cat(xs)), torch.cat(ys)).backward()
         ropt.step()
-    torch.cuda.synchronize()
+    if device != "cpu":
+        torch.cuda.synchronize()
     want = {f"{n}.{k.split('.', 1)[1]}": v for i, n in keymap.items()
             for k, v in ref.state_dict().items() if k.split(".")[0] == i}
     for name, ((t, o), ns) in var.items():
