@@ -122,12 +122,14 @@ def parse():
                          "the optimizer's HBM traffic); with world_size 1 in the weight-gradient "
                          "GEMM epilogues (no gradient write/re-read). auto = on")
     ap.add_argument("--no-fused-opt", action="store_true", help="alias of --fused-opt off")
-    ap.add_argument("--parallel", choices=["auto", "ddp", "tensor"], default="auto",
-                    help="N > 1 toy MLP: 'tensor' = the tensor-sharded step "
-                         "(parallel/tensor_parallel.py: activations cross xGMI, not weights), "
-                         "'ddp' = the DDP reducer's ladder, 'auto' = time both, keep the faster")
+    ap.add_argument("--parallel", choices=["ddp", "auto", "tensor"], default="ddp",
+                    help="N > 1 toy MLP: 'ddp' (default, the headline) = the DDP reducer's "
+                         "ladder, recorded as dp{N}; 'tensor' = the tensor-sharded step "
+                         "(parallel/tensor_parallel.py: activations cross xGMI, not weights; not "
+                         "DDP), recorded as tp{N}; 'auto' = the DDP headline plus the "
+                         "tensor-sharded variants' timings as side numbers in config.selection")
     ap.add_argument("--select-steps", type=int, default=20,
-                    help="timed steps per candidate of --parallel auto")
+                    help="timed steps per candidate of --parallel tensor / auto")
     ap.add_argument("--comm-cus", type=int, default=None,
                     help="CUs left to RCCL: grid-sized kernels (persistent GEMMs, split-K "
                          "planners) plan for (CUs - N) (TDP_COMM_CUS; default 0)")
@@ -468,7 +470,7 @@ def self_launch(a) -> int:
     try:
         rec = json.loads(lines[-1])
         want_n = n if not a.cpu else 0
-        ok = rec["n_gpus"] == want_n and rec["config"]["parallelism"] == f"dp{n}"
+        ok = rec["n_gpus"] == want_n and rec["config"]["parallelism"] in (f"dp{n}", f"tp{n}")
     except Exception:  # noqa: BLE001 - anything unparsable is a malformed record
         ok, rec = False, None
     if not ok:
@@ -510,9 +512,9 @@ LADDER = (
 )
 
 
-# The tensor-sharded step (parallel/tensor_parallel.py): tried before the ladder at N > 1 for the
-# toy MLP; with --parallel auto both it and the ladder's first working rung are timed, the faster
-# one is measured.
+# The tensor-sharded step (parallel/tensor_parallel.py), opt-in: with --parallel tensor the faster
+# of these is measured and recorded as tp{N} (it is not DDP: SURVEY.md section 2.4 lists DDP as
+# the reference's only strategy); with --parallel auto they are timed as side numbers only.
 TENSOR_RUNGS = (
     {"name": "tensor-sharded", "factor": None, "fused": True, "graph": True, "tensor": 1},
     # fc2's reduce-scatter / all-gather in column chunks behind the chunk GEMMs
@@ -984,9 +986,17 @@ def main():
             rt.all_reduce(t, "max")
             return float(t.item()) * 1000.0 / n
 
+        def free_job():
+            gc.collect()
+            if use_gpu:
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+
         tensor_job, selection = None, None
         if world > 1 and a.parallel != "ddp" and a.model == "toy_mlp" and a.api == "ddp":
-            # every tensor-sharded variant that builds is timed; the fastest is kept
+            # every tensor-sharded variant that builds is timed (same replay form as the timed
+            # region: step.many); --parallel tensor measures the fastest, --parallel auto only
+            # records their timings next to the DDP headline
             selection = {}
             for tcfg in TENSOR_RUNGS:
                 ok, err, tj = True, None, None
@@ -1005,21 +1015,22 @@ def main():
                     tj = None
                 else:
                     selection[f"{tcfg['name']}_ms"] = round(timed_ms(tj, a.select_steps), 4)
-                    if tensor_job is None or selection[f"{tcfg['name']}_ms"] < \
-                            selection[f"{tensor_job.rung}_ms"]:
-                        tensor_job = tj
+                    if a.parallel == "tensor" and (tensor_job is None or
+                                                   selection[f"{tcfg['name']}_ms"] <
+                                                   selection[f"{tensor_job.rung}_ms"]):
+                        tensor_job = tj  # the previous best (if any) is released here
                     tj = None
-                gc.collect()
-                if use_gpu:
-                    torch.cuda.synchronize()
-                    torch.cuda.empty_cache()
+                free_job()
+        # --parallel auto / ddp: the headline is ALWAYS the DDP reducer's step (BASELINE metric
+        # "toy-MLP DDP"); no tensor-sharded job survives into the ladder
         rungs = LADDER if world > 1 or os.environ.get("TDP_BENCH_LADDER") == "1" else LADDER[:1]
-        if tensor_job is not None and a.parallel == "tensor":
+        if tensor_job is not None:
             rungs = ()
             job = tensor_job
             selection["chosen"] = job.rung
-        elif tensor_job is None:
-            selection = None
+        elif selection is not None and a.parallel == "tensor":
+            fallbacks.append("--parallel tensor: no tensor-sharded variant built; measured the "
+                             "DDP ladder instead")
         for attempt, cfg in enumerate(rungs):
             ok, err = True, None
             try:
@@ -1041,26 +1052,21 @@ def main():
             print(f"[bench] rung {cfg['name']} failed on some rank: {err!r}", file=sys.stderr,
                   flush=True)
             job = None
-            gc.collect()
-            if use_gpu:
-                torch.cuda.synchronize()
-                torch.cuda.empty_cache()
+            free_job()
         else:
-            if rungs and tensor_job is None:
+            if rungs:
                 print("[bench] every rung of the fallback ladder failed: no timed step ran",
                       file=sys.stderr, flush=True)
                 sys.exit(1)
-            job = tensor_job if job is None else job
-        if selection is not None and job is not tensor_job:
+        if selection is not None and job.tp is None:
+            # auto: the DDP rung's own selection-form timing beside the tensor side numbers
             selection[f"{job.rung}_ms"] = round(timed_ms(job, a.select_steps), 4)
-            if selection[f"{tensor_job.rung}_ms"] < selection[f"{job.rung}_ms"]:
-                job = tensor_job
             selection["chosen"] = job.rung
-            # the loser's graphs and buffers go before the timed run
-            gc.collect()
-            if use_gpu:
-                torch.cuda.synchronize()
-                torch.cuda.empty_cache()
+        if selection is not None and job.tp is not None:
+            # the chosen tensor job was timed before the other candidates were built: bring it
+            # back to its warm state before the timed region
+            job.step.many(a.warmup)
+            sync()
         tensor_job = None
         ddp, opt, fused, step, run, graph = (job.ddp, job.opt, job.fused, job.step, job.run,
                                              job.graph)
@@ -1127,10 +1133,25 @@ def main():
     if a.impl == "tdp" and rt.comm() is not None:
         comm_nranks = int(rt.comm().nranks)
 
+    sel_ms = sel_warn = None
+    if a.impl == "tdp" and selection and f"{rung}_ms" in selection:
+        sel_ms = selection[f"{rung}_ms"]
+        if abs(sel_ms - ms) > 0.2 * ms:
+            sel_warn = (f"the selection clock ({sel_ms:.4f} ms) and the timed region "
+                        f"({ms:.4f} ms) differ by more than 20 %")
+            print(f"[bench] warning: {sel_warn}", file=sys.stderr, flush=True)
+
     def record(diag):
         desc = MODEL_DESC[a.model].format(s=a.image_size, dims="-".join(map(str, dims + (10,))),
                                           bn=", +SyncBatchNorm" if a.syncbn else "")
-        if a.impl == "tdp":
+        tensor = a.impl == "tdp" and getattr(job, "tp", None) is not None
+        if tensor:
+            # not DDP: Megatron-style column/row-sharded fc1/fc2 (parallel/tensor_parallel.py),
+            # labelled tp{N} so it is never read as the DDP headline
+            impl = ("tdp tensor-sharded execution (column-parallel fc1, row-parallel fc2, "
+                    f"replicated head; execution '{rung}'" +
+                    (", hipGraph step)" if graph else ", eager)"))
+        elif a.impl == "tdp":
             impl = "tdp (native gfx950 kernels + RCCL reducer" + \
                 (", hipGraph step)" if graph else ", eager)")
             if a.api == "accelerate":
@@ -1138,7 +1159,8 @@ def main():
         else:
             impl = "stock torch DDP + torch.optim"
         rec = {
-            "metric": metric,
+            "metric": metric if not tensor else
+            "samples/sec (whole node) toy-MLP tensor-sharded (not DDP) at N MI355X",
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": world if use_gpu else 0,
@@ -1154,7 +1176,7 @@ def main():
                 "model": desc,
                 "global_batch": a.batch * world,
                 "seq_len": None,
-                "parallelism": f"dp{world}",
+                "parallelism": f"{'tp' if tensor else 'dp'}{world}",
                 "impl": impl,
                 "optimizer": a.optim + ((" (shards: fused into their weight-gradient GEMMs)"
                                          if job.tp is not None else
@@ -1175,8 +1197,11 @@ def main():
                 # the fallback ladder (LADDER): the rung that ran and what failed before it
                 "rung": rung,
                 "fallbacks": fallbacks,
-                # --parallel auto at N > 1: ms/step of each candidate, and the one measured
+                # --parallel tensor / auto at N > 1: ms/step of each candidate (same replay
+                # form as the timed region) and the one measured (auto: always the DDP rung)
                 "selection": selection if a.impl == "tdp" else None,
+                "selection_ms": sel_ms,
+                "selection_gap_warning": sel_warn,
                 "baseline": {"samples_per_s": round(base, 2), "source": base_src}
                 if base else None,
             },

@@ -176,33 +176,56 @@ def test_bench_clean_run_reports_no_fallback():
     assert rec["config"]["rung"] == "full" and rec["config"]["fallbacks"] == []
 
 
-def test_bench_parallel_auto_times_both_and_records_the_choice():
-    """--parallel auto (the default) at N > 1: the tensor-sharded step and the DDP ladder's
-    first working rung are both timed; the faster one is measured and the record says so."""
-    r = _bench_cpu2({}, "--select-steps", "2")
+LADDER_NAMES = ("full", "sharded-buckets", "allreduce+optimizer.step", "eager-allreduce")
+
+
+def test_bench_default_is_the_ddp_headline():
+    """with no --parallel flag the N > 1 record is the DDP reducer's step,
+    labelled dp{N}, and no tensor-sharded candidate is built or timed."""
+    r = _bench_cpu2({})
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
+    assert c["parallelism"] == "dp2" and c["rung"] in LADDER_NAMES, c
+    assert c["selection"] is None and c["bucket_mb"], c
+    assert "tensor" not in c["impl"], c
+
+
+def test_bench_parallel_auto_keeps_the_ddp_headline():
+    """--parallel auto at N > 1: the tensor-sharded variants are timed as SIDE numbers; the
+    measured value is always the DDP rung's, recorded as dp{N}."""
+    r = _bench_cpu2({}, "--select-steps", "2", "--parallel", "auto")
     assert r.returncode == 0, r.stderr[-3000:]
     c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
     sel = c["selection"]
     assert set(sel) == {"tensor-sharded_ms", "tensor-overlap_ms", "full_ms", "chosen"}, sel
-    fast = min(("tensor-sharded", "tensor-overlap", "full"), key=lambda k: sel[k + "_ms"])
-    assert sel["chosen"] == fast == c["rung"], c
+    assert sel["chosen"] == "full" == c["rung"] and c["parallelism"] == "dp2", c
+    assert c["selection_ms"] == sel["full_ms"], c
     assert c["sync"]["replicas_identical"] is True, c["sync"]
 
 
-def test_bench_parallel_tensor_runs_the_sharded_step():
+def test_bench_parallel_tensor_is_labelled_tp():
     r = _bench_cpu2({}, "--parallel", "tensor")
     assert r.returncode == 0, r.stderr[-3000:]
-    c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    c = rec["config"]
     assert c["rung"] in ("tensor-sharded", "tensor-overlap"), c
-    assert c["selection"]["chosen"] == c["rung"], c
-    assert c["sync"]["modes"]["fc1"] == "column-sharded" and c["parallelism"] == "dp2"
+    assert c["selection"]["chosen"] == c["rung"] and c["selection_ms"] > 0, c
+    assert c["parallelism"] == "tp2" and "tensor-sharded" in c["impl"], c
+    assert "DDP" not in rec["metric"].replace("not DDP", ""), rec["metric"]
+    assert c["sync"]["modes"]["fc1"] == "column-sharded" and c["bucket_mb"] is None
     assert c["sync"]["replicas_identical"] is True
 
 
-def test_bench_parallel_auto_survives_an_exhausted_ladder():
-    """Every DDP rung fails its warm-up: the tensor-sharded step (built first) still yields the
-    number."""
-    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"})
+def test_bench_parallel_tensor_ignores_the_ladder():
+    """--parallel tensor never builds the DDP ladder: a ladder-wide fault does not touch it."""
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"}, "--parallel", "tensor")
     assert r.returncode == 0, r.stderr[-3000:]
     c = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])["config"]
-    assert c["rung"].startswith("tensor-") and len(c["fallbacks"]) == 4, c
+    assert c["rung"].startswith("tensor-") and c["fallbacks"] == [], c
+
+
+def test_bench_parallel_auto_needs_a_ddp_rung():
+    """auto never falls back to the tensor-sharded step for its headline."""
+    r = _bench_cpu2({"TDP_BENCH_FAULT": "warmup@*"}, "--parallel", "auto", "--select-steps", "1")
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert "every rung of the fallback ladder failed" in r.stderr

@@ -97,6 +97,7 @@ def test_rccl_bench_tensor_record(world):
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     c = rec["config"]
     assert rec["n_gpus"] == world and c["comm_nranks"] == world, c
+    assert c["parallelism"] == f"tp{world}", c
     assert c["rung"].startswith("tensor-") and c["fallbacks"] == [], c
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
 
@@ -104,8 +105,10 @@ def test_rccl_bench_tensor_record(world):
 @pytest.mark.parametrize("world", WORLDS)
 def test_rccl_bench_record(world):
     """``python bench.py --gpus N`` on N real GPUs: one valid record, captured, replicas
-    bit-identical, RCCL saw N ranks, no fallback taken (``--parallel auto``: whichever of the
-    tensor-sharded and DDP executions timed faster)."""
+    bit-identical, RCCL saw N ranks, no fallback taken; the default execution is the DDP
+    reducer's ladder (labelled dp{N}), never the tensor-sharded step."""
+    from bench import LADDER
+
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "TDP_GPU_PEER", "TDP_GPU_RELAY")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "6",
@@ -116,6 +119,7 @@ def test_rccl_bench_record(world):
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     c = rec["config"]
     assert rec["n_gpus"] == world and c["parallelism"] == f"dp{world}"
+    assert c["rung"] in [r["name"] for r in LADDER] and c["bucket_mb"], c
     assert c["comm_nranks"] == world and c["sync"]["backend"] == "rccl"
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
     assert c["fallbacks"] == [], c["fallbacks"]

@@ -66,13 +66,24 @@ def _peer_bench(*args, diag=False):
 def test_bench_tensor_sharded_step_captured():
     c = _peer_bench("--parallel", "tensor")["config"]
     assert c["rung"].startswith("tensor-") and c["fallbacks"] == [], c
+    assert c["parallelism"] == "tp2", c
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
 
 
 def test_bench_parallel_auto_records_selection():
-    c = _peer_bench("--select-steps", "4")["config"]
+    c = _peer_bench("--select-steps", "4", "--parallel", "auto")["config"]
     sel = c["selection"]
-    assert sel is not None and sel["chosen"] == c["rung"], c
+    # auto: tensor timings are side numbers, the DDP rung is measured
+    assert sel is not None and sel["chosen"] == c["rung"] == "full", c
+    assert c["parallelism"] == "dp2" and "tensor-sharded_ms" in sel, c
+    assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
+
+
+def test_bench_default_is_ddp_on_the_peer_vehicle():
+    """``TDP_GPU_PEER=1 python bench.py --gpus 2`` with no --parallel flag
+    measures the DDP ladder's full rung and says dp2."""
+    c = _peer_bench()["config"]
+    assert c["parallelism"] == "dp2" and c["rung"] == "full" and c["selection"] is None, c
     assert c["sync"]["captured"] is True and c["sync"]["replicas_identical"] is True, c["sync"]
 
 
