@@ -50,3 +50,9 @@ def test_tensor_parallel_gradient_accumulation_cpu(tmp_path, world):
     optimizer is GPU-only and refuses here) == the torch step on the summed global-batch
     gradients."""
     run(TW.accumulation_parity, tmp_path, n=world, backend="gloo", device="cpu")
+
+
+@pytest.mark.parametrize("kind,bn", [("sgd", False), ("adam", False), ("sgd", True)])
+def test_tensor_parallel_resume_is_bitwise(tmp_path, kind, bn):
+    """3 steps, save, resume into a fresh job, 2 steps == 5 uninterrupted steps (gloo, W=2)."""
+    run(TW.resume_parity, tmp_path, n=2, kind=kind, bn=bn)

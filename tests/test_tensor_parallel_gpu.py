@@ -52,6 +52,12 @@ def test_tensor_parallel_gradient_accumulation(tmp_path, world):
     run(TW.accumulation_parity, tmp_path, n=world)
 
 
+def test_tensor_parallel_accumulation_waits_for_a_late_aux_stream(tmp_path):
+    """with the aux stream held back by a long kernel, the second
+    micro-batch's accumulation into fc2's weight gradient still sees the first pass's value."""
+    run(TW.accumulation_parity, tmp_path, n=2, delay_aux=True)
+
+
 def _peer_bench(*args, diag=False):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     env.update(TDP_GPU_PEER="1")

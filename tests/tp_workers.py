@@ -200,6 +200,10 @@ def checkpoint_roundtrip(rank, out_dir):
     path = save_ddp_checkpoint(tp, out_dir, 0)
     assert os.path.exists(path)
     full = tp.state_dict()
+    # the DDP key contract (REF/multi-GPU-training-torch.py:221): "module."-prefixed keys that a
+    # DDP-wrapped ToyMLP loads with load_state_dict as they are
+    raw = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(raw) == {f"module.{k}" for k in full}, sorted(raw)
     plain = ToyMLP(**DIMS)
     load_checkpoint(plain, path)
     for k, v in plain.state_dict().items():
@@ -213,7 +217,7 @@ def checkpoint_roundtrip(rank, out_dir):
     tdp.destroy_process_group()
 
 
-def accumulation_parity(rank, out_dir, backend="peer", steps=3, device="cuda"):
+def accumulation_parity(rank, out_dir, backend="peer", steps=3, device="cuda", delay_aux=False):
     """GPU: gradient accumulation over two micro-batches, three ways -- the fused optimizer with
     the first micro-batch under ``no_sync()``; unfused without no_sync (the first backward
     all-reduces the replicated gradients early, the second waits for it and sync_grads reduces
@@ -251,6 +255,15 @@ def accumulation_parity(rank, out_dir, backend="peer", steps=3, device="cuda"):
             for micro in range(2):
                 xs, ys = zip(*[_gbatch(r, 2 * step + micro, device) for r in range(W)])
                 ctx = t.no_sync() if micro == 0 and ns else contextlib.nullcontext()
+                if delay_aux and micro == 0 and t.aux_stream() is not None:
+                    # a long kernel queued on the aux stream makes the first pass's
+                    # fc2 weight gradient land late; the second pass's accumulation must wait
+                    # for it (without the forward's wait it read the slot before the write)
+                    big = torch.randn(2048, 2048, device=device)
+                    with torch.cuda.stream(t.aux_stream()):
+                        for _ in range(24):
+                            big = big @ big
+                            big = big / big.abs().max()
                 with ctx:
                     tdp.ops.backward(tdp.ops.cross_entropy(t(xs[rank]), ys[rank]))
             t.sync_grads()
@@ -271,4 +284,63 @@ def accumulation_parity(rank, out_dir, backend="peer", steps=3, device="cuda"):
                                        msg=lambda m: f"{name} {k}: {m}")
         t.check_replicas()
     rt.barrier()
+    tdp.destroy_process_group()
+
+
+def resume_parity(rank, out_dir, kind="sgd", bn=False):
+    """train 3 steps, save_training_state, resume into a FRESH wrapper and
+    optimizer (different init), 2 more steps == 5 uninterrupted steps, bitwise, on every rank;
+    the saved optimizer state is the full model's (every rank's momentum / moment slices), and
+    save_model_safetensors of the sharded model completes (a collective every rank joins)."""
+    import os
+
+    from tutorial_torch_distributed_data_parallel_amd.utils.checkpoint import (
+        load_training_state, save_model_safetensors, save_training_state)
+
+    tdp.init_process_group("gloo")
+    W = rt.get_world_size()
+
+    def build(seed):
+        torch.manual_seed(seed)
+        m = ToyMLP(batchnorm=bn, **DIMS)
+        if bn:
+            m = tdp.nn.convert_sync_batchnorm(m)
+        t = TensorParallelMLP(m)
+        o = (tdp.optim.SGD(t.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-3)
+             if kind == "sgd" else tdp.optim.Adam(t.parameters(), lr=1e-2, weight_decay=1e-3))
+        return t, o
+
+    def train(t, o, steps):
+        for step in steps:
+            x, y = _batch(rank, step)
+            o.zero_grad()
+            tdp.ops.cross_entropy(t(x), y).backward()
+            t.sync_grads()
+            o.step()
+
+    ta, oa = build(0)
+    train(ta, oa, range(5))
+    tb, ob = build(0)
+    train(tb, ob, range(3))
+    path = os.path.join(out_dir, "state.pt")
+    save_training_state(path, tb, ob, epoch=3)
+    sf = save_model_safetensors(tb, out_dir)
+    rt.barrier()
+    assert os.path.exists(sf)
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    full = obj["optimizer"]
+    key = "momentum_buffer" if kind == "sgd" else "exp_avg"
+    # state index 0 = fc1.weight in the full layout: all W row slices present, not one
+    assert full["state"][0][key].shape == ta.full_state_dict()["fc1.weight"].shape
+    tc, oc = build(123)  # a fresh job with different weights
+    load_training_state(path, tc, oc)
+    train(tc, oc, range(3, 5))
+    for (n, a), (_, c) in zip(ta.named_parameters(), tc.named_parameters()):
+        assert torch.equal(a, c), f"rank {rank} W={W} {kind}: {n} differs after resume " \
+                                  f"(max {float((a - c).abs().max())})"
+    for qa, qc in zip(ta.parameters(), tc.parameters()):
+        sa, sc = oa.state[qa], oc.state[qc]
+        for k, v in sa.items():
+            if torch.is_tensor(v) and v.dim():
+                assert torch.equal(v, sc[k]), (kind, k)
     tdp.destroy_process_group()

@@ -452,6 +452,11 @@ class TensorParallelMLP(nn.Module):
             # sync_grads then reduces the sum again (averaging averaged values is exact)
             torch.cuda.current_stream().wait_event(ev)
             self._reduced = None
+        if self._aux_done is not None:
+            # an earlier backward of this accumulation computed fc2's weight gradient on the
+            # aux stream; this pass's AccumulateGrad adds into it on the compute stream, so
+            # the compute stream waits for it (the event stays for sync_grads)
+            torch.cuda.current_stream().wait_event(self._aux_done)
         self._fresh = self._epi_on and all(q.grad is None for q in self._replicated)
         if self._fopt is not None and torch.is_grad_enabled() and self.training:
             if self._fstate is None:  # once per optimizer step (accumulation: several forwards)
@@ -526,14 +531,18 @@ class TensorParallelMLP(nn.Module):
         # the compute stream is ordered after every side-stream read of these (the gathered
         # event, or the join above): their memory may be reused from here on
         self._keep.clear()
+        late = False  # a replicated gradient that was not in its slot at the early all-reduce
         with torch.no_grad():
             for i, q in enumerate(a.params):
                 if q.grad is not None and not a.is_arena_grad(i):
                     g = a.grad_view(i)
                     g.copy_(q.grad)
                     q.grad = g
-        if self.world == 1 or _FAKE_WORLD or ev is not None:
+                    late = late or a.offsets[i] < self._rep_end
+        if self.world == 1 or _FAKE_WORLD or (ev is not None and not late):
             return
+        # (after an early all-reduce: averaging the already-averaged slots again leaves every
+        # rank with identical values, and the late gradient gets its average)
         runtime.all_reduce(a.grad[: self._rep_end], "avg")
 
     # ------------------------------------------------------------------ fused optimizer
@@ -768,6 +777,89 @@ class TensorParallelMLP(nn.Module):
                                           if k.startswith(b2n + ".")})
             self.fc3.load_state_dict({k[len(n3) + 1:]: v for k, v in sd.items()
                                       if k.startswith(n3 + ".")})
+
+    # ------------------------------------------------- optimizer state in the full layout
+    def _full_params(self):
+        """[(full ToyMLP parameter name, this rank's parameter, layout)] in the full model's
+        parameters() order; layout "rows" / "cols": this rank holds rows / columns
+        [rank*s, (rank+1)*s) of the full tensor, "rep": the whole tensor (replicated)."""
+        n1, n2, n3 = self._names
+        b1n, b2n = self._bn_names
+        out = [(f"{n1}.weight", self.fc1.weight, "rows")]
+        if self.fc1.bias is not None:
+            out.append((f"{n1}.bias", self.fc1.bias, "rows"))
+        if self.bn1 is not None and self.bn1.weight is not None:
+            out += [(f"{b1n}.weight", self.bn1.weight, "rows"),
+                    (f"{b1n}.bias", self.bn1.bias, "rows")]
+        out.append((f"{n2}.weight", self.fc2.weight, "cols"))
+        if self.b2 is not None:
+            out.append((f"{n2}.bias", self.b2, "rep"))
+        if self.bn2 is not None and self.bn2.weight is not None:
+            out += [(f"{b2n}.weight", self.bn2.weight, "rep"),
+                    (f"{b2n}.bias", self.bn2.bias, "rep")]
+        out += [(f"{n3}.{k}", q, "rep") for k, q in self.fc3.named_parameters()]
+        return out
+
+    def full_optim_state_dict(self, optimizer) -> dict:
+        """``optimizer.state_dict()`` in the layout of an optimizer over the FULL ToyMLP's
+        ``parameters()`` (collective: every rank must call it): each sharded state tensor
+        (momentum, Adam's moments) is all-gathered from the ranks' slices the way
+        ``full_state_dict`` gathers the weights, so a resumed job -- sharded at any W, or a DDP
+        job -- gets the whole state, not rank 0's shard."""
+        if len(optimizer.param_groups) != 1:
+            raise ValueError("full_optim_state_dict: one parameter group over parameters()")
+        local = optimizer.state_dict()
+        order = optimizer.param_groups[0]["params"]
+        pos = {id(q): i for i, q in enumerate(order)}
+        full_state = {}
+        for j, (_, q, how) in enumerate(self._full_params()):
+            st = local["state"].get(pos[id(q)])
+            # the same parameters have state on every rank (one group, same steps)
+            if st is None:
+                continue
+            ent = {}
+            for k, v in st.items():
+                if not torch.is_tensor(v) or v.shape != q.shape or how == "rep":
+                    ent[k] = v.detach().clone() if torch.is_tensor(v) else v
+                elif how == "rows":
+                    ent[k] = self._gather_rows(v)
+                else:
+                    ent[k] = self._gather_rows(v.t().contiguous()).t().contiguous()
+            full_state[j] = ent
+        group = {k: v for k, v in local["param_groups"][0].items() if k != "params"}
+        group["params"] = list(range(len(self._full_params())))
+        return {"state": full_state, "param_groups": [group]}
+
+    def load_full_optim_state_dict(self, optimizer, sd: dict) -> None:
+        """Inverse of ``full_optim_state_dict``: this rank keeps its slices of every sharded
+        state tensor and loads them into ``optimizer`` (over this wrapper's parameters())."""
+        if len(optimizer.param_groups) != 1 or len(sd["param_groups"]) != 1:
+            raise ValueError("load_full_optim_state_dict: one parameter group")
+        s = self._dims[1] // self.world
+        lo, hi = self.rank * s, (self.rank + 1) * s
+        order = optimizer.param_groups[0]["params"]
+        pos = {id(q): i for i, q in enumerate(order)}
+        state = {}
+        for j, (name, q, how) in enumerate(self._full_params()):
+            st = sd["state"].get(j)
+            if st is None:
+                continue
+            ent = {}
+            for k, v in st.items():
+                if torch.is_tensor(v) and how != "rep" and v.dim() == q.dim() and \
+                        v.numel() == q.numel() * self.world:
+                    v = v[lo:hi] if how == "rows" else v[:, lo:hi]
+                ent[k] = v.detach().clone().to(q.device) if torch.is_tensor(v) and v.dim() \
+                    else v
+                if torch.is_tensor(v) and v.dim() and ent[k].shape != q.shape:
+                    raise ValueError(f"load_full_optim_state_dict: {name}.{k} has shape "
+                                     f"{tuple(v.shape)}, this rank's slice needs "
+                                     f"{tuple(q.shape)}")
+            state[pos[id(q)]] = ent
+        group = dict(sd["param_groups"][0])
+        group["params"] = list(range(len(order)))
+        self._fstate = None
+        optimizer.load_state_dict({"state": state, "param_groups": [group]})
 
 
 def rank_compute_ms(W: int, dims=(9216, 4096, 4096), classes: int = 10, B: int = 128,

@@ -38,9 +38,11 @@ def save_ddp_checkpoint(ddp_model, save_dir: str, epoch: int) -> str:
     path = os.path.join(save_dir, f"ckpt_{epoch}.pt")
     if getattr(ddp_model, "full_state_dict", None) is not None:
         # a sharded model (parallel/tensor_parallel.py): assembling the full state dict is a
-        # collective every rank joins; rank 0 writes it
+        # collective every rank joins; rank 0 writes it with the DDP key contract ("module."
+        # prefix, REF/multi-GPU-training-torch.py:221), so a DDP model loads it unchanged
         full = ddp_model.full_state_dict()
-        sd = _detach_clone(full) if rt.get_rank() == 0 else None
+        sd = {f"module.{k}": v for k, v in _detach_clone(full).items()} \
+            if rt.get_rank() == 0 else None
     else:
         sd = _detach_clone(ddp_model.state_dict()) if rt.get_rank() == 0 else None
     save_on_main(sd, path)
@@ -72,31 +74,47 @@ def load_checkpoint(model, path: str, map_location=None, strict: bool = True):
 def save_model_safetensors(model, save_dir: str, filename: str = "model.safetensors") -> str:
     """Accelerate-style save_model: unwrapped keys, main process only."""
     path = os.path.join(save_dir, filename)
+    m = unwrap_model(model)
+    full = None
+    if getattr(m, "full_state_dict", None) is not None:
+        # a sharded model: the full state dict is a collective (all-gathers) every rank joins
+        full = m.full_state_dict()
     if rt.get_rank() == 0:
         from safetensors.torch import save_file
 
         os.makedirs(save_dir, exist_ok=True)
         sd = {k: v.detach().to("cpu").contiguous().clone()
-              for k, v in unwrap_model(model).state_dict().items()}
+              for k, v in (full if full is not None else m.state_dict()).items()}
         save_file(sd, path, metadata={"format": "pt"})
     return path
 
 
 def save_training_state(path: str, model, optimizer=None, epoch: int | None = None,
                         extra: dict | None = None) -> None:
-    obj = {"model": _detach_clone(unwrap_model(model).state_dict()), "epoch": epoch,
-           "extra": extra or {}}
+    """Model + optimizer + epoch, rank 0 writes (every rank must call it: a sharded model's
+    state and a sharded optimizer's state are assembled by collectives first)."""
+    m = unwrap_model(model)
+    obj = {"model": _detach_clone(m.state_dict()), "epoch": epoch, "extra": extra or {}}
     if optimizer is not None:
         ddp = getattr(optimizer, "_fused_ddp", None)
         if ddp is not None:  # sharded in-reduction updates: gather the state slices first
             ddp.consolidate_optimizer_state()
-        obj["optimizer"] = optimizer.state_dict()
+        if getattr(m, "full_optim_state_dict", None) is not None:
+            # tensor-sharded model: every rank's slice of the momentum / moments, gathered into
+            # the full model's layout (not rank 0's shard)
+            obj["optimizer"] = m.full_optim_state_dict(optimizer)
+        else:
+            obj["optimizer"] = optimizer.state_dict()
     save_on_main(obj if rt.get_rank() == 0 else None, path)
 
 
 def load_training_state(path: str, model, optimizer=None, map_location=None) -> dict:
     obj = torch.load(path, map_location=map_location, weights_only=True)
-    unwrap_model(model).load_state_dict(obj["model"])
+    m = unwrap_model(model)
+    m.load_state_dict(strip_prefix(obj["model"]))
     if optimizer is not None and "optimizer" in obj:
-        optimizer.load_state_dict(obj["optimizer"])
+        if getattr(m, "load_full_optim_state_dict", None) is not None:
+            m.load_full_optim_state_dict(optimizer, obj["optimizer"])  # re-shard
+        else:
+            optimizer.load_state_dict(obj["optimizer"])
     return obj
