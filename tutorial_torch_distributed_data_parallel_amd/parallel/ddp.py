@@ -585,6 +585,13 @@ class DistributedDataParallel(nn.Module):
             self._factor = cand
             self._factor_bufs.clear()
             self._bounds = self._plan_buckets()
+            if cand and self._busbw is None and not (
+                    self._gpu and torch.cuda.is_current_stream_capturing()):
+                #  the factored set became non-empty after registration too (a
+                # clipping change, a comm hook): measure the all-gather input of the
+                # replicated-vs-sharded choice here, eagerly, instead of silently using the
+                # fixed price model
+                self._probe_bandwidth(max(4 * o * n for o, n, _ in cand.values()))
             return True
         return False
 
@@ -970,8 +977,10 @@ class DistributedDataParallel(nn.Module):
         rows = {self._param_name(self.arena.params[i]): {"rep_rows": int(r),
                                                          "out_rows": int(self._factor[i][0])}
                 for i, r in self._factor_rep.items() if i in self._factor}
+        src = ("fallback price model (no bandwidth measured)" if self._busbw is None else
+               "pinned (TDP_FACTOR_BUSBW)" if self._busbw.get("pinned") else "measured")
         return {"rows": rows, "slot_rows": sorted(set(self._factor_cap.values())),
-                "busbw": self._busbw}
+                "busbw": self._busbw, "busbw_source": src}
 
     # Fallback price model when no bandwidth was measured (CPU twin, tests): the replicated
     # update's extra GEMM rows cost 2*W*B*(1 - 1/W) FLOP at ~150 TF/s plus (1 - 1/W) * 16 B of
