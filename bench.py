@@ -130,6 +130,11 @@ def parse():
                          "tensor-sharded variants' timings as side numbers in config.selection")
     ap.add_argument("--select-steps", type=int, default=20,
                     help="timed steps per candidate of --parallel tensor / auto")
+    ap.add_argument("--head-loss", choices=["fused", "separate"], default="fused",
+                    help="toy MLP: the head Linear + cross-entropy as one fused op "
+                         "(model(x, target=y): ops.linear_cross_entropy, one launch for the head "
+                         "GEMM, the loss and the head's input gradient) or as the reference's two "
+                         "calls (criterion(model(x), y)); bit-identical results")
     ap.add_argument("--comm-cus", type=int, default=None,
                     help="CUs left to RCCL: grid-sized kernels (persistent GEMMs, split-K "
                          "planners) plan for (CUs - N) (TDP_COMM_CUS; default 0)")
@@ -581,6 +586,15 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
     def loss_fn(out_, y):
         return tdp.ops.cross_entropy(out_, y, acc=acc)
 
+    # the toy MLP's head and loss as ONE op (models/mlp.py forward(x, target)): the same
+    # criterion(model(inputs), labels) (REF/multi-GPU-training-torch.py:121-122), bit for bit
+    fused_head = a.model == "toy_mlp" and a.head_loss == "fused"
+
+    def model_loss(mod, x, y):
+        if fused_head:
+            return mod(x, target=y, acc=acc)
+        return loss_fn(mod(x), y)
+
     tp = None
     bsz = a.batch  # rows one step gathers (the tensor-sharded step: the node's batch)
     if cfg.get("tensor"):
@@ -655,7 +669,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
 
         def body(x, y):  # REF/multi-GPU-training-accelerate.py:45-55
             opt.zero_grad(set_to_none=True)
-            loss = loss_fn(model(x), y)
+            loss = model_loss(model, x, y)
             accel.backward(loss)
             opt.step()
             return loss
@@ -673,7 +687,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
 
         def body(x, y):  # REF/multi-GPU-training-torch.py:118-126
             opt.zero_grad(set_to_none=True)
-            loss = loss_fn(ddp(x), y)
+            loss = model_loss(ddp, x, y)
             tdp.ops.backward(loss)  # loss.backward() seeded by a cached 1: no fill kernel
             opt.step()
             return loss
@@ -699,7 +713,7 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
         def st():
             x, y = gather_batch(data.x, data.y, idx_static)
             o2.zero_grad(set_to_none=True)
-            tdp.ops.backward(loss_fn(d2(x), y))
+            tdp.ops.backward(model_loss(d2, x, y))
             o2.step()
         return d2, st
 
@@ -1183,6 +1197,8 @@ def main():
                                          " (fused into the gradient reduction)")
                                         if a.impl == "tdp" and fused else ""),
                 "final_loss": final_loss,
+                # the toy MLP's head Linear + cross-entropy: one fused op or the two calls
+                "head_loss": a.head_loss if a.model == "toy_mlp" and a.impl == "tdp" else None,
                 "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,
                 "comm_cus": _reserved_cus(a.impl, use_gpu),
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)

@@ -115,3 +115,22 @@ def test_tensor_sharded_model_beats_factored_at_w8():
     # gathering the node's batch locally saves the 33 MB input all-gather
     assert cm.simulate_tensor(8, hw=hw, global_batch=False)["step_us"] > t1["step_us"] + 90
     assert cm.simulate_tensor(1)["exposed_us"] == 0.0
+
+
+def test_factored_bound_is_below_every_simulated_plan():
+    """factored_bound: no simulated DDP plan beats the schedule-independent bound, and at W = 8
+    the bound itself stays under 70 % of the dp1 model step at the default link figure
+    (docs/COMM_MODEL.md "What ANY DDP schedule can reach")."""
+    from tutorial_torch_distributed_data_parallel_amd.parallel import commmodel as cm
+
+    L = cm.toy_mlp_layers(128)
+    hw = cm.Hardware()
+    alone = sum(x.fwd_us + x.dgrad_us + x.wgrad_us for x in L)
+    for W in (2, 4, 8):
+        b = cm.factored_bound(L, W, 128, hw)
+        assert b["step_us"] == max(b["compute_us"], b["wire_us"])
+        for m1 in cm.MODES[2:]:
+            for m2 in cm.MODES[2:]:
+                r = cm.simulate(L, {"fc1": m1, "fc2": m2}, W, 128, hw)
+                assert r["step_us"] >= b["step_us"] - 1.0, (W, m1, m2, r["step_us"], b)
+    assert alone / cm.factored_bound(L, 8, 128, hw)["step_us"] < 0.70

@@ -252,18 +252,28 @@ Tensor split_planes_op(const Tensor& x) {
 
 // Head Linear backward in one launch (planes.h head_bwd): fills dx, dw, db (optional); returns
 // (launched, planes of dx or None). g [B, O] (O <= 16), x [B, I], w [O, I], dx [B, I], dw [O, I].
-py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor& dx, Tensor& dw,
+py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w,
+                      const c10::optional<Tensor>& dx_opt, Tensor& dw,
                       const c10::optional<Tensor>& db, const c10::optional<Tensor>& gate,
                       bool planes, SyncBackend* backend, int64_t w_offset, int64_t b_offset,
                       int64_t b_span) {
-  CHECK_GPU(g); CHECK_GPU(x); CHECK_GPU(w); CHECK_GPU(dx); CHECK_GPU(dw);
-  CHECK_F32(g); CHECK_F32(x); CHECK_F32(w); CHECK_F32(dx); CHECK_F32(dw);
-  CHECK_ROWMAJOR(g); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w); CHECK_ROWMAJOR(dx);
+  CHECK_GPU(g); CHECK_GPU(x); CHECK_GPU(w); CHECK_GPU(dw);
+  CHECK_F32(g); CHECK_F32(x); CHECK_F32(w); CHECK_F32(dw);
+  CHECK_ROWMAJOR(g); CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(w);
   CHECK_ROWMAJOR(dw);
   const int B = (int)g.size(0), O = (int)g.size(1), I = (int)x.size(1);
-  TORCH_CHECK(x.size(0) == B && w.size(0) == O && w.size(1) == I && dx.size(0) == B &&
-                  dx.size(1) == I && dw.size(0) == O && dw.size(1) == I,
+  TORCH_CHECK(x.size(0) == B && w.size(0) == O && w.size(1) == I && dw.size(0) == O &&
+                  dw.size(1) == I,
               "head_bwd: shape mismatch");
+  // dx None: only dW / db (the input gradient came out of head_ce's forward)
+  const bool has_dx = dx_opt.has_value() && dx_opt->defined();
+  Tensor dx;
+  if (has_dx) {
+    dx = *dx_opt;
+    CHECK_GPU(dx); CHECK_F32(dx); CHECK_ROWMAJOR(dx);
+    TORCH_CHECK(dx.size(0) == B && dx.size(1) == I, "head_bwd: dx shape mismatch");
+  }
+  planes = planes && has_dx;
   float* dbp = nullptr;
   if (db.has_value() && db->defined()) {
     CHECK_GPU(*db); CHECK_F32(*db); CHECK_CONTIG(*db);
@@ -307,7 +317,8 @@ py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor&
     }
   }
   const bool ok = head_bwd(g.data_ptr<float>(), g.stride(0), x.data_ptr<float>(), x.stride(0),
-                           w.data_ptr<float>(), w.stride(0), dx.data_ptr<float>(), dx.stride(0),
+                           w.data_ptr<float>(), w.stride(0),
+                           has_dx ? dx.data_ptr<float>() : nullptr, has_dx ? dx.stride(0) : 0,
                            gp, ldgate,
                            planes ? reinterpret_cast<uint16_t*>(pl.data_ptr()) : nullptr,
                            planes ? pl.stride(0) : 0, dw.data_ptr<float>(), dw.stride(0), dbp, B,
@@ -316,6 +327,65 @@ py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w, Tensor&
   if (ok && bo.kind) backend->note_epilogue(b_offset, b_span);
   if (ok && planes) return py::make_tuple(true, pl);
   return py::make_tuple(ok, py::none());
+}
+
+// Head Linear + cross-entropy forward in one launch (planes.h head_ce). x [B, I] (B <= 256),
+// w [O, I] (O <= 16), labels [B] int64, ticket: a zeroed int32 scratch word (zero again after
+// the launch). Returns [loss, lse [B + 1], logits [B, O]] + with_grad: [dlogits (unit seed),
+// dx [B, I], planes of dx or an empty tensor]; an empty list when the shape is not supported.
+std::vector<Tensor> head_ce_op(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                               const Tensor& labels, int64_t ignore_index, double smoothing,
+                               bool mean, const c10::optional<Tensor>& acc, bool with_grad,
+                               const c10::optional<Tensor>& gate, bool planes,
+                               Tensor& ticket) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_ROWMAJOR(x);
+  CHECK_GPU(w); CHECK_F32(w); CHECK_ROWMAJOR(w);
+  CHECK_GPU(labels); CHECK_CONTIG(labels); CHECK_GPU(ticket); CHECK_CONTIG(ticket);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  TORCH_CHECK(ticket.scalar_type() == at::kInt && ticket.numel() >= 1, "ticket: int32 word");
+  const int B = (int)x.size(0), I = (int)x.size(1), O = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == I && labels.numel() == B, "head_ce: shape mismatch");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_GPU(*bias); CHECK_F32(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == O, "head_ce: bias must have O elements");
+    bp = bias->data_ptr<float>();
+  }
+  float* accp = nullptr;
+  if (acc.has_value() && acc->defined()) {
+    CHECK_GPU(*acc); CHECK_F32(*acc);
+    TORCH_CHECK(acc->numel() >= 3, "acc needs 3 floats");
+    accp = acc->data_ptr<float>();
+  }
+  const float* gp = nullptr;
+  long ldgate = 0;
+  if (gate.has_value() && gate->defined()) {
+    CHECK_GPU(*gate); CHECK_F32(*gate); CHECK_ROWMAJOR(*gate);
+    TORCH_CHECK(gate->size(0) == B && gate->size(1) == I, "head_ce: gate must have x's shape");
+    gp = gate->data_ptr<float>();
+    ldgate = gate->stride(0);
+  }
+  auto o = x.options();
+  Tensor loss = at::empty({}, o), lse = at::empty({B + 1}, o), logits = at::empty({B, O}, o);
+  Tensor rowbuf = at::empty({B, 4}, o);
+  Tensor d, dx, pl;
+  if (with_grad) {
+    d = at::empty({B, O}, o);
+    dx = at::empty({B, I}, o);
+    if (planes) pl = at::empty({3, (long)B, (long)I}, o.dtype(at::kBFloat16));
+  }
+  const bool ok = head_ce(
+      x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(), w.stride(0), bp,
+      labels.data_ptr<int64_t>(), B, O, I, (int)ignore_index, (float)smoothing, mean,
+      logits.data_ptr<float>(), lse.data_ptr<float>(), rowbuf.data_ptr<float>(),
+      reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), loss.data_ptr<float>(), accp,
+      with_grad ? d.data_ptr<float>() : nullptr, with_grad ? dx.data_ptr<float>() : nullptr,
+      with_grad ? dx.stride(0) : 0, gp, ldgate,
+      (with_grad && planes) ? reinterpret_cast<uint16_t*>(pl.data_ptr()) : nullptr,
+      (with_grad && planes) ? pl.stride(0) : 0, cur_stream());
+  if (!ok) return {};
+  if (!with_grad) return {loss, lse, logits};
+  return {loss, lse, logits, d, dx, planes ? pl : at::empty({0}, o)};
 }
 
 std::vector<int64_t> gemm_planes_plan_op(int M, int N, int K, int cus) {
@@ -1531,6 +1601,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dw"), py::arg("db") = py::none(), py::arg("gate") = py::none(),
         py::arg("planes") = false, py::arg("backend") = nullptr, py::arg("w_offset") = -1,
         py::arg("b_offset") = -1, py::arg("b_span") = 0);
+  m.def("head_ce", &head_ce_op, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("labels"),
+        py::arg("ignore_index"), py::arg("smoothing"), py::arg("mean"), py::arg("acc"),
+        py::arg("with_grad"), py::arg("gate"), py::arg("planes"), py::arg("ticket"));
   m.def("gemm_planes_plan", &gemm_planes_plan_op);
   m.def("gemm_planes_set_cfg", &gemm_planes_set_cfg,
         "planes GEMM variant: stages 2 / 3 (one wave group), 4 = default (3 stages, two wave "

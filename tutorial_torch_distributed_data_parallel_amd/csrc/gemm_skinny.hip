@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "ce_row.h"
 #include "common.h"
 #include "kernels.h"
 #include "optim_elem.h"
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   float rs = 0.f;
   if (p.db && bid == 0 && threadIdx.x < p.O)
     for (int k = 0; k < p.B; ++k) rs += smem[k * MMAX + threadIdx.x];
-  if (p.wopt.kind) {
+  if (p.wopt.kind && p.dx) {
     // The update below overwrites W[:, cols] in place, and the input gradient needs the OLD W:
     // dx[:, c] depends on column c of W only, so this workgroup computes dx for its own columns
     // before updating them (no separate dx workgroups: they would read W while other
@@ -355,6 +356,195 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
   }
 }
 
+
+// Forward of a classifier head Linear(I -> O <= 16) + its cross-entropy loss in ONE launch (the
+// toy MLP / AlexNet fc3 + nn.CrossEntropyLoss: REF/multi-GPU-training-torch.py:121-122), one
+// 256-thread workgroup per batch row:
+//   * the row's O logits exactly as skinny_n_kernel computes them (same K split, same reduction
+//     order), + bias;
+//   * the row's cross-entropy terms exactly as ce_fwd_kernel's one-row-per-lane path (ce_row.h)
+//     and -- training -- the row's logits gradient for a unit upstream gradient; the mean's
+//     denominator (valid labels of the batch) is counted by every workgroup from the labels;
+//   * training: the row's input gradient dx = dlogits . W, gated by the previous ReLU's output,
+//     and its bf16 split planes, exactly as head_bwd_kernel's dx workgroups compute them (the
+//     backward then only reduces dW / db: head_bwd with dx == null);
+//   * the batch sums (loss, correct, valid -> loss scalar, lse[B], the device metric
+//     accumulator) by the LAST workgroup to arrive, over per-row values handed off through
+//     write-through (sc1) stores and an agent-scope ticket (no fences; MI355X_MICROARCH.md
+//     inter-workgroup visibility), in ce_fwd_kernel's summation order: bit-identical loss.
+// The ticket counter is zero between launches (the last arriver resets it).
+struct HeadCeParams {
+  const float* x;
+  const float* w;
+  const float* bias;
+  const int64_t* labels;
+  float* logits;   // [B][O]
+  float* lse;      // [B + 1]
+  float* rowbuf;   // [B][4] per-row loss / correct / valid
+  unsigned* ticket;
+  float* loss;
+  float* acc;      // optional [3]: += loss sum, correct, rows
+  float* dpre;     // optional [B][O]: training (dlogits for a unit seed)
+  float* dx;       // optional [B][I] (with dpre)
+  const float* gate;
+  uint16_t* dxp;   // optional planes of dx [3][B][I]
+  long ldx, ldw, lddx, ldgate, dxps;
+  int B, O, I, ignore_index, mean;
+  float eps;
+};
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
+  __shared__ float red[4][NMAX + 4];  // partial dot products; [w][NMAX..] batch sums
+  __shared__ float lg[NMAX];          // this row's logits, then its logits gradient
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x;
+  // ---- logits (skinny_n_kernel's body)
+  const float* a = p.x + (long)row * p.ldx;
+  float acc[NMAX];
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) acc[n] = 0.f;
+  const float* brow[NMAX];
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) brow[n] = p.w + (long)(n < p.O ? n : p.O - 1) * p.ldw;
+#pragma unroll 4
+  for (int k = threadIdx.x * 4; k < p.I; k += 1024) {
+    const f32x4 av = *reinterpret_cast<const f32x4*>(a + k);
+    f32x4 bv[NMAX];
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) bv[n] = *reinterpret_cast<const f32x4*>(brow[n] + k);
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n)
+      acc[n] = fmaf(av[0], bv[n][0], fmaf(av[1], bv[n][1], fmaf(av[2], bv[n][2],
+                                                                fmaf(av[3], bv[n][3], acc[n]))));
+  }
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) {
+    const float v = wave_sum(acc[n]);
+    if (lane == 0) red[w][n] = v;
+  }
+  // the mean's denominator: valid labels of the whole batch (B <= 256: one per thread)
+  float valid = 0.f;
+  if ((int)threadIdx.x < p.B) {
+    const int64_t y = p.labels[threadIdx.x];
+    valid = (y != p.ignore_index && y >= 0 && y < p.O) ? 1.f : 0.f;
+  }
+  valid = wave_sum(valid);
+  if (lane == 0) red[w][NMAX] = valid;
+  __syncthreads();
+  if ((int)threadIdx.x < p.O) {
+    const int n = threadIdx.x;
+    float v = red[0][n] + red[1][n] + red[2][n] + red[3][n];
+    if (p.bias) v += p.bias[n];
+    lg[n] = v;
+    p.logits[(long)row * p.O + n] = v;
+  }
+  __syncthreads();
+  const float vd = red[0][NMAX] + red[1][NMAX] + red[2][NMAX] + red[3][NMAX];
+  // ---- the row's loss terms and logits gradient (ce_fwd_kernel, one row per lane)
+  if (threadIdx.x == 0) {
+    const int64_t y = p.labels[row];
+    const RowOut o = row_serial(lg, p.O, y, p.ignore_index, p.eps);
+    p.lse[row] = o.lse;
+    if (p.dpre) {
+      const float g = p.mean ? 1.f / vd : 1.f;
+      const bool ok = o.valid != 0.f;
+      float d[NMAX];
+#pragma unroll
+      for (int c = 0; c < NMAX; ++c) {
+        float v = 0.f;
+        if (c < p.O && ok) {
+          const float pr = __expf(lg[c] - o.lse);
+          v = g * (pr - (c == (int)y ? (1.f - p.eps) : 0.f) - p.eps / p.O);
+        }
+        d[c] = v;
+      }
+#pragma unroll
+      for (int c = 0; c < NMAX; ++c) {
+        if (c < p.O) {
+          lg[c] = d[c];
+          p.dpre[(long)row * p.O + c] = d[c];
+        }
+      }
+    }
+    // per-row sums, handed to the last workgroup write-through (sc1)
+    float* rb = p.rowbuf + 4L * row;
+    __hip_atomic_store(rb + 0, o.loss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rb + 1, o.correct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rb + 2, o.valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // ---- the row's input gradient (head_bwd_kernel's dx workgroups: 4 adjacent columns per
+  // thread, the O gradients of the row broadcast; same fmaf order)
+  if (p.dpre && p.dx) {
+    for (int col = threadIdx.x * 4; col < p.I; col += 1024) {
+      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < p.O; ++k) {
+        const float gv = lg[k];
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (long)k * p.ldw + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s4[e] = fmaf(gv, wv[e], s4[e]);
+      }
+      if (p.gate) {
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(p.gate + (long)row * p.ldgate + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s4[e] = gv[e] > 0.f ? s4[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(p.dx + (long)row * p.lddx + col) = s4;
+      if (p.dxp) {
+        typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+        unsigned h0, m0, l0, h1, m1, l1;
+        split4_pair(s4[0], s4[1], h0, m0, l0);
+        split4_pair(s4[2], s4[3], h1, m1, l1);
+        uint16_t* o = p.dxp + (long)row * p.I + col;
+        *reinterpret_cast<u32x2_*>(o) = u32x2_{h0, h1};
+        *reinterpret_cast<u32x2_*>(o + p.dxps) = u32x2_{m0, m1};
+        *reinterpret_cast<u32x2_*>(o + 2 * p.dxps) = u32x2_{l0, l1};
+      }
+    }
+  }
+  // ---- ticket: the last workgroup reduces the per-row values
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 row stores have landed
+    const unsigned t =
+        __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (unsigned)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  float ls = 0.f, cr = 0.f, vv = 0.f;
+  if ((int)threadIdx.x < p.B) {
+    const float* rb = p.rowbuf + 4L * threadIdx.x;
+    ls = __hip_atomic_load(rb + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cr = __hip_atomic_load(rb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    vv = __hip_atomic_load(rb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ls = wave_sum(ls);
+  cr = wave_sum(cr);
+  vv = wave_sum(vv);
+  __syncthreads();  // every wave has read lg / red above: reuse red for the batch sums
+  if (lane == 0) {
+    red[w][0] = ls;
+    red[w][1] = cr;
+    red[w][2] = vv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ls = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    cr = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    vv = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+    if (p.loss) p.loss[0] = p.mean ? (vv > 0.f ? ls / vv : NAN) : ls;
+    p.lse[p.B] = vv;
+    if (p.acc) {
+      p.acc[0] += ls;
+      p.acc[1] += cr;
+      p.acc[2] += vv;
+    }
+    __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 SkinnyParams params_of(const GemmF32Args& a) {
@@ -389,7 +579,7 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
               float* dx, long lddx, const float* gate, long ldgate, uint16_t* dxp, long dxps,
               float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s,
               const OptEpilogue* wopt, const OptEpilogue* bopt) {
-  if (O < 1 || O > kSkinnyMax || I % 4 || B < 1 || !al16(w) || !al16(dx) || ldw % 4 ||
+  if (O < 1 || O > kSkinnyMax || I % 4 || B < 1 || !al16(w) || (dx && !al16(dx)) || ldw % 4 ||
       lddx % 4 || (gate && (!al16(gate) || ldgate % 4)) || ((uintptr_t)dxp & 7) ||
       (long)B * (O <= 8 ? 8 : kSkinnyMax) * 4 > 65536)
     return false;
@@ -399,7 +589,8 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
   if (bopt && db) p.bopt = *bopt;
   const long threads = (long)B * (I / 4);
   // with the in-place update the weight workgroups compute dx themselves (kernel comment)
-  p.nb_dx = p.wopt.kind ? 0 : (int)((threads + 255) / 256);
+  // (dx == null: the input gradient exists already -- head_ce computed it in the forward)
+  p.nb_dx = (p.wopt.kind || dx == nullptr) ? 0 : (int)((threads + 255) / 256);
   const int cw = p.wopt.kind ? kHeadColsOpt : kHeadCols;
   const int nb_dw = (I + cw - 1) / cw;
   // the 10-class heads get their own width (no FMAs on 6 padding classes)
@@ -414,6 +605,23 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
   };
   if (p.wopt.kind) launch(std::integral_constant<int, kHeadColsOpt>{});
   else launch(std::integral_constant<int, kHeadCols>{});
+  return true;
+}
+
+bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bias,
+             const int64_t* labels, int B, int O, int I, int ignore_index, float smoothing,
+             bool mean, float* logits, float* lse, float* rowbuf, unsigned* ticket, float* loss,
+             float* acc, float* dpre, float* dx, long lddx, const float* gate, long ldgate,
+             uint16_t* dxp, long dxps, hipStream_t s) {
+  if (O < 1 || O > kSkinnyMax || B < 1 || B > 256 || I % 4 || !al16(x) || !al16(w) ||
+      ldx % 4 || ldw % 4 || (dx && (!al16(dx) || lddx % 4 || !dpre)) ||
+      (gate && (!al16(gate) || ldgate % 4)) || ((uintptr_t)dxp & 7) || (dxp && !dx))
+    return false;
+  HeadCeParams p{x, w, bias, labels, logits, lse, rowbuf, ticket, loss, acc, dpre, dx, gate, dxp,
+                 ldx, ldw, lddx, ldgate, dxps, B, O, I, ignore_index, mean ? 1 : 0, smoothing};
+  if (O <= 8) hipLaunchKernelGGL(head_ce_kernel<8>, dim3(B), dim3(256), 0, s, p);
+  else if (O <= 10) hipLaunchKernelGGL(head_ce_kernel<10>, dim3(B), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(head_ce_kernel<kSkinnyMax>, dim3(B), dim3(256), 0, s, p);
   return true;
 }
 

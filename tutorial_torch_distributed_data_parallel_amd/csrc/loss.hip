@@ -9,39 +9,12 @@
 // Semantics follow torch.nn.functional.cross_entropy with class-index targets: ignore_index rows
 // contribute nothing and are excluded from the mean's denominator; label_smoothing eps mixes
 // (1-eps)*nll with eps*mean_c(-log p_c).
+#include "ce_row.h"
 #include "common.h"
 #include "kernels.h"
 
 namespace tdp {
 namespace {
-
-struct RowOut {
-  float lse;
-  float loss;
-  float correct;
-  float valid;
-};
-
-// One row handled by one lane (small C) -- logits row in registers-free sequential scan.
-__device__ RowOut row_serial(const float* x, int C, int64_t y, int ignore_index, float eps) {
-  float mx = -INFINITY;
-  int arg = 0;
-  float sumx = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float v = x[c];
-    if (v > mx) { mx = v; arg = c; }
-    sumx += v;
-  }
-  float se = 0.f;
-  for (int c = 0; c < C; ++c) se += __expf(x[c] - mx);
-  RowOut o;
-  o.lse = mx + __logf(se);
-  const bool valid = (y != ignore_index) && y >= 0 && y < C;
-  o.valid = valid ? 1.f : 0.f;
-  o.loss = valid ? (o.lse - (1.f - eps) * x[y] - (eps / C) * sumx) : 0.f;
-  o.correct = (valid && arg == (int)y) ? 1.f : 0.f;
-  return o;
-}
 
 // One row handled by a whole wave (large C).
 __device__ RowOut row_wave(const float* x, int C, int64_t y, int ignore_index, float eps) {

@@ -49,11 +49,24 @@ void gather_batch_planes(const float* x, const int64_t* y, const int64_t* idx, l
 // Backward of a head Linear(I -> O <= 16) in one launch (csrc/gemm_skinny.hip): dx = g . W
 // (gated by gate > 0 when given, planes of dx when dxp != null), dW = g^T . x, db = sum_b g
 // (when db != null). g [B][O], x [B][I], W [O][I]; I % 4 == 0, 16-B aligned W / dx / gate rows.
+// dx == null: no input gradient (head_ce computed it in the forward).
 // wopt / bopt (kind != 0): apply that optimizer update to W / b instead of storing dW / db.
 // false = shape not supported (nothing launched).
 bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w, long ldw,
               float* dx, long lddx, const float* gate, long ldgate, uint16_t* dxp, long dxps,
               float* dw, long lddw, float* db, int B, int O, int I, hipStream_t s,
               const OptEpilogue* wopt = nullptr, const OptEpilogue* bopt = nullptr);
+
+// Forward of a head Linear(I -> O <= 16) + cross-entropy in one launch (csrc/gemm_skinny.hip
+// head_ce_kernel, B <= 256 rows): logits [B][O], lse [B + 1] (lse[B] = valid rows), loss, the
+// metric accumulator acc [3] (optional); with dpre (training): the logits gradient for a unit
+// upstream gradient and, with dx, the input gradient dlogits . W (gated by gate > 0, planes into
+// dxp when given). rowbuf [B][4] scratch; ticket: one zeroed unsigned, zero again afterwards.
+// false = shape not supported (nothing launched).
+bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bias,
+             const int64_t* labels, int B, int O, int I, int ignore_index, float smoothing,
+             bool mean, float* logits, float* lse, float* rowbuf, unsigned* ticket, float* loss,
+             float* acc, float* dpre, float* dx, long lddx, const float* gate, long ldgate,
+             uint16_t* dxp, long dxps, hipStream_t s);
 
 }  // namespace tdp

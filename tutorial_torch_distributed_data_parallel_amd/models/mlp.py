@@ -34,11 +34,22 @@ class ToyMLP(nn.Module):
             self.add_module(name, m)
         self._order = [n for n, _ in layers]
 
-    def forward(self, x):
+    def forward(self, x, target=None, acc=None):
+        """Logits; with ``target`` the mean cross-entropy loss instead (``acc``: the device
+        metric accumulator of ops.cross_entropy): the head Linear and the loss run as ONE fused
+        op (ops.linear_cross_entropy: head GEMM, loss, logits gradient and the head's input
+        gradient in one launch on MI355X) -- ``model(x, target=y)`` equals
+        ``cross_entropy(model(x), y)`` bit for bit."""
         x = x.reshape(x.shape[0], -1)
-        for n in self._order:
+        order = self._order if target is None else self._order[:-1]
+        for n in order:
             x = getattr(self, n)(x)
-        return x
+        if target is None:
+            return x
+        from ..ops import linear_cross_entropy
+
+        head = getattr(self, self._order[-1])
+        return linear_cross_entropy(x, head.weight, head.bias, target, acc=acc)
 
 
 def toy_mlp(**kw) -> ToyMLP:

@@ -42,7 +42,11 @@ MODES = ("allreduce", "sharded", "factored-sharded", "factored-replicated", "fac
 @dataclass
 class Hardware:
     link_GBps: float = 51.0        # effective unidirectional GB/s per xGMI link (64 peak x 0.8)
-    gemm_TFps: float = 170.0       # split-bf16 fp32 GEMM (profiles/micro: 168-170 TF/s at 4096^3)
+    # split-bf16 fp32 GEMM with the optimizer epilogue, the kernel a factored job runs
+    # (gemm_f32_fast: 175.2 TF/s at 4096 x 4096 x 9216, profiles/r9/gemm_emu8_r9.md; the
+    # 205 TF/s 256 x 256 kernel of that table has no optimizer epilogue and is not dispatched
+    # for these jobs)
+    gemm_TFps: float = 175.0
     hbm_TBps: float = 5.0          # optimizer streams (profiles/r7: 4.3-4.5 in the epilogue)
     latency_us: float = 12.0       # per collective launch + sync on xGMI
     busbw_GBps: dict = field(default_factory=dict)  # measured: {"all_gather": x, ...} overrides
@@ -237,6 +241,49 @@ def simulate_tensor(W: int, B: int = 128, dims=(9216, 4096, 4096), classes: int 
     return {"W": W, "compute_us": round(comp, 1), "exposed_us": round(exposed, 1),
             "step_us": round(comp + exposed, 1), "wire_MB": round(wire / 1e6, 1),
             "scaling_eff": round(TP_DP1_US / (comp + exposed), 3)}
+
+
+def factored_bound(layers: list[Layer], W: int, B: int, hw: Hardware, steps: int = 40) -> dict:
+    """Schedule-independent lower bound of the factored DDP step: whatever the order of jobs,
+    forks and joins (including overlap ACROSS steps: the next forward waiting only for the
+    parameters it reads), the compute stream must run the forward, the input gradients, the
+    small layers and every job's arithmetic, and the links must carry every job's factor
+    gathers plus the all-gather of its sharded rows. With a fraction f of a weight's rows
+    replicated (0 = factored-sharded, 1 = factored-replicated) the step is at least
+    max(compute(f), wire(f)); this minimises that over f per weight (grid of ``steps``). The
+    achieved schedule (``simulate``) can only be slower."""
+    import itertools
+
+    big = [L for L in layers if L.out > 16]
+    base = sum(L.fwd_us + L.dgrad_us for L in layers) + \
+        sum(L.wgrad_us for L in layers if L not in big)
+    small_bytes = sum(4.0 * L.out * L.inp for L in layers if L not in big)
+    wire0 = _coll_us(hw, "all_reduce", W, small_bytes)
+
+    def parts(L, f):
+        o, n = L.out, L.inp
+
+        def arith(rows):
+            return max(2.0 * W * B * rows * n / (hw.gemm_TFps * 1e6),
+                       16.0 * rows * n / (hw.hbm_TBps * 1e6))
+        comp = arith(f * o) + arith((1.0 - f) * o / W)
+        wire = _coll_us(hw, "all_gather", W, 4.0 * B * n * W) + \
+            _coll_us(hw, "all_gather", W, 4.0 * B * o * W) + \
+            (_coll_us(hw, "all_gather", W, (1.0 - f) * 4.0 * o * n) if f < 1.0 else 0.0)
+        return comp, wire
+    grid = [i / steps for i in range(steps + 1)]
+    best = None
+    for fs in itertools.product(grid, repeat=len(big)):
+        c, w = base, wire0
+        for L, f in zip(big, fs):
+            dc, dw = parts(L, f)
+            c += dc
+            w += dw
+        t = max(c, w)
+        if best is None or t < best["step_us"]:
+            best = {"step_us": round(t, 1), "compute_us": round(c, 1), "wire_us": round(w, 1),
+                    "rep_fraction": {L.name: f for L, f in zip(big, fs)}}
+    return best
 
 
 def best_plan(layers: list[Layer], W: int, B: int, hw: Hardware,
