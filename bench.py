@@ -128,6 +128,9 @@ def parse():
                          "(parallel/tensor_parallel.py: activations cross xGMI, not weights; not "
                          "DDP), recorded as tp{N}; 'auto' = the DDP headline plus the "
                          "tensor-sharded variants' timings as side numbers in config.selection")
+    ap.add_argument("--tp-replicated-data", action="store_true",
+                    help="--parallel tensor: every rank holds the whole dataset and gathers the "
+                         "node's batch locally instead of all-gathering the ranks' inputs")
     ap.add_argument("--select-steps", type=int, default=20,
                     help="timed steps per candidate of --parallel tensor / auto")
     ap.add_argument("--head-loss", choices=["fused", "separate"], default="fused",
@@ -410,7 +413,8 @@ def tensor_diagnostics(a, job, step_ms, world, barrier):
     dims = tuple(int(v) for v in a.mlp_dims.split(",")) if a.mlp_dims else (9216, 4096, 4096)
     hw = cm.Hardware(busbw_GBps={op: bw for op, (_, bw) in big.items()})
     pred = cm.simulate_tensor(world, B=a.batch, dims=dims, hw=hw, rank_us=compute_ms * 1e3,
-                              chunks=int(job.tp.overlap_chunks))
+                              chunks=int(job.tp.overlap_chunks),
+                              global_batch=bool(a.tp_replicated_data))
     out.update(predicted_step_ms=round(pred["step_us"] / 1e3, 4),
                predicted_exposed_ms=round(pred["exposed_us"] / 1e3, 4))
     return out
@@ -523,8 +527,7 @@ LADDER = (
 TENSOR_RUNGS = (
     {"name": "tensor-sharded", "factor": None, "fused": True, "graph": True, "tensor": 1},
     # fc2's reduce-scatter / all-gather in column chunks behind the chunk GEMMs
-    {"name": "tensor-overlap", "factor": None, "fused": True, "graph": True,
-     "tensor": int(os.environ.get("TDP_TP_CHUNKS", "2"))},
+    {"name": "tensor-overlap", "factor": None, "fused": True, "graph": True, "tensor": 2},
 )
 
 
@@ -603,12 +606,12 @@ def build_tdp(a, ctx, cfg, attempt, fallbacks, fault):
 
         if a.model != "toy_mlp" or a.api != "ddp":
             raise RuntimeError("tensor-sharded step: the toy MLP through the native DDP API only")
-        # every rank holds the same dataset and every rank's DistributedSampler: it gathers the
-        # node's batch (rank 0's samples, rank 1's, ...) from its own HBM instead of receiving
-        # the other ranks' inputs over xGMI (33 MB per step at W = 8); the loss stays on this
-        # rank's samples. TDP_TP_GLOBAL=0: each rank gathers its own batch, the wrapper
-        # all-gathers the inputs.
-        shared = os.environ.get("TDP_TP_GLOBAL", "1") == "1"
+        # default: each rank gathers its own batch (its DistributedSampler share) and the
+        # wrapper all-gathers the node's inputs over xGMI (33 MB per step at W = 8), as a real
+        # per-rank input pipeline would. --tp-replicated-data: every rank holds the whole
+        # dataset and every rank's sampler and gathers the node's batch from its own HBM (a
+        # data-layout assumption the DDP path does not make; recorded in config.tp_data)
+        shared = bool(a.tp_replicated_data)
         tp = TensorParallelMLP(model, global_batch=shared, overlap_chunks=int(cfg["tensor"]))
         ddp = None
         opt = make_opt(tp.parameters())
@@ -1199,6 +1202,9 @@ def main():
                 "final_loss": final_loss,
                 # the toy MLP's head Linear + cross-entropy: one fused op or the two calls
                 "head_loss": a.head_loss if a.model == "toy_mlp" and a.impl == "tdp" else None,
+                "tp_data": ("replicated dataset, node batch gathered locally"
+                            if a.tp_replicated_data else "per-rank batches, inputs all-gathered")
+                if tensor else None,
                 "device_warmup_ms": a.device_warmup_ms if use_gpu else 0,
                 "comm_cus": _reserved_cus(a.impl, use_gpu),
                 "bucket_mb": [round((ddp._bounds[i + 1] - ddp._bounds[i]) * 4 / 2 ** 20, 2)

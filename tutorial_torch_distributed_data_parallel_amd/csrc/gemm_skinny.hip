@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
     float v = red[0][n] + red[1][n] + red[2][n] + red[3][n];
     if (p.bias) v += p.bias[n];
     lg[n] = v;
-    p.logits[(long)row * p.O + n] = v;
+    if (blockIdx.y == 0) p.logits[(long)row * p.O + n] = v;
   }
   __syncthreads();
   const float vd = red[0][NMAX] + red[1][NMAX] + red[2][NMAX] + red[3][NMAX];
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
   if (threadIdx.x == 0) {
     const int64_t y = p.labels[row];
     const RowOut o = row_serial(lg, p.O, y, p.ignore_index, p.eps);
-    p.lse[row] = o.lse;
+    if (blockIdx.y == 0) p.lse[row] = o.lse;
     if (p.dpre) {
       const float g = p.mean ? 1.f / vd : 1.f;
       const bool ok = o.valid != 0.f;
@@ -464,27 +464,39 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
       for (int c = 0; c < NMAX; ++c) {
         if (c < p.O) {
           lg[c] = d[c];
-          p.dpre[(long)row * p.O + c] = d[c];
+          if (blockIdx.y == 0) p.dpre[(long)row * p.O + c] = d[c];
         }
       }
     }
     // per-row sums, handed to the last workgroup write-through (sc1)
-    float* rb = p.rowbuf + 4L * row;
-    __hip_atomic_store(rb + 0, o.loss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(rb + 1, o.correct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(rb + 2, o.valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.y == 0) {
+      float* rb = p.rowbuf + 4L * row;
+      __hip_atomic_store(rb + 0, o.loss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rb + 1, o.correct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rb + 2, o.valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   // ---- the row's input gradient (head_bwd_kernel's dx workgroups: 4 adjacent columns per
-  // thread, the O gradients of the row broadcast; same fmaf order)
+  // thread, the O gradients of the row broadcast; same fmaf order), columns split over the
+  // gridDim.y workgroups of the row. Every W row of a chunk is loaded up front (rows past O
+  // clamped, their terms skipped): the chunk costs one L2 round trip, not O dependent ones.
   if (p.dpre && p.dx) {
-    for (int col = threadIdx.x * 4; col < p.I; col += 1024) {
-      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < p.O; ++k) {
-        const float gv = lg[k];
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(p.w + (long)k * p.ldw + col);
+    const int span = (p.I / 4 + gridDim.y - 1) / gridDim.y * 4;
+    const int c0 = blockIdx.y * span, c1 = min(p.I, c0 + span);
+    for (int col = c0 + threadIdx.x * 4; col < c1; col += 1024) {
+      f32x4 wv[NMAX];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) s4[e] = fmaf(gv, wv[e], s4[e]);
+      for (int k = 0; k < NMAX; ++k)
+        wv[k] = *reinterpret_cast<const f32x4*>(brow[k] + col);
+      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NMAX; ++k) {
+        if (k < p.O) {
+          const float gv = lg[k];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s4[e] = fmaf(gv, wv[k][e], s4[e]);
+        }
       }
       if (p.gate) {
         const f32x4 gv = *reinterpret_cast<const f32x4*>(p.gate + (long)row * p.ldgate + col);
@@ -509,7 +521,7 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 row stores have landed
     const unsigned t =
         __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == (unsigned)(gridDim.x - 1);
+    last = t == (unsigned)(gridDim.x * gridDim.y - 1);
   }
   __syncthreads();
   if (!last) return;
@@ -619,9 +631,14 @@ bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bi
     return false;
   HeadCeParams p{x, w, bias, labels, logits, lse, rowbuf, ticket, loss, acc, dpre, dx, gate, dxp,
                  ldx, ldw, lddx, ldgate, dxps, B, O, I, ignore_index, mean ? 1 : 0, smoothing};
-  if (O <= 8) hipLaunchKernelGGL(head_ce_kernel<8>, dim3(B), dim3(256), 0, s, p);
-  else if (O <= 10) hipLaunchKernelGGL(head_ce_kernel<10>, dim3(B), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(head_ce_kernel<kSkinnyMax>, dim3(B), dim3(256), 0, s, p);
+  // training: the row's input-gradient columns split over ys workgroups (each recomputes the
+  // row's logits, a few us of L2 reads): B = 128 rows alone would leave half the CUs idle and
+  // give every thread 4 dependent column chunks at I = 4096
+  const int ys = dx ? std::max(1, std::min(4, (int)((I / 4 + 511) / 512))) : 1;
+  const dim3 grid(B, ys);
+  if (O <= 8) hipLaunchKernelGGL(head_ce_kernel<8>, grid, dim3(256), 0, s, p);
+  else if (O <= 10) hipLaunchKernelGGL(head_ce_kernel<10>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(head_ce_kernel<kSkinnyMax>, grid, dim3(256), 0, s, p);
   return true;
 }
 

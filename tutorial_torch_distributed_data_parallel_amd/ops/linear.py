@@ -53,7 +53,7 @@ _EARLY_PREV_G = True  # the consumer's backward starts the previous layer's g ga
 
 
 def set_early_prev_g(on: bool) -> bool:
-    """Turn the one-layer-early g gather on/off (A/B: scripts/archive/run_with_variant.py); returns the
+    """Turn the one-layer-early g gather on/off (A/B: profiles/archive/scripts/run_with_variant.py); returns the
     previous setting."""
     global _EARLY_PREV_G
     old, _EARLY_PREV_G = _EARLY_PREV_G, bool(on)
