@@ -133,11 +133,12 @@ def parse():
                          "node's batch locally instead of all-gathering the ranks' inputs")
     ap.add_argument("--select-steps", type=int, default=20,
                     help="timed steps per candidate of --parallel tensor / auto")
-    ap.add_argument("--head-loss", choices=["fused", "separate"], default="fused",
-                    help="toy MLP: the head Linear + cross-entropy as one fused op "
-                         "(model(x, target=y): ops.linear_cross_entropy, one launch for the head "
-                         "GEMM, the loss and the head's input gradient) or as the reference's two "
-                         "calls (criterion(model(x), y)); bit-identical results")
+    ap.add_argument("--head-loss", choices=["fused", "separate"], default="separate",
+                    help="toy MLP: the head Linear + cross-entropy as the reference's two calls "
+                         "(criterion(model(x), y), default) or as one fused op (model(x, "
+                         "target=y): ops.linear_cross_entropy, one launch for the head GEMM, the "
+                         "loss and the head's input gradient); bit-identical results, measured at "
+                         "parity (profiles/r10/head_ce_r10.md)")
     ap.add_argument("--comm-cus", type=int, default=None,
                     help="CUs left to RCCL: grid-sized kernels (persistent GEMMs, split-K "
                          "planners) plan for (CUs - N) (TDP_COMM_CUS; default 0)")

@@ -330,7 +330,7 @@ py::tuple head_bwd_op(const Tensor& g, const Tensor& x, const Tensor& w,
 }
 
 // Head Linear + cross-entropy forward in one launch (planes.h head_ce). x [B, I] (B <= 256),
-// w [O, I] (O <= 16), labels [B] int64, ticket: a zeroed int32 scratch word (zero again after
+// w [O, I] (O <= 16), labels [B] int64, ticket: 9 zeroed int32 scratch words (zero again after
 // the launch). Returns [loss, lse [B + 1], logits [B, O]] + with_grad: [dlogits (unit seed),
 // dx [B, I], planes of dx or an empty tensor]; an empty list when the shape is not supported.
 std::vector<Tensor> head_ce_op(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
@@ -342,7 +342,7 @@ std::vector<Tensor> head_ce_op(const Tensor& x, const Tensor& w, const c10::opti
   CHECK_GPU(w); CHECK_F32(w); CHECK_ROWMAJOR(w);
   CHECK_GPU(labels); CHECK_CONTIG(labels); CHECK_GPU(ticket); CHECK_CONTIG(ticket);
   TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
-  TORCH_CHECK(ticket.scalar_type() == at::kInt && ticket.numel() >= 1, "ticket: int32 word");
+  TORCH_CHECK(ticket.scalar_type() == at::kInt && ticket.numel() >= 9, "ticket: 9 int32 words");
   const int B = (int)x.size(0), I = (int)x.size(1), O = (int)w.size(0);
   TORCH_CHECK(w.size(1) == I && labels.numel() == B, "head_ce: shape mismatch");
   const float* bp = nullptr;

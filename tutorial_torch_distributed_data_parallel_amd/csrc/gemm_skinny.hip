@@ -372,7 +372,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwdParams p) {
 //     accumulator) by the LAST workgroup to arrive, over per-row values handed off through
 //     write-through (sc1) stores and an agent-scope ticket (no fences; MI355X_MICROARCH.md
 //     inter-workgroup visibility), in ce_fwd_kernel's summation order: bit-identical loss.
-// The ticket counter is zero between launches (the last arriver resets it).
+// The ticket counters (9 words) are zero between launches (each shard's / the global last
+// arriver resets its own).
 struct HeadCeParams {
   const float* x;
   const float* w;
@@ -432,6 +433,21 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
   }
   valid = wave_sum(valid);
   if (lane == 0) red[w][NMAX] = valid;
+  // the input gradient's W rows (training), loaded now: their L2 round trip overlaps the
+  // logits / loss math below instead of following it
+  constexpr int kDxChunks = 2;  // column chunks of 4 per thread (I <= 2048 per workgroup)
+  const bool do_dx = p.dpre && p.dx;
+  const int span = (p.I / 4 + gridDim.y - 1) / gridDim.y * 4;
+  const int c0 = blockIdx.y * span, c1 = min(p.I, c0 + span);
+  f32x4 wv[kDxChunks][NMAX];
+  if (do_dx) {
+#pragma unroll
+    for (int j = 0; j < kDxChunks; ++j) {
+      const int col = min(c0 + (int)threadIdx.x * 4 + 1024 * j, p.I - 4);
+#pragma unroll
+      for (int k = 0; k < NMAX; ++k) wv[j][k] = *reinterpret_cast<const f32x4*>(brow[k] + col);
+    }
+  }
   __syncthreads();
   if ((int)threadIdx.x < p.O) {
     const int n = threadIdx.x;
@@ -481,21 +497,18 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
   // thread, the O gradients of the row broadcast; same fmaf order), columns split over the
   // gridDim.y workgroups of the row. Every W row of a chunk is loaded up front (rows past O
   // clamped, their terms skipped): the chunk costs one L2 round trip, not O dependent ones.
-  if (p.dpre && p.dx) {
-    const int span = (p.I / 4 + gridDim.y - 1) / gridDim.y * 4;
-    const int c0 = blockIdx.y * span, c1 = min(p.I, c0 + span);
-    for (int col = c0 + threadIdx.x * 4; col < c1; col += 1024) {
-      f32x4 wv[NMAX];
+  if (do_dx) {
 #pragma unroll
-      for (int k = 0; k < NMAX; ++k)
-        wv[k] = *reinterpret_cast<const f32x4*>(brow[k] + col);
+    for (int j = 0; j < kDxChunks; ++j) {
+      const int col = c0 + (int)threadIdx.x * 4 + 1024 * j;
+      if (col >= c1) break;
       f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < NMAX; ++k) {
         if (k < p.O) {
           const float gv = lg[k];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) s4[e] = fmaf(gv, wv[k][e], s4[e]);
+          for (int e = 0; e < 4; ++e) s4[e] = fmaf(gv, wv[j][k][e], s4[e]);
         }
       }
       if (p.gate) {
@@ -516,12 +529,24 @@ __global__ __launch_bounds__(256) void head_ce_kernel(HeadCeParams p) {
       }
     }
   }
-  // ---- ticket: the last workgroup reduces the per-row values
+  // ---- tickets: the row workgroups (blockIdx.y == 0, the ones that stored row values) arrive
+  // on 8 shard counters (row % 8); each shard's last arrival adds to the global counter, whose
+  // last arrival reduces the per-row values (one 255 -> 1 fan-in on one address costs ~3 us:
+  // MI355X_MICROARCH.md "fanin")
+  if (blockIdx.y != 0) return;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 row stores have landed
-    const unsigned t =
-        __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == (unsigned)(gridDim.x * gridDim.y - 1);
+    const int sh = row & 7;
+    const unsigned n_sh = (unsigned)(p.B / 8 + (sh < p.B % 8 ? 1 : 0));
+    const unsigned n_glob = (unsigned)(p.B < 8 ? p.B : 8);
+    unsigned* tk = p.ticket + 1 + sh;
+    int l = 0;
+    if (__hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_sh - 1) {
+      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      l = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          n_glob - 1;
+    }
+    last = l;
   }
   __syncthreads();
   if (!last) return;
@@ -625,7 +650,7 @@ bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bi
              bool mean, float* logits, float* lse, float* rowbuf, unsigned* ticket, float* loss,
              float* acc, float* dpre, float* dx, long lddx, const float* gate, long ldgate,
              uint16_t* dxp, long dxps, hipStream_t s) {
-  if (O < 1 || O > kSkinnyMax || B < 1 || B > 256 || I % 4 || !al16(x) || !al16(w) ||
+  if (O < 1 || O > kSkinnyMax || B < 1 || B > 256 || I % 4 || I < 4 || !al16(x) || !al16(w) ||
       ldx % 4 || ldw % 4 || (dx && (!al16(dx) || lddx % 4 || !dpre)) ||
       (gate && (!al16(gate) || ldgate % 4)) || ((uintptr_t)dxp & 7) || (dxp && !dx))
     return false;
@@ -634,7 +659,8 @@ bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bi
   // training: the row's input-gradient columns split over ys workgroups (each recomputes the
   // row's logits, a few us of L2 reads): B = 128 rows alone would leave half the CUs idle and
   // give every thread 4 dependent column chunks at I = 4096
-  const int ys = dx ? std::max(1, std::min(4, (int)((I / 4 + 511) / 512))) : 1;
+  // (at most 2 chunks of 4 columns per thread: kDxChunks)
+  const int ys = dx ? (int)((I + 2047) / 2048) : 1;
   const dim3 grid(B, ys);
   if (O <= 8) hipLaunchKernelGGL(head_ce_kernel<8>, grid, dim3(256), 0, s, p);
   else if (O <= 10) hipLaunchKernelGGL(head_ce_kernel<10>, grid, dim3(256), 0, s, p);

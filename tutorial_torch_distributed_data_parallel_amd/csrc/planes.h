@@ -61,7 +61,7 @@ bool head_bwd(const float* g, long ldg, const float* x, long ldx, const float* w
 // head_ce_kernel, B <= 256 rows): logits [B][O], lse [B + 1] (lse[B] = valid rows), loss, the
 // metric accumulator acc [3] (optional); with dpre (training): the logits gradient for a unit
 // upstream gradient and, with dx, the input gradient dlogits . W (gated by gate > 0, planes into
-// dxp when given). rowbuf [B][4] scratch; ticket: one zeroed unsigned, zero again afterwards.
+// dxp when given). rowbuf [B][4] scratch; ticket: 9 zeroed unsigned words, zero again afterwards.
 // false = shape not supported (nothing launched).
 bool head_ce(const float* x, long ldx, const float* w, long ldw, const float* bias,
              const int64_t* labels, int B, int O, int I, int ignore_index, float smoothing,

@@ -72,12 +72,12 @@ _TICKETS: dict = {}
 
 
 def _ticket(device) -> torch.Tensor:
-    """A zeroed int32 word per (device, stream) for head_ce's last-arriver ticket (the kernel
-    leaves it zero again; one stream's launches never overlap)."""
+    """Zeroed int32 ticket words per (device, stream) for head_ce's last-arriver hand-off (the
+    kernel leaves them zero again; one stream's launches never overlap)."""
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     t = _TICKETS.get(key)
     if t is None:
-        t = torch.zeros(4, dtype=torch.int32, device=device)
+        t = torch.zeros(16, dtype=torch.int32, device=device)
         _TICKETS[key] = t
     return t
 
