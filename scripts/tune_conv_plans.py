@@ -20,8 +20,19 @@ from tutorial_torch_distributed_data_parallel_amd import ops
 from tutorial_torch_distributed_data_parallel_amd._native import native
 from tutorial_torch_distributed_data_parallel_amd.models.registry import build_model
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from ab_cvec import timeit  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    """us per call of ``fn`` (device events, one untimed call first)."""
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
 
 FD = [(fn, s) for fn in (1, 2) for s in (1, 2, 3, 4, 6, 8)]
 
