@@ -119,6 +119,19 @@ def _prefetch_prev_g(ctx, dx: torch.Tensor):
     return prev if prev is not None and prev.factor_prefetch_g(ctx.prev_w, dx) else None
 
 
+def _dx_buffer(ctx, x2: torch.Tensor) -> torch.Tensor:
+    """The input gradient of a layer whose input is the ReLU output of a factored Linear IS that
+    layer's g (this layer's epilogue applies the mask): written straight into the factored job's
+    gather slot (DDP.factor_g_dest), the g all-gather then runs in place; else a fresh tensor."""
+    if ctx.prev_w is not None and ctx.gate_in and x2.is_cuda:
+        prev = factor_target(ctx.prev_w)
+        if prev is not None:
+            d = prev.factor_g_dest(ctx.prev_w, x2.shape[0])
+            if d is not None and d.shape == x2.shape:
+                return d
+    return torch.empty_like(x2)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, weight, bias, relu: bool, gate_in: bool, fac=None, prev=None):
@@ -170,7 +183,7 @@ class _LinearFn(torch.autograd.Function):
             # update to W (and b) in place and marks them done through note_epilogue (hand_off):
             # the reducer's bucket pass then skips them; otherwise it writes dw / db and the
             # update happens in the reducer's pass
-            dx = torch.empty_like(x2)
+            dx = _dx_buffer(ctx, x2)
             dw = grad_dest(w_param)
             gate = x2 if ctx.gate_in else None
             kw = {}
@@ -199,7 +212,7 @@ class _LinearFn(torch.autograd.Function):
         # input-gradient GEMM it then overlaps (DDP.factor_prefetch_g)
         g_pref = fac is not None and g.is_cuda and fac.factor_prefetch_g(w_param, g)
         if needs(ctx, 0):
-            dx = torch.empty_like(x2)
+            dx = _dx_buffer(ctx, x2)
             # dx[B, in] = g . W : A = g [M=B][K=out], B = W stored [K=out][N=in]
             # (before the weight-gradient GEMM: with an optimizer epilogue that one updates W).
             # When the input is a ReLU output (the previous fused Linear+ReLU), the epilogue

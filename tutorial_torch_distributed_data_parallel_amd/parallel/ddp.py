@@ -756,6 +756,32 @@ class DistributedDataParallel(nn.Module):
             return None
         return self
 
+    def factor_g_dest(self, p, B: int):
+        """Where the producer of factored weight ``p``'s output gradient g [B][out] should write
+        it: this rank's slot of the job's gather buffer, so the g all-gather runs IN PLACE (no
+        local copy of g -- part of RCCL's all-gather at W > 1, a whole blit on the critical path
+        of the one-GPU rehearsal). The producer is the consumer layer's input-gradient GEMM,
+        whose epilogue applies ``p``'s ReLU mask (ops/linear.py): its output IS g. None when
+        ``p`` is not factored in this backward or the slot does not fit (the producer then
+        allocates as usual and the gather reads g out of place)."""
+        if not self._gpu:
+            return None
+        i = self._epi_index.get(id(p))
+        if i is None or i not in self._factor or self.factor_slot(p) is None:
+            return None
+        o, n, _ = self._factor[i]
+        cap = self._factor_cap.get(i)
+        if cap is None or B != cap or self._factor_x_ready.get(i) != B or \
+                2 * self.world_size * cap * (o + n) > o * n:
+            return None
+        g_all = self._factor_buffers(i, cap)[0]
+        return g_all[self.rank * cap * o:(self.rank + 1) * cap * o].view(cap, o)
+
+    def _g_in_slot(self, i, cap, g) -> bool:
+        """``g`` is this rank's slot of weight ``i``'s gather buffer (factor_g_dest)."""
+        o = self._factor[i][0]
+        return g.data_ptr() == self._factor_buffers(i, cap)[0][self.rank * cap * o:].data_ptr()
+
     def _factor_buffers(self, i, cap):
         o, n, _ = self._factor[i]
         key = (i, cap)
@@ -839,7 +865,10 @@ class DistributedDataParallel(nn.Module):
                 2 * self.world_size * cap * (o + n) > o * n:
             return False
         bufs = self._factor_buffers(i, cap)
-        if B == cap:
+        if B == cap and self._g_in_slot(i, cap, g):
+            # the producer wrote g into this rank's slot (factor_g_dest): gathered in place
+            self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o)
+        elif B == cap:
             self._factor_keep.append(g)  # read by the side stream; alive until the next forward
             # the same generic rows all-gather as x's (W slots of cap rows), out of place
             self._backend.prefetch_factor_x(self._factor_bucket[i], bufs[0], cap, o, g)
@@ -914,6 +943,8 @@ class DistributedDataParallel(nn.Module):
         g_src = None
         if g_ready:
             pass  # gathered before the dgrad GEMM (factor_prefetch_g), from g itself
+        elif self._gpu and x_ready and B == cap and self._g_in_slot(i, cap, g):
+            pass  # written into this rank's slot by its producer (factor_g_dest): in place
         elif self._gpu and x_ready and B == cap:
             # out of place: the all-gather reads this rank's g where the layer's backward wrote
             # it (no staging kernel at all)
