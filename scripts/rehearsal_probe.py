@@ -25,6 +25,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--skip-collectives", action="store_true")
     ap.add_argument("--dp1", action="store_true")
+    ap.add_argument("--opt-variant", type=int, default=None,
+                    help="SGD epilogue flags for gemm_f32_set_opt_variant (A/B: 24 = LDS + "
+                         "non-temporal, the default; 88 = + kOptPre)")
     a = ap.parse_args()
     import torch
 
@@ -34,6 +37,10 @@ def main() -> None:
     from tutorial_torch_distributed_data_parallel_amd.parallel import runtime as rt
     from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
 
+    if a.opt_variant is not None:
+        from tutorial_torch_distributed_data_parallel_amd._native import native
+
+        native().gemm_f32_set_opt_variant(a.opt_variant, -1, -1, 0)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     tdp.init_process_group("nccl", rank=0, world_size=1, local_rank=0)
     dev = rt.device()
@@ -65,6 +72,7 @@ def main() -> None:
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1000.0 / a.steps
     print(f"{'dp1' if a.dp1 else 'rehearsal'}{' (no collectives)' if a.skip_collectives else ''}"
+          f"{'' if a.opt_variant is None else f' opt_variant {a.opt_variant}'}"
           f": {ms:.4f} ms/step, buckets {len(ddp._bounds) - 1}, plan {ddp.sync_plan()}",
           flush=True)
     tdp.destroy_process_group()
