@@ -153,10 +153,6 @@ __device__ __forceinline__ f32x16 mfma_emu6(const bf8& ah, const bf8& am, const 
 // optimizer-epilogue variant flags, or-ed into the OPTK template argument next to the kind
 constexpr int kOptWide = 4;  // wider HBM batches: register SGD both row tiles, LDS paths 2x loads
 constexpr int kOptNT = 8;    // non-temporal p / state loads and stores
-// kOptPre (with kOptLds SGD): the tile's first batch of p / momentum loads is issued right after
-// the K loop's first operand DMA, so its HBM round trip runs under the K loop (which moves no
-// HBM bytes of its own) instead of opening the epilogue
-constexpr int kOptPre = 64;
 constexpr int kOptLds = 16;  // 128-wide paired tiles: gradient tile staged through LDS,
                              // float4 p / optimizer-state traffic (SGD and Adam)
 constexpr int kOptG = 32;    // the lockstep kernel's math waves: the finished gradient tile goes
@@ -507,29 +503,6 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
 #pragma unroll
   for (int t = 0; t < S - 1; ++t) issue(t);
 
-  // kOptPre: the HBM lines of the epilogue's first batch (p and momentum rows of the tile's first
-  // half) are touched by one dword load each right after the K loop's first operand DMA, so
-  // their HBM round trip runs under the K loop (which moves no HBM bytes of its own) and the
-  // epilogue's first batch hits L2. Two dummy VGPRs, no data kept in registers (holding the
-  // batch itself spilled: the kernel is at 250 VGPRs); the K loop's first counted wait covers
-  // the loads.
-  constexpr bool PRE = (OPTK & kOptPre) != 0 && (OPTK & 3) == 1 && !AK && FN == 2 &&
-                       (OPTK & kOptLds) != 0 && (OPTK & kOptG) == 0;
-  float pre_d0 = 0.f, pre_d1 = 0.f;
-  if constexpr (PRE) {
-    // the first batch covers tile rows [0, 64): 64 rows x 512 B per array = 256 lines each;
-    // thread t touches line (t & 3) of row t >> 2 in p and in the momentum buffer
-    const int row = m0 + (int)(threadIdx.x >> 2), col = n0 + (int)(threadIdx.x & 3) * 32;
-    if (row < p.M && col < p.N) {
-      const long off = (long)row * p.ldc + col;
-      const float* a0 = p.opt.p + off;
-      asm volatile("global_load_dword %0, %1, off" : "=v"(pre_d0) : "v"(a0) : "memory");
-      if (p.opt.s0 != nullptr) {
-        const float* a1 = p.opt.s0 + off;
-        asm volatile("global_load_dword %0, %1, off" : "=v"(pre_d1) : "v"(a1) : "memory");
-      }
-    }
-  }
   const int h = lane >> 5, l31 = lane & 31;
   // per-lane LDS byte offsets of the fragment reads (within a stage)
   int a_off[FM], b_off[FN];
@@ -730,7 +703,6 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
   for (int kt = 0; kt < nk - 1; ++kt) ktile(kt, std::false_type{});
   if (nk > 0) ktile(nk - 1, std::true_type{});
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
-  if constexpr (PRE) asm volatile("" ::"v"(pre_d0), "v"(pre_d1));  // (kOptPre: landed by now)
   if (do_rs && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
     const int m = m0 + threadIdx.x;
     if (OPTK != 0 && p.bopt.kind != 0) {
@@ -1492,7 +1464,7 @@ static OptVariant& opt_variant() {
 
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs) {
   OptVariant& v = opt_variant();
-  if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds | kOptPre);
+  if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds);
   if (adam >= 0) v.adam = adam & (kOptWide | kOptNT | kOptLds);
   if (persist >= 0) v.persist = persist != 0;
   if (wgs > 0) v.wgs = wgs;
@@ -1643,9 +1615,6 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
           break;
         case kOptLds | kOptNT | kOptWide:
           launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT | kOptWide>(p, fn, st, nb, s);
-          break;
-        case kOptLds | kOptNT | kOptPre:
-          launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT | kOptPre>(p, fn, st, nb, s);
           break;
         case kOptWide: launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide>(p, fn, st, nb, s); break;
         case kOptNT: launch_kinds<kDenseMN, kDenseMN, 1 | kOptNT>(p, fn, st, nb, s); break;
