@@ -97,6 +97,8 @@ def test_bench_self_launch_peer_captured():
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    from bench import LADDER
+    assert rec["config"]["rung"] in [c["name"] for c in LADDER], rec["config"]["rung"]
     assert rec["config"]["launched_by"].startswith("bench.py (self-launched 2 ranks")
     assert rec["config"]["comm_nranks"] == 2
     sync = rec["config"]["sync"]
@@ -118,6 +120,9 @@ def _peer_bench(extra_env, *args):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
     assert rec["n_gpus"] == 2 and rec["value"] > 0
+    if rec["config"]["parallelism"] == "dp2":  # a dp{N} record is always a DDP ladder rung
+        from bench import LADDER
+        assert rec["config"]["rung"] in [c["name"] for c in LADDER], rec["config"]
     return rec
 
 
