@@ -669,29 +669,15 @@ gemm_planes_dual_kernel(PParams p) {
   }
 }
 
-// C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread, the
-// partials summed in z order. NS > 0 (the split count, known at launch): every partial load
-// of a thread is issued before the first add -- one HBM round trip per thread instead of the
-// runtime loop's dependent batches.
-template <int NS>
+// C = epilogue(sum_z ws[z]) over [M][N] (N % 4 == 0), four adjacent outputs per thread
 __global__ __launch_bounds__(kT) void planes_reduce_kernel(PParams p) {
   const long ng = (long)p.M * p.N / 4;
   const long idx = (long)blockIdx.x * kT + threadIdx.x;
   if (idx >= ng) return;
   const f32x4* src = reinterpret_cast<const f32x4*>(p.ws) + idx;
-  f32x4 a;
-  if constexpr (NS > 0) {
-    f32x4 v[NS];
-#pragma unroll
-    for (int z = 0; z < NS; ++z) v[z] = src[z * ng];
-    a = v[0];
-#pragma unroll
-    for (int z = 1; z < NS; ++z) a += v[z];
-  } else {
-    a = src[0];
+  f32x4 a = src[0];
 #pragma unroll 4
-    for (int z = 1; z < p.splits; ++z) a += src[z * ng];
-  }
+  for (int z = 1; z < p.splits; ++z) a += src[z * ng];
   const long e0 = idx * 4;
   const int row = (int)(e0 / p.N), col = (int)(e0 - (long)row * p.N);
   finish4(p, row, col, a);
@@ -913,13 +899,8 @@ void gemm_planes_run(const GemmPlanesArgs& a, const GemmPlan& plan, float* ws, h
   else launch_cfg<false>(p, planes_cfg(), nblocks, s);
   if (plan.splits > 1) {
     const long ng = (long)a.M * a.N / 4;
-    const dim3 grid((unsigned)((ng + kT - 1) / kT));
-    switch (plan.splits) {  // (the toy MLP's skinny GEMMs plan 8 splits on 256 CUs)
-      case 2: hipLaunchKernelGGL(planes_reduce_kernel<2>, grid, dim3(kT), 0, s, p); break;
-      case 4: hipLaunchKernelGGL(planes_reduce_kernel<4>, grid, dim3(kT), 0, s, p); break;
-      case 8: hipLaunchKernelGGL(planes_reduce_kernel<8>, grid, dim3(kT), 0, s, p); break;
-      default: hipLaunchKernelGGL(planes_reduce_kernel<0>, grid, dim3(kT), 0, s, p);
-    }
+    hipLaunchKernelGGL(planes_reduce_kernel, dim3((unsigned)((ng + kT - 1) / kT)), dim3(kT), 0, s,
+                       p);
   }
 }
 
