@@ -2,14 +2,14 @@
 same process -- the A/B switches are setters, not environment knobs (README "Environment
 knobs"). Example (optimizer-epilogue variant 28 = LDS + non-temporal + one batch per tile):
 
-    python scripts/archive/run_with_variant.py --sgd 28 -- bench.py --steps 100
+    python scripts/run_with_variant.py --sgd 28 -- bench.py --steps 100
 """
 import argparse
 import os
 import runpy
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--planes", type=str, default=None, help="stages,pf,splits")
     ap.add_argument("--no-early-g", action="store_true",
                     help="factored g gathers only from the layer's own backward")
+    ap.add_argument("--no-pair-wgrad", action="store_true",
+                    help="world size 1: one launch per weight-gradient + optimizer GEMM")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
@@ -39,6 +41,11 @@ def main():
 
         importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear") \
             .set_early_prev_g(False)
+    if a.no_pair_wgrad:
+        import importlib
+
+        importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear") \
+            .set_pair_wgrad(False)
     sys.argv = [script] + rest[1:]
     runpy.run_path(script if os.path.isabs(script) else os.path.join(ROOT, script),
                    run_name="__main__")

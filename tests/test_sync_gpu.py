@@ -62,8 +62,8 @@ def _reference(kind, init, batches, lr_change_at):
     return out
 
 
-SGD_VARIANTS = [(v, persist) for v in (0, 4, 8, 12, 16, 24, 28) for persist in (1, 0)]
-ADAM_VARIANTS = [(v, persist) for v in (0, 16, 24, 28) for persist in (1, 0)]
+SGD_VARIANTS = [(v, persist) for v in (0, 4, 8, 12, 16, 24, 28, 88) for persist in (1, 0)]
+ADAM_VARIANTS = [(v, persist) for v in (0, 16, 24, 28, 88) for persist in (1, 0)]
 
 
 @pytest.mark.parametrize("kind,variant,persist",
@@ -110,6 +110,62 @@ def test_headline_epilogue_variants_match_torch(pg, kind, variant, persist, monk
                 assert float(d.mean()) < 2e-6, (n, float(d.mean()))
     finally:
         C.gemm_f32_set_opt_variant(*old)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("hidden,captured", [((4096, 4096), False), ((4096, 4096), True),
+                                             ((4096,), False)])
+def test_paired_wgrad_launch_is_bitwise(pg, kind, hidden, captured, monkeypatch):
+    """World size 1: consecutive weight-gradient + optimizer GEMMs held back and run as ONE
+    persistent launch (bindings.cpp gemm_f32_opt hold, gemm_f32_fast_run_pair) give the same
+    parameters, bitwise, as one launch each -- eager and hipGraph-captured; with one hidden layer
+    the held GEMM runs alone at the end of backward (SyncBackend::wait_all)."""
+    tdp = pg
+    from tutorial_torch_distributed_data_parallel_amd.models import ToyMLP
+    import importlib
+
+    from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
+
+    L = importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear")
+
+    monkeypatch.setenv("TDP_OPT_EPILOGUE", "1")
+    batches = _batches(6)
+    out = {}
+    for pair in (False, True):
+        old = L.set_pair_wgrad(pair)
+        try:
+            torch.manual_seed(5)
+            model = ToyMLP(in_features=DIMS[0], hidden=hidden, num_classes=10, device="cuda")
+            init = [p.detach().clone() for p in model.parameters()]
+            ddp = tdp.DDP(model, device_ids=[0])
+            opt = (tdp.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9) if kind == "sgd"
+                   else tdp.optim.Adam(ddp.parameters(), lr=1e-4))
+            assert ddp.register_fused_optimizer(opt) and ddp._epi_on
+            xb = torch.empty_like(batches[0][0])
+            yb = torch.empty_like(batches[0][1])
+
+            def step():
+                opt.zero_grad(set_to_none=True)
+                tdp.ops.cross_entropy(ddp(xb), yb).backward()
+                opt.step()
+
+            if captured:
+                xb.copy_(batches[0][0]); yb.copy_(batches[0][1])
+                g = CapturedStep(step, warmup=1)  # warmup step = batch 0
+                for x, y in batches[1:]:
+                    xb.copy_(x); yb.copy_(y)
+                    g.replay()
+            else:
+                for x, y in batches:
+                    xb.copy_(x); yb.copy_(y)
+                    step()
+            torch.cuda.synchronize()
+            out[pair] = [p.detach().clone() for p in model.parameters()]
+        finally:
+            L.set_pair_wgrad(old)
+    for (n, _), a, b, p0 in zip(model.named_parameters(), out[False], out[True], init):
+        assert not torch.equal(a, p0), n  # every parameter was updated
+        assert torch.equal(a, b), (n, float((a - b).abs().max()))
 
 
 def test_captured_adam_with_lr_change_matches_eager(pg):

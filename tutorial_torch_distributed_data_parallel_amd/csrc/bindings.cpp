@@ -104,9 +104,23 @@ void gemm_f32_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bo
 // [offset, offset + M*N) instead of storing the gradient into C (world size 1, see
 // RcclBackend::epilogue_opt). C must be that contiguous arena slice (its contents are left as
 // they were: the gradient is never materialised).
+// The weight-gradient + optimizer GEMM behind SyncBackend::held_epilogue (gemm_f32_opt
+// hold=True): its arguments, plan and tensors until the next held call pairs with it
+// (gemm_f32_fast_run_pair) or the backend runs it alone at the end of backward.
+struct HeldGemm {
+  GemmF32Args a;
+  GemmPlan plan;
+  // A and B, which the launch reads. Not C or the row sums: the epilogue writes neither, and an
+  // extra reference to a gradient slot would make autograd clone it instead of taking it
+  std::vector<Tensor> keep;
+  hipStream_t stream = nullptr;
+};
+static std::shared_ptr<HeldGemm> g_held;
+static const SyncBackend* g_held_backend = nullptr;
+
 bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig, bool b_kcontig,
                      SyncBackend& backend, int64_t offset, const c10::optional<Tensor>& rowsum,
-                     double rowsum_beta, int64_t bias_offset, int64_t bias_span) {
+                     double rowsum_beta, int64_t bias_offset, int64_t bias_span, bool hold) {
   CHECK_GPU(A); CHECK_GPU(B); CHECK_GPU(C);
   CHECK_F32(A); CHECK_F32(B); CHECK_F32(C);
   CHECK_ROWMAJOR(A); CHECK_ROWMAJOR(B); CHECK_CONTIG(C);
@@ -159,9 +173,38 @@ bool gemm_f32_opt_op(const Tensor& A, const Tensor& B, Tensor& C, bool a_kcontig
     }
   }
   const GemmPlan plan = gemm_f32_plan(a, num_cus(C.get_device()));
+  const hipStream_t s = cur_stream();
+  if (epi && hold) {
+    // world size 1, consecutive layers: the first weight-gradient GEMM waits for the second and
+    // both run as one persistent launch (nothing reads the updated weights before the next
+    // forward; the end of backward runs a GEMM still held)
+    if (backend.held_epilogue && g_held && g_held_backend == &backend && g_held->stream == s &&
+        gemm_f32_fast_pair_ok(g_held->a, g_held->plan, a, plan)) {
+      backend.held_epilogue = nullptr;
+      gemm_f32_fast_run_pair(g_held->a, g_held->plan, a, plan, s);
+      g_held.reset();
+      return epi;
+    }
+    backend.run_held_epilogue(s);  // a held GEMM this one cannot pair with runs alone first
+    if (plan.ws_floats == 0 && (a.rowsum == nullptr || a.bias_opt.kind != 0) &&
+        gemm_f32_fast_pair_ok(a, plan, a, plan)) {
+      auto h = std::make_shared<HeldGemm>();
+      h->a = a;
+      h->plan = plan;
+      h->keep = {A, B};
+      h->stream = s;
+      g_held = h;
+      g_held_backend = &backend;
+      backend.held_epilogue = [h](hipStream_t st) {
+        gemm_f32_run(h->a, h->plan, nullptr, st);
+        h->keep.clear();  // stream-ordered: later users of the memory run after this launch
+      };
+      return epi;
+    }
+  }
   Tensor ws;
   if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, C.options());
-  gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
+  gemm_f32_run(a, plan, plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, s);
   return epi;
 }
 
@@ -1583,7 +1626,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32_opt", &gemm_f32_opt_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("backend"), py::arg("offset"),
         py::arg("rowsum") = py::none(), py::arg("rowsum_beta") = 0.0,
-        py::arg("bias_offset") = -1, py::arg("bias_span") = 0);
+        py::arg("bias_offset") = -1, py::arg("bias_span") = 0, py::arg("hold") = false);
   m.def("gemm_f32_sgd", &gemm_f32_sgd_op, py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("p"), py::arg("buf"),
         py::arg("hyper"), py::arg("nesterov") = false, py::arg("maximize") = false,

@@ -157,6 +157,9 @@ constexpr int kOptLds = 16;  // 128-wide paired tiles: gradient tile staged thro
                              // float4 p / optimizer-state traffic (SGD and Adam)
 constexpr int kOptG = 32;    // the lockstep kernel's math waves: the finished gradient tile goes
                              // to the LDS buffer after the stages (wgrad_lockstep_kernel), no update
+constexpr int kOptPT = 64;   // with kOptNT | kOptLds (SGD, Adam): the updated parameters are stored with
+                             // the default policy (momentum stays non-temporal), so the next
+                             // forward's weight read can hit the 256 MiB Infinity Cache
 
 template <bool NT>
 __device__ __forceinline__ f32x2 ld_epi(const float* q) {
@@ -828,7 +831,8 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             be[c] = bc;
           }
           if constexpr (NT) {
-            __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
+            if constexpr ((OPTK & kOptPT) != 0) *reinterpret_cast<f32x4*>(o.p + gi[i]) = pe;
+            else __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
             if (mom_wr) __builtin_nontemporal_store(be, reinterpret_cast<f32x4*>(o.s0 + gi[i]));
           } else {
             *reinterpret_cast<f32x4*>(o.p + gi[i]) = pe;
@@ -891,7 +895,8 @@ __device__ __forceinline__ void gemm_tile(const FastParams& p, const int lid, ld
             ve[c] = vc;
           }
           if constexpr (NT) {
-            __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
+            if constexpr ((OPTK & kOptPT) != 0) *reinterpret_cast<f32x4*>(o.p + gi[i]) = pe;
+            else __builtin_nontemporal_store(pe, reinterpret_cast<f32x4*>(o.p + gi[i]));
             __builtin_nontemporal_store(me, reinterpret_cast<f32x4*>(o.s0 + gi[i]));
             __builtin_nontemporal_store(ve, reinterpret_cast<f32x4*>(o.s1 + gi[i]));
           } else {
@@ -1224,6 +1229,36 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ge
   }
 }
 
+// Two weight-gradient + optimizer GEMMs of one backward in ONE persistent launch (world size 1,
+// consecutive Linear layers: ops/linear.py holds the first back until the second arrives,
+// SyncBackend::held_epilogue). Each persistent kernel ends on a partial round of tiles (toy MLP
+// fc2: 1024 tiles, fc1: 2304, on 512 workgroups) and restarts its MFMA-only first tiles with
+// no epilogue traffic to overlap; one launch over both tile sets pays that once. Tiles
+// [0, T_p) are p's, the rest q's; same XCD-contiguous split as the single kernel.
+template <int OPTK>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void
+gemm_f32_pair_kernel(FastParams p, FastParams q) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = smem_raw;
+  if (p.prio && ((blockIdx.x >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b % 8;
+  const int Tp = p.tiles_m * p.tiles_n, T = Tp + q.tiles_m * q.tiles_n;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int per = q8 + (xcd < r8 ? 1 : 0);
+  const int before = xcd * q8 + (xcd < r8 ? xcd : r8);
+  const int j = b / 8;
+  const int t0 = (int)((long)T * before / nwg), t1 = (int)((long)T * (before + per) / nwg);
+  if (t1 - t0 > per && j >= per / 2) {
+    __builtin_amdgcn_s_sleep(127);
+    __builtin_amdgcn_s_sleep(127);
+  }
+  for (int lid = t0 + j; lid < t1; lid += per) {
+    if (lid < Tp) gemm_tile<2, kDenseMN, kDenseMN, 2, OPTK, 2, true>(p, lid, smem);
+    else gemm_tile<2, kDenseMN, kDenseMN, 2, OPTK, 2, true>(q, lid - Tp, smem);
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 // Weight gradient + optimizer update with the roles split inside ONE 512-thread workgroup per
 // CU, in lockstep (profiles/r9/wgrad_lockstep_r9*.md). The persistent epilogue kernel above
 // alternates, in every workgroup, a K loop (no HBM traffic) with an HBM-bound update; the two
@@ -1458,14 +1493,14 @@ struct OptVariant {
   bool persist;
 };
 static OptVariant& opt_variant() {
-  static OptVariant v{kOptLds | kOptNT, kOptLds | kOptNT, 2, true};
+  static OptVariant v{kOptLds | kOptNT | kOptPT, kOptLds | kOptNT, 2, true};
   return v;
 }
 
 std::vector<int> gemm_f32_set_opt_variant(int sgd, int adam, int persist, int wgs) {
   OptVariant& v = opt_variant();
-  if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds);
-  if (adam >= 0) v.adam = adam & (kOptWide | kOptNT | kOptLds);
+  if (sgd >= 0) v.sgd = sgd & (kOptWide | kOptNT | kOptLds | kOptPT);
+  if (adam >= 0) v.adam = adam & (kOptWide | kOptNT | kOptLds | kOptPT);
   if (persist >= 0) v.persist = persist != 0;
   if (wgs > 0) v.wgs = wgs;
   return {v.sgd, v.adam, v.persist ? 1 : 0, v.wgs};
@@ -1549,7 +1584,7 @@ void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan) {
   if (o_stages == 2 || o_stages == 3) plan.stages = o_stages;
 }
 
-void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+static FastParams fast_params(const GemmF32Args& a, const GemmPlan& plan, float* ws) {
   FastParams p{};  // zero: every optional pointer (stats, wt, ...) unset unless assigned below
   p.prio = o_emu_prio;
   p.A = a.A; p.B = a.B; p.C = a.C; p.bias = a.bias; p.ws = ws;
@@ -1567,6 +1602,55 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   p.opt = a.opt;
   p.bopt = (a.opt.kind != 0 && a.rowsum != nullptr && a.rowsum_beta == 0.f) ? a.bias_opt
                                                                              : OptEpilogue{};
+  return p;
+}
+
+// The pair launch exists for the default epilogue variants on the persistent 128 x 128 plan.
+static int pair_variant(const GemmF32Args& a, const GemmPlan& plan) {
+  if (!o_emu || plan.lockstep || !plan.fast || plan.skinny || plan.emu8 || plan.grid <= 0 ||
+      plan.splits != 1 || plan.tile != 2 || plan.stages != 2 || plan.bm != 128 ||
+      a.a_kcontig || a.b_kcontig || a.mask || a.gate)
+    return -1;
+  const int v = a.opt.kind == 1 ? opt_variant().sgd : a.opt.kind == 2 ? opt_variant().adam : -1;
+  if (v != (kOptLds | kOptNT) && v != (kOptLds | kOptNT | kOptPT)) return -1;
+  return a.opt.kind | v;
+}
+
+bool gemm_f32_fast_pair_ok(const GemmF32Args& a1, const GemmPlan& p1, const GemmF32Args& a2,
+                           const GemmPlan& p2) {
+  const int v = pair_variant(a1, p1);
+  return v >= 0 && v == pair_variant(a2, p2) && p1.grid == p2.grid;
+}
+
+template <int OPTK>
+static void launch_pair(const FastParams& p, const FastParams& q, int nb, hipStream_t s) {
+  constexpr int STG = 64 * 2 * kBK * 4 + 64 * 2 * kBK * 4;
+  const size_t lds = (size_t)2 * STG;
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)gemm_f32_pair_kernel<OPTK>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    configured = true;
+  }
+  hipLaunchKernelGGL(gemm_f32_pair_kernel<OPTK>, dim3(nb), dim3(kT), lds, s, p, q);
+}
+
+void gemm_f32_fast_run_pair(const GemmF32Args& a1, const GemmPlan& p1, const GemmF32Args& a2,
+                            const GemmPlan& p2, hipStream_t s) {
+  if (!gemm_f32_fast_pair_ok(a1, p1, a2, p2))
+    throw std::runtime_error("gemm_f32_fast_run_pair: the two GEMMs do not share a pair plan");
+  const FastParams p = fast_params(a1, p1, nullptr), q = fast_params(a2, p2, nullptr);
+  const int nb = std::max(1, std::min(p1.grid, p.tiles_m * p.tiles_n + q.tiles_m * q.tiles_n));
+  switch (pair_variant(a1, p1)) {
+    case 1 | kOptLds | kOptNT: launch_pair<1 | kOptLds | kOptNT>(p, q, nb, s); break;
+    case 1 | kOptLds | kOptNT | kOptPT: launch_pair<1 | kOptLds | kOptNT | kOptPT>(p, q, nb, s); break;
+    case 2 | kOptLds | kOptNT: launch_pair<2 | kOptLds | kOptNT>(p, q, nb, s); break;
+    default: launch_pair<2 | kOptLds | kOptNT | kOptPT>(p, q, nb, s); break;
+  }
+}
+
+void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s) {
+  FastParams p = fast_params(a, plan, ws);
   const int nblocks = p.tiles_m * p.tiles_n * plan.splits;
   const bool ak = a.a_kcontig, bk = a.b_kcontig;
   const int fn = plan.tile, st = plan.stages;
@@ -1598,10 +1682,12 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
   }
   if (opt) {
     const int nb = plan.grid > 0 && plan.grid < nblocks ? plan.grid : nblocks;
-    // SGD epilogue variant flags (kOptWide | kOptNT | kOptLds, gemm_f32_set_opt_variant).
-    // Default kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four 0.498), kOptLds
-    // alone 0.468, kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure;
-    // profiles/opt_epilogue_variants.md). With kOptLds, kOptWide = one batch per tile.
+    // SGD epilogue variant flags (kOptWide | kOptNT | kOptLds | kOptPT,
+    // gemm_f32_set_opt_variant). kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four
+    // 0.498), kOptLds alone 0.468, kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure;
+    // profiles/opt_epilogue_variants.md). With kOptLds, kOptWide = one batch per tile. Default
+    // + kOptPT: 0.3588-0.3589 vs 0.3604-0.3628 ms/step interleaved on one box, the forward
+    // planes GEMMs 3.6 us shorter (profiles/r10/param_store_policy_r10m.md).
     // Non-128-wide tiles ignore kOptLds.
     const int variant = opt_variant().sgd;
     // Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam 0.555 ms/step vs 0.566
@@ -1616,6 +1702,9 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
         case kOptLds | kOptNT | kOptWide:
           launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT | kOptWide>(p, fn, st, nb, s);
           break;
+        case kOptLds | kOptNT | kOptPT:
+          launch_kinds<kDenseMN, kDenseMN, 1 | kOptLds | kOptNT | kOptPT>(p, fn, st, nb, s);
+          break;
         case kOptWide: launch_kinds<kDenseMN, kDenseMN, 1 | kOptWide>(p, fn, st, nb, s); break;
         case kOptNT: launch_kinds<kDenseMN, kDenseMN, 1 | kOptNT>(p, fn, st, nb, s); break;
         case kOptWide | kOptNT:
@@ -1625,6 +1714,8 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
       }
     } else if (adam_variant == (kOptLds | kOptNT)) {
       launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT>(p, fn, st, nb, s);
+    } else if (adam_variant == (kOptLds | kOptNT | kOptPT)) {
+      launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT | kOptPT>(p, fn, st, nb, s);
     } else if (adam_variant == (kOptLds | kOptNT | kOptWide)) {
       launch_kinds<kDenseMN, kDenseMN, 2 | kOptLds | kOptNT | kOptWide>(p, fn, st, nb, s);
     } else if (adam_variant == kOptLds) {

@@ -144,6 +144,12 @@ void gemm_skinny_run(int kind, const GemmF32Args& a, hipStream_t s);
 void gemm_opt_fallback(const GemmF32Args& a, hipStream_t s);
 void gemm_f32_fast_plan(const GemmF32Args& a, int num_cus, GemmPlan& plan);
 void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hipStream_t s);
+// two weight-gradient + optimizer GEMMs (both with a.opt) in one persistent launch, when their
+// plans allow it (gemm_f32_fast_pair_ok: the default epilogue variants, persistent 128 x 128)
+bool gemm_f32_fast_pair_ok(const GemmF32Args& a1, const GemmPlan& p1, const GemmF32Args& a2,
+                           const GemmPlan& p2);
+void gemm_f32_fast_run_pair(const GemmF32Args& a1, const GemmPlan& p1, const GemmF32Args& a2,
+                            const GemmPlan& p2, hipStream_t s);
 void gemm_f32_set_lockstep(bool on);  // A/B: false = the persistent epilogue kernel
 bool gemm_f32_lockstep();
 // set by tests/benchmarks: 0 = auto, 1 = force generic kernel, 2 = force fast kernel

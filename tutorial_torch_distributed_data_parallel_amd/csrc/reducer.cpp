@@ -404,6 +404,7 @@ void SyncBackend::begin_iteration(hipStream_t compute) {
   // its stream choice into this one
   launched_side_ = launched_any_ = false;
   forks_.clear();
+  held_epilogue = nullptr;
   for (auto& f : factor_) f.B = 0;
   std::fill(factor_skip_.begin(), factor_skip_.end(), 0);
   std::fill(gdone_set_.begin(), gdone_set_.end(), 0);
@@ -649,6 +650,7 @@ void SyncBackend::run_clip_global(hipStream_t s) {
 }
 
 void SyncBackend::wait_all(hipStream_t compute) {
+  run_held_epilogue(compute);
   flush_forks(compute, true);  // end of backward: nothing left for the compute chain to own
   // 1. join the comm stream: the compute stream waits for every bucket launched on it
   if (launched_side_) {

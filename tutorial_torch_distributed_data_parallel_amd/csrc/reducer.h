@@ -238,6 +238,17 @@ class SyncBackend : public ReducerBackend {
   // storing the gradient; the range is recorded so the bucket update skips it.
   bool epilogue_allowed() const;
   void note_epilogue(int64_t off, int64_t n);
+  // A weight-gradient + optimizer GEMM held back so the next layer's can share its launch
+  // (bindings.cpp gemm_f32_opt hold=True, gemm_f32_fast_run_pair): run by that call, or alone
+  // at the start of wait_all (end of backward); dropped with the iteration's other state by
+  // begin_iteration. The held GEMM's tensors live in the closure until it runs.
+  std::function<void(hipStream_t)> held_epilogue;
+  void run_held_epilogue(hipStream_t s) {
+    if (!held_epilogue) return;
+    auto f = std::move(held_epilogue);
+    held_epilogue = nullptr;
+    f(s);
+  }
 
   // the shard of bucket [begin, end) this rank owns under the sharded update (tail excluded)
   Range owned_shard(int64_t begin, int64_t end) const;

@@ -53,10 +53,21 @@ _EARLY_PREV_G = True  # the consumer's backward starts the previous layer's g ga
 
 
 def set_early_prev_g(on: bool) -> bool:
-    """Turn the one-layer-early g gather on/off (A/B: profiles/archive/scripts/run_with_variant.py); returns the
+    """Turn the one-layer-early g gather on/off (A/B: scripts/run_with_variant.py); returns the
     previous setting."""
     global _EARLY_PREV_G
     old, _EARLY_PREV_G = _EARLY_PREV_G, bool(on)
+    return old
+
+
+_PAIR_WGRAD = True  # world size 1: consecutive weight-gradient + optimizer GEMMs share a launch
+
+
+def set_pair_wgrad(on: bool) -> bool:
+    """Turn the paired weight-gradient + optimizer launch on/off (A/B, tests); returns the
+    previous setting."""
+    global _PAIR_WGRAD
+    old, _PAIR_WGRAD = _PAIR_WGRAD, bool(on)
     return old
 
 
@@ -257,11 +268,13 @@ class _LinearFn(torch.autograd.Function):
                         hand_off(b_param, db)
             elif epi is not None:
                 # world size 1 + fused optimizer: the epilogue updates W and its optimizer state
-                # from the accumulators; the gradient itself is never written to HBM
+                # from the accumulators; the gradient itself is never written to HBM. hold: the
+                # launch waits for the next layer's, and the two run as one persistent kernel
+                # (the backend's end of backward runs one still held)
                 be = bias_epilogue(b_param) if db is not None else None
                 done = C.gemm_f32_opt(g, x2, dw, False, False, epi[0], epi[1], rowsum=db,
                                       bias_offset=be[1] if be else -1,
-                                      bias_span=be[2] if be else 0)
+                                      bias_span=be[2] if be else 0, hold=_PAIR_WGRAD)
                 if done:  # the epilogue ran: W (and b) were updated, their slots never written
                     hand_off(w_param, dw)
                     if be is not None:
