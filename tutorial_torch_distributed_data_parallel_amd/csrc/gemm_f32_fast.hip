@@ -1493,7 +1493,7 @@ struct OptVariant {
   bool persist;
 };
 static OptVariant& opt_variant() {
-  static OptVariant v{kOptLds | kOptNT | kOptPT, kOptLds | kOptNT, 2, true};
+  static OptVariant v{kOptLds | kOptNT, kOptLds | kOptNT | kOptPT, 2, true};
   return v;
 }
 
@@ -1685,13 +1685,14 @@ void gemm_f32_fast_run(const GemmF32Args& a, const GemmPlan& plan, float* ws, hi
     // SGD epilogue variant flags (kOptWide | kOptNT | kOptLds | kOptPT,
     // gemm_f32_set_opt_variant). kOptLds | kOptNT: toy MLP 0.457-0.460 ms/step (one run of four
     // 0.498), kOptLds alone 0.468, kOptNT 0.487, plain 0.507, kOptWide 0.56 (register pressure;
-    // profiles/opt_epilogue_variants.md). With kOptLds, kOptWide = one batch per tile. Default
-    // + kOptPT: 0.3588-0.3589 vs 0.3604-0.3628 ms/step interleaved on one box, the forward
-    // planes GEMMs 3.6 us shorter (profiles/r10/param_store_policy_r10m.md).
+    // profiles/opt_epilogue_variants.md). With kOptLds, kOptWide = one batch per tile. + kOptPT
+    // was -0.6 %, +0.8 % and +-0 % on three boxes: the default stays without it
+    // (profiles/r10/param_store_policy_r10m.md).
     // Non-128-wide tiles ignore kOptLds.
     const int variant = opt_variant().sgd;
-    // Adam epilogue flags (kOptLds | kOptNT). Default both: toy MLP + Adam 0.555 ms/step vs 0.566
-    // LDS only, 0.594 register epilogue (profiles/opt_epilogue_variants.md)
+    // Adam epilogue flags (kOptLds | kOptNT): toy MLP + Adam 0.555 ms/step vs 0.566 LDS only,
+    // 0.594 register epilogue (profiles/opt_epilogue_variants.md); default + kOptPT: -1.2 % and
+    // -0.8 % on two boxes (profiles/r10/param_store_policy_r10m.md)
     const int adam_variant = opt_variant().adam;
     if (a.opt.kind == 1) {
       switch (variant) {
