@@ -105,16 +105,16 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo plumbing config")
     ap.add_argument("--compression", choices=["none", "bf16"], default="none")
     ap.add_argument("--graph", action="store_true",
-                    help="tdp: capture the whole step into a hipGraph and replay it (the default "
-                         "at world size > 1: bucket collectives then overlap backward on the comm "
-                         "stream)")
+                    help="tdp: capture the whole step into a hipGraph and replay it (the default; "
+                         "at world size > 1 the bucket collectives then overlap backward on the "
+                         "comm stream)")
     ap.add_argument("--graph-steps", type=int, default=4,
                     help="training steps per captured hipGraph replay (G steps per graph pay "
                          "the graph-launch gap once per G steps; a group that would cross an "
                          "epoch boundary runs step by step)")
     ap.add_argument("--eager", action="store_true",
-                    help="tdp: run eagerly (the default at world size 1; collectives then run on "
-                         "the compute stream without overlap)")
+                    help="tdp: run eagerly (collectives then run on the compute stream without "
+                         "overlap)")
     ap.add_argument("--fused-opt", choices=["auto", "on", "off"], default="auto",
                     help="tdp: apply the optimizer inside the gradient reduction (DDP "
                          "register_fused_optimizer): with world_size > 1 per bucket and sharded "
@@ -867,11 +867,12 @@ def main():
     if world != a.gpus and "RANK" in os.environ:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_gpu = torch.cuda.is_available() and not a.cpu
-    # captured by default at world size > 1 (collective overlap) and for the toy MLP at world
-    # size 1 too: its eager step is bound by host-side launch work (r6j: eager 0.375-0.47 ms,
-    # captured 0.371-0.374 ms on one box, profiles/r6/bench_modes_r6j.txt)
-    graph = use_gpu and not a.eager and (a.graph or world > 1 or a.model == "toy_mlp") and \
-        a.impl == "tdp"
+    # captured by default: at world size > 1 for the collective overlap; at world size 1 the
+    # toy MLP's eager step is bound by host-side launch work (r6j: eager 0.375-0.47 ms, captured
+    # 0.371-0.374 ms, profiles/r6/bench_modes_r6j.txt) and the CNN steps measured faster
+    # captured on two boxes (ResNet-50 -0.4 / -0.6 %, AlexNet -2.0 %: profiles/r10/bench/r10s_*,
+    # r10t_*); --eager for the eager step
+    graph = use_gpu and not a.eager and a.impl == "tdp"
     in_shape = (dims[0],) if a.model == "toy_mlp" else (3, a.image_size, a.image_size)
     fused = False
     fallbacks = []

@@ -158,19 +158,22 @@ __global__ __launch_bounds__(256) void moments_final(const float* __restrict__ w
   if (cnt_out && blockIdx.x == 0 && threadIdx.x == 0) *cnt_out = cnt;
 }
 
-// First level of the per-tile partial merge: block (channel group of 16, chunk of 256 tiles);
-// 16 lane groups take every 16th tile of the chunk, merged through LDS -> ws [chunks][3][C]
-// (moments_final finishes). Parallel over chunks: a 3136-tile layer-1 output is 13 chunks.
+// First level of the per-tile partial merge: block (channel group of 16, chunk of kPartChunk
+// tiles); 16 lane groups take every 16th tile of the chunk, merged through LDS -> ws
+// [chunks][3][C] (moments_final finishes). Parallel over chunks: a 3136-tile layer-1 output is
+// 49 chunks of 64 (256-tile chunks left 52 workgroups for a 64-channel layer, each lane on a
+// 16-step dependent merge chain: 12.7 us per BN layer in profiles/r9/resnet50_dp1_kernels_r9ai.md)
+constexpr int kPartChunk = 64;
 __global__ __launch_bounds__(256) void moments_partials_l1(const float* __restrict__ part, int T,
                                                            int C, float* __restrict__ ws) {
   __shared__ Wf sh[16][16];
   const int lane = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + lane;
-  const int z0 = blockIdx.y * 256;
+  const int z0 = blockIdx.y * kPartChunk;
   Wf w{0.f, 0.f, 0.f};
   if (c < C) {
 #pragma unroll 4
-    for (int z = z0 + g; z < z0 + 256 && z < T; z += 16) {
+    for (int z = z0 + g; z < z0 + kPartChunk && z < T; z += 16) {
       const float* o = part + (long)z * 3 * C;
       w = wf_merge(w, Wf{o[c], o[C + c], o[2 * C + c]});
     }
@@ -689,11 +692,11 @@ int bn_splits(int N, int C, int HW, int num_cus) {
 
 long bn_ws_floats(int C, int splits) { return 3L * C * (splits > 0 ? splits : 1); }
 
-long bn_partials_ws_floats(int T, int C) { return 3L * C * ((T + 255) / 256); }
+long bn_partials_ws_floats(int T, int C) { return 3L * C * ((T + kPartChunk - 1) / kPartChunk); }
 
 void bn_moments_partials(const float* part, int T, int C, float* ws, float* mean, float* var,
                          float* count_out, float cnt, hipStream_t s) {
-  const int chunks = (T + 255) / 256;
+  const int chunks = (T + kPartChunk - 1) / kPartChunk;
   hipLaunchKernelGGL(moments_partials_l1, dim3((C + 15) / 16, chunks), dim3(256), 0, s, part, T,
                      C, ws);
   hipLaunchKernelGGL(moments_final, dim3((C + 15) / 16), dim3(256), 0, s, ws, C, chunks, mean,
