@@ -418,7 +418,9 @@ def test_padded_channels_last_input_and_native_flatten():
 
 
 @pytest.mark.parametrize("shape", [(8, 64, 28, 28, 64, 3, 1), (4, 256, 14, 14, 1024, 1, 1),
-                                   (2, 4, 33, 29, 64, 7, 2), (3, 128, 9, 9, 512, 1, 1)])
+                                   (2, 4, 33, 29, 64, 7, 2), (3, 128, 9, 9, 512, 1, 1),
+                                   # 113 row tiles: two chunks of the partial merge (64 + 49)
+                                   (16, 64, 30, 30, 64, 3, 1)])
 def test_conv_epilogue_bn_stats(shape):
     """The forward GEMM epilogue's per-tile (count, mean, M2) merged by bn_moments_partials equal
     the moments pass over the stored output; ops.conv2d(bn_stats=True) -> batch_norm uses them."""
