@@ -24,6 +24,9 @@ def main():
                     help="factored g gathers only from the layer's own backward")
     ap.add_argument("--no-pair-wgrad", action="store_true",
                     help="world size 1: one launch per weight-gradient + optimizer GEMM")
+    ap.add_argument("--no-local1d", action="store_true",
+                    help="one-rank BatchNorm1d through the split kernels (statistics, then "
+                         "normalisation; sums, then input gradient)")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
@@ -46,6 +49,11 @@ def main():
 
         importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.linear") \
             .set_pair_wgrad(False)
+    if a.no_local1d:
+        import importlib
+
+        importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.norm") \
+            .set_local1d(False)
     sys.argv = [script] + rest[1:]
     runpy.run_path(script if os.path.isabs(script) else os.path.join(ROOT, script),
                    run_name="__main__")

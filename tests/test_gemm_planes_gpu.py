@@ -286,14 +286,25 @@ def test_cursor_gather_sliced_rows_and_legacy_state(C):
     assert int(cur.state[0]) == 96 and int(cur.state[1:].abs().sum()) == 0
 
 
-def test_batchnorm1d_planes_and_local_merge_match_torch():
+@pytest.mark.parametrize("local1d", [True, False])
+def test_batchnorm1d_planes_and_local_merge_match_torch(local1d):
     """Linear -> BatchNorm1d(+ReLU) -> Linear (the toy MLP's SyncBN config at one rank): the BN
     forward merges its own statistics (one launch) and emits bf16 planes for the next skinny GEMM,
     its backward emits the input gradient's planes; forward, gradients and running statistics
-    match torch in fp64."""
+    match torch in fp64 -- with the one-launch whole-column kernels (local1d) and without."""
     import torch.nn.functional as F
 
     from tutorial_torch_distributed_data_parallel_amd import ops
+    from tutorial_torch_distributed_data_parallel_amd.ops import norm as norm_mod
+
+    prev = norm_mod.set_local1d(local1d)
+    try:
+        _bn1d_chain(F, ops)
+    finally:
+        norm_mod.set_local1d(prev)
+
+
+def _bn1d_chain(F, ops):
 
     torch.manual_seed(11)
     B, I, H, O = 128, 512, 1024, 1024
@@ -349,3 +360,69 @@ def test_split_k_reduce_is_deterministic(C):
         ref = torch.relu((A.double() @ (B.double().t() if bk else B.double())) + bias.double())
         # |C| ~ sqrt(K): fp32 accumulation over K terms, scaled like the other planes tests
         torch.testing.assert_close(outs[0][0].double(), ref, rtol=1e-4, atol=2e-5 * K ** 0.5)
+
+
+@pytest.mark.parametrize("N,Cn", [(128, 4096), (37, 16), (64, 48), (300, 1024), (512, 2064),
+                                  (2, 32)])
+@pytest.mark.parametrize("relu,affine", [(True, True), (False, False)])
+def test_bn1d_local_kernels_match_the_split_path(N, Cn, relu, affine):
+    """csrc/norm.hip bn1d_local_fwd / bn1d_local_bwd (a workgroup per 16 channels over all rows)
+    against the split kernels they replace (bn_moments + bn_elemt_local; bn_bwd_reduce +
+    bn_bwd_elemt) and an fp64 torch oracle: y, stats, running statistics, mask, planes, dx,
+    dw, db."""
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    torch.manual_seed(N + Cn)
+    x = torch.randn(N, Cn, device="cuda") * 1.7 + 0.4
+    w = torch.randn(Cn, device="cuda") if affine else None
+    b = torch.randn(Cn, device="cuda") if affine else None
+    rm1, rv1 = torch.randn(Cn, device="cuda"), torch.rand(Cn, device="cuda") + 0.5
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1, nb2 = (torch.zeros(1, dtype=torch.long, device="cuda") for _ in range(2))
+    mk1 = torch.empty((N, Cn // 4), dtype=torch.uint8, device="cuda") if relu else None
+    mk2 = torch.empty((N, Cn // 4), dtype=torch.uint8, device="cuda") if relu else None
+    pl1, pl2 = (torch.empty((3, N, Cn), dtype=torch.bfloat16, device="cuda") for _ in range(2))
+    y1, st1 = C.bn1d_local_fwd(x, w, b, relu, 1e-5, 0.1, rmean=rm1, rvar=rv1, num_batches=nb1,
+                               mask_out=mk1, planes_out=pl1)
+    mom = C.bn_moments(x)[0]
+    y2, st2 = C.bn_elemt_local(x, mom, w, b, relu, 1e-5, 0.1, rmean=rm2, rvar=rv2,
+                               num_batches=nb2, mask_out=mk2, planes_out=pl2)
+    torch.testing.assert_close(st1, st2, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(y1, y2, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(rm1, rm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-5, atol=1e-6)
+    assert int(nb1) == 1 == int(nb2)
+    xd = x.double()
+    yr = torch.nn.functional.batch_norm(xd, None, None, None if w is None else w.double(),
+                                        None if b is None else b.double(), True, 0.0, 1e-5)
+    if relu:
+        yr = torch.relu(yr)
+        bits = (y1 > 0).view(N, Cn // 4, 4).to(torch.int32)
+        packed = (bits * torch.tensor([1, 2, 4, 8], device="cuda", dtype=torch.int32)).sum(-1)
+        assert torch.equal(mk1.to(torch.int32), packed)
+    torch.testing.assert_close(y1.double(), yr, rtol=1e-4, atol=1e-4)
+    # the planes are the exact split of y
+    assert torch.equal(pl1.double().sum(0).float(), y1)
+    dy = torch.randn(N, Cn, device="cuda")
+    dw1, db1, dw2, db2 = (torch.empty(Cn, device="cuda") for _ in range(4))
+    dpl = torch.empty((3, N, Cn), dtype=torch.bfloat16, device="cuda")
+    dx1 = C.bn1d_local_bwd(dy, x, st1, w, mask=mk1, dw=dw1 if affine else None,
+                           db=db1 if affine else None, planes_out=dpl)
+    kw = {} if mk2 is None else {"mask": mk2}
+    sums = C.bn_bwd_reduce(dy, x, st2, None, dw2 if affine else None, db2 if affine else None,
+                           0.0, **kw)
+    dx2 = C.bn_bwd_elemt(dy, x, st2, w, sums, None, False, **kw)[0]
+    torch.testing.assert_close(dx1, dx2, rtol=1e-4, atol=1e-4)
+    if affine:
+        torch.testing.assert_close(dw1, dw2, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-4)
+    # fp64 oracle of the input gradient
+    xr = xd.clone().requires_grad_()
+    out = torch.nn.functional.batch_norm(xr, None, None, None if w is None else w.double(),
+                                         None if b is None else b.double(), True, 0.0, 1e-5)
+    if relu:
+        out = torch.relu(out)
+    (out * dy.double()).sum().backward()
+    torch.testing.assert_close(dx1.double(), xr.grad, rtol=1e-3, atol=1e-3)
+

@@ -794,6 +794,59 @@ std::vector<Tensor> bn_elemt_local_op(const Tensor& x, const Tensor& moments,
   return {y, stats};
 }
 
+// one rank, a batch of rows: (y, stats) with the statistics computed in the same launch
+// (bn1d_local_fwd); [] when the shape is not taken (the caller runs bn_moments + bn_elemt_local)
+std::vector<Tensor> bn1d_local_fwd_op(const Tensor& x, const c10::optional<Tensor>& w,
+                                      const c10::optional<Tensor>& b, bool relu, double eps,
+                                      double momentum, const c10::optional<Tensor>& rmean,
+                                      const c10::optional<Tensor>& rvar,
+                                      const c10::optional<Tensor>& num_batches,
+                                      const c10::optional<Tensor>& mask_out,
+                                      const c10::optional<Tensor>& planes_out) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2, "bn1d_local_fwd: [rows, C] input");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+                "bn1d_local_fwd: num_batches_tracked must be one int64");
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  for (const auto* t : {&w, &b, &rmean, &rvar})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->numel() == C && (*t)->is_contiguous(), "bn1d_local_fwd: [C] parameters");
+  auto y = at::empty_like(x);
+  auto stats = at::empty({2 * C + 1}, x.options());
+  const bool ok = bn1d_local_fwd(x.data_ptr<float>(), fptr(w), fptr(b), N, C, relu, (float)eps,
+                                 (float)momentum, stats.data_ptr<float>(), fptr(rmean),
+                                 fptr(rvar), nb, y.data_ptr<float>(),
+                                 const_cast<uint8_t*>(mask_ptr(mask_out, x)),
+                                 planes_ptr(planes_out, x), cur_stream());
+  if (!ok) return {};
+  return {y, stats};
+}
+
+// its backward: dx (dw / db overwritten when given); undefined when the shape is not taken
+Tensor bn1d_local_bwd_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
+                         const c10::optional<Tensor>& w, const c10::optional<Tensor>& mask,
+                         const c10::optional<Tensor>& dw, const c10::optional<Tensor>& db,
+                         const c10::optional<Tensor>& planes_out) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "bn1d_local_bwd: [rows, C] dy and x");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  TORCH_CHECK(stats.numel() == 2 * C + 1, "bn1d_local_bwd: stats must be [2C+1]");
+  for (const auto* t : {&dw, &db})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->numel() == C && (*t)->is_contiguous(), "bn1d_local_bwd: [C] gradients");
+  auto dx = at::empty_like(x);
+  const bool ok = bn1d_local_bwd(dy.data_ptr<float>(), x.data_ptr<float>(),
+                                 stats.data_ptr<float>(), fptr(w), N, C, mask_ptr(mask, x),
+                                 dx.data_ptr<float>(), fptr(dw), fptr(db),
+                                 planes_ptr(planes_out, x), cur_stream());
+  if (!ok) return Tensor();
+  return dx;
+}
+
 Tensor bn_eval_op(const Tensor& x, const Tensor& rmean, const Tensor& rvar,
                   const c10::optional<Tensor>& w, const c10::optional<Tensor>& b, double eps,
                   bool relu) {
@@ -1808,6 +1861,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rmean") = py::none(), py::arg("rvar") = py::none(),
         py::arg("num_batches") = py::none(), py::arg("mask_out") = py::none(),
         py::arg("planes_out") = py::none(), py::arg("residual") = py::none());
+  m.def("bn1d_local_fwd", &bn1d_local_fwd_op, py::arg("x"), py::arg("w"), py::arg("b"),
+        py::arg("relu"), py::arg("eps"), py::arg("momentum"), py::arg("rmean") = py::none(),
+        py::arg("rvar") = py::none(), py::arg("num_batches") = py::none(),
+        py::arg("mask_out") = py::none(), py::arg("planes_out") = py::none());
+  m.def("bn1d_local_bwd", &bn1d_local_bwd_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
+        py::arg("w"), py::arg("mask") = py::none(), py::arg("dw") = py::none(),
+        py::arg("db") = py::none(), py::arg("planes_out") = py::none());
   m.def("bn_eval", &bn_eval_op);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("y_relu"), py::arg("dw"), py::arg("db"), py::arg("grad_beta"),

@@ -335,5 +335,20 @@ void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const floa
                   const float* w, const float* sums, const float* y_relu, const float* count,
                   int N, int C, int HW, float* dx, hipStream_t s, float* dres = nullptr,
                   const uint8_t* mask = nullptr, uint16_t* planes_out = nullptr);
+// One rank, a batch of rows (BatchNorm1d on [N][C], N <= kBn1dMaxRows, C % 16 == 0): the
+// statistics and the normalisation in ONE launch -- a workgroup owns 16 channels and ALL N rows,
+// so it needs nobody else's partial sums (bn_moments + bn_elemt_local otherwise). Writes y, the
+// stats [mean | invstd | count], the running statistics, the batch counter, and optionally the
+// ReLU mask / bf16 planes exactly as bn_elemt_local does. false = shape not taken (nothing ran).
+constexpr int kBn1dMaxRows = 512;
+bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C, bool relu,
+                    float eps, float momentum, float* stats, float* rmean, float* rvar,
+                    int64_t* nbt, float* y, uint8_t* mask_out, uint16_t* planes_out,
+                    hipStream_t s);
+// The matching backward, one launch: sums (bn_bwd_reduce), dw / db (overwritten, when given) and
+// dx (+ planes) from the same registers (bn_bwd_elemt). mask: the forward's ReLU mask or null.
+bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const float* w, int N,
+                    int C, const uint8_t* mask, float* dx, float* dw, float* db,
+                    uint16_t* planes_out, hipStream_t s);
 
 }  // namespace tdp

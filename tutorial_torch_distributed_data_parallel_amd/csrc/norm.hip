@@ -638,6 +638,158 @@ __global__ __launch_bounds__(256) void bwd_elemt_rows4(
   }
 }
 
+// ------------------------------------------------------- BatchNorm1d, one rank, whole columns
+// A workgroup owns 16 channels (4 quads) and every row of a [N <= 512][C] batch: thread t takes
+// quad t & 3 and rows t >> 2, t >> 2 + 64, ... (IT = ceil(N / 64) float4 per thread, held in
+// registers between the reduction and the element pass), so the column sums need no cross-
+// workgroup partials: statistics + normalisation (and sums + input gradient in the backward) are
+// one launch each instead of bn_moments + bn_elemt_local (bn_bwd_reduce + its final merge +
+// bn_bwd_elemt). The element formulas are elemt_rows4's / bwd_elemt_rows4's.
+constexpr int kB1Cols = 16, kB1Lanes = 64;
+
+// per-channel sums of the block's 64 row groups, tree-reduced in a fixed order; every thread
+// returns its quad's 4 totals
+__device__ __forceinline__ f32x4 b1_reduce(f32x4 v, f32x4 (*sh)[4]) {
+  const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  sh[rg][q] = v;
+#pragma unroll
+  for (int st = kB1Lanes / 2; st > 0; st >>= 1) {
+    __syncthreads();
+    if (rg < st) sh[rg][q] += sh[rg + st][q];
+  }
+  __syncthreads();
+  const f32x4 r = sh[0][q];
+  __syncthreads();  // sh is reused by the next reduction
+  return r;
+}
+
+template <int IT>
+__global__ __launch_bounds__(256) void bn1d_local_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bb, int N,
+    int C, int relu, float eps, float momentum, float* __restrict__ stats,
+    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float* __restrict__ y, uint8_t* __restrict__ mk, uint16_t* __restrict__ pl) {
+  __shared__ f32x4 sh[kB1Lanes][4];
+  const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int c = blockIdx.x * kB1Cols + 4 * q;
+  f32x4 v[IT];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rg + kB1Lanes * i;
+    v[i] = r < N ? *reinterpret_cast<const f32x4*>(x + (long)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i];
+  }
+  const float n = (float)N;
+  const f32x4 mean = b1_reduce(s, sh) / n;
+  f32x4 m2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    if (rg + kB1Lanes * i < N) {
+      const f32x4 d = v[i] - mean;
+      m2 += d * d;
+    }
+  }
+  const f32x4 var = b1_reduce(m2, sh) / n;
+  float sc[4], sf[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float is = rsqrtf(var[j] + eps);
+    sc[j] = is * (w ? w[c + j] : 1.f);
+    sf[j] = (bb ? bb[c + j] : 0.f) - mean[j] * sc[j];
+    if (rg == 0) {
+      stats[c + j] = mean[j];
+      stats[C + c + j] = is;
+      if (rmean) {
+        const float unbiased = n > 1.f ? var[j] * n / (n - 1.f) : var[j];
+        rmean[c + j] = fmaf(momentum, mean[j] - rmean[c + j], rmean[c + j]);
+        rvar[c + j] = fmaf(momentum, unbiased - rvar[c + j], rvar[c + j]);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stats[2 * C] = n;
+    if (nbt) *nbt += 1;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rg + kB1Lanes * i;
+    if (r >= N) continue;
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = fmaf(v[i][j], sc[j], sf[j]);
+      o[j] = relu ? fmaxf(t, 0.f) : t;
+    }
+    *reinterpret_cast<f32x4*>(y + (long)r * C + c) = o;
+    if (pl) store_planes4(pl + (long)r * C + c, (long)N * C, o[0], o[1], o[2], o[3]);
+    if (mk)
+      mk[((long)r * C + c) >> 2] = (uint8_t)((o[0] > 0.f ? 1 : 0) | (o[1] > 0.f ? 2 : 0) |
+                                             (o[2] > 0.f ? 4 : 0) | (o[3] > 0.f ? 8 : 0));
+  }
+}
+
+template <int IT>
+__global__ __launch_bounds__(256) void bn1d_local_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ stats,
+    const float* __restrict__ w, int N, int C, const uint8_t* __restrict__ mk,
+    float* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
+    uint16_t* __restrict__ pl) {
+  __shared__ f32x4 sh[kB1Lanes][4];
+  const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int c = blockIdx.x * kB1Cols + 4 * q;
+  const f32x4 mu = *reinterpret_cast<const f32x4*>(stats + c);
+  f32x4 d[IT], xv[IT];
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rg + kB1Lanes * i;
+    if (r < N) {
+      const long off = (long)r * C + c;
+      d[i] = *reinterpret_cast<const f32x4*>(dy + off);
+      xv[i] = *reinterpret_cast<const f32x4*>(x + off);
+      if (mk) {
+        const uint32_t bits = mk[off >> 2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = ((bits >> j) & 1u) ? d[i][j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] += d[i][j];
+        m[j] = fmaf(d[i][j], xv[i][j] - mu[j], m[j]);
+      }
+    }
+  }
+  const f32x4 sdy = b1_reduce(a, sh);
+  const f32x4 sdyx = b1_reduce(m, sh);
+  const float inv_count = 1.f / stats[2 * C];
+  float k1[4], k2[4], k3[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float is = stats[C + c + j];
+    if (rg == 0) {
+      if (dw) dw[c + j] = sdyx[j] * is;
+      if (db) db[c + j] = sdy[j];
+    }
+    const float mdy = sdy[j] * inv_count, mdyx = sdyx[j] * inv_count;
+    const float sw = is * (w ? w[c + j] : 1.f);
+    const float qq = is * is * mdyx;
+    k1[j] = sw;
+    k2[j] = -qq * sw;
+    k3[j] = (mu[j] * qq - mdy) * sw;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = rg + kB1Lanes * i;
+    if (r >= N) continue;
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaf(d[i][j], k1[j], fmaf(xv[i][j], k2[j], k3[j]));
+    *reinterpret_cast<f32x4*>(dx + (long)r * C + c) = o;
+    if (pl) store_planes4(pl + (long)r * C + c, (long)N * C, o[0], o[1], o[2], o[3]);
+  }
+}
+
 inline bool rows4_ok(int C, int HW, std::initializer_list<const void*> ptrs) {
   if (HW != 1 || C % 4) return false;
   for (const void* q : ptrs)
@@ -807,6 +959,43 @@ void bn_bwd_elemt(const float* dy, const float* x, const float* mean, const floa
   const long total = (long)N * C * HW;
   hipLaunchKernelGGL(bwd_elemt_kernel, dim3(ew_grid(total)), dim3(256), 0, s, dy, x, mean, invstd,
                      w, sums, y_relu, count, total, C, HW, dx);
+}
+
+bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C, bool relu,
+                    float eps, float momentum, float* stats, float* rmean, float* rvar,
+                    int64_t* nbt, float* y, uint8_t* mask_out, uint16_t* planes_out,
+                    hipStream_t s) {
+  if (N < 1 || N > kBn1dMaxRows || C % kB1Cols) return false;
+  for (const void* q : {(const void*)x, (const void*)y, (const void*)w, (const void*)b})
+    if (q && ((uintptr_t)q & 15)) return false;
+  const dim3 g(C / kB1Cols), t(256);
+  const int r = relu ? 1 : 0;
+  uint8_t* mk = relu ? mask_out : nullptr;
+#define B1F(IT) hipLaunchKernelGGL(bn1d_local_fwd_kernel<IT>, g, t, 0, s, x, w, b, N, C, r, eps, \
+                                   momentum, stats, rmean, rvar, nbt, y, mk, planes_out)
+  if (N <= 64) B1F(1);
+  else if (N <= 128) B1F(2);
+  else if (N <= 256) B1F(4);
+  else B1F(8);
+#undef B1F
+  return true;
+}
+
+bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const float* w, int N,
+                    int C, const uint8_t* mask, float* dx, float* dw, float* db,
+                    uint16_t* planes_out, hipStream_t s) {
+  if (N < 1 || N > kBn1dMaxRows || C % kB1Cols) return false;
+  for (const void* q : {(const void*)dy, (const void*)x, (const void*)dx, (const void*)stats})
+    if (q && ((uintptr_t)q & 15)) return false;
+  const dim3 g(C / kB1Cols), t(256);
+#define B1B(IT) hipLaunchKernelGGL(bn1d_local_bwd_kernel<IT>, g, t, 0, s, dy, x, stats, w, N, C, \
+                                   mask, dx, dw, db, planes_out)
+  if (N <= 64) B1B(1);
+  else if (N <= 128) B1B(2);
+  else if (N <= 256) B1B(4);
+  else B1B(8);
+#undef B1B
+  return true;
 }
 
 }  // namespace tdp

@@ -97,6 +97,16 @@ _TORCH_K = _TorchKernels()
 
 
 
+_LOCAL1D = True  # one-rank BatchNorm1d in one launch per direction (set_local1d: A/B, tests)
+
+
+def set_local1d(on: bool) -> bool:
+    """Turn the one-launch one-rank BatchNorm1d path on/off; returns the previous setting."""
+    global _LOCAL1D
+    old, _LOCAL1D = _LOCAL1D, bool(on)
+    return old
+
+
 def _is_nhwc(x) -> bool:
     return x.dim() == 4 and not x.is_contiguous() and \
         x.is_contiguous(memory_format=torch.channels_last)
@@ -129,11 +139,6 @@ class _BatchNormFn(torch.autograd.Function):
         if residual is not None:
             residual = _rows(residual.contiguous(memory_format=torch.channels_last)) \
                 if ctx.nhwc else residual.contiguous()
-        if part is not None and ctx.nhwc:
-            # statistics from the producing convolution's GEMM epilogue (per-tile Chan merge)
-            st = native().bn_moments_partials(part, float(x.shape[0]))
-        else:
-            st = K.bn_moments(x)[0]
         # [rows, C % 4] form on the GPU: the backward reads a 1-byte-per-4-channels ReLU mask
         # instead of the float output (1/16 of the bytes, twice per backward)
         mask = None
@@ -145,7 +150,24 @@ class _BatchNormFn(torch.autograd.Function):
         if rows4 and not ctx.nhwc and planes_input_fit(x.shape[0], C):
             pl = torch.empty((3, x.shape[0], C), dtype=torch.bfloat16, device=x.device)
         y = None
-        if group is None and rows4:
+        # one rank, a batch of rows (BatchNorm1d): statistics + normalisation in one launch, and
+        # the backward likewise (csrc/norm.hip bn1d_local_fwd / bn1d_local_bwd)
+        ctx.local1d = False
+        if group is None and rows4 and not ctx.nhwc and residual is None and part is None and \
+                _LOCAL1D:
+            r = native().bn1d_local_fwd(x, weight, bias, relu, float(eps), float(momentum),
+                                        rmean=running_mean, rvar=running_var,
+                                        num_batches=num_batches, mask_out=mask, planes_out=pl)
+            if r:
+                y, stats = r
+                ctx.local1d = True
+        if y is None:
+            if part is not None and ctx.nhwc:
+                # statistics from the producing convolution's GEMM epilogue (per-tile Chan merge)
+                st = native().bn_moments_partials(part, float(x.shape[0]))
+            else:
+                st = K.bn_moments(x)[0]
+        if y is None and group is None and rows4:
             # one rank: bn_merge's work runs inside the normalisation pass (one launch fewer)
             r = native().bn_elemt_local(x, st, weight, bias, relu, float(eps), float(momentum),
                                         rmean=running_mean, rvar=running_var,
@@ -181,6 +203,17 @@ class _BatchNormFn(torch.autograd.Function):
         dw = grad_dest(w_param) if (w_param is not None and needs(ctx, 1)) else None
         db = grad_dest(b_param) if (b_param is not None and needs(ctx, 2)) else None
         mk = {} if mask is None else {"mask": mask}
+        if ctx.local1d and ctx.group is None:
+            # one launch: the column sums, dw / db and dx (+ its planes) of a whole-rows batch
+            pl = None
+            if needs(ctx, 0) and planes_input_fit(x.shape[0], x.shape[1]):
+                pl = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+            dx = native().bn1d_local_bwd(dy, x, stats, weight, mask=mask, dw=dw, db=db,
+                                         planes_out=pl)
+            if pl is not None:
+                attach_planes(dx, pl)
+            return (dx if needs(ctx, 0) else None), dw, db, None, None, None, None, None, None, \
+                None, None, None, None
         sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0, **mk)
         dx = dres = None
         want_res = ctx.has_res and needs(ctx, 9)
