@@ -830,7 +830,8 @@ std::vector<Tensor> bn1d_local_fwd_op(const Tensor& x, const c10::optional<Tenso
 Tensor bn1d_local_bwd_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
                          const c10::optional<Tensor>& w, const c10::optional<Tensor>& mask,
                          const c10::optional<Tensor>& dw, const c10::optional<Tensor>& db,
-                         const c10::optional<Tensor>& planes_out) {
+                         const c10::optional<Tensor>& planes_out, SyncBackend* backend,
+                         int64_t w_offset, int64_t w_span, int64_t b_offset, int64_t b_span) {
   CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "bn1d_local_bwd: [rows, C] dy and x");
   const int N = (int)x.size(0), C = (int)x.size(1);
@@ -838,12 +839,45 @@ Tensor bn1d_local_bwd_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
   for (const auto* t : {&dw, &db})
     if (t->has_value() && (*t)->defined())
       TORCH_CHECK((*t)->numel() == C && (*t)->is_contiguous(), "bn1d_local_bwd: [C] gradients");
+  // world size 1 + fused optimizer (backend given): w / b updated in place by the kernel, their
+  // arena ranges marked done for the reducer (as head_bwd does)
+  OptEpilogue wo, bo;
+  if (backend != nullptr && (w_offset >= 0 || b_offset >= 0)) {
+    TORCH_CHECK(backend->epilogue_allowed(), "bn1d_local_bwd: optimizer epilogue not allowed");
+    auto ops = std::dynamic_pointer_cast<RcclOps>(backend->ops());
+    TORCH_CHECK(ops != nullptr, "bn1d_local_bwd: optimizer epilogue needs the device backend");
+    const FusedOptimizer& f = ops->fused;
+    auto at_off = [&](int64_t off) {
+      OptEpilogue o;
+      o.kind = f.kind;
+      o.p = f.p + off;
+      o.s0 = f.s0 ? f.s0 + off : nullptr;
+      o.s1 = f.s1 ? f.s1 + off : nullptr;
+      o.s2 = f.s2 ? f.s2 + off : nullptr;
+      o.sgd = f.sgd;
+      o.adam = f.adam;
+      return o;
+    };
+    if (w_offset >= 0) {
+      TORCH_CHECK(w_span >= C && w.has_value() && w->defined() &&
+                      w->data_ptr<float>() == f.p + w_offset,
+                  "bn1d_local_bwd: w must be the arena parameter at w_offset");
+      wo = at_off(w_offset);
+    }
+    if (b_offset >= 0) {
+      TORCH_CHECK(b_span >= C, "bn1d_local_bwd: bias span shorter than the bias");
+      bo = at_off(b_offset);
+    }
+  }
   auto dx = at::empty_like(x);
   const bool ok = bn1d_local_bwd(dy.data_ptr<float>(), x.data_ptr<float>(),
                                  stats.data_ptr<float>(), fptr(w), N, C, mask_ptr(mask, x),
                                  dx.data_ptr<float>(), fptr(dw), fptr(db),
-                                 planes_ptr(planes_out, x), cur_stream());
+                                 planes_ptr(planes_out, x), cur_stream(), wo.kind ? &wo : nullptr,
+                                 bo.kind ? &bo : nullptr);
   if (!ok) return Tensor();
+  if (wo.kind) backend->note_epilogue(w_offset, w_span);
+  if (bo.kind) backend->note_epilogue(b_offset, b_span);
   return dx;
 }
 
@@ -1867,7 +1901,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask_out") = py::none(), py::arg("planes_out") = py::none());
   m.def("bn1d_local_bwd", &bn1d_local_bwd_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("w"), py::arg("mask") = py::none(), py::arg("dw") = py::none(),
-        py::arg("db") = py::none(), py::arg("planes_out") = py::none());
+        py::arg("db") = py::none(), py::arg("planes_out") = py::none(),
+        py::arg("backend") = nullptr, py::arg("w_offset") = -1, py::arg("w_span") = 0,
+        py::arg("b_offset") = -1, py::arg("b_span") = 0);
   m.def("bn_eval", &bn_eval_op);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("y_relu"), py::arg("dw"), py::arg("db"), py::arg("grad_beta"),

@@ -347,8 +347,10 @@ bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C
                     hipStream_t s);
 // The matching backward, one launch: sums (bn_bwd_reduce), dw / db (overwritten, when given) and
 // dx (+ planes) from the same registers (bn_bwd_elemt). mask: the forward's ReLU mask or null.
+// wopt / bopt (world size 1, fused optimizer): update w / b in place instead of writing dw / db.
 bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const float* w, int N,
                     int C, const uint8_t* mask, float* dx, float* dw, float* db,
-                    uint16_t* planes_out, hipStream_t s);
+                    uint16_t* planes_out, hipStream_t s, const OptEpilogue* wopt = nullptr,
+                    const OptEpilogue* bopt = nullptr);
 
 }  // namespace tdp

@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "optim_elem.h"
 #include "split_bf16.h"
 
 namespace tdp {
@@ -729,15 +730,56 @@ __global__ __launch_bounds__(256) void bn1d_local_fwd_kernel(
   }
 }
 
+// One parameter element's optimizer step, split so that its loads (hyper block, p, state) are
+// issued at kernel start and the update itself costs no memory round trip at the end
+struct OptElem {
+  OptEpilogue o;
+  float p, s0, s1;
+  __device__ __forceinline__ void load(const OptEpilogue& e, int i) {
+    o = e;
+    if (o.kind == 1) {
+      load_hyper(o.sgd);
+      p = o.p[i];
+      s0 = (o.sgd.momentum != 0.f && !o.sgd.first_step) ? o.s0[i] : 0.f;
+    } else if (o.kind == 2) {
+      load_hyper(o.adam);
+      p = o.p[i];
+      s0 = o.s0[i];
+      s1 = o.s1[i];
+    }
+  }
+  __device__ __forceinline__ void step(int i, float g) {
+    if (o.kind == 1) {
+      sgd_elem(p, g, s0, o.sgd);
+      o.p[i] = p;
+      if (o.sgd.momentum != 0.f) o.s0[i] = s0;
+    } else if (o.kind == 2) {
+      adam_elem(p, g, s0, s1, o.s2 ? o.s2 + i : nullptr, o.adam);
+      o.p[i] = p;
+      o.s0[i] = s0;
+      o.s1[i] = s1;
+    }
+  }
+};
+
 template <int IT>
 __global__ __launch_bounds__(256) void bn1d_local_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ stats,
     const float* __restrict__ w, int N, int C, const uint8_t* __restrict__ mk,
     float* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    uint16_t* __restrict__ pl) {
+    uint16_t* __restrict__ pl, OptEpilogue wo, OptEpilogue bo) {
   __shared__ f32x4 sh[kB1Lanes][4];
+  __shared__ float tot[2][kB1Cols];  // this block's sum dy | sum dy (x - mean), per channel
   const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
   const int c = blockIdx.x * kB1Cols + 4 * q;
+  // in-place update (wo / bo): thread t < 32 owns element t & 15 of w (t < 16) or b; its loads go
+  // out now, behind the streaming loads below
+  const bool upd = (wo.kind || bo.kind) && threadIdx.x < 2 * kB1Cols;
+  const int uc = blockIdx.x * kB1Cols + (threadIdx.x & (kB1Cols - 1));
+  const bool ub = threadIdx.x >= kB1Cols;
+  OptElem ue;
+  ue.o.kind = 0;
+  if (upd) ue.load(ub ? bo : wo, uc);
   const f32x4 mu = *reinterpret_cast<const f32x4*>(stats + c);
   f32x4 d[IT], xv[IT];
   f32x4 a = {0.f, 0.f, 0.f, 0.f}, m = {0.f, 0.f, 0.f, 0.f};
@@ -767,16 +809,29 @@ __global__ __launch_bounds__(256) void bn1d_local_bwd_kernel(
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float is = stats[C + c + j];
-    if (rg == 0) {
-      if (dw) dw[c + j] = sdyx[j] * is;
-      if (db) db[c + j] = sdy[j];
-    }
     const float mdy = sdy[j] * inv_count, mdyx = sdyx[j] * inv_count;
     const float sw = is * (w ? w[c + j] : 1.f);
     const float qq = is * is * mdyx;
     k1[j] = sw;
     k2[j] = -qq * sw;
     k3[j] = (mu[j] * qq - mdy) * sw;
+  }
+  // dw / db are complete here. World size 1 + fused optimizer: the affine parameters are
+  // updated in place (the optimizer's element update, as the weight-gradient GEMM epilogue does)
+  // instead of storing their gradients, once every thread has read w
+  if (rg == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gw = sdyx[j] * stats[C + c + j], gb = sdy[j];
+      if (!wo.kind && dw) dw[c + j] = gw;
+      if (!bo.kind && db) db[c + j] = gb;
+      tot[0][4 * q + j] = gb;
+      tot[1][4 * q + j] = gw;
+    }
+  }
+  if (wo.kind || bo.kind) {
+    __syncthreads();
+    if (upd && ue.o.kind) ue.step(uc, tot[ub ? 0 : 1][threadIdx.x & (kB1Cols - 1)]);
   }
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -983,13 +1038,15 @@ bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C
 
 bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const float* w, int N,
                     int C, const uint8_t* mask, float* dx, float* dw, float* db,
-                    uint16_t* planes_out, hipStream_t s) {
+                    uint16_t* planes_out, hipStream_t s, const OptEpilogue* wopt,
+                    const OptEpilogue* bopt) {
   if (N < 1 || N > kBn1dMaxRows || C % kB1Cols) return false;
   for (const void* q : {(const void*)dy, (const void*)x, (const void*)dx, (const void*)stats})
     if (q && ((uintptr_t)q & 15)) return false;
   const dim3 g(C / kB1Cols), t(256);
+  const OptEpilogue wo = wopt ? *wopt : OptEpilogue{}, bo = bopt ? *bopt : OptEpilogue{};
 #define B1B(IT) hipLaunchKernelGGL(bn1d_local_bwd_kernel<IT>, g, t, 0, s, dy, x, stats, w, N, C, \
-                                   mask, dx, dw, db, planes_out)
+                                   mask, dx, dw, db, planes_out, wo, bo)
   if (N <= 64) B1B(1);
   else if (N <= 128) B1B(2);
   else if (N <= 256) B1B(4);

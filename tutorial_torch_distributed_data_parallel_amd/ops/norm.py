@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import native
-from ._grad import grad_dest, needs
+from ._grad import bias_epilogue, grad_dest, hand_off, needs
 from .linear import attach_planes, planes_input_fit
 
 
@@ -98,12 +98,16 @@ _TORCH_K = _TorchKernels()
 
 
 _LOCAL1D = True  # one-rank BatchNorm1d in one launch per direction (set_local1d: A/B, tests)
+_LOCAL1D_UPDATE = True  # ... whose backward also applies the fused optimizer to w / b
 
 
-def set_local1d(on: bool) -> bool:
-    """Turn the one-launch one-rank BatchNorm1d path on/off; returns the previous setting."""
-    global _LOCAL1D
+def set_local1d(on: bool, update: bool | None = None) -> bool:
+    """Turn the one-launch one-rank BatchNorm1d path on/off (``update``: its in-place optimizer
+    step on w / b); returns the previous setting of the path."""
+    global _LOCAL1D, _LOCAL1D_UPDATE
     old, _LOCAL1D = _LOCAL1D, bool(on)
+    if update is not None:
+        _LOCAL1D_UPDATE = bool(update)
     return old
 
 
@@ -208,8 +212,25 @@ class _BatchNormFn(torch.autograd.Function):
             pl = None
             if needs(ctx, 0) and planes_input_fit(x.shape[0], x.shape[1]):
                 pl = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+            # world size 1 + fused optimizer: the kernel that completes dw / db also applies the
+            # update to w / b (hand_off: their slots go to autograd unwritten)
+            kw = {}
+            be_w = bias_epilogue(w_param) if (dw is not None and _LOCAL1D_UPDATE) else None
+            be_b = bias_epilogue(b_param) if (db is not None and _LOCAL1D_UPDATE) else None
+            if be_w is not None and (be_b is None or be_b[0] is be_w[0]):
+                kw.update(backend=be_w[0], w_offset=be_w[1], w_span=be_w[2])
+            else:
+                be_w = None
+            if be_b is not None and (not kw or kw["backend"] is be_b[0]):
+                kw.update(backend=be_b[0], b_offset=be_b[1], b_span=be_b[2])
+            else:
+                be_b = None
             dx = native().bn1d_local_bwd(dy, x, stats, weight, mask=mask, dw=dw, db=db,
-                                         planes_out=pl)
+                                         planes_out=pl, **kw)
+            if be_w is not None:
+                hand_off(w_param, dw)
+            if be_b is not None:
+                hand_off(b_param, db)
             if pl is not None:
                 attach_planes(dx, pl)
             return (dx if needs(ctx, 0) else None), dw, db, None, None, None, None, None, None, \
