@@ -217,6 +217,9 @@ class _BatchNormFn(torch.autograd.Function):
             kw = {}
             be_w = bias_epilogue(w_param) if (dw is not None and _LOCAL1D_UPDATE) else None
             be_b = bias_epilogue(b_param) if (db is not None and _LOCAL1D_UPDATE) else None
+            # only a DDP reducer backend (a tensor-sharded wrapper's target has no span)
+            be_w = be_w if (be_w is not None and be_w[2] is not None) else None
+            be_b = be_b if (be_b is not None and be_b[2] is not None) else None
             if be_w is not None and (be_b is None or be_b[0] is be_w[0]):
                 kw.update(backend=be_w[0], w_offset=be_w[1], w_span=be_w[2])
             else:
