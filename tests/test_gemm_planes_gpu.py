@@ -426,3 +426,45 @@ def test_bn1d_local_kernels_match_the_split_path(N, Cn, relu, affine):
     (out * dy.double()).sum().backward()
     torch.testing.assert_close(dx1.double(), xr.grad, rtol=1e-3, atol=1e-3)
 
+
+
+@pytest.mark.parametrize("Cn", [16, 1024])
+def test_bn1d_sync_halves_match_the_split_path(Cn):
+    """SyncBatchNorm halves of the whole-column kernels: bn1d_moments (= bn_moments), then --
+    over the all-gathered moments of three ranks (one of them empty, dropped as torch does) --
+    bn1d_gathered_fwd (= bn_merge + bn_elemt, bitwise: the same merge order and formulas), and
+    bn1d_sums (= bn_bwd_reduce: local sums, dw, db)."""
+    from tutorial_torch_distributed_data_parallel_amd._native import native
+
+    C = native()
+    torch.manual_seed(Cn)
+    xs = [torch.randn(n, Cn, device="cuda") * (1 + r) + r for r, n in enumerate((128, 77, 200))]
+    moms = [C.bn1d_moments(x) for x in xs]
+    for x, m in zip(xs, moms):
+        ref = C.bn_moments(x)[0]
+        torch.testing.assert_close(m[:2 * Cn], ref[:2 * Cn], rtol=1e-5, atol=1e-5)
+        assert m[2 * Cn].item() == x.shape[0]
+    empty = torch.zeros(2 * Cn + 1, device="cuda")  # a rank with no samples
+    gathered = torch.cat([moms[0], empty, moms[1], moms[2]])
+    x = xs[1]
+    w, b = torch.randn(Cn, device="cuda"), torch.randn(Cn, device="cuda")
+    rm1, rv1 = torch.randn(Cn, device="cuda"), torch.rand(Cn, device="cuda") + 0.5
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1, nb2 = (torch.zeros(1, dtype=torch.long, device="cuda") for _ in range(2))
+    mk1, mk2 = (torch.empty((x.shape[0], Cn // 4), dtype=torch.uint8, device="cuda")
+                for _ in range(2))
+    y1, st1 = C.bn1d_gathered_fwd(x, gathered, w, b, True, 1e-5, 0.1, rmean=rm1, rvar=rv1,
+                                  num_batches=nb1, mask_out=mk1)
+    st2 = C.bn_merge(gathered, Cn, 1e-5, 0.1, rm2, rv2, nb2)
+    y2 = C.bn_elemt(x, st2, w, b, True, None, mask_out=mk2)
+    assert torch.equal(st1, st2) and torch.equal(y1, y2) and torch.equal(mk1, mk2)
+    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and int(nb1) == int(nb2) == 1
+    xa = torch.cat(xs).double()
+    torch.testing.assert_close(st1[:Cn].double(), xa.mean(0), rtol=1e-5, atol=1e-5)
+    dy = torch.randn_like(x)
+    dw1, db1, dw2, db2 = (torch.empty(Cn, device="cuda") for _ in range(4))
+    s1 = C.bn1d_sums(dy, x, st1, mask=mk1, dw=dw1, db=db1)
+    s2 = C.bn_bwd_reduce(dy, x, st2, None, dw2, db2, 0.0, mask=mk2)
+    torch.testing.assert_close(s1, s2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dw1, dw2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-4)

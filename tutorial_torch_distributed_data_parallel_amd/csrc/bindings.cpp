@@ -826,6 +826,69 @@ std::vector<Tensor> bn1d_local_fwd_op(const Tensor& x, const c10::optional<Tenso
   return {y, stats};
 }
 
+// SyncBatchNorm halves (csrc/norm.hip whole-column kernels); undefined / [] when not taken
+Tensor bn1d_moments_op(const Tensor& x) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2, "bn1d_moments: [rows, C] input");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  auto m = at::empty({2 * C + 1}, x.options());
+  if (!bn1d_moments(x.data_ptr<float>(), N, C, m.data_ptr<float>(), cur_stream())) return Tensor();
+  return m;
+}
+
+std::vector<Tensor> bn1d_gathered_fwd_op(const Tensor& x, const Tensor& gathered,
+                                         const c10::optional<Tensor>& w,
+                                         const c10::optional<Tensor>& b, bool relu, double eps,
+                                         double momentum, const c10::optional<Tensor>& rmean,
+                                         const c10::optional<Tensor>& rvar,
+                                         const c10::optional<Tensor>& num_batches,
+                                         const c10::optional<Tensor>& mask_out,
+                                         const c10::optional<Tensor>& planes_out) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_GPU(gathered); CHECK_CONTIG(gathered);
+  TORCH_CHECK(x.dim() == 2, "bn1d_gathered_fwd: [rows, C] input");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  TORCH_CHECK(gathered.scalar_type() == at::kFloat && gathered.numel() % (2 * C + 1) == 0,
+              "bn1d_gathered_fwd: gathered must be [R][2C+1] fp32 moments");
+  const int R = (int)(gathered.numel() / (2 * C + 1));
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+                "bn1d_gathered_fwd: num_batches_tracked must be one int64");
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  for (const auto* t : {&w, &b, &rmean, &rvar})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->numel() == C && (*t)->is_contiguous(),
+                  "bn1d_gathered_fwd: [C] parameters");
+  auto y = at::empty_like(x);
+  auto stats = at::empty({2 * C + 1}, x.options());
+  const bool ok = bn1d_gathered_fwd(x.data_ptr<float>(), gathered.data_ptr<float>(), R, fptr(w),
+                                    fptr(b), N, C, relu, (float)eps, (float)momentum,
+                                    stats.data_ptr<float>(), fptr(rmean), fptr(rvar), nb,
+                                    y.data_ptr<float>(),
+                                    const_cast<uint8_t*>(mask_ptr(mask_out, x)),
+                                    planes_ptr(planes_out, x), cur_stream());
+  if (!ok) return {};
+  return {y, stats};
+}
+
+Tensor bn1d_sums_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
+                    const c10::optional<Tensor>& mask, const c10::optional<Tensor>& dw,
+                    const c10::optional<Tensor>& db) {
+  CHECK_GPU(dy); CHECK_F32(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "bn1d_sums: [rows, C] dy and x");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  TORCH_CHECK(stats.numel() == 2 * C + 1, "bn1d_sums: stats must be [2C+1]");
+  for (const auto* t : {&dw, &db})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->numel() == C && (*t)->is_contiguous(), "bn1d_sums: [C] gradients");
+  auto sums = at::empty({2 * C}, x.options());
+  if (!bn1d_sums(dy.data_ptr<float>(), x.data_ptr<float>(), stats.data_ptr<float>(), N, C,
+                 mask_ptr(mask, x), sums.data_ptr<float>(), fptr(dw), fptr(db), cur_stream()))
+    return Tensor();
+  return sums;
+}
+
 // its backward: dx (dw / db overwritten when given); undefined when the shape is not taken
 Tensor bn1d_local_bwd_op(const Tensor& dy, const Tensor& x, const Tensor& stats,
                          const c10::optional<Tensor>& w, const c10::optional<Tensor>& mask,
@@ -1904,6 +1967,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("db") = py::none(), py::arg("planes_out") = py::none(),
         py::arg("backend") = nullptr, py::arg("w_offset") = -1, py::arg("w_span") = 0,
         py::arg("b_offset") = -1, py::arg("b_span") = 0);
+  m.def("bn1d_moments", &bn1d_moments_op, py::arg("x"));
+  m.def("bn1d_gathered_fwd", &bn1d_gathered_fwd_op, py::arg("x"), py::arg("gathered"),
+        py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("eps"), py::arg("momentum"),
+        py::arg("rmean") = py::none(), py::arg("rvar") = py::none(),
+        py::arg("num_batches") = py::none(), py::arg("mask_out") = py::none(),
+        py::arg("planes_out") = py::none());
+  m.def("bn1d_sums", &bn1d_sums_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
+        py::arg("mask") = py::none(), py::arg("dw") = py::none(), py::arg("db") = py::none());
   m.def("bn_eval", &bn_eval_op);
   m.def("bn_bwd_reduce", &bn_bwd_reduce_op, py::arg("dy"), py::arg("x"), py::arg("stats"),
         py::arg("y_relu"), py::arg("dw"), py::arg("db"), py::arg("grad_beta"),

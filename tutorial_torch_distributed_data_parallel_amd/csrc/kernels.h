@@ -348,6 +348,16 @@ bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C
 // The matching backward, one launch: sums (bn_bwd_reduce), dw / db (overwritten, when given) and
 // dx (+ planes) from the same registers (bn_bwd_elemt). mask: the forward's ReLU mask or null.
 // wopt / bopt (world size 1, fused optimizer): update w / b in place instead of writing dw / db.
+// SyncBatchNorm halves of the same whole-column kernels (N <= kBn1dMaxRows, C % 16 == 0):
+// bn1d_moments = bn_moments ([mean | var | count]); bn1d_gathered_fwd = bn_merge + bn_elemt over
+// the all-gathered [R][2C+1] moments; bn1d_sums = bn_bwd_reduce (local sums + dw / db).
+bool bn1d_moments(const float* x, int N, int C, float* moments, hipStream_t s);
+bool bn1d_gathered_fwd(const float* x, const float* gathered, int R, const float* w,
+                       const float* b, int N, int C, bool relu, float eps, float momentum,
+                       float* stats, float* rmean, float* rvar, int64_t* nbt, float* y,
+                       uint8_t* mask_out, uint16_t* planes_out, hipStream_t s);
+bool bn1d_sums(const float* dy, const float* x, const float* stats, int N, int C,
+               const uint8_t* mask, float* sums, float* dw, float* db, hipStream_t s);
 bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const float* w, int N,
                     int C, const uint8_t* mask, float* dx, float* dw, float* db,
                     uint16_t* planes_out, hipStream_t s, const OptEpilogue* wopt = nullptr,

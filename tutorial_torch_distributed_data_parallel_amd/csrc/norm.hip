@@ -664,12 +664,21 @@ __device__ __forceinline__ f32x4 b1_reduce(f32x4 v, f32x4 (*sh)[4]) {
   return r;
 }
 
-template <int IT>
+// MODE kB1Local: this batch's statistics, then the normalisation (one rank).
+// MODE kB1Moments (SyncBatchNorm, before the all-gather): only the batch's moments
+//   [mean | var | count] -- bn_moments' layout -- into `stats`.
+// MODE kB1Gathered (after it): the R ranks' gathered moments `g` [R][2C+1] merged per channel in
+//   rank order exactly as merge_kernel does (zero-count ranks dropped), then the normalisation:
+//   bn_merge + bn_elemt in one launch.
+constexpr int kB1Local = 0, kB1Moments = 1, kB1Gathered = 2;
+
+template <int IT, int MODE>
 __global__ __launch_bounds__(256) void bn1d_local_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bb, int N,
     int C, int relu, float eps, float momentum, float* __restrict__ stats,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-    float* __restrict__ y, uint8_t* __restrict__ mk, uint16_t* __restrict__ pl) {
+    float* __restrict__ y, uint8_t* __restrict__ mk, uint16_t* __restrict__ pl,
+    const float* __restrict__ g, int R) {
   __shared__ f32x4 sh[kB1Lanes][4];
   const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
   const int c = blockIdx.x * kB1Cols + 4 * q;
@@ -681,17 +690,51 @@ __global__ __launch_bounds__(256) void bn1d_local_fwd_kernel(
     v[i] = r < N ? *reinterpret_cast<const f32x4*>(x + (long)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     s += v[i];
   }
-  const float n = (float)N;
-  const f32x4 mean = b1_reduce(s, sh) / n;
-  f32x4 m2 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 mean, var;
+  float n, m2t[4];
+  if constexpr (MODE == kB1Gathered) {
+    Wf wf[4] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    const long stride = 2L * C + 1;
+    for (int rk = 0; rk < R; ++rk) {
+      const float* row = g + rk * stride;
+      const float nr = row[2 * C];
+      if (nr <= 0.f) continue;
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    if (rg + kB1Lanes * i < N) {
-      const f32x4 d = v[i] - mean;
-      m2 += d * d;
+      for (int j = 0; j < 4; ++j) wf[j] = wf_merge(wf[j], Wf{nr, row[c + j], row[C + c + j] * nr});
     }
+    n = wf[0].n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mean[j] = wf[j].mean;
+      var[j] = wf[j].n > 0.f ? wf[j].m2 / wf[j].n : 0.f;
+      m2t[j] = wf[j].m2;
+    }
+  } else {
+    n = (float)N;
+    mean = b1_reduce(s, sh) / n;
+    f32x4 m2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      if (rg + kB1Lanes * i < N) {
+        const f32x4 d = v[i] - mean;
+        m2 += d * d;
+      }
+    }
+    var = b1_reduce(m2, sh) / n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m2t[j] = var[j] * n;
   }
-  const f32x4 var = b1_reduce(m2, sh) / n;
+  if constexpr (MODE == kB1Moments) {
+    if (rg == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[c + j] = mean[j];
+        stats[C + c + j] = var[j];
+      }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) stats[2 * C] = n;
+    return;
+  }
   float sc[4], sf[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -702,7 +745,9 @@ __global__ __launch_bounds__(256) void bn1d_local_fwd_kernel(
       stats[c + j] = mean[j];
       stats[C + c + j] = is;
       if (rmean) {
-        const float unbiased = n > 1.f ? var[j] * n / (n - 1.f) : var[j];
+        const float unbiased = MODE == kB1Gathered
+                                   ? (n > 1.f ? m2t[j] / (n - 1.f) : var[j])
+                                   : (n > 1.f ? var[j] * n / (n - 1.f) : var[j]);
         rmean[c + j] = fmaf(momentum, mean[j] - rmean[c + j], rmean[c + j]);
         rvar[c + j] = fmaf(momentum, unbiased - rvar[c + j], rvar[c + j]);
       }
@@ -762,12 +807,14 @@ struct OptElem {
   }
 };
 
-template <int IT>
+// SUMS (SyncBatchNorm, before the all-reduce): only this batch's [sum dy | sum dy (x - mean)]
+// into `sums` and the local dw / db -- bn_bwd_reduce in one launch; bn_bwd_elemt follows
+template <int IT, bool SUMS>
 __global__ __launch_bounds__(256) void bn1d_local_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ stats,
     const float* __restrict__ w, int N, int C, const uint8_t* __restrict__ mk,
     float* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    uint16_t* __restrict__ pl, OptEpilogue wo, OptEpilogue bo) {
+    uint16_t* __restrict__ pl, OptEpilogue wo, OptEpilogue bo, float* __restrict__ sums) {
   __shared__ f32x4 sh[kB1Lanes][4];
   __shared__ float tot[2][kB1Cols];  // this block's sum dy | sum dy (x - mean), per channel
   const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
@@ -804,6 +851,18 @@ __global__ __launch_bounds__(256) void bn1d_local_bwd_kernel(
   }
   const f32x4 sdy = b1_reduce(a, sh);
   const f32x4 sdyx = b1_reduce(m, sh);
+  if constexpr (SUMS) {
+    if (rg == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sums[c + j] = sdy[j];
+        sums[C + c + j] = sdyx[j];
+        if (dw) dw[c + j] = sdyx[j] * stats[C + c + j];
+        if (db) db[c + j] = sdy[j];
+      }
+    }
+    return;
+  }
   const float inv_count = 1.f / stats[2 * C];
   float k1[4], k2[4], k3[4];
 #pragma unroll
@@ -1026,8 +1085,9 @@ bool bn1d_local_fwd(const float* x, const float* w, const float* b, int N, int C
   const dim3 g(C / kB1Cols), t(256);
   const int r = relu ? 1 : 0;
   uint8_t* mk = relu ? mask_out : nullptr;
-#define B1F(IT) hipLaunchKernelGGL(bn1d_local_fwd_kernel<IT>, g, t, 0, s, x, w, b, N, C, r, eps, \
-                                   momentum, stats, rmean, rvar, nbt, y, mk, planes_out)
+#define B1F(IT) hipLaunchKernelGGL((bn1d_local_fwd_kernel<IT, kB1Local>), g, t, 0, s, x, w, b, N, \
+                                   C, r, eps, momentum, stats, rmean, rvar, nbt, y, mk, \
+                                   planes_out, (const float*)nullptr, 0)
   if (N <= 64) B1F(1);
   else if (N <= 128) B1F(2);
   else if (N <= 256) B1F(4);
@@ -1045,13 +1105,67 @@ bool bn1d_local_bwd(const float* dy, const float* x, const float* stats, const f
     if (q && ((uintptr_t)q & 15)) return false;
   const dim3 g(C / kB1Cols), t(256);
   const OptEpilogue wo = wopt ? *wopt : OptEpilogue{}, bo = bopt ? *bopt : OptEpilogue{};
-#define B1B(IT) hipLaunchKernelGGL(bn1d_local_bwd_kernel<IT>, g, t, 0, s, dy, x, stats, w, N, C, \
-                                   mask, dx, dw, db, planes_out, wo, bo)
+#define B1B(IT) hipLaunchKernelGGL((bn1d_local_bwd_kernel<IT, false>), g, t, 0, s, dy, x, stats, \
+                                   w, N, C, mask, dx, dw, db, planes_out, wo, bo, (float*)nullptr)
   if (N <= 64) B1B(1);
   else if (N <= 128) B1B(2);
   else if (N <= 256) B1B(4);
   else B1B(8);
 #undef B1B
+  return true;
+}
+
+bool bn1d_moments(const float* x, int N, int C, float* moments, hipStream_t s) {
+  if (N < 1 || N > kBn1dMaxRows || C % kB1Cols || ((uintptr_t)x & 15)) return false;
+  const dim3 g(C / kB1Cols), t(256);
+#define B1M(IT) hipLaunchKernelGGL((bn1d_local_fwd_kernel<IT, kB1Moments>), g, t, 0, s, x, \
+                                   (const float*)nullptr, (const float*)nullptr, N, C, 0, 0.f, \
+                                   0.f, moments, (float*)nullptr, (float*)nullptr, \
+                                   (int64_t*)nullptr, (float*)nullptr, (uint8_t*)nullptr, \
+                                   (uint16_t*)nullptr, (const float*)nullptr, 0)
+  if (N <= 64) B1M(1);
+  else if (N <= 128) B1M(2);
+  else if (N <= 256) B1M(4);
+  else B1M(8);
+#undef B1M
+  return true;
+}
+
+bool bn1d_gathered_fwd(const float* x, const float* gathered, int R, const float* w,
+                       const float* b, int N, int C, bool relu, float eps, float momentum,
+                       float* stats, float* rmean, float* rvar, int64_t* nbt, float* y,
+                       uint8_t* mask_out, uint16_t* planes_out, hipStream_t s) {
+  if (N < 1 || N > kBn1dMaxRows || C % kB1Cols || R < 1) return false;
+  for (const void* q : {(const void*)x, (const void*)y, (const void*)w, (const void*)b})
+    if (q && ((uintptr_t)q & 15)) return false;
+  const dim3 g(C / kB1Cols), t(256);
+  const int r = relu ? 1 : 0;
+  uint8_t* mk = relu ? mask_out : nullptr;
+#define B1G(IT) hipLaunchKernelGGL((bn1d_local_fwd_kernel<IT, kB1Gathered>), g, t, 0, s, x, w, b, \
+                                   N, C, r, eps, momentum, stats, rmean, rvar, nbt, y, mk, \
+                                   planes_out, gathered, R)
+  if (N <= 64) B1G(1);
+  else if (N <= 128) B1G(2);
+  else if (N <= 256) B1G(4);
+  else B1G(8);
+#undef B1G
+  return true;
+}
+
+bool bn1d_sums(const float* dy, const float* x, const float* stats, int N, int C,
+               const uint8_t* mask, float* sums, float* dw, float* db, hipStream_t s) {
+  if (N < 1 || N > kBn1dMaxRows || C % kB1Cols) return false;
+  for (const void* q : {(const void*)dy, (const void*)x, (const void*)stats})
+    if (q && ((uintptr_t)q & 15)) return false;
+  const dim3 g(C / kB1Cols), t(256);
+#define B1S(IT) hipLaunchKernelGGL((bn1d_local_bwd_kernel<IT, true>), g, t, 0, s, dy, x, stats, \
+                                   (const float*)nullptr, N, C, mask, (float*)nullptr, dw, db, \
+                                   (uint16_t*)nullptr, OptEpilogue{}, OptEpilogue{}, sums)
+  if (N <= 64) B1S(1);
+  else if (N <= 128) B1S(2);
+  else if (N <= 256) B1S(4);
+  else B1S(8);
+#undef B1S
   return true;
 }
 

@@ -99,6 +99,15 @@ _TORCH_K = _TorchKernels()
 
 _LOCAL1D = True  # one-rank BatchNorm1d in one launch per direction (set_local1d: A/B, tests)
 _LOCAL1D_UPDATE = True  # ... whose backward also applies the fused optimizer to w / b
+_SYNC1D = False  # ... and SyncBatchNorm's local halves (set_sync1d: A/B, tests)
+
+
+def set_sync1d(on: bool) -> bool:
+    """Turn the whole-column SyncBatchNorm halves (moments; merge + normalisation; sums) on/off;
+    returns the previous setting."""
+    global _SYNC1D
+    old, _SYNC1D = _SYNC1D, bool(on)
+    return old
 
 
 def set_local1d(on: bool, update: bool | None = None) -> bool:
@@ -163,6 +172,25 @@ class _BatchNormFn(torch.autograd.Function):
                                         rmean=running_mean, rvar=running_var,
                                         num_batches=num_batches, mask_out=mask, planes_out=pl)
             if r:
+                y, stats = r
+                ctx.local1d = True
+        # SyncBatchNorm over a batch of rows: the same whole-column kernels around the gather
+        # (moments in one launch; merge + normalisation in one launch)
+        sync1d = group is not None and rows4 and not ctx.nhwc and residual is None and \
+            part is None and _LOCAL1D and _SYNC1D
+        st = None
+        if y is None and sync1d:
+            st = native().bn1d_moments(x)
+            if st is not None and st.numel() == 0:
+                st = None
+            if st is not None:
+                gathered = group.all_gather_flat(st)
+                r = native().bn1d_gathered_fwd(x, gathered, weight, bias, relu, float(eps),
+                                               float(momentum), rmean=running_mean,
+                                               rvar=running_var, num_batches=num_batches,
+                                               mask_out=mask, planes_out=pl)
+                if not r:
+                    raise RuntimeError("bn1d_gathered_fwd refused the shape bn1d_moments took")
                 y, stats = r
                 ctx.local1d = True
         if y is None:
@@ -238,7 +266,14 @@ class _BatchNormFn(torch.autograd.Function):
                 attach_planes(dx, pl)
             return (dx if needs(ctx, 0) else None), dw, db, None, None, None, None, None, None, \
                 None, None, None, None
-        sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0, **mk)
+        sums = None
+        if ctx.local1d:
+            # SyncBatchNorm (ctx.group set): the local sums + dw / db in one launch
+            sums = native().bn1d_sums(dy, x, stats, mask=mask, dw=dw, db=db)
+            if sums is not None and sums.numel() == 0:
+                sums = None
+        if sums is None:
+            sums = K.bn_bwd_reduce(dy, x, stats, y, dw, db, 0.0, **mk)
         dx = dres = None
         want_res = ctx.has_res and needs(ctx, 9)
         if needs(ctx, 0) or want_res:
