@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--no-bn-update", action="store_true",
                     help="one-launch BatchNorm1d backward without the in-place optimizer step "
                          "on w / b (the reducer's flat pass updates them)")
+    ap.add_argument("--no-sync1d", action="store_true",
+                    help="SyncBatchNorm over a batch of rows through the split kernels")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
@@ -62,6 +64,11 @@ def main():
 
         importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.norm") \
             .set_local1d(True, update=False)
+    if a.no_sync1d:
+        import importlib
+
+        importlib.import_module("tutorial_torch_distributed_data_parallel_amd.ops.norm") \
+            .set_sync1d(False)
     sys.argv = [script] + rest[1:]
     runpy.run_path(script if os.path.isabs(script) else os.path.join(ROOT, script),
                    run_name="__main__")

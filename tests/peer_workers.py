@@ -242,7 +242,7 @@ def _assert_bitwise(m1, m2, tag):
             assert torch.equal(a, b), f"rank {r} {tag}: captured != eager for buffer {n}"
 
 
-def captured_syncbn_parity(rank, out_dir, steps=5, backend="peer"):
+def captured_syncbn_parity(rank, out_dir, steps=5, backend="peer", sync1d=False):
     """BASELINE config 3 (toy MLP + SyncBatchNorm) as a CAPTURED multi-rank step with real peers:
     the forward statistics all-gather and the backward all-reduce of every BN layer are recorded
     inline on the compute stream, the bucket / factored collectives on the side stream. Captured
@@ -251,6 +251,9 @@ def captured_syncbn_parity(rank, out_dir, steps=5, backend="peer"):
     import torch.nn as nn
     import torch.nn.functional as F
 
+    from tutorial_torch_distributed_data_parallel_amd.ops import norm as norm_mod
+
+    norm_mod.set_sync1d(sync1d)  # the whole-column SyncBN halves (csrc/norm.hip) or the split ones
     tdp.init_process_group(backend)
     r, W = rt.get_rank(), rt.get_world_size()
 

@@ -155,9 +155,10 @@ def test_bench_ladder_capture_failure_on_one_rank_runs_eagerly():
     assert any("capture failed" in f for f in c["fallbacks"]), c
 
 
+@pytest.mark.parametrize("sync1d", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_captured_syncbn_with_real_peers(tmp_path, world):
-    run(PW.captured_syncbn_parity, tmp_path, n=world)
+def test_captured_syncbn_with_real_peers(tmp_path, world, sync1d):
+    run(PW.captured_syncbn_parity, tmp_path, n=world, sync1d=sync1d)
 
 
 @pytest.mark.parametrize("world", [2, 3])

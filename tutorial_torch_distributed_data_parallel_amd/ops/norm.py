@@ -99,7 +99,7 @@ _TORCH_K = _TorchKernels()
 
 _LOCAL1D = True  # one-rank BatchNorm1d in one launch per direction (set_local1d: A/B, tests)
 _LOCAL1D_UPDATE = True  # ... whose backward also applies the fused optimizer to w / b
-_SYNC1D = False  # ... and SyncBatchNorm's local halves (set_sync1d: A/B, tests)
+_SYNC1D = True  # ... and SyncBatchNorm's local halves (set_sync1d: A/B, tests)
 
 
 def set_sync1d(on: bool) -> bool:
