@@ -189,10 +189,16 @@ class _BatchNormFn(torch.autograd.Function):
                                                float(momentum), rmean=running_mean,
                                                rvar=running_var, num_batches=num_batches,
                                                mask_out=mask, planes_out=pl)
-                if not r:
-                    raise RuntimeError("bn1d_gathered_fwd refused the shape bn1d_moments took")
-                y, stats = r
-                ctx.local1d = True
+                if r:
+                    y, stats = r
+                    ctx.local1d = True
+                else:  # (unaligned parameters) the split merge + normalisation, same moments
+                    stats = K.bn_merge(gathered, C, eps, momentum, running_mean, running_var,
+                                       num_batches)
+                    kw = {} if mask is None else {"mask_out": mask}
+                    if pl is not None:
+                        kw["planes_out"] = pl
+                    y = K.bn_elemt(x, stats, weight, bias, relu, residual, **kw)
         if y is None:
             if part is not None and ctx.nhwc:
                 # statistics from the producing convolution's GEMM epilogue (per-tile Chan merge)
