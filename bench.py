@@ -332,10 +332,20 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
     elif build_rehearsal is not None:
         from tutorial_torch_distributed_data_parallel_amd.train.graph import CapturedStep
 
-        d2, st = build_rehearsal()
+        d2, st1 = build_rehearsal()
+        # the timed step's replay form: G training steps per graph launch when the measured
+        # step ran that way (a W > 1 bench captures the same G-step graph), so the ratio to dp1
+        # compares schedules, not graph-launch counts
+        G = max(1, int(getattr(step, "graph_steps", 1) or 1))
+
+        def st():
+            for _ in range(G):
+                st1()
+        reps = max(1, n // G)
         g = CapturedStep(st, warmup=3)
-        out["rehearsal_ms"] = round(_time_steps(g.replay, n), 4)
+        out["rehearsal_ms"] = round(_time_steps(g.replay, reps) / G, 4)
         out["rehearsal_buckets"] = len(d2._bounds) - 1
+        out["rehearsal_graph_steps"] = G
         del g
         # the same schedule with its one-rank collectives turned into no-ops: at world size 1 an
         # all-gather / reduce-scatter is a local copy on the comm queue (factors, buckets) that
@@ -345,7 +355,7 @@ def diagnostics(a, ddp, step, step_ms, world, graph, barrier, build_rehearsal):
         d2._ops.skip_collectives = True
         try:
             g = CapturedStep(st, warmup=2)
-            out["rehearsal_schedule_ms"] = round(_time_steps(g.replay, n), 4)
+            out["rehearsal_schedule_ms"] = round(_time_steps(g.replay, reps) / G, 4)
             del g
         finally:
             d2._ops.skip_collectives = False
