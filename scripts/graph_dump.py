@@ -3,7 +3,7 @@
 comparing the dp1 step's graph with its multi-GPU rehearsal's. Also tries hipGraphDebugDotPrint
 into $DUMP_DIR/graph_<n>.dot.
 
-    python dev/gpu/graph_dump.py -- --steps 20 --warmup 5
+    python scripts/graph_dump.py -- --steps 20 --warmup 5
 """
 import ctypes
 import json
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.abspath(os.environ.get("DUMP_DIR", os.path.join(ROOT, "gpurun_out", "graphs")))
 os.makedirs(OUT, exist_ok=True)
