@@ -8,6 +8,15 @@ Protocol (same as torch's SyncBatchNorm, TORCH/nn/modules/_functions.py:7-209):
 With ``group=None`` the same kernels implement plain BatchNorm (one "rank").
 On CPU the identical protocol runs on torch ops (``_TorchKernels``), which is what the gloo
 multi-process tests exercise.
+
+A batch of rows (BatchNorm1d, N <= 512 rows, C % 16 == 0) runs the whole-column kernels instead
+(a workgroup owns 16 channels and every row): one launch per direction at one rank
+(``bn1d_local_fwd`` / ``bn1d_local_bwd``, the latter also applying the fused optimizer to w / b),
+``bn1d_moments`` -> all-gather -> ``bn1d_gathered_fwd`` and ``bn1d_sums`` -> all-reduce under
+SyncBatchNorm (``set_local1d`` / ``set_sync1d`` switch back to the split kernels).
+
+Reference: the README's SyncBatchNorm pitfall (/root/reference/README.md:79-81) -- BatchNorm
+statistics must be synced across ranks, via ``convert_sync_batchnorm`` before wrapping in DDP.
 """
 from __future__ import annotations
 
